@@ -1,0 +1,178 @@
+"""ctypes binding of libbcm3hip.so (include/bcm3hip.h).
+
+The product path: every evaluation goes through the HIP kernels in ``bcm3_amd/csrc``. There is
+no CPU fallback -- if the library is missing or no GPU is present, opening a context raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libbcm3hip.so")
+
+PK_TYPES = {"one": 0, "two": 1, "one_biphasic": 2, "two_biphasic": 3, "one_transit": 4, "two_transit": 5}
+ANALYTIC_BANANA, ANALYTIC_CIRCULAR = 1, 2
+OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES = 1, 2
+
+
+class PopPKModel(C.Structure):
+    """bcm3hip_popk_model"""
+    _fields_ = [
+        ("pk_type", C.c_int32), ("N", C.c_int32), ("num_pk_params", C.c_int32),
+        ("num_pk_pop_params", C.c_int32), ("d", C.c_int32), ("P", C.c_int32), ("T", C.c_int32),
+        ("sd_ix", C.c_int32), ("n_transit_ix", C.c_int32), ("transit_time_ix", C.c_int32),
+        ("biphasic_time_ix", C.c_int32), ("absorption2_ix", C.c_int32), ("max_steps", C.c_int32),
+        ("pad_", C.c_int32),
+        ("rtol", C.c_double), ("atol", C.c_double), ("MW", C.c_double), ("fixed_vod", C.c_double),
+        ("fixed_kf", C.c_double), ("fixed_kb", C.c_double),
+        ("transforms", C.c_void_p), ("time", C.c_void_p), ("observed", C.c_void_p), ("dose", C.c_void_p),
+        ("dosing_interval", C.c_void_p), ("dose_after_dose_change", C.c_void_p),
+        ("dose_change_time", C.c_void_p), ("intermittent", C.c_void_p), ("skipped_days", C.c_void_p),
+        ("simulate_until", C.c_void_p),
+    ]
+
+
+class AnalyticModel(C.Structure):
+    """bcm3hip_analytic_model"""
+    _fields_ = [("kind", C.c_int32), ("d", C.c_int32), ("p0", C.c_double), ("p1", C.c_double),
+                ("p2", C.c_double)]
+
+
+class TrajStats(C.Structure):
+    """bcm3hip_traj_stats"""
+    _fields_ = [(k, C.c_int32) for k in ("nst", "nfe", "nni", "nsetups", "nje", "netf", "ncfn", "nreinit")]
+
+
+STATS_DTYPE = np.dtype([(k, np.int32) for k in ("nst", "nfe", "nni", "nsetups", "nje", "netf", "ncfn", "nreinit")])
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libbcm3hip.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libbcm3hip.so not built at {LIB_PATH}; run __graft_entry__.build()")
+    # PyTorch-ROCm ships its own libamdhip64 (same SONAME libamdhip64.so.7). Loading torch first
+    # makes the dynamic loader bind this library to torch's copy, so the process has ONE HIP
+    # runtime and torch tensors / torch.distributed streams can be handed to our kernels.
+    # (Two runtimes in one process make the second initialisation fail.)
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    L = C.CDLL(LIB_PATH)
+    vp, sz, i32, i64 = C.c_void_p, C.c_size_t, C.c_int32, C.c_int64
+    L.bcm3hip_device_count.restype = C.c_int
+    L.bcm3hip_error_string.argtypes = [C.c_int]
+    L.bcm3hip_error_string.restype = C.c_char_p
+    L.bcm3hip_open_popk.argtypes = [C.c_int, C.POINTER(PopPKModel), C.POINTER(vp)]
+    L.bcm3hip_open_analytic.argtypes = [C.c_int, C.POINTER(AnalyticModel), C.POINTER(vp)]
+    L.bcm3hip_close.argtypes = [vp]
+    L.bcm3hip_set_option.argtypes = [vp, C.c_int, i64]
+    L.bcm3hip_num_variables.argtypes = [vp]
+    L.bcm3hip_eval_batch.argtypes = [vp, sz, sz, vp, vp, vp]
+    L.bcm3hip_eval_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
+    L.bcm3hip_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    L.bcm3hip_eval_batch_detail.argtypes = [vp, sz, sz, vp, vp, vp, vp, vp, vp]
+    for f in ("bcm3hip_open_popk", "bcm3hip_open_analytic", "bcm3hip_close", "bcm3hip_set_option",
+              "bcm3hip_num_variables", "bcm3hip_eval_batch", "bcm3hip_eval_batch_device",
+              "bcm3hip_last_kernel_ms", "bcm3hip_eval_batch_detail"):
+        getattr(L, f).restype = C.c_int
+    _lib = L
+    return L
+
+
+def check(code: int, what: str = "bcm3hip"):
+    if code != 0:
+        msg = lib().bcm3hip_error_string(code).decode()
+        raise RuntimeError(f"{what} failed: {msg} ({code})")
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+class Context:
+    """One GPU likelihood context (not thread-safe; one per host thread / GPU)."""
+
+    def __init__(self, handle, d: int, P: int = 1, N: int = 0, T: int = 0, keep=None):
+        self.h = handle
+        self.d, self.P, self.N, self.T = d, P, N, T
+        self._keep = keep
+
+    @classmethod
+    def popk(cls, model_fields: dict, device: int = 0) -> "Context":
+        """model_fields: the bcm3hip_popk_model fields; arrays as numpy arrays."""
+        m = PopPKModel()
+        keep = []
+        arrays = {"transforms": np.int32, "time": np.float64, "observed": np.float64, "dose": np.float64,
+                  "dosing_interval": np.float64, "dose_after_dose_change": np.float64,
+                  "dose_change_time": np.float64, "intermittent": np.int32, "skipped_days": np.uint8,
+                  "simulate_until": np.int32}
+        for name, _ in PopPKModel._fields_:
+            if name == "pad_":
+                continue
+            v = model_fields[name]
+            if name in arrays:
+                a = np.ascontiguousarray(v, dtype=arrays[name])
+                keep.append(a)
+                setattr(m, name, a.ctypes.data)
+            else:
+                setattr(m, name, v)
+        h = C.c_void_p()
+        check(lib().bcm3hip_open_popk(device, C.byref(m), C.byref(h)), "bcm3hip_open_popk")
+        return cls(h, int(m.d), int(m.P), int(m.N), int(m.T))
+
+    @classmethod
+    def analytic(cls, kind: int, d: int, p0: float, p1: float, p2: float = 0.0, device: int = 0) -> "Context":
+        m = AnalyticModel(kind, d, p0, p1, p2)
+        h = C.c_void_p()
+        check(lib().bcm3hip_open_analytic(device, C.byref(m), C.byref(h)), "bcm3hip_open_analytic")
+        return cls(h, d)
+
+    def set_option(self, opt: int, value: int):
+        check(lib().bcm3hip_set_option(self.h, opt, int(value)), "bcm3hip_set_option")
+
+    def eval(self, values: np.ndarray, detail: bool = False):
+        v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, self.d)
+        n = v.shape[0]
+        logp = np.empty(n)
+        status = np.empty(n, dtype=np.int32)
+        if not detail:
+            check(lib().bcm3hip_eval_batch(self.h, n, self.d, _ptr(v), _ptr(logp), _ptr(status)), "eval_batch")
+            return logp, status
+        pllh = np.empty(n * self.P)
+        traj = np.empty(n * self.P * self.N * self.T)
+        stats = np.empty(n * self.P, dtype=STATS_DTYPE)
+        check(lib().bcm3hip_eval_batch_detail(self.h, n, self.d, _ptr(v), _ptr(logp), _ptr(status), _ptr(pllh),
+                                              _ptr(traj), _ptr(stats)), "eval_batch_detail")
+        return dict(logp=logp, status=status, patient_llh=pllh.reshape(n, self.P),
+                    traj=traj.reshape(n, self.P, self.N, self.T), stats=stats.reshape(n, self.P))
+
+    def eval_device(self, n: int, values_ptr: int, logp_ptr: int, status_ptr: Optional[int] = None,
+                    stream: Optional[int] = None):
+        check(lib().bcm3hip_eval_batch_device(self.h, n, values_ptr, logp_ptr, status_ptr, stream),
+              "eval_batch_device")
+
+    def last_kernel_ms(self) -> float:
+        ms = C.c_float()
+        check(lib().bcm3hip_last_kernel_ms(self.h, C.byref(ms)), "last_kernel_ms")
+        return float(ms.value)
+
+    def close(self):
+        if self.h:
+            lib().bcm3hip_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

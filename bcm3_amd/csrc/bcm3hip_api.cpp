@@ -1,0 +1,330 @@
+// bcm3hip_api.cpp -- C-ABI of libbcm3hip.so (include/bcm3hip.h).
+//
+// Owns one HIP stream, the device copy of the model data and grow-only scratch buffers per
+// context. The batched evaluation replaces the reference's per-chain TaskManager fan-out
+// (SamplerPT::DoMutateMove, src/sampler/SamplerPT.cpp:308-319): one launch evaluates every
+// chain's proposal of a mutate step.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/bcm3hip.h"
+#include "popk_kernel.h"
+
+using namespace bcm3hip;
+
+struct bcm3hip_ctx {
+    int device = 0;
+    int kind = 0;  // 1 popk, 2 analytic
+    int d = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool timed = false;
+    PopPKDevModel pm{};
+    AnalyticDevModel am{};
+    std::vector<void*> model_allocs;
+    // grow-only scratch
+    double* values = nullptr;
+    size_t cap_values = 0;
+    double* logp = nullptr;
+    int32_t* status = nullptr;
+    size_t cap_n = 0;
+    double* pllh = nullptr;
+    int32_t* tstatus = nullptr;
+    size_t cap_traj = 0, cap_tstatus = 0, cap_status = 0;
+    double* traj = nullptr;
+    size_t cap_trajout = 0;
+    bcm3hip_traj_stats* stats = nullptr;
+    size_t cap_stats = 0;
+    int lanes_per_wave = 64;
+    int block_waves = 1;
+};
+
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t e_ = (x);                                                                               \
+        if (e_ != hipSuccess) {                                                                            \
+            fprintf(stderr, "bcm3hip: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return BCM3HIP_ERR_HIP;                                                                        \
+        }                                                                                                  \
+    } while (0)
+
+template <class T>
+static int grow(T*& p, size_t& cap, size_t need)
+{
+    if (need <= cap) return 0;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t n = need < 256 ? 256 : need;
+    if (hipMalloc((void**)&p, n * sizeof(T)) != hipSuccess) return BCM3HIP_ERR_ALLOC;
+    cap = n;
+    return 0;
+}
+
+template <class T>
+static int upload(bcm3hip_ctx* c, const T* host, size_t count, const T** dev_out)
+{
+    *dev_out = nullptr;
+    if (count == 0) return 0;
+    if (!host) return BCM3HIP_ERR_ARG;
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, count * sizeof(T)));
+    c->model_allocs.push_back(p);
+    HIPCHK(hipMemcpy(p, host, count * sizeof(T), hipMemcpyHostToDevice));
+    *dev_out = (const T*)p;
+    return 0;
+}
+
+static int ctx_common_init(bcm3hip_ctx* c, int device)
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return BCM3HIP_ERR_NODEVICE;
+    if (device < 0 || device >= count) return BCM3HIP_ERR_ARG;
+    c->device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev0));
+    HIPCHK(hipEventCreate(&c->ev1));
+    return 0;
+}
+
+extern "C" {
+
+int bcm3hip_device_count(void)
+{
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess) return 0;
+    return count;
+}
+
+const char* bcm3hip_error_string(int code)
+{
+    switch (code) {
+    case BCM3HIP_OK: return "success";
+    case BCM3HIP_ERR_ARG: return "invalid argument";
+    case BCM3HIP_ERR_HIP: return "HIP runtime error";
+    case BCM3HIP_ERR_NODEVICE: return "no HIP device";
+    case BCM3HIP_ERR_MODEL: return "invalid model description";
+    case BCM3HIP_ERR_ALLOC: return "device allocation failed";
+    default: return "unknown error";
+    }
+}
+
+int bcm3hip_open_popk(int device, const bcm3hip_popk_model* m, bcm3hip_ctx** out)
+{
+    if (!m || !out) return BCM3HIP_ERR_ARG;
+    *out = nullptr;
+    if (m->pk_type < BCM3HIP_PK_ONE || m->pk_type > BCM3HIP_PK_TWO_TRANSIT) return BCM3HIP_ERR_MODEL;
+    const bool two = m->pk_type == BCM3HIP_PK_TWO || m->pk_type == BCM3HIP_PK_TWO_BIPHASIC ||
+                     m->pk_type == BCM3HIP_PK_TWO_TRANSIT;
+    const bool transit = m->pk_type == BCM3HIP_PK_ONE_TRANSIT || m->pk_type == BCM3HIP_PK_TWO_TRANSIT;
+    const bool biphasic = m->pk_type == BCM3HIP_PK_ONE_BIPHASIC || m->pk_type == BCM3HIP_PK_TWO_BIPHASIC;
+    if (m->N != (two ? 3 : 2)) return BCM3HIP_ERR_MODEL;
+    if (m->d <= 0 || m->P <= 0 || m->T < 0 || m->sd_ix < 0 || m->sd_ix + 1 >= m->d) return BCM3HIP_ERR_MODEL;
+    if (m->num_pk_params + m->num_pk_pop_params * m->P + 1 >= m->d) return BCM3HIP_ERR_MODEL;
+    if (transit && (m->n_transit_ix < 0 || m->transit_time_ix < 0)) return BCM3HIP_ERR_MODEL;
+    if (biphasic && (m->biphasic_time_ix < 0 || m->absorption2_ix < 0)) return BCM3HIP_ERR_MODEL;
+    for (int j = 0; j < m->P; j++) {
+        if (m->simulate_until[j] < 0 || m->simulate_until[j] > m->T) return BCM3HIP_ERR_MODEL;
+        // ODESolver::SetDiscontinuity ignores t <= 0 (history-dependent in the reference): reject
+        if (!(m->dosing_interval[j] > 0.0)) return BCM3HIP_ERR_MODEL;
+    }
+    bcm3hip_ctx* c = new (std::nothrow) bcm3hip_ctx();
+    if (!c) return BCM3HIP_ERR_ALLOC;
+    int r = ctx_common_init(c, device);
+    if (r) {
+        bcm3hip_close(c);
+        return r;
+    }
+    c->kind = 1;
+    c->d = m->d;
+    PopPKDevModel& pm = c->pm;
+    pm.pk_type = m->pk_type;
+    pm.N = m->N;
+    pm.num_pk_params = m->num_pk_params;
+    pm.num_pk_pop_params = m->num_pk_pop_params;
+    pm.d = m->d;
+    pm.P = m->P;
+    pm.T = m->T;
+    pm.sd_ix = m->sd_ix;
+    pm.n_transit_ix = m->n_transit_ix;
+    pm.transit_time_ix = m->transit_time_ix;
+    pm.biphasic_time_ix = m->biphasic_time_ix;
+    pm.absorption2_ix = m->absorption2_ix;
+    pm.max_steps = m->max_steps;
+    pm.rtol = m->rtol;
+    pm.atol = m->atol;
+    pm.MW = m->MW;
+    pm.fixed_vod = m->fixed_vod;
+    pm.fixed_kf = m->fixed_kf;
+    pm.fixed_kb = m->fixed_kb;
+    const size_t P = m->P, T = m->T;
+    if ((r = upload(c, m->transforms, (size_t)m->d, &pm.transforms)) ||
+        (r = upload(c, m->time, T, &pm.time)) || (r = upload(c, m->observed, P * T, &pm.observed)) ||
+        (r = upload(c, m->dose, P, &pm.dose)) || (r = upload(c, m->dosing_interval, P, &pm.dosing_interval)) ||
+        (r = upload(c, m->dose_after_dose_change, P, &pm.dose_after_dose_change)) ||
+        (r = upload(c, m->dose_change_time, P, &pm.dose_change_time)) ||
+        (r = upload(c, m->intermittent, P, &pm.intermittent)) ||
+        (r = upload(c, m->skipped_days, P * 29, &pm.skipped_days)) ||
+        (r = upload(c, m->simulate_until, P, &pm.simulate_until))) {
+        bcm3hip_close(c);
+        return r;
+    }
+    *out = c;
+    return 0;
+}
+
+int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* m, bcm3hip_ctx** out)
+{
+    if (!m || !out) return BCM3HIP_ERR_ARG;
+    *out = nullptr;
+    if (m->kind != BCM3HIP_ANALYTIC_BANANA && m->kind != BCM3HIP_ANALYTIC_CIRCULAR) return BCM3HIP_ERR_MODEL;
+    if (m->d < (m->kind == BCM3HIP_ANALYTIC_BANANA ? 2 : 1)) return BCM3HIP_ERR_MODEL;
+    bcm3hip_ctx* c = new (std::nothrow) bcm3hip_ctx();
+    if (!c) return BCM3HIP_ERR_ALLOC;
+    int r = ctx_common_init(c, device);
+    if (r) {
+        bcm3hip_close(c);
+        return r;
+    }
+    c->kind = 2;
+    c->d = m->d;
+    c->am.kind = m->kind;
+    c->am.d = m->d;
+    c->am.p0 = m->p0;
+    c->am.p1 = m->p1;
+    c->am.p2 = m->p2;
+    *out = c;
+    return 0;
+}
+
+int bcm3hip_close(bcm3hip_ctx* c)
+{
+    if (!c) return 0;
+    if (c->stream) hipSetDevice(c->device);
+    for (void* p : c->model_allocs) hipFree(p);
+    hipFree(c->values);
+    hipFree(c->logp);
+    hipFree(c->status);
+    hipFree(c->pllh);
+    hipFree(c->tstatus);
+    hipFree(c->traj);
+    hipFree(c->stats);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int bcm3hip_set_option(bcm3hip_ctx* c, int option, int64_t value)
+{
+    if (!c) return BCM3HIP_ERR_ARG;
+    switch (option) {
+    case BCM3HIP_OPT_LANES_PER_WAVE:
+        if (value < 1 || value > 64) return BCM3HIP_ERR_ARG;
+        c->lanes_per_wave = (int)value;
+        return 0;
+    case BCM3HIP_OPT_BLOCK_WAVES:
+        if (value < 1 || value > 4) return BCM3HIP_ERR_ARG;
+        c->block_waves = (int)value;
+        return 0;
+    default: return BCM3HIP_ERR_ARG;
+    }
+}
+
+int bcm3hip_num_variables(const bcm3hip_ctx* c) { return c ? c->d : -1; }
+
+static int ensure_traj_scratch(bcm3hip_ctx* c, size_t n)
+{
+    size_t ntraj = n * (size_t)c->pm.P;
+    if (grow(c->pllh, c->cap_traj, ntraj)) return BCM3HIP_ERR_ALLOC;
+    if (grow(c->tstatus, c->cap_tstatus, ntraj)) return BCM3HIP_ERR_ALLOC;
+    return 0;
+}
+
+static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp, int32_t* dstatus,
+                  double* dtraj, bcm3hip_traj_stats* dstats, hipStream_t s)
+{
+    hipError_t e;
+    if (c->kind == 1) {
+        int r = ensure_traj_scratch(c, n);
+        if (r) return r;
+        e = launch_popk(c->pm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, dtraj, dstats,
+                        c->lanes_per_wave, c->block_waves, s, c->ev0, c->ev1);
+    } else {
+        e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, c->ev0, c->ev1);
+    }
+    if (e != hipSuccess) {
+        fprintf(stderr, "bcm3hip: kernel launch failed: %s\n", hipGetErrorString(e));
+        return BCM3HIP_ERR_HIP;
+    }
+    c->timed = true;
+    return 0;
+}
+
+int bcm3hip_eval_batch_device(bcm3hip_ctx* c, size_t n, const double* values_dev, double* logp_dev,
+                              int32_t* status_dev, void* stream)
+{
+    if (!c || (n > 0 && (!values_dev || !logp_dev))) return BCM3HIP_ERR_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch(c, n, values_dev, logp_dev, status_dev, nullptr, nullptr, s);
+}
+
+int bcm3hip_last_kernel_ms(bcm3hip_ctx* c, float* ms)
+{
+    if (!c || !ms || !c->timed) return BCM3HIP_ERR_ARG;
+    HIPCHK(hipEventSynchronize(c->ev1));
+    HIPCHK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return 0;
+}
+
+int bcm3hip_eval_batch_detail(bcm3hip_ctx* c, size_t n, size_t d, const double* values, double* logp,
+                              int32_t* status, double* patient_llh, double* traj, bcm3hip_traj_stats* stats)
+{
+    if (!c || (int)d != c->d || (n > 0 && (!values || !logp))) return BCM3HIP_ERR_ARG;
+    if (n == 0) return 0;
+    if ((patient_llh || traj || stats) && c->kind != 1) return BCM3HIP_ERR_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    if (grow(c->values, c->cap_values, n * d)) return BCM3HIP_ERR_ALLOC;
+    if (grow(c->logp, c->cap_n, n)) return BCM3HIP_ERR_ALLOC;
+    if (grow(c->status, c->cap_status, n)) return BCM3HIP_ERR_ALLOC;
+    size_t ntraj = (c->kind == 1) ? n * (size_t)c->pm.P : 0;
+    double* dtraj = nullptr;
+    bcm3hip_traj_stats* dstats = nullptr;
+    if (traj) {
+        if (grow(c->traj, c->cap_trajout, ntraj * (size_t)c->pm.N * (size_t)c->pm.T)) return BCM3HIP_ERR_ALLOC;
+        dtraj = c->traj;
+    }
+    if (stats) {
+        if (grow(c->stats, c->cap_stats, ntraj)) return BCM3HIP_ERR_ALLOC;
+        dstats = c->stats;
+    }
+    HIPCHK(hipMemcpyAsync(c->values, values, n * d * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    int r = launch(c, n, c->values, c->logp, c->status, dtraj, dstats, c->stream);
+    if (r) return r;
+    HIPCHK(hipMemcpyAsync(logp, c->logp, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (status) HIPCHK(hipMemcpyAsync(status, c->status, n * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    if (patient_llh)
+        HIPCHK(hipMemcpyAsync(patient_llh, c->pllh, ntraj * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    if (traj)
+        HIPCHK(hipMemcpyAsync(traj, dtraj, ntraj * c->pm.N * c->pm.T * sizeof(double), hipMemcpyDeviceToHost,
+                              c->stream));
+    if (stats)
+        HIPCHK(hipMemcpyAsync(stats, dstats, ntraj * sizeof(bcm3hip_traj_stats), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+int bcm3hip_eval_batch(bcm3hip_ctx* c, size_t n, size_t d, const double* values, double* logp, int32_t* status)
+{
+    return bcm3hip_eval_batch_detail(c, n, d, values, logp, status, nullptr, nullptr, nullptr);
+}
+
+}  // extern "C"

@@ -1,0 +1,41 @@
+// popk_kernel.h -- device-side model descriptor and launchers (internal to libbcm3hip.so).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/bcm3hip.h"
+
+namespace bcm3hip {
+
+// Same fields as bcm3hip_popk_model, with device pointers.
+struct PopPKDevModel {
+    int32_t pk_type, N, num_pk_params, num_pk_pop_params, d, P, T, sd_ix;
+    int32_t n_transit_ix, transit_time_ix, biphasic_time_ix, absorption2_ix, max_steps;
+    double rtol, atol, MW, fixed_vod, fixed_kf, fixed_kb;
+    const int32_t* transforms;
+    const double* time;
+    const double* observed;
+    const double* dose;
+    const double* dosing_interval;
+    const double* dose_after_dose_change;
+    const double* dose_change_time;
+    const int32_t* intermittent;
+    const uint8_t* skipped_days;
+    const int32_t* simulate_until;
+};
+
+hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
+                       double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
+                       bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, hipStream_t stream,
+                       hipEvent_t ev_start, hipEvent_t ev_stop);
+
+struct AnalyticDevModel {
+    int32_t kind, d;
+    double p0, p1, p2;
+};
+
+hipError_t launch_analytic(const AnalyticDevModel& m, int64_t n, const double* values, double* logp,
+                           int32_t* status, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
+
+}  // namespace bcm3hip

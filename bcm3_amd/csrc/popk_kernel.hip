@@ -1,0 +1,487 @@
+// popk_kernel.hip -- batched PopPK likelihood on MI355X (gfx950).
+//
+// One lane = one (chain-eval, patient) trajectory. Per lane:
+//   parameter map        LikelihoodPopPKTrajectory.cpp:283-310 (QuantileNormal, fastpow10,
+//                        VariableSet::TransformVariable)
+//   CVODE solve          ODESolver::SolveReturnSolution + ODESolverCVODE::Solve
+//                        (ODESolver.cpp:93-134, ODESolverCVODE.cpp:322-463) on bdf_lane.h
+//   dosing callbacks     TreatmentCallback / TreatmentCallbackBiphasic / CheckGiveTreatment
+//                        (.cpp:644-718)
+//   observation model    Student-t(nu=4), streamed as each output time is interpolated
+//                        (.cpp:410-424)
+// A second tiny kernel sums the per-patient terms of one evaluation in patient order with the
+// reference's break at -inf (.cpp:427-440) when P > 1.
+//
+// HBM layout: values[n][d] row-major (the sampler's layout); per-patient data arrays [P] / [P][T]
+// are read a handful of times per trajectory (L2/L1 resident). No other global traffic: the
+// whole integrator state lives in VGPRs.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "bdf_lane.h"
+#include "popk_kernel.h"
+
+namespace bcm3hip {
+
+// ---------------------------------------------------------------------------------------------
+// math on the path (ProbabilityDistributions.cpp, MathFunctions.h, VariableSet.cpp)
+
+BDF_INL double fastpow10(double x) { return exp(x * 2.3025850929940459); }
+
+BDF_INL double transform_var(int tf, double x)
+{
+    switch (tf) {
+    case 1: return exp(x);
+    case 2: return fastpow10(x);
+    case 3:
+        if (x > 0) {
+            double z = exp(-x);
+            return 1.0 / (1.0 + z);
+        } else {
+            double z = exp(x);
+            return z / (1.0 + z);
+        }
+    default: return x;
+    }
+}
+
+// standard normal quantile for p in (0, 0.5]: rational initial guess + Halley refinement
+__device__ double ndtri_lower(double p)
+{
+    double x;
+    if (p < 0.02425) {
+        double q = sqrt(-2.0 * log(p));
+        x = (((((-7.784894002430293e-03 * q - 3.223964580411365e-01) * q - 2.400758277161838e+00) * q -
+               2.549732539343734e+00) * q + 4.374664141464968e+00) * q + 2.938163982698783e+00) /
+            ((((7.784695709041462e-03 * q + 3.224671290700398e-01) * q + 2.445134137142996e+00) * q +
+              3.754408661907416e+00) * q + 1.0);
+    } else {
+        double q = p - 0.5, r = q * q;
+        x = (((((-3.969683028665376e+01 * r + 2.209460984245205e+02) * r - 2.759285104469687e+02) * r +
+               1.383577518672690e+02) * r - 3.066479806614716e+01) * r + 2.506628277459239e+00) * q /
+            (((((-5.447609879822406e+01 * r + 1.615858368580409e+02) * r - 1.556989798598866e+02) * r +
+               6.680131188771972e+01) * r - 1.328068155288572e+01) * r + 1.0);
+    }
+    for (int it = 0; it < 3; it++) {
+        double e = 0.5 * erfc(-x / 1.4142135623730951) - p;
+        double u = e * 2.5066282746310002 * exp(0.5 * x * x);
+        x = x - u / (1.0 + 0.5 * x * u);
+    }
+    return x;
+}
+
+// bcm3::QuantileNormal = Boost quantile(normal(mu, sigma), p) = mean - sigma*sqrt2*erfc_inv(2p)
+__device__ double quantile_normal(double p, double mu, double sigma)
+{
+    double z;
+    if (!(p > 0.0))
+        z = (p == 0.0) ? -INFINITY : NAN;
+    else if (!(p < 1.0))
+        z = (p == 1.0) ? INFINITY : NAN;
+    else if (p <= 0.5)
+        z = ndtri_lower(p);
+    else
+        z = -ndtri_lower(1.0 - p);
+    double r = z / 1.4142135623730951;  // -erfc_inv(2p)
+    r *= sigma * 1.4142135623730951;
+    r += mu;
+    return r;
+}
+
+BDF_INL double log_pdf_tnu4(double x, double mu, double sigma)
+{
+    double xn = (x - mu) / sigma;
+    return -0.9808292530117262 - 2.5 * log1p(0.25 * xn * xn) - log(sigma);
+}
+
+// ---------------------------------------------------------------------------------------------
+// PK models (LikelihoodPopPKTrajectory.cpp:446-642)
+
+template <int PKT>
+struct PKTraits {
+    static constexpr bool two = (PKT == BCM3HIP_PK_TWO || PKT == BCM3HIP_PK_TWO_BIPHASIC ||
+                                 PKT == BCM3HIP_PK_TWO_TRANSIT);
+    static constexpr bool transit = (PKT == BCM3HIP_PK_ONE_TRANSIT || PKT == BCM3HIP_PK_TWO_TRANSIT);
+    static constexpr bool biphasic = (PKT == BCM3HIP_PK_ONE_BIPHASIC || PKT == BCM3HIP_PK_TWO_BIPHASIC);
+    static constexpr int NS = two ? 3 : 2;
+};
+
+template <int PKT>
+struct PKLane {
+    using TR = PKTraits<PKT>;
+    static constexpr int NS = TR::NS;
+    double ka, ke, kel, kf, kb, ktr, ntr, lnf, ka2;
+    double dose, dose_after, dose_change_time, last_treatment;
+    bool biphasic_switch;
+
+    BDF_INL double cur_ka() const
+    {
+        if constexpr (TR::biphasic) return biphasic_switch ? ka : ka2;
+        return ka;
+    }
+
+    BDF_INL void rhs(double t, const double (&y)[NS], double (&dydt)[NS]) const
+    {
+        double a = cur_ka();
+        if constexpr (TR::transit) {
+            double d = dose;
+            if (t >= dose_change_time) d = dose_after;
+            double tst = t - last_treatment;
+            double transit = exp((ntr * log(ktr * tst) - ktr * tst) - lnf);
+            transit = ktr * transit * d;
+            dydt[0] = transit - (a + ke) * y[0];
+        } else {
+            dydt[0] = -(a + ke) * y[0];
+        }
+        if constexpr (TR::two) {
+            dydt[1] = a * y[0] - kel * y[1] - kf * y[1] + kb * y[2];
+            dydt[2] = kf * y[1] - kb * y[2];
+        } else {
+            dydt[1] = a * y[0] - kel * y[1];
+        }
+    }
+
+    BDF_INL void jac(double t, double (&J)[NS][NS]) const
+    {
+        double a = cur_ka();
+        J[0][0] = -(a + ke);
+        J[1][0] = a;
+        if constexpr (TR::two) {
+            J[1][1] = -(kel + kf);
+            J[1][2] = kb;
+            J[2][1] = kf;
+            J[2][2] = -kb;
+        } else {
+            J[1][1] = -kel;
+        }
+    }
+};
+
+// CheckGiveTreatment (.cpp:644-671)
+BDF_INL bool check_give_treatment(double t, const uint8_t* skipped, int intermittent)
+{
+    bool give = true;
+    int day = (int)floor(t / 24.0);
+    if (day >= 0 && day < 29 && skipped[day]) give = false;
+    if (intermittent == 1) {
+        double tiw = t - 7.0 * 24.0 * floor(t / (7.0 * 24.0));
+        if (tiw >= 5.0 * 24.0) give = false;
+    } else if (intermittent == 2) {
+        double tic = t - 28.0 * 24.0 * floor(t / (28.0 * 24.0));
+        if (tic >= 21.0 * 24.0) give = false;
+    } else if (intermittent == 3) {
+        double tiw = t - 7.0 * 24.0 * floor(t / (7.0 * 24.0));
+        if (tiw >= 4.0 * 24.0) give = false;
+    }
+    return give;
+}
+
+// ---------------------------------------------------------------------------------------------
+
+template <int PKT>
+__global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t ntraj, int lpw,
+                                                        const double* __restrict__ values,
+                                                        double* __restrict__ logp_direct,
+                                                        double* __restrict__ patient_llh,
+                                                        int32_t* __restrict__ traj_status,
+                                                        double* __restrict__ traj_out,
+                                                        bcm3hip_traj_stats* __restrict__ stats_out)
+{
+    using TR = PKTraits<PKT>;
+    constexpr int NS = TR::NS;
+    const int lane = threadIdx.x & 63;
+    if (lane >= lpw) return;
+    const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t g = gwave * lpw + lane;
+    if (g >= ntraj) return;
+    const int P = m.P;
+    const int64_t e = g / P;
+    const int j = (int)(g - e * P);
+    const int T = m.T;
+    const double* v = values + e * m.d;
+    const int npk = m.num_pk_params, npop = m.num_pk_pop_params;
+
+    // ---- parameter map (.cpp:263-310)
+    const int sdix = m.sd_ix;
+    const double sd = transform_var(m.transforms[sdix], v[sdix]);
+    const double sd2 = transform_var(m.transforms[sdix + 1], v[sdix + 1]);
+    PKLane<PKT> mdl;
+    mdl.ka = fastpow10(quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
+    mdl.ke = transform_var(m.transforms[1], v[1]);
+    const double vod = isnan(m.fixed_vod) ? transform_var(m.transforms[3], v[3]) : m.fixed_vod;
+    mdl.kel = fastpow10(quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / vod;
+    mdl.kf = mdl.kb = 0.0;
+    if constexpr (TR::two) {
+        if (isnan(m.fixed_kf)) {
+            mdl.kf = transform_var(m.transforms[4], v[4]);
+            mdl.kb = transform_var(m.transforms[5], v[5]);
+        } else {
+            mdl.kf = m.fixed_kf;
+            mdl.kb = m.fixed_kb;
+        }
+    }
+    mdl.ktr = mdl.ntr = mdl.lnf = 0.0;
+    if constexpr (TR::transit) {
+        const int ni = m.n_transit_ix, ti = m.transit_time_ix;
+        mdl.ntr = transform_var(m.transforms[ni], v[ni]);
+        mdl.ktr = (mdl.ntr + 1) / transform_var(m.transforms[ti], v[ti]);
+        const double n = mdl.ntr;
+        mdl.lnf = 0.9189385332046727 + (n + 0.5) * log(n) - n + log(1 + 1 / (12.0 * n));
+    }
+    const double interval = m.dosing_interval[j];
+    double tsw = 0.0;
+    mdl.ka2 = 0.0;
+    if constexpr (TR::biphasic) {
+        const int bi = m.biphasic_time_ix, ai = m.absorption2_ix;
+        tsw = transform_var(m.transforms[bi], v[bi]);
+        const double lim = interval - 1e-2;
+        tsw = (lim < tsw) ? lim : tsw;
+        mdl.ka2 = transform_var(m.transforms[ai], v[ai]);
+    }
+    mdl.dose = m.dose[j];
+    mdl.dose_after = m.dose_after_dose_change[j];
+    mdl.dose_change_time = m.dose_change_time[j];
+    mdl.last_treatment = 0.0;
+    mdl.biphasic_switch = true;
+    const int intermittent = m.intermittent[j];
+    const uint8_t* skipped = m.skipped_days + 29 * j;
+
+    // SetDiscontinuity (.cpp:357-364)
+    double current_dose_time;
+    double next_disc;
+    if constexpr (TR::biphasic) {
+        current_dose_time = 0.0;
+        next_disc = tsw;
+    } else {
+        current_dose_time = interval;
+        next_disc = interval;
+    }
+    // (a non-positive discontinuity time is ignored by ODESolver::SetDiscontinuity; the
+    //  host rejects such models, so next_disc > 0 here)
+
+    const double conversion = (1e6 / m.MW) / vod;
+    const int nsim = m.simulate_until[j];
+    const double* obs = m.observed + (int64_t)j * T;
+    double* tro = traj_out ? traj_out + g * (int64_t)NS * T : nullptr;
+
+    double llh = 0.0;
+    bool llh_done = false;  // NaN concentration seen: llh = -inf, stop accumulating
+    int status = BCM3HIP_STATUS_OK;
+
+    BdfState<NS> s;
+    s.cnt = BdfCounters{0, 0, 0, 0, 0, 0, 0, 0};
+    s.nst = 0;
+
+    // observation term for output index i with state yi (.cpp:412-423)
+    auto observe = [&](int i, const double (&yi)[NS]) {
+        if (tro) {
+#pragma unroll
+            for (int k = 0; k < NS; k++) tro[k * T + i] = yi[k];
+        }
+        if (llh_done) return;
+        const double x = conversion * yi[1];
+        const double yo = obs[i];
+        if (!isnan(yo)) {
+            const double xm = (x < 0.0) ? 0.0 : x;
+            llh += log_pdf_tnu4(x, yo, sd + sd2 * xm);
+        }
+        if (isnan(x)) {
+            llh = -INFINITY;
+            llh_done = true;
+        }
+    };
+
+    if (tro) {
+        for (int k = 0; k < NS * T; k++) tro[k] = NAN;
+    }
+
+    if (nsim > 0) {
+        double y0[NS];
+        y0[0] = TR::transit ? 0.0 : mdl.dose;
+#pragma unroll
+        for (int k = 1; k < NS; k++) y0[k] = 0.0;
+
+        // ODESolver::SolveReturnSolution: rows with t < DBL_EPSILON take y0
+        int tpi = 0;
+        bool done = false;
+        while (m.time[tpi] < 2.220446049250313e-16) {
+            observe(tpi, y0);
+            tpi++;
+            if (tpi == nsim) {
+                done = true;
+                break;
+            }
+        }
+        if (!done) {
+            const double end_time = m.time[nsim - 1];
+            double next_out = m.time[tpi];
+            // ODESolverCVODE::Solve
+            s.rtol = m.rtol;
+            s.atol = m.atol;
+#pragma unroll
+            for (int k = 0; k <= QMAX + 1; k++) s.tau[k] = 0.0;
+            s.saved_tq5 = 0.0;
+            s.hprime = s.h = s.eta = 0.0;
+            s.tstopset = 0;
+            double y[NS];
+#pragma unroll
+            for (int k = 0; k < NS; k++) y[k] = y0[k];
+            reinit<NS>(s, 0.0, y);
+            s.tstop = next_disc;
+            s.tstopset = 1;
+            int current_step = 0;
+            for (;;) {
+                double tret = 0.0;
+                int result = cvode_one_step<NS>(s, mdl, end_time, y, tret);
+                if (result < 0) {
+                    status = BCM3HIP_STATUS_SOLVER_FAIL;
+                    break;
+                }
+                const double t = tret;
+                current_step++;
+                while (tret >= next_out) {
+                    double dky[NS];
+                    if (get_dky<NS>(s, m.time[tpi], dky) != CV_SUCCESS) {
+                        status = BCM3HIP_STATUS_SOLVER_FAIL;
+                        break;
+                    }
+                    observe(tpi, dky);
+                    tpi++;
+                    if (tpi >= nsim) {
+                        next_out = INFINITY;
+                        break;
+                    }
+                    next_out = m.time[tpi];
+                }
+                if (status != BCM3HIP_STATUS_OK) break;
+                if (t >= end_time) break;
+                if (current_step == m.max_steps) {
+                    status = BCM3HIP_STATUS_SOLVER_FAIL;
+                    break;
+                }
+                if (result == CV_TSTOP_RETURN || next_disc == t) {
+                    // discontinuity callback
+                    if constexpr (TR::biphasic) {
+                        if (mdl.biphasic_switch) {
+                            mdl.biphasic_switch = false;
+                            current_dose_time += interval;
+                            next_disc = current_dose_time;
+                        } else if (check_give_treatment(t, skipped, intermittent)) {
+                            double d = mdl.dose;
+                            if (t >= mdl.dose_change_time) d = mdl.dose_after;
+                            y[0] = y[0] + d;
+                            mdl.biphasic_switch = true;
+                            next_disc = current_dose_time + tsw;
+                        } else {
+                            current_dose_time += interval;
+                            next_disc = current_dose_time;
+                        }
+                    } else {
+                        current_dose_time += interval;
+                        if (check_give_treatment(t, skipped, intermittent)) {
+                            double d = mdl.dose;
+                            if (t >= mdl.dose_change_time) d = mdl.dose_after;
+                            if constexpr (TR::transit)
+                                mdl.last_treatment = t;
+                            else
+                                y[0] = y[0] + d;
+                        }
+                        next_disc = current_dose_time;
+                    }
+                    reinit<NS>(s, t, y);
+                    s.tstop = next_disc;
+                    s.tstopset = 1;
+                }
+            }
+        }
+    }
+    if (status != BCM3HIP_STATUS_OK) llh = -INFINITY;
+
+    if (logp_direct) logp_direct[e] = 0.0 + llh;  // P == 1: logp = 0 + patient term
+    if (patient_llh) patient_llh[g] = llh;
+    if (traj_status) traj_status[g] = status;
+    if (stats_out) {
+        bcm3hip_traj_stats st;
+        st.nst = s.cnt.nst_total;
+        st.nfe = s.cnt.nfe;
+        st.nni = s.cnt.nni;
+        st.nsetups = s.cnt.nsetups;
+        st.nje = s.cnt.nje;
+        st.netf = s.cnt.netf;
+        st.ncfn = s.cnt.ncfn;
+        st.nreinit = s.cnt.nreinit;
+        stats_out[g] = st;
+    }
+}
+
+// Sequential per-evaluation sum over patients with the reference's break at -inf
+// (LikelihoodPopPKTrajectory.cpp:427-440); status = max over patients.
+__global__ void __launch_bounds__(256) popk_reduce_kernel(int64_t n, int P, const double* __restrict__ patient_llh,
+                                                          const int32_t* __restrict__ traj_status,
+                                                          double* __restrict__ logp, int32_t* __restrict__ status)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    double acc = 0.0;
+    int32_t st = 0;
+    for (int j = 0; j < P; j++) {
+        acc += patient_llh[e * P + j];
+        int32_t sj = traj_status[e * P + j];
+        st = sj > st ? sj : st;
+        if (acc == -INFINITY) break;
+    }
+    logp[e] = acc;
+    if (status) status[e] = st;
+}
+
+__global__ void copy_status_kernel(int64_t n, const int32_t* __restrict__ src, int32_t* __restrict__ dst)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) dst[e] = src[e];
+}
+
+hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
+                       double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
+                       bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, hipStream_t stream,
+                       hipEvent_t ev_start, hipEvent_t ev_stop)
+{
+    const int64_t ntraj = n * (int64_t)m.P;
+    if (ntraj == 0) return hipSuccess;
+    const int lpw = lanes_per_wave < 1 ? 1 : (lanes_per_wave > 64 ? 64 : lanes_per_wave);
+    const int bw = block_waves < 1 ? 1 : (block_waves > 4 ? 4 : block_waves);
+    const int64_t nwaves = (ntraj + lpw - 1) / lpw;
+    const int64_t nblocks = (nwaves + bw - 1) / bw;
+    dim3 grid((unsigned)nblocks), block(64 * bw);
+    const bool direct = (m.P == 1);
+    double* logp_direct = direct ? logp : nullptr;
+    if (ev_start) hipEventRecord(ev_start, stream);
+#define LAUNCH(PKT)                                                                                           \
+    hipLaunchKernelGGL(popk_traj_kernel<PKT>, grid, block, 0, stream, m, ntraj, lpw, values, logp_direct,     \
+                       patient_llh_scratch, traj_status_scratch, traj_out, stats_out)
+    switch (m.pk_type) {
+    case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;
+    case BCM3HIP_PK_TWO: LAUNCH(BCM3HIP_PK_TWO); break;
+    case BCM3HIP_PK_ONE_BIPHASIC: LAUNCH(BCM3HIP_PK_ONE_BIPHASIC); break;
+    case BCM3HIP_PK_TWO_BIPHASIC: LAUNCH(BCM3HIP_PK_TWO_BIPHASIC); break;
+    case BCM3HIP_PK_ONE_TRANSIT: LAUNCH(BCM3HIP_PK_ONE_TRANSIT); break;
+    case BCM3HIP_PK_TWO_TRANSIT: LAUNCH(BCM3HIP_PK_TWO_TRANSIT); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef LAUNCH
+    if (ev_stop) hipEventRecord(ev_stop, stream);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    const int tb = 256;
+    const unsigned rb = (unsigned)((n + tb - 1) / tb);
+    if (!direct) {
+        hipLaunchKernelGGL(popk_reduce_kernel, dim3(rb), dim3(tb), 0, stream, n, m.P, patient_llh_scratch,
+                           traj_status_scratch, logp, status);
+    } else if (status) {
+        hipLaunchKernelGGL(copy_status_kernel, dim3(rb), dim3(tb), 0, stream, n, traj_status_scratch, status);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace bcm3hip

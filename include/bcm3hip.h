@@ -1,0 +1,152 @@
+/*
+ * bcm3hip.h -- C-ABI of the MI355X likelihood-evaluation library (libbcm3hip.so).
+ *
+ * This is the drop-in boundary for BCM3's per-chain likelihood fan-out. It replaces, for the
+ * batched GPU path:
+ *   - the per-chain task fan-out SamplerPT::DoMutateMove -> TaskManager::AddTask ->
+ *     SamplerPTChain::MutateMove -> Sampler::EvaluateLikelihood ->
+ *     bcm3::Likelihood::EvaluateLogProbability
+ *     (src/sampler/SamplerPT.cpp:308-319, src/utils/TaskManager.cpp:36-116,
+ *      src/sampler/Sampler.cpp:164-180, src/sampler/Likelihood.h:29);
+ *   - LikelihoodPopPKTrajectory::EvaluateLogProbability and its CVODE solve
+ *     (src/likelihoods/LikelihoodPopPKTrajectory.cpp:259-718,
+ *      src/odecommon/ODESolverCVODE.cpp:322-463, dependencies/cvode-5.3.0/src/cvode/cvode.c);
+ *   - TestLikelihoodBanana / TestLikelihoodCircular::EvaluateLogProbability
+ *     (src/likelihoods/TestLikelihoodBanana.cpp:42-55, TestLikelihoodCircular.cpp:42-53).
+ * The reference's own C-ABI plugin (LikelihoodDLL: initialize_likelihood /
+ * evaluate_log_probability, src/likelihoods/LikelihoodDLL.cpp:34-116) is single-vector; its
+ * replacement symbols live in bcm3_dll.h on top of this header.
+ *
+ * Plain C types only; no torch / HIP types in signatures. Streams are passed as void*.
+ * Return codes: 0 = success, < 0 = fatal error (see bcm3hip_error_string). A fatal error maps
+ * to EvaluateLogProbability returning false in the host layer. Per-item model failures
+ * (solver failure / max_steps) are NOT errors: logp = -inf and status = 1, exactly as the
+ * reference (LikelihoodPopPKTrajectory.cpp:400-408).
+ * Threading: a context is not thread-safe; use one context per host thread / GPU.
+ * Determinism: logp[i] depends only on values[i] and the model (no batch coupling).
+ */
+#ifndef BCM3HIP_H
+#define BCM3HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BCM3HIP_OK 0
+#define BCM3HIP_ERR_ARG (-1)
+#define BCM3HIP_ERR_HIP (-2)
+#define BCM3HIP_ERR_NODEVICE (-3)
+#define BCM3HIP_ERR_MODEL (-4)
+#define BCM3HIP_ERR_ALLOC (-5)
+
+/* per-item status */
+#define BCM3HIP_STATUS_OK 0
+#define BCM3HIP_STATUS_SOLVER_FAIL 1 /* CVODE error or max_steps: logp = -inf */
+
+/* PKModelType after the reference's string mapping (LikelihoodPopPKTrajectory.h:28-36,
+ * .cpp:69-83; "one_biphasic_uptake" maps to TWO_BIPHASIC there). */
+enum {
+    BCM3HIP_PK_ONE = 0,
+    BCM3HIP_PK_TWO = 1,
+    BCM3HIP_PK_ONE_BIPHASIC = 2,
+    BCM3HIP_PK_TWO_BIPHASIC = 3,
+    BCM3HIP_PK_ONE_TRANSIT = 4,
+    BCM3HIP_PK_TWO_TRANSIT = 5
+};
+
+/* VariableSet::TransformVariable codes (src/sampler/VariableSet.cpp:97-124). */
+enum { BCM3HIP_TF_NONE = 0, BCM3HIP_TF_LOG = 1, BCM3HIP_TF_LOG10 = 2, BCM3HIP_TF_LOGIT = 3 };
+
+/* Flat PopPK model: everything LikelihoodPopPKTrajectory::Initialize derives from
+ * likelihood.xml + prior.xml + the pkdata file (.cpp:50-252). Host pointers; the arrays are
+ * copied to device memory by bcm3hip_open_popk and need not outlive the call. */
+typedef struct {
+    int32_t pk_type;           /* BCM3HIP_PK_* */
+    int32_t N;                 /* ODE states: 2 or 3 */
+    int32_t num_pk_params;     /* .cpp:99-120 */
+    int32_t num_pk_pop_params; /* 2 */
+    int32_t d;                 /* number of sampled variables */
+    int32_t P;                 /* patients */
+    int32_t T;                 /* time points */
+    int32_t sd_ix;             /* index of "standard_deviation" */
+    int32_t n_transit_ix;      /* "n_transit" or -1 */
+    int32_t transit_time_ix;   /* "mean_transit_time" or -1 */
+    int32_t biphasic_time_ix;  /* "biphasic_uptake_time" or -1 */
+    int32_t absorption2_ix;    /* "mean_absorption2" or -1 */
+    int32_t max_steps;         /* 2000 (ODESolverCVODE.cpp:45) */
+    int32_t pad_;
+    double rtol;               /* (double)1e-6f */
+    double atol;               /* min dose * (double)1e-6f */
+    double MW;                 /* molecular weight of the drug */
+    double fixed_vod;          /* NaN if sampled */
+    double fixed_kf;           /* NaN if sampled */
+    double fixed_kb;           /* NaN if sampled */
+    const int32_t* transforms; /* [d] BCM3HIP_TF_* */
+    const double* time;        /* [T] */
+    const double* observed;    /* [P*T], NaN = unobserved */
+    const double* dose;        /* [P] */
+    const double* dosing_interval;        /* [P] */
+    const double* dose_after_dose_change; /* [P] (NaN = none) */
+    const double* dose_change_time;       /* [P] (NaN = none) */
+    const int32_t* intermittent;          /* [P] 0..3 */
+    const uint8_t* skipped_days;          /* [P*29] treatment_interruptions flags */
+    const int32_t* simulate_until;        /* [P] number of time points simulated */
+} bcm3hip_popk_model;
+
+enum { BCM3HIP_ANALYTIC_BANANA = 1, BCM3HIP_ANALYTIC_CIRCULAR = 2 };
+typedef struct {
+    int32_t kind; /* BCM3HIP_ANALYTIC_* */
+    int32_t d;    /* dimension */
+    double p0;    /* banana: sd1 ; circular: radius */
+    double p1;    /* banana: sd2 ; circular: offset */
+    double p2;    /* circular: width */
+} bcm3hip_analytic_model;
+
+typedef struct bcm3hip_ctx bcm3hip_ctx;
+
+/* Per-trajectory solver counters (parity/diagnostics), one record per (item, patient). */
+typedef struct {
+    int32_t nst, nfe, nni, nsetups, nje, netf, ncfn, nreinit;
+} bcm3hip_traj_stats;
+
+/* Options (bcm3hip_set_option) */
+enum {
+    BCM3HIP_OPT_LANES_PER_WAVE = 1, /* trajectories per 64-lane wavefront: 1..64 (default 64) */
+    BCM3HIP_OPT_BLOCK_WAVES = 2     /* wavefronts per workgroup: 1..16 (default 1) */
+};
+
+int bcm3hip_device_count(void);
+const char* bcm3hip_error_string(int code);
+
+int bcm3hip_open_popk(int device, const bcm3hip_popk_model* model, bcm3hip_ctx** out);
+int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* model, bcm3hip_ctx** out);
+int bcm3hip_close(bcm3hip_ctx* ctx);
+int bcm3hip_set_option(bcm3hip_ctx* ctx, int option, int64_t value);
+int bcm3hip_num_variables(const bcm3hip_ctx* ctx);
+
+/* Host-buffer batch: values[n*d] row-major (one sampler-space vector per row, prior.xml order),
+ * logp[n], status[n] (may be NULL). Synchronous. */
+int bcm3hip_eval_batch(bcm3hip_ctx* ctx, size_t n, size_t d, const double* values, double* logp,
+                       int32_t* status);
+
+/* Device-resident batch on a caller stream (hipStream_t as void*, NULL = ctx stream):
+ * values_dev[n*d], logp_dev[n], status_dev[n] (may be NULL) are device pointers.
+ * Asynchronous; the kernel time of the launch is readable by bcm3hip_last_kernel_ms after the
+ * stream has synchronised. */
+int bcm3hip_eval_batch_device(bcm3hip_ctx* ctx, size_t n, const double* values_dev, double* logp_dev,
+                              int32_t* status_dev, void* stream);
+int bcm3hip_last_kernel_ms(bcm3hip_ctx* ctx, float* ms);
+
+/* Parity/diagnostic batch (host buffers, any output may be NULL):
+ * patient_llh[n*P], traj[n*P*N*T] (states at output times, NaN where not simulated),
+ * stats[n*P]. PopPK contexts only. */
+int bcm3hip_eval_batch_detail(bcm3hip_ctx* ctx, size_t n, size_t d, const double* values, double* logp,
+                              int32_t* status, double* patient_llh, double* traj, bcm3hip_traj_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
