@@ -273,8 +273,8 @@ int bcm3hip_eval_batch_device(bcm3hip_ctx* c, size_t n, const double* values_dev
 {
     if (!c || (n > 0 && (!values_dev || !logp_dev))) return BCM3HIP_ERR_ARG;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    return launch(c, n, values_dev, logp_dev, status_dev, nullptr, nullptr, s);
+    // the caller's stream as given (NULL = the null/default stream, e.g. torch's default stream)
+    return launch(c, n, values_dev, logp_dev, status_dev, nullptr, nullptr, (hipStream_t)stream);
 }
 
 int bcm3hip_last_kernel_ms(bcm3hip_ctx* c, float* ms)

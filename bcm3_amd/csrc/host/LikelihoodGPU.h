@@ -1,0 +1,99 @@
+// LikelihoodGPU.h -- MI355X-backed implementations of the reference's likelihood types on the
+// hot path, behind the bcm3::Likelihood interface:
+//   pop_pk_trajectory  LikelihoodPopPKTrajectory (src/likelihoods/LikelihoodPopPKTrajectory.h:10-115)
+//   banana             TestLikelihoodBanana      (src/likelihoods/TestLikelihoodBanana.cpp)
+//   circular           TestLikelihoodCircular    (src/likelihoods/TestLikelihoodCircular.cpp)
+// Each owns one libbcm3hip context (include/bcm3hip.h) on the configured device. There is no
+// CPU fallback: without a GPU, Initialize fails.
+#pragma once
+#include <mutex>
+#include <set>
+
+#include "../../../include/bcm3hip.h"
+#include "Likelihood.h"
+
+namespace bcm3 {
+
+class LikelihoodGPUBase : public Likelihood {
+public:
+    ~LikelihoodGPUBase() override;
+    // Reentrant: concurrent single evaluations are serialised on the context; the sampler's
+    // batched path issues one launch per mutate step.
+    bool IsReentrant() override { return true; }
+    bool EvaluateLogProbability(size_t threadix, const VectorReal& values, Real& logp) override;
+    bool EvaluateLogProbabilityBatch(size_t n, const Real* values, Real* logp, int32_t* status) override;
+    bool EvaluateLogProbabilityBatchDevice(size_t n, const Real* values_dev, Real* logp_dev, int32_t* status_dev,
+                                           void* stream) override;
+    float LastKernelMilliseconds() override;
+    bool SetBackendOption(int option, int64_t value) override;
+
+protected:
+    bool OpenDevice(const OptionsMap& vm);
+    virtual bool CheckEvaluable() { return true; }
+    int device = 0;
+    bcm3hip_ctx* ctx = nullptr;
+    std::mutex mutex;
+};
+
+class LikelihoodPopPKTrajectory : public LikelihoodGPUBase {
+public:
+    LikelihoodPopPKTrajectory(size_t sampling_threads, size_t evaluation_threads);
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+    bool PostInitialize() override { return true; }
+
+    size_t GetNumPatients() const { return patient_ids.size(); }
+    const std::vector<Real>& GetTimepoints() const { return time; }
+    // the flat model handed to the device (for diagnostics / tests)
+    const bcm3hip_popk_model& GetDeviceModel() const { return model; }
+
+protected:
+    bool CheckEvaluable() override;
+
+private:
+    enum PKModelType {
+        PKMT_OneCompartment,
+        PKMT_TwoCompartment,
+        PKMT_OneCompartmentBiphasicUptake,
+        PKMT_TwoCompartmentBiphasicUptake,
+        PKMT_OneCompartmentTransit,
+        PKMT_TwoCompartmentTransit,
+        PKMT_Undefined
+    };
+    size_t sampling_threads;
+    std::string drug;
+    PKModelType pk_type = PKMT_Undefined;
+    size_t num_pk_params = 0, num_pk_pop_params = 0;
+    Real fixed_vod, fixed_periphery_fwd, fixed_periphery_bwd;
+    std::vector<Real> time;
+    std::vector<std::string> patient_ids;
+    std::vector<Real> observed, dose, dosing_interval, dose_after_dose_change, dose_change_time;
+    std::vector<int32_t> intermittent, simulate_until, transforms;
+    std::vector<uint8_t> skipped_days;
+    Real MW;
+    bcm3hip_popk_model model{};
+};
+
+class TestLikelihoodBanana : public LikelihoodGPUBase {
+public:
+    TestLikelihoodBanana(size_t sampling_threads, size_t evaluation_threads) {}
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+
+private:
+    size_t dim = 0;
+    Real sd1 = 0, sd2 = 0;
+};
+
+class TestLikelihoodCircular : public LikelihoodGPUBase {
+public:
+    TestLikelihoodCircular(size_t sampling_threads, size_t evaluation_threads) {}
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+
+private:
+    size_t dimension = 0;
+    Real r = 2.0, offset = 3.5, w = 0.1;
+};
+
+}  // namespace bcm3

@@ -1,0 +1,126 @@
+// capi.cpp -- include/bcm3.h on top of the C++ host layer.
+#include <cstring>
+#include <memory>
+
+#include "../../../include/bcm3.h"
+#include "../../../include/bcm3hip.h"
+#include "Likelihood.h"
+#include "LikelihoodGPU.h"
+#include "log.h"
+
+struct bcm3_likelihood {
+    std::shared_ptr<bcm3::VariableSet> varset;
+    std::shared_ptr<bcm3::Likelihood> ll;
+};
+
+extern "C" {
+
+static int create(const char* likelihood_xml, const char* prior_xml, const bcm3::OptionsMap& vm,
+                  bcm3_likelihood** out)
+{
+    if (!likelihood_xml || !prior_xml || !out) return -1;
+    *out = nullptr;
+    auto h = std::make_unique<bcm3_likelihood>();
+    h->varset = std::make_shared<bcm3::VariableSet>();
+    if (!h->varset->LoadFromXML(prior_xml)) return -2;
+    h->ll = bcm3::LikelihoodFactory::CreateLikelihood(likelihood_xml, h->varset, vm, 1, 1, true);
+    if (!h->ll) return -3;
+    if (!h->ll->PostInitialize()) return -4;
+    *out = h.release();
+    return 0;
+}
+
+int bcm3_likelihood_create(const char* likelihood_xml, const char* prior_xml, int device, bcm3_likelihood** out)
+{
+    bcm3::OptionsMap vm;
+    if (device >= 0) vm["device"] = std::to_string(device);
+    return create(likelihood_xml, prior_xml, vm, out);
+}
+
+int bcm3_likelihood_create_ex(const char* likelihood_xml, const char* prior_xml, const char* options,
+                              bcm3_likelihood** out)
+{
+    bcm3::OptionsMap vm;
+    std::string s = options ? options : "";
+    size_t p = 0;
+    while (p < s.size()) {
+        size_t e = s.find(';', p);
+        if (e == std::string::npos) e = s.size();
+        std::string kv = s.substr(p, e - p);
+        size_t eq = kv.find('=');
+        if (eq != std::string::npos) vm[kv.substr(0, eq)] = kv.substr(eq + 1);
+        p = e + 1;
+    }
+    return create(likelihood_xml, prior_xml, vm, out);
+}
+
+int bcm3_likelihood_popk_model(const bcm3_likelihood* h, void* model)
+{
+    if (!h || !model) return -1;
+    auto* p = dynamic_cast<bcm3::LikelihoodPopPKTrajectory*>(h->ll.get());
+    if (!p) return -2;
+    *(bcm3hip_popk_model*)model = p->GetDeviceModel();
+    return 0;
+}
+
+void bcm3_likelihood_destroy(bcm3_likelihood* h) { delete h; }
+
+int bcm3_likelihood_num_variables(const bcm3_likelihood* h) { return h ? (int)h->varset->GetNumVariables() : -1; }
+
+int bcm3_likelihood_variable_name(const bcm3_likelihood* h, int i, char* buf, size_t buflen)
+{
+    if (!h || i < 0 || (size_t)i >= h->varset->GetNumVariables()) return -1;
+    const std::string& n = h->varset->GetVariableName((size_t)i);
+    if (buf && buflen) {
+        std::strncpy(buf, n.c_str(), buflen - 1);
+        buf[buflen - 1] = 0;
+    }
+    return (int)n.size();
+}
+
+int bcm3_likelihood_variable_transform(const bcm3_likelihood* h, int i)
+{
+    if (!h || i < 0 || (size_t)i >= h->varset->GetNumVariables()) return -1;
+    return (int)h->varset->GetVariableTransform((size_t)i);
+}
+
+int bcm3_likelihood_set_learning_rate(bcm3_likelihood* h, double lr)
+{
+    return (h && h->ll->SetLearningRate(lr)) ? 0 : -1;
+}
+
+int bcm3_likelihood_evaluate(bcm3_likelihood* h, size_t threadix, const double* values, double* logp)
+{
+    if (!h || !values || !logp) return -1;
+    bcm3::VectorReal v(values, values + h->varset->GetNumVariables());
+    return h->ll->EvaluateLogProbability(threadix, v, *logp) ? 0 : -2;
+}
+
+int bcm3_likelihood_evaluate_batch(bcm3_likelihood* h, size_t n, const double* values, double* logp, int32_t* status)
+{
+    if (!h || (n && (!values || !logp))) return -1;
+    return h->ll->EvaluateLogProbabilityBatch(n, values, logp, status) ? 0 : -2;
+}
+
+int bcm3_likelihood_evaluate_batch_device(bcm3_likelihood* h, size_t n, const double* values_dev, double* logp_dev,
+                                          int32_t* status_dev, void* stream)
+{
+    if (!h) return -1;
+    return h->ll->EvaluateLogProbabilityBatchDevice(n, values_dev, logp_dev, status_dev, stream) ? 0 : -2;
+}
+
+int bcm3_likelihood_last_kernel_ms(bcm3_likelihood* h, float* ms)
+{
+    if (!h || !ms) return -1;
+    *ms = h->ll->LastKernelMilliseconds();
+    return *ms < 0 ? -2 : 0;
+}
+
+int bcm3_likelihood_set_option(bcm3_likelihood* h, int option, int64_t value)
+{
+    return (h && h->ll->SetBackendOption(option, value)) ? 0 : -1;
+}
+
+const char* bcm3_last_error(void) { return bcm3::log_last_error(); }
+
+}  // extern "C"

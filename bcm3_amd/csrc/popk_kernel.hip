@@ -64,8 +64,10 @@ __device__ double ndtri_lower(double p)
             (((((-5.447609879822406e+01 * r + 1.615858368580409e+02) * r - 1.556989798598866e+02) * r +
                6.680131188771972e+01) * r - 1.328068155288572e+01) * r + 1.0);
     }
+    const bool central = (p > 0.25);  // residual via erf near p = 0.5 (p - 0.5 exact)
     for (int it = 0; it < 3; it++) {
-        double e = 0.5 * erfc(-x / 1.4142135623730951) - p;
+        double e = central ? 0.5 * erf(x / 1.4142135623730951) - (p - 0.5)
+                           : 0.5 * erfc(-x / 1.4142135623730951) - p;
         double u = e * 2.5066282746310002 * exp(0.5 * x * x);
         x = x - u / (1.0 + 0.5 * x * u);
     }
@@ -143,18 +145,53 @@ struct PKLane {
         }
     }
 
-    BDF_INL void jac(double t, double (&J)[NS][NS]) const
+    // Jacobian (CalculateJacobian_*, .cpp:457-642) is constant within a dosing segment, so the
+    // saved Jacobian of cvLsLinSys is re-derived here. Structural zeros of J (and hence of
+    // A = I - gamma J, sunmatrix_dense_eigen.cpp:128-133) are exploited in the closed-form inverse
+    // of sunlinsol_dense_eigen.cpp:111-178 / Eigen compute_inverse<3>: every cofactor term with a
+    // structural-zero factor is an exact zero there too.
+    struct Inv {
+        double i00, i10, i11, i12, i20, i21, i22;
+    };
+
+    BDF_INL void lin_setup(double gamma, Inv& r) const
     {
-        double a = cur_ka();
-        J[0][0] = -(a + ke);
-        J[1][0] = a;
+        const double a = cur_ka();
+        const double ng = -gamma;
+        const double a00 = (-(a + ke)) * ng + 1.0;
+        const double a10 = a * ng;
         if constexpr (TR::two) {
-            J[1][1] = -(kel + kf);
-            J[1][2] = kb;
-            J[2][1] = kf;
-            J[2][2] = -kb;
+            const double a11 = (-(kel + kf)) * ng + 1.0;
+            const double a12 = kb * ng;
+            const double a21 = kf * ng;
+            const double a22 = (-kb) * ng + 1.0;
+            const double c0 = a11 * a22 - a12 * a21;  // cofactor(0,0)
+            const double invdet = frcp(c0 * a00);    // det = c0*a00 + 0*a10 + 0*a20
+            r.i00 = c0 * invdet;
+            r.i10 = (-(a10 * a22)) * invdet;
+            r.i11 = (a22 * a00) * invdet;
+            r.i12 = (-(a00 * a12)) * invdet;
+            r.i20 = (a10 * a21) * invdet;
+            r.i21 = (-(a21 * a00)) * invdet;
+            r.i22 = (a00 * a11) * invdet;
         } else {
-            J[1][1] = -kel;
+            const double a11 = (-kel) * ng + 1.0;
+            const double invdet = frcp(a00 * a11);  // a00*a11 - a01*a10, a01 = 0
+            r.i00 = a11 * invdet;
+            r.i10 = -a10 * invdet;
+            r.i11 = a00 * invdet;
+            r.i12 = r.i20 = r.i21 = r.i22 = 0.0;
+        }
+    }
+
+    BDF_INL void lin_solve(const Inv& r, const double (&b)[NS], double (&x)[NS]) const
+    {
+        x[0] = r.i00 * b[0];
+        if constexpr (TR::two) {
+            x[1] = r.i10 * b[0] + r.i11 * b[1] + r.i12 * b[2];
+            x[2] = r.i20 * b[0] + r.i21 * b[1] + r.i22 * b[2];
+        } else {
+            x[1] = r.i10 * b[0] + r.i11 * b[1];
         }
     }
 };
@@ -270,7 +307,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     bool llh_done = false;  // NaN concentration seen: llh = -inf, stop accumulating
     int status = BCM3HIP_STATUS_OK;
 
-    BdfState<NS> s;
+    BdfState<NS, typename PKLane<PKT>::Inv> s;
     s.cnt = BdfCounters{0, 0, 0, 0, 0, 0, 0, 0};
     s.nst = 0;
 

@@ -1,0 +1,64 @@
+/*
+ * bcm3.h -- C-ABI of the host library libbcm3.so: the bcm3::Likelihood / LikelihoodFactory
+ * plugin surface of the reference (src/sampler/Likelihood.h:9-35,
+ * src/likelihoods/LikelihoodFactory.cpp:31-100, wired as in src/bcminf/main.cpp:47-121) built
+ * from the reference's own input files (prior.xml, likelihood.xml), backed by libbcm3hip.so.
+ *
+ * Replaces, for a caller that cannot link C++ (Python/ctypes, R .C(), Go cgo ...):
+ *   VariableSet::LoadFromXML (src/sampler/VariableSet.cpp:16-69)
+ *   LikelihoodFactory::CreateLikelihood + Likelihood::Initialize/PostInitialize
+ *   Likelihood::EvaluateLogProbability (single vector) and the batched fan-out of
+ *   SamplerPT::DoMutateMove (src/sampler/SamplerPT.cpp:308-319).
+ * Return codes: 0 ok, < 0 error (message in bcm3_last_error()). EvaluateLogProbability's
+ * "return false" maps to a negative return; logp = -inf is a legal result.
+ */
+#ifndef BCM3_H
+#define BCM3_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bcm3_likelihood bcm3_likelihood;
+
+/* Load prior.xml (variable set) + likelihood.xml, create and initialise the likelihood on HIP
+ * device `device` (-1: $BCM3_DEVICE or 0). */
+int bcm3_likelihood_create(const char* likelihood_xml, const char* prior_xml, int device, bcm3_likelihood** out);
+/* Same with options "key=value;key=value" (config.txt keys; "device=N", "backend=none" to
+ * initialise without a device -- evaluation then fails; used to test the host logic on CPU). */
+int bcm3_likelihood_create_ex(const char* likelihood_xml, const char* prior_xml, const char* options,
+                              bcm3_likelihood** out);
+/* The flat PopPK model derived by LikelihoodPopPKTrajectory::Initialize (type
+ * pop_pk_trajectory only). Pointers stay valid while the likelihood lives. `model` points to a
+ * bcm3hip_popk_model (bcm3hip.h). */
+int bcm3_likelihood_popk_model(const bcm3_likelihood* ll, void* model);
+void bcm3_likelihood_destroy(bcm3_likelihood* ll);
+int bcm3_likelihood_num_variables(const bcm3_likelihood* ll);
+/* name of variable i (prior.xml order, repeat-expanded); returns the name length or < 0 */
+int bcm3_likelihood_variable_name(const bcm3_likelihood* ll, int i, char* buf, size_t buflen);
+/* VariableSet::TransformVariable code of variable i (0 none, 1 log, 2 log10, 3 logit) */
+int bcm3_likelihood_variable_transform(const bcm3_likelihood* ll, int i);
+int bcm3_likelihood_set_learning_rate(bcm3_likelihood* ll, double learning_rate);
+
+/* EvaluateLogProbability(threadix, values[d], logp) */
+int bcm3_likelihood_evaluate(bcm3_likelihood* ll, size_t threadix, const double* values, double* logp);
+/* batched: values[n*d] row-major host buffers; status may be NULL */
+int bcm3_likelihood_evaluate_batch(bcm3_likelihood* ll, size_t n, const double* values, double* logp,
+                                   int32_t* status);
+/* batched on device buffers, asynchronous on `stream` (hipStream_t; NULL = null stream) */
+int bcm3_likelihood_evaluate_batch_device(bcm3_likelihood* ll, size_t n, const double* values_dev,
+                                          double* logp_dev, int32_t* status_dev, void* stream);
+/* duration of the last kernel launch in ms (HIP events on the launch stream) */
+int bcm3_likelihood_last_kernel_ms(bcm3_likelihood* ll, float* ms);
+/* backend option (BCM3HIP_OPT_* of bcm3hip.h) */
+int bcm3_likelihood_set_option(bcm3_likelihood* ll, int option, int64_t value);
+
+const char* bcm3_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

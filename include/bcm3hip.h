@@ -132,7 +132,7 @@ int bcm3hip_num_variables(const bcm3hip_ctx* ctx);
 int bcm3hip_eval_batch(bcm3hip_ctx* ctx, size_t n, size_t d, const double* values, double* logp,
                        int32_t* status);
 
-/* Device-resident batch on a caller stream (hipStream_t as void*, NULL = ctx stream):
+/* Device-resident batch on a caller stream (hipStream_t as void*; NULL = the null stream):
  * values_dev[n*d], logp_dev[n], status_dev[n] (may be NULL) are device pointers.
  * Asynchronous; the kernel time of the launch is readable by bcm3hip_last_kernel_ms after the
  * stream has synchronised. */

@@ -150,9 +150,12 @@ def _f32(x: float) -> float:
 
 
 def build_problem(pkdata: dict, trial: str, drug: str, pk_type_str: str, variables: List[Variable],
-                  fixed_vod=math.nan, fixed_kf=math.nan, fixed_kb=math.nan) -> PopPKProblem:
+                  fixed_vod=math.nan, fixed_kf=math.nan, fixed_kb=math.nan, check_count=True) -> PopPKProblem:
     """Restates LikelihoodPopPKTrajectory::Initialize (.cpp:50-252) for a pkdata dict in the
-    JSON sidecar layout (group -> variables, NaN as null)."""
+    JSON sidecar layout (group -> variables, NaN as null).
+
+    check_count=False skips the variable-count check of .cpp:127-130 (needed only to exercise the
+    biphasic models, whose named parameters cannot all fit the reference's count formula)."""
     g = pkdata[trial]
     pk_type = PK_TYPES[pk_type_str]
     names = [v.name for v in variables]
@@ -175,7 +178,7 @@ def build_problem(pkdata: dict, trial: str, drug: str, pk_type_str: str, variabl
     npk = NUM_PK_PARAMS[pk_type]
     npop = 2
     nfixed = sum(0 if math.isnan(x) else 1 for x in (fixed_vod, fixed_kf, fixed_kb))
-    if len(variables) != npk - nfixed + npop * (P + 1) + 2:
+    if check_count and len(variables) != npk - nfixed + npop * (P + 1) + 2:
         raise ValueError("Incorrect number of variables in prior")
     sim_until = np.zeros(P, dtype=np.int32)
     min_dose = float(np.finfo(np.float64).max)

@@ -51,9 +51,12 @@ static double ndtri_lower(double p) /* p in (0, 0.5] */
         x = (((((a[0] * r + a[1]) * r + a[2]) * r + a[3]) * r + a[4]) * r + a[5]) * q /
             (((((b[0] * r + b[1]) * r + b[2]) * r + b[3]) * r + b[4]) * r + 1.0);
     }
-    /* Halley refinement on Phi(x) = 0.5*erfc(-x/sqrt2) */
+    /* Halley refinement on Phi(x) = 0.5*erfc(-x/sqrt2); in the central region the residual is
+       formed as 0.5*erf(x/sqrt2) - (p - 0.5) (p - 0.5 exact) for relative accuracy near 0 */
+    const int central = (p > 0.25);
     for (int it = 0; it < 3; it++) {
-        double e = 0.5 * erfc(-x / 1.4142135623730951) - p;
+        double e = central ? 0.5 * erf(x / 1.4142135623730951) - (p - 0.5)
+                           : 0.5 * erfc(-x / 1.4142135623730951) - p;
         double u = e * 2.5066282746310002 * exp(0.5 * x * x);
         x = x - u / (1.0 + 0.5 * x * u);
     }

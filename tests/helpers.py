@@ -51,13 +51,23 @@ def make_problem(pk_type_str: str, P: int = 2, T_days: int = 7, intermittent=0, 
     base = [("pk_absorption_mean", -1.0, 0.0, False), ("k_excretion", -3.0, -1.5, True),
             ("pk_clearance_mean", 0.5, 1.5, False), ("volume_of_distribution", 1.5, 2.5, True)]
     extra = []
+    tail = []
+    if pk_type in (0, 2, 4):
+        extra += [("unused4", 0.0, 1.0, False), ("unused5", 0.0, 1.0, False)]
     if pk_type in (1, 3, 5):
         extra += [("k_periphery_fwd", -2.5, -1.0, True), ("k_periphery_bwd", -2.5, -1.0, True)]
     if pk_type in (2, 3):
-        extra += [("biphasic_uptake_time", 0.0, 1.0, True), ("mean_absorption2", -1.5, -0.5, True)]
+        # num_pk_params = 7 leaves one positional slot; the second named biphasic parameter can
+        # only be appended (see oracle.build_problem(check_count=False))
+        extra += [("biphasic_uptake_time", 0.0, 1.0, True)]
+        tail = [("mean_absorption2", -1.5, -0.5, True)]
     if pk_type in (4, 5):
-        extra += [("n_transit", 0.0, 1.0, True), ("mean_transit_time", 0.0, 0.7, True)]
-    pop = base + extra
+        extra = extra[:4 - len(base) + 2] if pk_type == 4 else extra
+        if pk_type == 4:
+            extra = [("n_transit", 0.0, 1.0, True), ("mean_transit_time", 0.0, 0.7, True)]
+        else:
+            extra += [("n_transit", 0.0, 1.0, True), ("mean_transit_time", 0.0, 0.7, True)]
+    pop = (base + extra)[:npk]
     while len(pop) < npk:
         pop.append((f"unused{len(pop)}", 0.0, 1.0, False))
     pop += [("pk_absorption_sd", 0.05, 0.3, False), ("pk_clearance_sd", 0.05, 0.3, False)]
@@ -65,7 +75,7 @@ def make_problem(pk_type_str: str, P: int = 2, T_days: int = 7, intermittent=0, 
     for j in range(P):
         pats += [(f"patient{j}_absorption", 0.05, 0.95, False), (f"patient{j}_clearance", 0.05, 0.95, False)]
     sds = [("standard_deviation", -1.0, 1.0, True), ("standard_deviation_proportional", -2.0, -0.7, True)]
-    allv = pop + pats + sds
+    allv = pop + pats + sds + tail
     variables = [O.Variable(n, lo, hi, O.TF_LOG10 if ls else O.TF_NONE) for n, lo, hi, ls in allv]
     nan = None
     obs = [[nan] + [float(x) for x in rng.uniform(50, 2000, T - 1)] for _ in range(P)]
@@ -83,7 +93,7 @@ def make_problem(pk_type_str: str, P: int = 2, T_days: int = 7, intermittent=0, 
         "lapatinib_intermittent": [intermittent] * P,
         "treatment_interruptions": ti,
     }}
-    prob = O.build_problem(pk, "TRIAL", "lapatinib", pk_type_str, variables)
+    prob = O.build_problem(pk, "TRIAL", "lapatinib", pk_type_str, variables, check_count=not tail)
     lo = np.array([v.lower for v in variables])
     hi = np.array([v.upper for v in variables])
     return prob, lo, hi
