@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libbcm3hip.so")
 
 PK_TYPES = {"one": 0, "two": 1, "one_biphasic": 2, "two_biphasic": 3, "one_transit": 4, "two_transit": 5}
 ANALYTIC_BANANA, ANALYTIC_CIRCULAR = 1, 2
-OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES = 1, 2
+OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES, OPT_TIMING_LOG = 1, 2, 3
 
 
 class PopPKModel(C.Structure):
@@ -77,6 +77,7 @@ def lib() -> C.CDLL:
     L.bcm3hip_close.argtypes = [vp]
     L.bcm3hip_set_option.argtypes = [vp, C.c_int, i64]
     L.bcm3hip_num_variables.argtypes = [vp]
+    L.bcm3hip_kernel_time_log.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(i64), C.POINTER(C.c_double)]
     L.bcm3hip_eval_batch.argtypes = [vp, sz, sz, vp, vp, vp]
     L.bcm3hip_eval_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
     L.bcm3hip_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float)]
@@ -165,6 +166,12 @@ class Context:
         ms = C.c_float()
         check(lib().bcm3hip_last_kernel_ms(self.h, C.byref(ms)), "last_kernel_ms")
         return float(ms.value)
+
+    def kernel_time_log(self):
+        """(total_ms, launches, max_ms) of the launches logged since the last call (OPT_TIMING_LOG)."""
+        tot, n, mx = C.c_double(), C.c_int64(), C.c_double()
+        check(lib().bcm3hip_kernel_time_log(self.h, C.byref(tot), C.byref(n), C.byref(mx)), "kernel_time_log")
+        return tot.value, n.value, mx.value
 
     def close(self):
         if self.h:

@@ -23,7 +23,12 @@ struct bcm3hip_ctx {
     int d = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t last0 = nullptr, last1 = nullptr;  // pair of the most recent launch
     bool timed = false;
+    // kernel-time log (BCM3HIP_OPT_TIMING_LOG): one event pair per launch, resolved lazily
+    bool log_timing = false;
+    std::vector<hipEvent_t> log_ev;
+    size_t log_used = 0;
     PopPKDevModel pm{};
     AnalyticDevModel am{};
     std::vector<void*> model_allocs;
@@ -40,7 +45,7 @@ struct bcm3hip_ctx {
     size_t cap_trajout = 0;
     bcm3hip_traj_stats* stats = nullptr;
     size_t cap_stats = 0;
-    int lanes_per_wave = 64;
+    int lanes_per_wave = 0;  // 0 = auto (auto_lanes_per_wave)
     int block_waves = 1;
 };
 
@@ -217,6 +222,7 @@ int bcm3hip_close(bcm3hip_ctx* c)
     hipFree(c->stats);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
+    for (hipEvent_t e : c->log_ev) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
     return 0;
@@ -227,12 +233,17 @@ int bcm3hip_set_option(bcm3hip_ctx* c, int option, int64_t value)
     if (!c) return BCM3HIP_ERR_ARG;
     switch (option) {
     case BCM3HIP_OPT_LANES_PER_WAVE:
-        if (value < 1 || value > 64) return BCM3HIP_ERR_ARG;
+        if (value < 0 || value > 64) return BCM3HIP_ERR_ARG;
         c->lanes_per_wave = (int)value;
         return 0;
     case BCM3HIP_OPT_BLOCK_WAVES:
         if (value < 1 || value > 4) return BCM3HIP_ERR_ARG;
         c->block_waves = (int)value;
+        return 0;
+    case BCM3HIP_OPT_TIMING_LOG:
+        if (value != 0 && value != 1) return BCM3HIP_ERR_ARG;
+        c->log_timing = value != 0;
+        c->log_used = 0;
         return 0;
     default: return BCM3HIP_ERR_ARG;
     }
@@ -248,22 +259,48 @@ static int ensure_traj_scratch(bcm3hip_ctx* c, size_t n)
     return 0;
 }
 
+// Measured on MI355X (profiles/r01_lpw_sweep.txt): the lane kernel runs best with about one
+// wavefront per CU -- a second wave on the same CU competes for the instruction cache -- so pack
+// trajectories into lanes only once there are more of them than CUs.
+static int auto_lanes_per_wave(size_t ntraj)
+{
+    int lpw = 1;
+    while (lpw < 64 && ntraj > (size_t)lpw * 256) lpw *= 2;
+    return lpw;
+}
+
 static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp, int32_t* dstatus,
                   double* dtraj, bcm3hip_traj_stats* dstats, hipStream_t s)
 {
     hipError_t e;
+    hipEvent_t e0 = c->ev0, e1 = c->ev1;
+    if (c->log_timing) {
+        if (c->log_ev.size() < 2 * (c->log_used + 1)) {
+            for (int k = 0; k < 2; k++) {
+                hipEvent_t ev;
+                HIPCHK(hipEventCreate(&ev));
+                c->log_ev.push_back(ev);
+            }
+        }
+        e0 = c->log_ev[2 * c->log_used];
+        e1 = c->log_ev[2 * c->log_used + 1];
+        c->log_used++;
+    }
     if (c->kind == 1) {
         int r = ensure_traj_scratch(c, n);
         if (r) return r;
         e = launch_popk(c->pm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, dtraj, dstats,
-                        c->lanes_per_wave, c->block_waves, s, c->ev0, c->ev1);
+                        c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
+                        c->block_waves, s, e0, e1);
     } else {
-        e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, c->ev0, c->ev1);
+        e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     }
     if (e != hipSuccess) {
         fprintf(stderr, "bcm3hip: kernel launch failed: %s\n", hipGetErrorString(e));
         return BCM3HIP_ERR_HIP;
     }
+    c->last0 = e0;
+    c->last1 = e1;
     c->timed = true;
     return 0;
 }
@@ -280,8 +317,26 @@ int bcm3hip_eval_batch_device(bcm3hip_ctx* c, size_t n, const double* values_dev
 int bcm3hip_last_kernel_ms(bcm3hip_ctx* c, float* ms)
 {
     if (!c || !ms || !c->timed) return BCM3HIP_ERR_ARG;
-    HIPCHK(hipEventSynchronize(c->ev1));
-    HIPCHK(hipEventElapsedTime(ms, c->ev0, c->ev1));
+    HIPCHK(hipEventSynchronize(c->last1));
+    HIPCHK(hipEventElapsedTime(ms, c->last0, c->last1));
+    return 0;
+}
+
+int bcm3hip_kernel_time_log(bcm3hip_ctx* c, double* total_ms, int64_t* launches, double* max_ms)
+{
+    if (!c || !total_ms || !launches) return BCM3HIP_ERR_ARG;
+    double tot = 0.0, mx = 0.0;
+    for (size_t i = 0; i < c->log_used; i++) {
+        float ms = 0.0f;
+        HIPCHK(hipEventSynchronize(c->log_ev[2 * i + 1]));
+        HIPCHK(hipEventElapsedTime(&ms, c->log_ev[2 * i], c->log_ev[2 * i + 1]));
+        tot += ms;
+        mx = ms > mx ? ms : mx;
+    }
+    *total_ms = tot;
+    *launches = (int64_t)c->log_used;
+    if (max_ms) *max_ms = mx;
+    c->log_used = 0;
     return 0;
 }
 

@@ -45,6 +45,8 @@ public:
                                                    int32_t* status_dev, void* stream);
     //! Duration of the last kernel launch (HIP events), < 0 if unknown.
     virtual float LastKernelMilliseconds() { return -1.0f; }
+    //! Summed / max kernel time and launch count since the last call (BCM3HIP_OPT_TIMING_LOG).
+    virtual bool KernelTimeLog(double& total_ms, int64_t& launches, double& max_ms) { return false; }
     //! Backend tuning option (bcm3hip_set_option); false if unsupported.
     virtual bool SetBackendOption(int option, int64_t value) { return false; }
 

@@ -82,6 +82,12 @@ float LikelihoodGPUBase::LastKernelMilliseconds()
     return ms;
 }
 
+bool LikelihoodGPUBase::KernelTimeLog(double& total_ms, int64_t& launches, double& max_ms)
+{
+    std::lock_guard<std::mutex> lock(mutex);
+    return ctx && bcm3hip_kernel_time_log(ctx, &total_ms, &launches, &max_ms) == 0;
+}
+
 bool LikelihoodGPUBase::SetBackendOption(int option, int64_t value) { return bcm3hip_set_option(ctx, option, value) == 0; }
 
 // ---------------------------------------------------------------------------------------------

@@ -25,6 +25,7 @@ public:
     bool EvaluateLogProbabilityBatchDevice(size_t n, const Real* values_dev, Real* logp_dev, int32_t* status_dev,
                                            void* stream) override;
     float LastKernelMilliseconds() override;
+    bool KernelTimeLog(double& total_ms, int64_t& launches, double& max_ms) override;
     bool SetBackendOption(int option, int64_t value) override;
 
 protected:

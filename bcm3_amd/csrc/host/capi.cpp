@@ -116,6 +116,15 @@ int bcm3_likelihood_last_kernel_ms(bcm3_likelihood* h, float* ms)
     return *ms < 0 ? -2 : 0;
 }
 
+int bcm3_likelihood_kernel_time_log(bcm3_likelihood* h, double* total_ms, int64_t* launches, double* max_ms)
+{
+    if (!h || !total_ms || !launches) return -1;
+    double mx = 0.0;
+    if (!h->ll->KernelTimeLog(*total_ms, *launches, mx)) return -2;
+    if (max_ms) *max_ms = mx;
+    return 0;
+}
+
 int bcm3_likelihood_set_option(bcm3_likelihood* h, int option, int64_t value)
 {
     return (h && h->ll->SetBackendOption(option, value)) ? 0 : -1;

@@ -41,6 +41,8 @@ def lib() -> C.CDLL:
     L.bcm3_likelihood_evaluate_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
     L.bcm3_likelihood_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.bcm3_likelihood_set_option.argtypes = [vp, C.c_int, C.c_int64]
+    L.bcm3_likelihood_kernel_time_log.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
+                                                  C.POINTER(C.c_double)]
     L.bcm3_last_error.restype = C.c_char_p
     _lib = L
     return L
@@ -117,6 +119,14 @@ class Likelihood:
         if r != 0:
             _err("last_kernel_ms", r)
         return float(ms.value)
+
+    def kernel_time_log(self):
+        """(total_ms, launches, max_ms) since the previous call; needs set_option(OPT_TIMING_LOG, 1)."""
+        tot, n, mx = C.c_double(), C.c_int64(), C.c_double()
+        r = lib().bcm3_likelihood_kernel_time_log(self.h, C.byref(tot), C.byref(n), C.byref(mx))
+        if r != 0:
+            _err("kernel_time_log", r)
+        return tot.value, n.value, mx.value
 
     def set_option(self, option: int, value: int):
         if lib().bcm3_likelihood_set_option(self.h, option, int(value)) != 0:

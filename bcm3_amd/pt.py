@@ -100,7 +100,7 @@ class PTExchange:
                               device=self.device)
         self.round = 0
         self.attempted = 0
-        self.accepted = 0
+        self.accepted = torch.zeros((), dtype=torch.int64, device=self.device)
 
     def lpowerposterior(self, llh, lprior):
         return torch.where(self.T == 0.0, lprior, lprior + self.T * llh)
@@ -135,7 +135,7 @@ class PTExchange:
             self._apply_local(values, llh, lprior, lpp, i1, i2, a, p1, p2)
             acc_mask[i1] = a
             self.attempted += len(loc_first)
-            self.accepted += int(a.sum())
+            self.accepted = self.accepted + a.sum()
         if wrap_local:
             i1 = torch.tensor([C - 1], dtype=torch.int64, device=dev)
             i2 = torch.tensor([0], dtype=torch.int64, device=dev)
@@ -144,7 +144,7 @@ class PTExchange:
             self._apply_local(values, llh, lprior, lpp, i1, i2, a, p1, p2)
             acc_mask[i1] = a
             self.attempted += 1
-            self.accepted += int(a.sum())
+            self.accepted = self.accepted + a.sum()
         if self.world > 1 and (g0 + C - 1 - start) % 2 == 0:
             self._cross(values, llh, lprior, lpp, acc_mask)
         self.round += 1
@@ -152,16 +152,18 @@ class PTExchange:
 
     @staticmethod
     def _apply_local(values, llh, lprior, lpp, i1, i2, a, p1, p2):
-        if not bool(a.any()):
-            return
-        s1, s2 = i1[a], i2[a]
-        v1, v2 = values[s1].clone(), values[s2].clone()
-        values[s1], values[s2] = v2, v1
-        l1, l2 = llh[s1].clone(), llh[s2].clone()
-        llh[s1], llh[s2] = l2, l1
-        q1, q2 = lprior[s1].clone(), lprior[s2].clone()
-        lprior[s1], lprior[s2] = q2, q1
-        lpp[s1], lpp[s2] = p1[a], p2[a]
+        """Swap accepted pairs without a host sync: gather through a pair permutation."""
+        C = llh.shape[0]
+        perm = torch.arange(C, device=llh.device)
+        perm[i1] = torch.where(a, i2, i1)
+        perm[i2] = torch.where(a, i1, i2)
+        new_lpp = lpp.clone()
+        new_lpp[i1] = torch.where(a, p1, lpp[i1])
+        new_lpp[i2] = torch.where(a, p2, lpp[i2])
+        values.copy_(values[perm])
+        llh.copy_(llh[perm])
+        lprior.copy_(lprior[perm])
+        lpp.copy_(new_lpp)
 
     def _cross(self, values, llh, lprior, lpp, acc_mask):
         """Slice-boundary pairs: (my last, next rank's first) and (prev rank's last, my first)."""
@@ -179,24 +181,25 @@ class PTExchange:
                dist.P2POp(dist.isend, send_first, prv, self.group), dist.P2POp(dist.irecv, recv_next, nxt, self.group)]
         for req in dist.batch_isend_irecv(ops):
             req.wait()
-        gl = self.rank * C + C - 1  # my last chain is the FIRST chain of the pair with the next rank
-        # pair A: (my last = chain1, next first = chain2)
+        dev = self.device
+        # pair A: (my last = chain1, next rank's first = chain2); its global index is my last chain's
         o = recv_next
-        a, p1, p2 = self._accept(self.T[C - 1:C], o[d + 3:d + 4], llh[C - 1:C], o[d:d + 1], lprior[C - 1:C],
-                                 o[d + 1:d + 2], lpp[C - 1:C], o[d + 2:d + 3],
-                                 torch.tensor([gl], dtype=torch.int64, device=self.device))
-        sendA = a.clone()
-        # pair B: (prev last = chain1, my first = chain2)
+        gl = torch.tensor([self.rank * C + C - 1], dtype=torch.int64, device=dev)
+        a, p1, _ = self._accept(self.T[C - 1:C], o[d + 3:d + 4], llh[C - 1:C], o[d:d + 1], lprior[C - 1:C],
+                                o[d + 1:d + 2], lpp[C - 1:C], o[d + 2:d + 3], gl)
+        # pair B: (previous rank's last = chain1, my first = chain2)
         q = recv_prev
-        gp = ((self.rank - 1) % self.world) * C + C - 1
-        b, r1, r2 = self._accept(q[d + 3:d + 4], self.T[0:1], q[d:d + 1], llh[0:1], q[d + 1:d + 2], lprior[0:1],
-                                 q[d + 2:d + 3], lpp[0:1], torch.tensor([gp], dtype=torch.int64, device=self.device))
-        if bool(a.item()):
-            values[C - 1] = o[:d]
-            llh[C - 1], lprior[C - 1], lpp[C - 1] = o[d], o[d + 1], p1[0]
-        if bool(b.item()):
-            values[0] = q[:d]
-            llh[0], lprior[0], lpp[0] = q[d], q[d + 1], r2[0]
-        acc_mask[C - 1] = sendA[0]
+        gp = torch.tensor([prv * C + C - 1], dtype=torch.int64, device=dev)
+        b, _, r2 = self._accept(q[d + 3:d + 4], self.T[0:1], q[d:d + 1], llh[0:1], q[d + 1:d + 2], lprior[0:1],
+                                q[d + 2:d + 3], lpp[0:1], gp)
+        values[C - 1] = torch.where(a, o[:d], values[C - 1])
+        llh[C - 1:C] = torch.where(a, o[d:d + 1], llh[C - 1:C])
+        lprior[C - 1:C] = torch.where(a, o[d + 1:d + 2], lprior[C - 1:C])
+        lpp[C - 1:C] = torch.where(a, p1, lpp[C - 1:C])
+        values[0] = torch.where(b, q[:d], values[0])
+        llh[0:1] = torch.where(b, q[d:d + 1], llh[0:1])
+        lprior[0:1] = torch.where(b, q[d + 1:d + 2], lprior[0:1])
+        lpp[0:1] = torch.where(b, r2, lpp[0:1])
+        acc_mask[C - 1:C] = a
         self.attempted += 1
-        self.accepted += int(sendA.sum())
+        self.accepted = self.accepted + a.sum()

@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Headline benchmark: PopPK ODE log-likelihood evaluations/s in the PT-MH loop.
+
+BASELINE.json metric "log-likelihood evals/sec (whole node), PopPK ODE @256 chains; HBM-roofline %"
+on configs[2] (PopPK ODE likelihood, 256 chains x 1 trajectory each, batched BDF on 1 MI355X) and,
+with --gpus N, configs[4] (256 chains per GPU, ladder sharded over N ranks, PT swap over RCCL).
+
+One step = one DeterministicEvenOdd PT-MH iteration of every chain on the rank
+(SamplerPT.cpp:203-212): exchange round, then a mutate move whose C likelihood evaluations
+run as ONE batched launch of the HIP BDF kernel (bcm3_likelihood_evaluate_batch_device).
+Everything stays in HBM; no host buffers inside the timed region.
+
+python bench.py --gpus N --steps K --warmup W        (N > 1: launched by torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+LIK_XML = os.path.join(GOLDEN, "c3_likelihood.xml")
+PRIOR_XML = os.path.join(GOLDEN, "c3_prior.xml")
+PROFILES = os.path.join(ROOT, "profiles")
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X spec, half the 157.3 TF FP32 vector rate
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--chains", type=int, default=256, help="tempered chains per GPU")
+    ap.add_argument("--lanes-per-wave", type=int, default=0, help="0 = auto")
+    ap.add_argument("--seed", type=int, default=20251016)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--throughput-batch", type=int, default=16384,
+                    help="extra: evals/s of one large batch (0 = skip); not the headline value")
+    return ap.parse_args()
+
+
+def algorithmic_bytes_per_eval(m) -> int:
+    """HBM bytes one likelihood evaluation must move at minimum: the parameter
+    vector in, the observations of every patient in, logp out. Output times / doses are shared
+    by every lane of a launch and counted once per launch, not per eval."""
+    return 8 * m.d + 8 * m.P * m.T + 8
+
+
+def traffic_from_profiles(tag: str, n: int):
+    """HBM bytes per launch from the committed PMC summary (tools/pmc_traffic.py), or None."""
+    path = os.path.join(PROFILES, f"r01_traffic_{tag}.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        if int(t.get("n", -1)) == n:
+            return float(t["bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def cpu_baseline(budget_s: float, seed: int):
+    """The reference CPU path on this box's host cores: the vendored CVODE 5.3.0 of the reference
+    (compiled from its sources into oracle/_ref, with the restated PopPK glue) evaluating prior
+    draws of the same C3 problem on a thread per core, like the reference's TaskManager fan-out."""
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), GOLDEN, os.path.join(ROOT, "tests")]
+    import numpy as np
+    import oracle as O
+    import helpers as H
+    kind = "reference"
+    try:
+        orc = O.Oracle("ref")
+    except FileNotFoundError:
+        orc, kind = O.Oracle("restated"), "port"
+    prob = H.c3_problem(1)
+    cores = len(os.sched_getaffinity(0))
+    rng = np.random.default_rng(seed)
+    lo = np.array([v.lower for v in prob.variables])
+    hi = np.array([v.upper for v in prob.variables])
+    batch = 256 * max(1, cores // 4)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        x = lo + rng.random((batch, prob.d)) * (hi - lo)
+        orc.popk_eval(prob, x, nthreads=cores, want_traj=False)
+        n += batch
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    return {"value": n / el, "unit": "log-likelihood evals/sec", "cores": cores, "kind": kind,
+            "sample": f"{n} uniform prior draws of the C3 PopPK problem in batches of {batch}, "
+                      f"{cores} threads, {el:.1f} s ({'oracle/_ref/libbcm3ref.so: reference CVODE 5.3.0 sources' if kind == 'reference' else 'oracle/liboracle.so restatement'})"}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)  # RCCL on ROCm
+
+    from bcm3_amd import _hip
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.pt import temperature_ladder
+    from bcm3_amd.sampler import DevicePrior, PTMHDevice, load_prior
+
+    ll = Likelihood(LIK_XML, PRIOR_XML, device=local)
+    if args.lanes_per_wave:
+        ll.set_option(_hip.OPT_LANES_PER_WAVE, args.lanes_per_wave)
+    m = ll.popk_model()
+    C = args.chains
+    prior = DevicePrior(load_prior(PRIOR_XML), device)
+    loop = PTMHDevice(ll, prior, temperature_ladder(C * world), rank=rank, world=world, seed=args.seed,
+                      device=device)
+
+    for _ in range(args.warmup):
+        loop.iteration()
+    torch.cuda.synchronize()
+    ll.set_option(_hip.OPT_TIMING_LOG, 1)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loop.iteration()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    k_total, k_launches, k_max = ll.kernel_time_log()
+    ll.set_option(_hip.OPT_TIMING_LOG, 0)
+    k_avg = k_total / max(1, k_launches)
+    if world > 1:
+        t = torch.tensor([dt, k_avg], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, k_avg = float(t[0]), float(t[1])
+
+    evals = C * world * args.steps * loop.exploration_steps
+    value = evals / dt
+    b_eval = algorithmic_bytes_per_eval(m)
+    achieved_gbs = b_eval * C / (k_avg * 1e-3) / 1e9
+    tb = traffic_from_profiles("c3_256", C)
+
+    extra = {}
+    if rank == 0 and args.throughput_batch > 0:
+        # extra (not the headline): one large batch of proposals, to show the chip-filling rate
+        n = args.throughput_batch
+        x = prior.sample(n, loop.gen).contiguous()
+        out = torch.empty(n, dtype=torch.float64, device=device)
+        stream = torch.cuda.current_stream(device).cuda_stream
+        ll.evaluate_batch_device(n, x.data_ptr(), out.data_ptr(), None, stream)
+        torch.cuda.synchronize()
+        ll.set_option(_hip.OPT_TIMING_LOG, 1)
+        reps = 3
+        for _ in range(reps):
+            ll.evaluate_batch_device(n, x.data_ptr(), out.data_ptr(), None, stream)
+        tt, nl, _ = ll.kernel_time_log()
+        ll.set_option(_hip.OPT_TIMING_LOG, 0)
+        extra["throughput_batch"] = {"n": n, "kernel_ms": tt / nl, "evals_per_s": n / (tt / nl * 1e-3)}
+
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    cpu = None
+    if world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args.cpu_seconds, args.seed)
+
+    acc_mut = float(loop.accepted_mutate) / max(1, loop.attempted_mutate)
+    line = {
+        "metric": "log-likelihood evals/sec (whole node), PopPK ODE @256 chains; HBM-roofline %",
+        "value": value,
+        "unit": "log-likelihood evals/sec",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (C3 PopPK data simulated from fixed true parameters; chains start at prior draws)",
+        "config": {
+            "workload": "PopPK ODE likelihood (pop_pk_trajectory, two-compartment lapatinib, 1 patient x 16 "
+                        "observations, 14 q24h doses, CVODE-BDF rtol 1e-6), 256 tempered chains per GPU; "
+                        "step = one PT-MH iteration (even/odd exchange + mutate with one batched eval)",
+            "chains_per_gpu": C,
+            "global_chains": C * world,
+            "lanes_per_wave": args.lanes_per_wave or "auto",
+            "parallelism": f"chains sharded over {world} rank(s); PT swap = RCCL neighbour send/recv",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": tb,
+            "kernel": "popk_traj_kernel<TWO>",
+            "kernel_ms_avg": k_avg,
+            "algorithmic_bytes_per_eval": b_eval,
+            "note": "the BDF lane kernel is FP64-VALU latency bound, not HBM bound (DESIGN.md §4)",
+        },
+        "cpu_baseline": cpu,
+        "kernel_share_of_step": k_avg / (dt / args.steps * 1e3),
+        "mutate_acceptance": acc_mut,
+        **extra,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -53,6 +53,9 @@ int bcm3_likelihood_evaluate_batch_device(bcm3_likelihood* ll, size_t n, const d
                                           double* logp_dev, int32_t* status_dev, void* stream);
 /* duration of the last kernel launch in ms (HIP events on the launch stream) */
 int bcm3_likelihood_last_kernel_ms(bcm3_likelihood* ll, float* ms);
+/* kernel time log (enable with option BCM3HIP_OPT_TIMING_LOG): summed / max kernel ms and the
+ * number of launches since the previous call; synchronises on the logged launches */
+int bcm3_likelihood_kernel_time_log(bcm3_likelihood* ll, double* total_ms, int64_t* launches, double* max_ms);
 /* backend option (BCM3HIP_OPT_* of bcm3hip.h) */
 int bcm3_likelihood_set_option(bcm3_likelihood* ll, int option, int64_t value);
 

@@ -114,8 +114,9 @@ typedef struct {
 
 /* Options (bcm3hip_set_option) */
 enum {
-    BCM3HIP_OPT_LANES_PER_WAVE = 1, /* trajectories per 64-lane wavefront: 1..64 (default 64) */
-    BCM3HIP_OPT_BLOCK_WAVES = 2     /* wavefronts per workgroup: 1..16 (default 1) */
+    BCM3HIP_OPT_LANES_PER_WAVE = 1, /* trajectories per wavefront: 1..64, 0 = auto (default) */
+    BCM3HIP_OPT_BLOCK_WAVES = 2,    /* wavefronts per workgroup: 1..4 (default 1) */
+    BCM3HIP_OPT_TIMING_LOG = 3      /* 1: keep one HIP event pair per launch (see kernel_time_log) */
 };
 
 int bcm3hip_device_count(void);
@@ -139,6 +140,10 @@ int bcm3hip_eval_batch(bcm3hip_ctx* ctx, size_t n, size_t d, const double* value
 int bcm3hip_eval_batch_device(bcm3hip_ctx* ctx, size_t n, const double* values_dev, double* logp_dev,
                               int32_t* status_dev, void* stream);
 int bcm3hip_last_kernel_ms(bcm3hip_ctx* ctx, float* ms);
+/* With BCM3HIP_OPT_TIMING_LOG on: synchronises on every launch logged since the last call and
+ * returns the summed / maximum kernel time (HIP events recorded on each launch's own stream) and
+ * the number of launches, then clears the log. Lets a timed loop run without host syncs. */
+int bcm3hip_kernel_time_log(bcm3hip_ctx* ctx, double* total_ms, int64_t* launches, double* max_ms);
 
 /* Parity/diagnostic batch (host buffers, any output may be NULL):
  * patient_llh[n*P], traj[n*P*N*T] (states at output times, NaN where not simulated),
