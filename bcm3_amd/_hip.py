@@ -12,7 +12,8 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libbcm3hip.so")
+# BCM3HIP_LIB overrides the library (profiling builds, tools/phase_probe.py only)
+LIB_PATH = os.environ.get("BCM3HIP_LIB") or os.path.join(_HERE, "lib", "libbcm3hip.so")
 
 PK_TYPES = {"one": 0, "two": 1, "one_biphasic": 2, "two_biphasic": 3, "one_transit": 4, "two_transit": 5}
 ANALYTIC_BANANA, ANALYTIC_CIRCULAR = 1, 2

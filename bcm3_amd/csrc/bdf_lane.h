@@ -15,8 +15,12 @@
 //    (I - gamma J)^-1 and all step-control scalars live in VGPRs for the whole solve;
 //  * every expensive operation has ONE call site (rescale, restore, residual/RHS in Newton,
 //    the h-ratio root), so the hot loop is short and the instruction cache stays warm;
-//  * loops over the runtime order q are unrolled over 1..QMAX with per-j guards (compile-time
-//    register indices; a runtime index would put the arrays in scratch memory);
+//  * every array index is a compile-time constant at the source level (cfor: template
+//    recursion, not loops), so the first SROA pass turns the whole state into SSA values before
+//    any pass can form a pointer select; loops over the runtime order q are expanded over
+//    1..QMAX with per-j guards on q. No inline-asm barriers: with one trajectory per wavefront
+//    (UNI launch) every value stays wave-uniform to the compiler and every solver branch is a
+//    scalar branch;
 //  * division / sqrt / x^(1/k) use hardware reciprocal + Newton refinement (faithfully rounded,
 //    i.e. within 1 ulp, the same order of perturbation as the reference's own FMA-contraction
 //    build differences -- see DESIGN.md "parity envelope");
@@ -68,6 +72,29 @@ enum { CV_SUCCESS = 0, CV_TSTOP_RETURN = 1, CV_TOO_MUCH_ACC = -2, CV_ERR_FAILURE
        CV_CONV_FAILURE = -4, CV_ILL_INPUT = -22, CV_BAD_T = -26, CV_TOO_CLOSE = -27 };
 
 #define BDF_INL __device__ __forceinline__
+
+// compile-time index loops: f(IC<j>{}) for j = B..E-1 (cfor) or j = B down to E (cfor_down)
+template <int V>
+struct IC {
+    static constexpr int value = V;
+};
+template <int B, int E, class F>
+BDF_INL void cfor(F&& f)
+{
+    if constexpr (B < E) {
+        f(IC<B>{});
+        cfor<B + 1, E>(static_cast<F&&>(f));
+    }
+}
+template <int B, int E, class F>
+BDF_INL void cfor_down(F&& f)
+{
+    if constexpr (B >= E) {
+        f(IC<B>{});
+        cfor_down<B - 1, E>(static_cast<F&&>(f));
+    }
+}
+#define CI(J) decltype(J)::value
 #define SUNMAX(A, B) ((A) > (B) ? (A) : (B))
 #define SUNMIN(A, B) ((A) < (B) ? (A) : (B))
 
@@ -131,9 +158,9 @@ BDF_INL double root_k(double x, int k)
 #pragma unroll 1
     for (int it = 0; it < 2; it++) {
         double p = y;  // y^(k-1), k >= 2
-#pragma unroll
-        for (int i = 2; i <= 6; i++)
-            if (i < k) p *= y;
+        cfor<2, 7>([&](auto I) __attribute__((always_inline)) {
+            if (CI(I) < k) p *= y;
+        });
         y = __builtin_fma(fdiv(x, p) - y, rk, y);
     }
     return y;
@@ -145,38 +172,48 @@ BDF_INL double eta_from(double bx, int k) { return frcp(root_k(bx, k) + ADDON); 
 BDF_INL double powI(double base, int e)
 {
     double prod = 1.0;
-#pragma unroll
-    for (int i = 1; i <= QMAX + 2; i++)
-        if (i <= e) prod *= base;
+    cfor<1, QMAX + 3>([&](auto I) __attribute__((always_inline)) {
+        if (CI(I) <= e) prod *= base;
+    });
     return prod;
 }
 
-// runtime-indexed read of a small register array: value selects over opaque copies (stops the
-// optimizer from forming a pointer select/phi, which would keep the array in scratch)
-BDF_INL double opq(double v)
-{
-    asm("" : "+v"(v));
-    return v;
-}
+// Runtime-indexed read of a small register array as a chain of constant-index selects whose
+// first link selects against a constant: a select between TWO loads would be folded by
+// InstCombine (run on this function before it is inlined into the kernel, where the array is
+// still behind a pointer) into a load through a selected pointer, and the state array could no
+// longer be promoted to registers.
 template <int K>
 BDF_INL double sel(const double (&a)[K], int i)
 {
-    double r = opq(a[0]);
-#pragma unroll
-    for (int k = 1; k < K; k++) r = (i == k) ? opq(a[k]) : r;
+    double r = 0.0;
+    cfor<0, K>([&](auto k) __attribute__((always_inline)) { r = (i == CI(k)) ? a[CI(k)] : r; });
     return r;
 }
 template <int NS>
 BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
 {
-#pragma unroll
-    for (int i = 0; i < NS; i++) {
-        double v = opq(zn[1][i]);
-#pragma unroll
-        for (int j = 2; j <= QMAX; j++) v = (q == j) ? opq(zn[j][i]) : v;
-        r[i] = v;
-    }
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+        double v = 0.0;
+        cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { v = (q == CI(j)) ? zn[CI(j)][CI(i)] : v; });
+        r[CI(i)] = v;
+    });
 }
+
+// BCM3_PHASES (profiling build only): per-phase s_memtime cycle accumulators
+#ifdef BCM3_PHASES
+#define BDF_PH(k)                          \
+    do {                                   \
+        const long long t_ = clock64();    \
+        s.ph[k] += t_ - s.tlast;           \
+        s.tlast = t_;                      \
+    } while (0)
+#else
+#define BDF_PH(k) \
+    do {          \
+    } while (0)
+#endif
+constexpr int NPHASES = 10;
 
 struct BdfCounters {
     int nst_total, nfe, nni, nsetups, nje, netf, ncfn, nreinit;
@@ -203,17 +240,20 @@ struct BdfState {
     int nst, nstlp, nstlj;
     int nls_jcur;
     BdfCounters cnt;
+#ifdef BCM3_PHASES
+    long long ph[NPHASES];
+    long long tlast;
+#endif
 };
 
 template <int NS>
 BDF_INL double wrms(const double (&x)[NS], const double (&w)[NS])
 {
     double s = 0.0;
-#pragma unroll
-    for (int i = 0; i < NS; i++) {
-        double p = x[i] * w[i];
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+        double p = x[CI(i)] * w[CI(i)];
         s += p * p;
-    }
+    });
     return fsqrt(fdiv(s, (double)NS));
 }
 
@@ -221,8 +261,7 @@ BDF_INL double wrms(const double (&x)[NS], const double (&w)[NS])
 template <int NS, class S>
 BDF_INL void ewt_set(const S& s, const double (&ycur)[NS], double (&w)[NS])
 {
-#pragma unroll
-    for (int i = 0; i < NS; i++) w[i] = frcp(s.rtol * fabs(ycur[i]) + s.atol);
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { w[CI(i)] = frcp(s.rtol * fabs(ycur[CI(i)]) + s.atol); });
 }
 
 // cvRescale (cvode.c:2393-2406): zn[j] *= eta^j, j = 1..q
@@ -230,14 +269,12 @@ template <int NS, class S>
 BDF_INL void rescale(S& s)
 {
     double c = s.eta;
-#pragma unroll
-    for (int j = 1; j <= QMAX; j++) {
-        if (j <= s.q) {
-#pragma unroll
-            for (int i = 0; i < NS; i++) s.zn[j][i] *= c;
+    cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] *= c; });
         }
         c = s.eta * c;
-    }
+    });
     s.h = s.hscale * s.eta;
     s.hscale = s.h;
 }
@@ -250,14 +287,13 @@ BDF_INL void predict(S& s)
     if (s.tstopset) {
         if ((s.tn - s.tstop) * s.h > 0.0) s.tn = s.tstop;
     }
-#pragma unroll
-    for (int k = 1; k <= QMAX; k++)
-#pragma unroll
-        for (int j = QMAX; j >= k; j--)
-            if (j <= s.q) {
-#pragma unroll
-                for (int i = 0; i < NS; i++) s.zn[j - 1][i] += s.zn[j][i];
+    cfor<1, QMAX + 1>([&](auto k) __attribute__((always_inline)) {
+        cfor_down<QMAX, CI(k)>([&](auto j) __attribute__((always_inline)) {
+            if (CI(j) <= s.q) {
+                cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j) - 1][CI(i)] += s.zn[CI(j)][CI(i)]; });
             }
+        });
+    });
 }
 
 // cvRestore: zn[j-1] += (-1)*zn[j]
@@ -265,14 +301,13 @@ template <int NS, class S>
 BDF_INL void restore(S& s, double saved_t)
 {
     s.tn = saved_t;
-#pragma unroll
-    for (int k = 1; k <= QMAX; k++)
-#pragma unroll
-        for (int j = QMAX; j >= k; j--)
-            if (j <= s.q) {
-#pragma unroll
-                for (int i = 0; i < NS; i++) s.zn[j - 1][i] -= s.zn[j][i];
+    cfor<1, QMAX + 1>([&](auto k) __attribute__((always_inline)) {
+        cfor_down<QMAX, CI(k)>([&](auto j) __attribute__((always_inline)) {
+            if (CI(j) <= s.q) {
+                cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j) - 1][CI(i)] -= s.zn[CI(j)][CI(i)]; });
             }
+        });
+    });
 }
 
 // cvSetBDF + cvSetTqBDF + cvSet (cvode.c:2445-2690); returns rl1
@@ -282,30 +317,28 @@ BDF_INL double set_bdf(S& s)
     const int q = s.q;
     double alpha0, alpha0_hat, xi_inv, xistar_inv, hsum;
     s.l[0] = s.l[1] = xi_inv = xistar_inv = 1.0;
-#pragma unroll
-    for (int i = 2; i <= QMAX; i++)
-        if (i <= q) s.l[i] = 0.0;
+    cfor<2, QMAX + 1>([&](auto i) __attribute__((always_inline)) {
+        if (CI(i) <= q) s.l[CI(i)] = 0.0;
+    });
     alpha0 = alpha0_hat = -1.0;
     hsum = s.h;
     if (q > 1) {
-#pragma unroll
-        for (int j = 2; j < QMAX; j++) {
-            if (j < q) {
-                hsum += s.tau[j - 1];
+        cfor<2, QMAX>([&](auto j) __attribute__((always_inline)) {
+            if (CI(j) < q) {
+                hsum += s.tau[CI(j) - 1];
                 xi_inv = fdiv(s.h, hsum);
-                alpha0 -= 1.0 / j;
-#pragma unroll
-                for (int i = j; i >= 1; i--) s.l[i] += s.l[i - 1] * xi_inv;
+                alpha0 -= 1.0 / CI(j);
+                cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] += s.l[CI(i) - 1] * xi_inv; });
             }
-        }
+        });
         alpha0 -= recip_int(q);
         xistar_inv = -s.l[1] - alpha0;
         hsum += sel(s.tau, q - 1);
         xi_inv = fdiv(s.h, hsum);
         alpha0_hat = -s.l[1] - xi_inv;
-#pragma unroll
-        for (int i = QMAX; i >= 1; i--)
-            if (i <= q) s.l[i] += s.l[i - 1] * xistar_inv;
+        cfor_down<QMAX, 1>([&](auto i) __attribute__((always_inline)) {
+            if (CI(i) <= q) s.l[CI(i)] += s.l[CI(i) - 1] * xistar_inv;
+        });
     }
     // cvSetTqBDF
     const double A1 = 1.0 - alpha0_hat + alpha0;
@@ -345,41 +378,33 @@ BDF_INL void increase_bdf(S& s)
 {
     double alpha0, alpha1, prod, xi, xiold, hsum, A1;
     double l[QMAX + 1];
-#pragma unroll
-    for (int i = 0; i <= QMAX; i++) l[i] = 0.0;
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = 0.0; });
     l[2] = alpha1 = prod = xiold = 1.0;
     alpha0 = -1.0;
     hsum = s.hscale;
-#pragma unroll
-    for (int j = 1; j < QMAX; j++) {
-        if (j < s.q) {
-            hsum += s.tau[j + 1];
+    cfor<1, QMAX>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) < s.q) {
+            hsum += s.tau[CI(j) + 1];
             xi = fdiv(hsum, s.hscale);
             prod *= xi;
-            alpha0 -= 1.0 / (j + 1);
+            alpha0 -= 1.0 / (CI(j) + 1);
             alpha1 += frcp(xi);
-#pragma unroll
-            for (int i = j + 2; i >= 2; i--) l[i] = l[i] * xiold + l[i - 1];
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = l[CI(i)] * xiold + l[CI(i) - 1]; });
             xiold = xi;
         }
-    }
+    });
     A1 = fdiv(-alpha0 - alpha1, prod);
     // zn[L] = A1 * zn[QMAX]; zn[j] += l[j]*zn[L], j = 2..q  (L = q+1)
     double znL[NS];
-#pragma unroll
-    for (int i = 0; i < NS; i++) znL[i] = A1 * s.zn[QMAX][i];
-#pragma unroll
-    for (int j = 2; j <= QMAX; j++) {
-        const bool isL = (j == s.q + 1), on = (j <= s.q);
-#pragma unroll
-        for (int i = 0; i < NS; i++) {
-            double z = opq(s.zn[j][i]);
-            z = isL ? znL[i] : z;
-            s.zn[j][i] = on ? z + l[j] * znL[i] : z;
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { znL[CI(i)] = A1 * s.zn[QMAX][CI(i)]; });
+    cfor<2, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) == s.q + 1) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = znL[CI(i)]; });
+        } else if (CI(j) <= s.q) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] += l[CI(j)] * znL[CI(i)]; });
         }
-    }
-#pragma unroll
-    for (int i = 0; i <= QMAX; i++) s.l[i] = l[i];
+    });
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
 }
 
 // cvDecreaseBDF (cvode.c:2352-2375)
@@ -387,29 +412,24 @@ template <int NS, class S>
 BDF_INL void decrease_bdf(S& s)
 {
     double l[QMAX + 1];
-#pragma unroll
-    for (int i = 0; i <= QMAX; i++) l[i] = 0.0;
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = 0.0; });
     l[2] = 1.0;
     double hsum = 0.0;
-#pragma unroll
-    for (int j = 1; j <= QMAX - 2; j++) {
-        if (j <= s.q - 2) {
-            hsum += s.tau[j];
+    cfor<1, QMAX - 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q - 2) {
+            hsum += s.tau[CI(j)];
             const double xi = fdiv(hsum, s.hscale);
-#pragma unroll
-            for (int i = j + 2; i >= 2; i--) l[i] = l[i] * xi + l[i - 1];
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = l[CI(i)] * xi + l[CI(i) - 1]; });
         }
-    }
+    });
     double znq[NS];
     sel_row<NS>(s.zn, s.q, znq);
-#pragma unroll
-    for (int j = 2; j < QMAX; j++) {
-        const bool on = (j < s.q);
-#pragma unroll
-        for (int i = 0; i < NS; i++) s.zn[j][i] = on ? s.zn[j][i] + (-l[j]) * znq[i] : s.zn[j][i];
-    }
-#pragma unroll
-    for (int i = 0; i <= QMAX; i++) s.l[i] = l[i];
+    cfor<2, QMAX>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) < s.q) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = s.zn[CI(j)][CI(i)] + (-l[CI(j)]) * znq[CI(i)]; });
+        }
+    });
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
 }
 
 // cvAdjustOrder (cvode.c:2212-2225)
@@ -435,16 +455,13 @@ BDF_INL int get_dky(const S& s, double t, double (&dky)[NS])
     const double sv = fdiv(t - s.tn, s.h);
     double c[QMAX + 1];
     c[0] = 1.0;
-#pragma unroll
-    for (int j = 1; j <= QMAX; j++) c[j] = c[j - 1] * sv;
-#pragma unroll
-    for (int i = 0; i < NS; i++) dky[i] = 0.0;
-#pragma unroll
-    for (int j = QMAX; j >= 0; j--)
-        if (j <= s.q) {
-#pragma unroll
-            for (int i = 0; i < NS; i++) dky[i] += c[j] * s.zn[j][i];
+    cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { c[CI(j)] = c[CI(j) - 1] * sv; });
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] = 0.0; });
+    cfor_down<QMAX, 0>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] += c[CI(j)] * s.zn[CI(j)][CI(i)]; });
         }
+    });
     return CV_SUCCESS;
 }
 
@@ -458,8 +475,10 @@ BDF_INL void reinit(S& s, double t0, const double (&y0)[NS])
     s.qwait = 2;
     s.etamax = ETAMX1;
     s.hu = 0.0;
-#pragma unroll
-    for (int i = 0; i < NS; i++) s.zn[0][i] = y0[i];
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = CI(I_);
+        s.zn[0][i] = y0[i];
+    });
     s.nst = 0;
     s.nstlp = 0;
     s.cnt.nreinit++;
@@ -477,15 +496,17 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
     for (;;) {
         // residual: y = zn0 + ycor; f(tn, y); res = rl1*zn1 + ycor; res += -gamma*f
         double y[NS], f[NS], delta[NS];
-#pragma unroll
-        for (int i = 0; i < NS; i++) y[i] = s.zn[0][i] + s.acor[i];
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            y[i] = s.zn[0][i] + s.acor[i];
+        });
         mdl.rhs(s.tn, y, f);
         s.cnt.nfe++;
-#pragma unroll
-        for (int i = 0; i < NS; i++) {
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
             delta[i] = rl1 * s.zn[1][i] + s.acor[i];
             delta[i] += (-s.gamma) * f[i];
-        }
+        });
         if (callSetup) {
             // cvNlsLSetup -> cvLsSetup (cvode_ls.c:1415-1500)
             if (jbad) convfail = CONV_BAD_J;
@@ -509,16 +530,22 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
         s.cnt.nni++;
         // cvLsSolve: x = A^-1 (-res); scale by 2/(1+gamrat) when gamma changed
         double b[NS], x[NS];
-#pragma unroll
-        for (int i = 0; i < NS; i++) b[i] = -delta[i];
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            b[i] = -delta[i];
+        });
         mdl.lin_solve(s.inv, b, x);
         if (s.gamrat != 1.0) {
             const double c = fdiv(2.0, 1.0 + s.gamrat);
-#pragma unroll
-            for (int i = 0; i < NS; i++) x[i] *= c;
+            cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+                constexpr int i = CI(I_);
+                x[i] *= c;
+            });
         }
-#pragma unroll
-        for (int i = 0; i < NS; i++) s.acor[i] += x[i];
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            s.acor[i] += x[i];
+        });
         // cvNlsConvTest (cvode_nls.c:236-280)
         const double del = wrms<NS>(x, s.ewt);
         if (curiter > 0) s.crate = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
@@ -538,8 +565,10 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
         if (!s.nls_jcur) {  // retry with a fresh Jacobian (jbad)
             callSetup = true;
             jbad = true;
-#pragma unroll
-            for (int i = 0; i < NS; i++) s.acor[i] = 0.0;
+            cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+                constexpr int i = CI(I_);
+                s.acor[i] = 0.0;
+            });
             continue;
         }
         return false;
@@ -559,13 +588,13 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
     const double hlb = HLB_FACTOR * tround;
     // cvUpperBoundH0 (cvode.c:2000-2035)
     double hub_inv = 0.0;
-#pragma unroll
-    for (int i = 0; i < NS; i++) {
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = CI(I_);
         double t1 = frcp(s.ewt[i]);  // N_VInv of the error weights
         t1 += HUB_FACTOR * fabs(s.zn[0][i]);
         const double r = fdiv(fabs(s.zn[1][i]), t1);
         hub_inv = (i == 0) ? r : ((r > hub_inv) ? r : hub_inv);  // maxCoeff
-    }
+    });
     double hub = HUB_FACTOR * tdist;
     if (hub * hub_inv > 1.0) hub = frcp(hub_inv);
     double hg = fsqrt(hlb * hub);
@@ -579,13 +608,17 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
         // cvYddNorm (cvode.c:2046-2066)
         const double hgs = hg * sign;
         double yy[NS], tv[NS];
-#pragma unroll
-        for (int i = 0; i < NS; i++) yy[i] = hgs * s.zn[1][i] + s.zn[0][i];
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            yy[i] = hgs * s.zn[1][i] + s.zn[0][i];
+        });
         mdl.rhs(s.tn + hgs, yy, tv);
         s.cnt.nfe++;
         const double a = frcp(hgs);
-#pragma unroll
-        for (int i = 0; i < NS; i++) tv[i] = a * (tv[i] - s.zn[1][i]);
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            tv[i] = a * (tv[i] - s.zn[1][i]);
+        });
         const double yddnrm = wrms<NS>(tv, s.ewt);
         hnew = (yddnrm * hub * hub > 2.0) ? fsqrt(fdiv(2.0, yddnrm)) : fsqrt(hg * hub);
         if (count1 == MAX_ITERS) break;
@@ -610,6 +643,7 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
 template <int NS, class S, class Model>
 BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret)
 {
+    BDF_PH(0);  // driver: output interpolation, callbacks, ReInit
     if (s.nst == 0) {
         s.tretlast = tret = s.tn;
         ewt_set<NS>(s, s.zn[0], s.ewt);
@@ -629,14 +663,18 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         }
         s.hscale = s.h;
         s.hprime = s.h;
-#pragma unroll
-        for (int i = 0; i < NS; i++) s.zn[1][i] *= s.h;
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            s.zn[1][i] *= s.h;
+        });
     } else {
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         if (fabs(s.tn - s.tretlast) > troundoff) {
             s.tretlast = tret = s.tn;
-#pragma unroll
-            for (int i = 0; i < NS; i++) yout[i] = s.zn[0][i];
+            cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+                constexpr int i = CI(I_);
+                yout[i] = s.zn[0][i];
+            });
             return CV_SUCCESS;
         }
         if (s.tstopset) {
@@ -656,19 +694,22 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
     // too much accuracy requested (cvode.c:1318-1331): uround * wrms(zn0) > 1
     {
         double ss = 0.0;
-#pragma unroll
-        for (int i = 0; i < NS; i++) {
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
             const double p = s.zn[0][i] * s.ewt[i];
             ss += p * p;
-        }
+        });
         if (ss > (double)NS * (1.0 / (UROUND * UROUND))) {
             s.tretlast = tret = s.tn;
-#pragma unroll
-            for (int i = 0; i < NS; i++) yout[i] = s.zn[0][i];
+            cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+                constexpr int i = CI(I_);
+                yout[i] = s.zn[0][i];
+            });
             return CV_TOO_MUCH_ACC;
         }
     }
 
+    BDF_PH(1);  // entry checks, error weights
     // ---------------- cvStep
     const double saved_t = s.tn;
     int ncf = 0, nef = 0, nflag = FIRST_CALL;
@@ -687,15 +728,21 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
     for (;;) {
         if (do_rescale) rescale<NS>(s);
         do_rescale = true;
+        BDF_PH(2);
         predict<NS>(s);
+        BDF_PH(3);
         const double rl1 = set_bdf(s);
+        BDF_PH(4);
         // cvNls
         const int convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
         const bool callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (s.nst == 0) ||
                                (s.nst >= s.nstlp + MSBP) || (fabs(s.gamrat - 1.0) > DGMAX);
-#pragma unroll
-        for (int i = 0; i < NS; i++) s.acor[i] = 0.0;
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            s.acor[i] = 0.0;
+        });
         const bool conv = newton<NS>(s, mdl, rl1, convfail, callSetup);
+        BDF_PH(5);
         if (conv) {
             // cvDoErrorTest (cvode.c:2958-3030)
             dsm = s.acnrm * s.tq[2];
@@ -738,33 +785,42 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         double tv[NS];
         mdl.rhs(s.tn, s.zn[0], tv);
         s.cnt.nfe++;
-#pragma unroll
-        for (int i = 0; i < NS; i++) s.zn[1][i] = s.h * tv[i];
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            s.zn[1][i] = s.h * tv[i];
+        });
         do_rescale = false;
     }
 
+    BDF_PH(6);  // error test, failure handling
     // cvCompleteStep (cvode.c:3043-3080)
     s.nst++;
     s.cnt.nst_total++;
     s.hu = s.h;
-#pragma unroll
-    for (int i = QMAX; i >= 2; i--)
-        if (i <= s.q) s.tau[i] = s.tau[i - 1];
+    cfor_down<QMAX, 2>([&](auto i) __attribute__((always_inline)) {
+        if (CI(i) <= s.q) s.tau[CI(i)] = s.tau[CI(i) - 1];
+    });
     if ((s.q == 1) && (s.nst > 1)) s.tau[2] = s.tau[1];
     s.tau[1] = s.h;
-#pragma unroll
-    for (int j = 0; j <= QMAX; j++)
+    cfor<0, QMAX + 1>([&](auto J_) __attribute__((always_inline)) {
+        constexpr int j = CI(J_);
         if (j <= s.q) {
-#pragma unroll
-            for (int i = 0; i < NS; i++) s.zn[j][i] += s.l[j] * s.acor[i];
+            cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+                constexpr int i = CI(I_);
+                s.zn[j][i] += s.l[j] * s.acor[i];
+            });
         }
+    });
     s.qwait--;
     if ((s.qwait == 1) && (s.q != QMAX)) {
-#pragma unroll
-        for (int i = 0; i < NS; i++) s.zn[QMAX][i] = s.acor[i];
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            s.zn[QMAX][i] = s.acor[i];
+        });
         s.saved_tq5 = s.tq[5];
     }
 
+    BDF_PH(7);
     // cvPrepareNextStep + cvComputeEtaqm1/qp1 + cvChooseEta + cvSetEta (cvode.c:3093-3258)
     if (s.etamax == 1.0) {
         s.qwait = SUNMAX(s.qwait, 2);
@@ -788,8 +844,10 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
             if (do_p) {
                 const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), s.L);
                 double tv[NS];
-#pragma unroll
-                for (int i = 0; i < NS; i++) tv[i] = (-cquot) * s.zn[QMAX][i] + s.acor[i];
+                cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+                    constexpr int i = CI(I_);
+                    tv[i] = (-cquot) * s.zn[QMAX][i] + s.acor[i];
+                });
                 xp = BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3];
             }
             // the two candidate ratios share one root call site
@@ -816,8 +874,10 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
             } else {
                 eta = etaqp1;
                 s.qprime = s.q + 1;
-#pragma unroll
-                for (int i = 0; i < NS; i++) s.zn[QMAX][i] = s.acor[i];
+                cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+                    constexpr int i = CI(I_);
+                    s.zn[QMAX][i] = s.acor[i];
+                });
             }
         }
         // cvSetEta (hmax_inv = 0)
@@ -829,9 +889,12 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
             s.hprime = s.h * s.eta;
         }
     }
+    BDF_PH(8);
     s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
-#pragma unroll
-    for (int i = 0; i < NS; i++) s.acor[i] *= s.tq[2];
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = CI(I_);
+        s.acor[i] *= s.tq[2];
+    });
 
     // stop tests after the step (cvode.c:1395-1437)
     if (s.tstopset) {
@@ -848,8 +911,11 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         }
     }
     s.tretlast = tret = s.tn;
-#pragma unroll
-    for (int i = 0; i < NS; i++) yout[i] = s.zn[0][i];
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = CI(I_);
+        yout[i] = s.zn[0][i];
+    });
+    BDF_PH(9);
     return CV_SUCCESS;
 }
 

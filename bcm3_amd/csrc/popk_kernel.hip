@@ -217,7 +217,11 @@ BDF_INL bool check_give_treatment(double t, const uint8_t* skipped, int intermit
 
 // ---------------------------------------------------------------------------------------------
 
-template <int PKT>
+// UNI (lanes_per_wave == 1): the wavefront integrates ONE trajectory and its index is made
+// wave-uniform (readfirstlane), so every value derived from it is uniform to the compiler: the
+// model data come in through scalar loads and every solver branch is a uniform (scalar) branch
+// instead of exec-mask manipulation. All 64 lanes compute the same numbers; lane 0 stores.
+template <int PKT, bool UNI>
 __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t ntraj, int lpw,
                                                         const double* __restrict__ values,
                                                         double* __restrict__ logp_direct,
@@ -229,10 +233,17 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     using TR = PKTraits<PKT>;
     constexpr int NS = TR::NS;
     const int lane = threadIdx.x & 63;
-    if (lane >= lpw) return;
-    const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int64_t g = gwave * lpw + lane;
-    if (g >= ntraj) return;
+    int64_t g;
+    if constexpr (UNI) {
+        g = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+        if (g >= ntraj) return;
+    } else {
+        if (lane >= lpw) return;
+        const int64_t gwave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        g = gwave * lpw + lane;
+        if (g >= ntraj) return;
+    }
+    const bool writer = !UNI || lane == 0;
     const int P = m.P;
     const int64_t e = g / P;
     const int j = (int)(g - e * P);
@@ -310,12 +321,15 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     BdfState<NS, typename PKLane<PKT>::Inv> s;
     s.cnt = BdfCounters{0, 0, 0, 0, 0, 0, 0, 0};
     s.nst = 0;
+#ifdef BCM3_PHASES
+    cfor<0, NPHASES>([&](auto k) __attribute__((always_inline)) { s.ph[CI(k)] = 0; });
+    s.tlast = clock64();
+#endif
 
     // observation term for output index i with state yi (.cpp:412-423)
-    auto observe = [&](int i, const double (&yi)[NS]) {
-        if (tro) {
-#pragma unroll
-            for (int k = 0; k < NS; k++) tro[k * T + i] = yi[k];
+    auto observe = [&](int i, const double (&yi)[NS]) __attribute__((always_inline)) {
+        if (tro && writer) {
+            cfor<0, NS>([&](auto k) __attribute__((always_inline)) { tro[CI(k) * T + i] = yi[CI(k)]; });
         }
         if (llh_done) return;
         const double x = conversion * yi[1];
@@ -330,15 +344,14 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         }
     };
 
-    if (tro) {
+    if (tro && writer) {
         for (int k = 0; k < NS * T; k++) tro[k] = NAN;
     }
 
     if (nsim > 0) {
         double y0[NS];
         y0[0] = TR::transit ? 0.0 : mdl.dose;
-#pragma unroll
-        for (int k = 1; k < NS; k++) y0[k] = 0.0;
+        cfor<1, NS>([&](auto k) __attribute__((always_inline)) { y0[CI(k)] = 0.0; });
 
         // ODESolver::SolveReturnSolution: rows with t < DBL_EPSILON take y0
         int tpi = 0;
@@ -357,14 +370,12 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             // ODESolverCVODE::Solve
             s.rtol = m.rtol;
             s.atol = m.atol;
-#pragma unroll
-            for (int k = 0; k <= QMAX + 1; k++) s.tau[k] = 0.0;
+            cfor<0, QMAX + 2>([&](auto k) __attribute__((always_inline)) { s.tau[CI(k)] = 0.0; });
             s.saved_tq5 = 0.0;
             s.hprime = s.h = s.eta = 0.0;
             s.tstopset = 0;
             double y[NS];
-#pragma unroll
-            for (int k = 0; k < NS; k++) y[k] = y0[k];
+            cfor<0, NS>([&](auto k) __attribute__((always_inline)) { y[CI(k)] = y0[CI(k)]; });
             reinit<NS>(s, 0.0, y);
             s.tstop = next_disc;
             s.tstopset = 1;
@@ -436,6 +447,10 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     }
     if (status != BCM3HIP_STATUS_OK) llh = -INFINITY;
 
+    if (!writer) return;
+#ifdef BCM3_PHASES
+    if (tro) cfor<0, NPHASES>([&](auto k) __attribute__((always_inline)) { tro[CI(k)] = (double)s.ph[CI(k)]; });
+#endif
     if (logp_direct) logp_direct[e] = 0.0 + llh;  // P == 1: logp = 0 + patient term
     if (patient_llh) patient_llh[g] = llh;
     if (traj_status) traj_status[g] = status;
@@ -492,11 +507,16 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
     const int64_t nblocks = (nwaves + bw - 1) / bw;
     dim3 grid((unsigned)nblocks), block(64 * bw);
     const bool direct = (m.P == 1);
+    const bool uni = (lpw == 1) && ntraj < (int64_t)1 << 30;
     double* logp_direct = direct ? logp : nullptr;
     if (ev_start) hipEventRecord(ev_start, stream);
 #define LAUNCH(PKT)                                                                                           \
-    hipLaunchKernelGGL(popk_traj_kernel<PKT>, grid, block, 0, stream, m, ntraj, lpw, values, logp_direct,     \
-                       patient_llh_scratch, traj_status_scratch, traj_out, stats_out)
+    if (uni)                                                                                                  \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, true>), grid, block, 0, stream, m, ntraj, lpw, values,        \
+                           logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out);         \
+    else                                                                                                      \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, false>), grid, block, 0, stream, m, ntraj, lpw, values,       \
+                           logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out)
     switch (m.pk_type) {
     case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;
     case BCM3HIP_PK_TWO: LAUNCH(BCM3HIP_PK_TWO); break;

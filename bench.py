@@ -65,6 +65,22 @@ def traffic_from_profiles(tag: str, n: int):
     return None
 
 
+def host_cores() -> int:
+    """CPU threads this process may use: the box's share (OMP_NUM_THREADS is set to it on the GPU
+    box), else the cgroup quota, else the affinity mask."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return n
+
+
 def cpu_baseline(budget_s: float, seed: int):
     """The reference CPU path on this box's host cores: the vendored CVODE 5.3.0 of the reference
     (compiled from its sources into oracle/_ref, with the restated PopPK glue) evaluating prior
@@ -79,7 +95,7 @@ def cpu_baseline(budget_s: float, seed: int):
     except FileNotFoundError:
         orc, kind = O.Oracle("restated"), "port"
     prob = H.c3_problem(1)
-    cores = len(os.sched_getaffinity(0))
+    cores = host_cores()
     rng = np.random.default_rng(seed)
     lo = np.array([v.lower for v in prob.variables])
     hi = np.array([v.upper for v in prob.variables])

@@ -1,0 +1,44 @@
+"""Per-phase cycle breakdown of the BDF kernel (profiling build lib/libbcm3hip_phases.so).
+
+    make -C bcm3_amd/csrc phases && python tools/phase_probe.py [n] [lpw]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["BCM3HIP_LIB"] = os.path.join(ROOT, "bcm3_amd", "lib", "libbcm3hip_phases.so")
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests"), os.path.join(ROOT, "tests", "golden")]
+
+import numpy as np  # noqa: E402
+
+import helpers as H  # noqa: E402
+import synthetic as S  # noqa: E402
+from bcm3_amd import _hip  # noqa: E402
+
+NAMES = ["driver(out/cb/reinit)", "entry+ewt", "adjust+rescale", "predict", "set_bdf", "newton",
+         "errtest/fail", "complete", "eta/next", "tstop/return"]
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    lpw = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    prob = H.c3_problem(1)
+    ctx = H.gpu_context(prob, lanes_per_wave=lpw)
+    vals = S.prior_draws(1, n, 7)
+    g = ctx.eval(vals, detail=True)
+    ms = ctx.last_kernel_ms()
+    ph = g["traj"].reshape(n, -1)[:, :len(NAMES)]
+    nst = g["stats"]["nst"][:, 0].astype(np.float64)
+    tot = ph.sum(axis=1)
+    imax = int(np.argmax(tot))
+    print(f"n={n} lpw={lpw} kernel {ms:.3f} ms; slowest traj {tot[imax]:.3e} cycles, {nst[imax]:.0f} steps "
+          f"-> {tot[imax] / nst[imax]:.0f} cycles/step; implied clock {tot[imax] / (ms * 1e-3) / 1e9:.2f} GHz")
+    per = ph.sum(axis=0) / nst.sum()
+    print(f"mean cycles per step {per.sum():.0f}:")
+    for k, name in enumerate(NAMES):
+        print(f"  {name:24s} {per[k]:8.0f}  {100 * per[k] / per.sum():5.1f}%")
+    print("stats means:", {k: float(g["stats"][k].mean()) for k in g["stats"].dtype.names})
+
+
+if __name__ == "__main__":
+    main()

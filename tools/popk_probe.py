@@ -33,7 +33,7 @@ def main():
         t = time.time()
         o = O.Oracle(which).popk_eval(prob, vals, nthreads=8)
         print(f"oracle {which}: {time.time()-t:.3f}s")
-        te = parity.traj_rel_err(g["traj"][:, 0], o["traj"][:, 0], prob.atol)
+        te = parity.y1_rel_err(g["traj"][:, 0, 1], o["traj"][:, 0, 1], prob.atol)
         le = parity.llh_err(g["logp"], o["logp"])
         s = parity.summarize(te, le, g["stats"]["nst"][:, 0], o["stats"][:, 0, 0])
         print(which, s)
@@ -46,7 +46,7 @@ def main():
         for nn, P in ((256, 1), (4096, 1), (16384, 1)):
             v = torch.tensor(S.prior_draws(1, nn, 7), device="cuda", dtype=torch.float64)
             lp = torch.empty(nn, device="cuda", dtype=torch.float64)
-            for lpw in (1, 4, 16, 64):
+            for lpw in (1, 2, 4, 8, 16, 64):
                 ctx.set_option(_hip.OPT_LANES_PER_WAVE, lpw)
                 ms = []
                 for rep in range(3):
