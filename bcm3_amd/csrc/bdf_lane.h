@@ -252,7 +252,7 @@ BDF_INL double wrms(const double (&x)[NS], const double (&w)[NS])
     double s = 0.0;
     cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
         double p = x[CI(i)] * w[CI(i)];
-        s += p * p;
+        s = __builtin_fma(p, p, s);
     });
     return fsqrt(fdiv(s, (double)NS));
 }
@@ -261,7 +261,7 @@ BDF_INL double wrms(const double (&x)[NS], const double (&w)[NS])
 template <int NS, class S>
 BDF_INL void ewt_set(const S& s, const double (&ycur)[NS], double (&w)[NS])
 {
-    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { w[CI(i)] = frcp(s.rtol * fabs(ycur[CI(i)]) + s.atol); });
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { w[CI(i)] = frcp(__builtin_fma(s.rtol, fabs(ycur[CI(i)]), s.atol)); });
 }
 
 // cvRescale (cvode.c:2393-2406): zn[j] *= eta^j, j = 1..q
@@ -328,7 +328,7 @@ BDF_INL double set_bdf(S& s)
                 hsum += s.tau[CI(j) - 1];
                 xi_inv = fdiv(s.h, hsum);
                 alpha0 -= 1.0 / CI(j);
-                cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] += s.l[CI(i) - 1] * xi_inv; });
+                cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xi_inv, s.l[CI(i)]); });
             }
         });
         alpha0 -= recip_int(q);
@@ -337,12 +337,12 @@ BDF_INL double set_bdf(S& s)
         xi_inv = fdiv(s.h, hsum);
         alpha0_hat = -s.l[1] - xi_inv;
         cfor_down<QMAX, 1>([&](auto i) __attribute__((always_inline)) {
-            if (CI(i) <= q) s.l[CI(i)] += s.l[CI(i) - 1] * xistar_inv;
+            if (CI(i) <= q) s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xistar_inv, s.l[CI(i)]);
         });
     }
     // cvSetTqBDF
     const double A1 = 1.0 - alpha0_hat + alpha0;
-    const double A2 = 1.0 + (double)q * A1;
+    const double A2 = __builtin_fma((double)q, A1, 1.0);
     const double lq = sel(s.l, q);
     s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
     s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
@@ -389,7 +389,7 @@ BDF_INL void increase_bdf(S& s)
             prod *= xi;
             alpha0 -= 1.0 / (CI(j) + 1);
             alpha1 += frcp(xi);
-            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = l[CI(i)] * xiold + l[CI(i) - 1]; });
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xiold, l[CI(i) - 1]); });
             xiold = xi;
         }
     });
@@ -401,7 +401,7 @@ BDF_INL void increase_bdf(S& s)
         if (CI(j) == s.q + 1) {
             cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = znL[CI(i)]; });
         } else if (CI(j) <= s.q) {
-            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] += l[CI(j)] * znL[CI(i)]; });
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = __builtin_fma(l[CI(j)], znL[CI(i)], s.zn[CI(j)][CI(i)]); });
         }
     });
     cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
@@ -419,14 +419,14 @@ BDF_INL void decrease_bdf(S& s)
         if (CI(j) <= s.q - 2) {
             hsum += s.tau[CI(j)];
             const double xi = fdiv(hsum, s.hscale);
-            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = l[CI(i)] * xi + l[CI(i) - 1]; });
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xi, l[CI(i) - 1]); });
         }
     });
     double znq[NS];
     sel_row<NS>(s.zn, s.q, znq);
     cfor<2, QMAX>([&](auto j) __attribute__((always_inline)) {
         if (CI(j) < s.q) {
-            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = s.zn[CI(j)][CI(i)] + (-l[CI(j)]) * znq[CI(i)]; });
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = __builtin_fma(-l[CI(j)], znq[CI(i)], s.zn[CI(j)][CI(i)]); });
         }
     });
     cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
@@ -459,7 +459,7 @@ BDF_INL int get_dky(const S& s, double t, double (&dky)[NS])
     cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] = 0.0; });
     cfor_down<QMAX, 0>([&](auto j) __attribute__((always_inline)) {
         if (CI(j) <= s.q) {
-            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] += c[CI(j)] * s.zn[CI(j)][CI(i)]; });
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] = __builtin_fma(c[CI(j)], s.zn[CI(j)][CI(i)], dky[CI(i)]); });
         }
     });
     return CV_SUCCESS;
@@ -504,8 +504,8 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
         s.cnt.nfe++;
         cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
             constexpr int i = CI(I_);
-            delta[i] = rl1 * s.zn[1][i] + s.acor[i];
-            delta[i] += (-s.gamma) * f[i];
+            delta[i] = __builtin_fma(rl1, s.zn[1][i], s.acor[i]);
+            delta[i] = __builtin_fma(-s.gamma, f[i], delta[i]);
         });
         if (callSetup) {
             // cvNlsLSetup -> cvLsSetup (cvode_ls.c:1415-1500)
@@ -591,7 +591,7 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
     cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
         constexpr int i = CI(I_);
         double t1 = frcp(s.ewt[i]);  // N_VInv of the error weights
-        t1 += HUB_FACTOR * fabs(s.zn[0][i]);
+        t1 = __builtin_fma(HUB_FACTOR, fabs(s.zn[0][i]), t1);
         const double r = fdiv(fabs(s.zn[1][i]), t1);
         hub_inv = (i == 0) ? r : ((r > hub_inv) ? r : hub_inv);  // maxCoeff
     });
@@ -610,7 +610,7 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
         double yy[NS], tv[NS];
         cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
             constexpr int i = CI(I_);
-            yy[i] = hgs * s.zn[1][i] + s.zn[0][i];
+            yy[i] = __builtin_fma(hgs, s.zn[1][i], s.zn[0][i]);
         });
         mdl.rhs(s.tn + hgs, yy, tv);
         s.cnt.nfe++;
@@ -697,7 +697,7 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
             constexpr int i = CI(I_);
             const double p = s.zn[0][i] * s.ewt[i];
-            ss += p * p;
+            ss = __builtin_fma(p, p, ss);
         });
         if (ss > (double)NS * (1.0 / (UROUND * UROUND))) {
             s.tretlast = tret = s.tn;
@@ -807,7 +807,7 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         if (j <= s.q) {
             cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
                 constexpr int i = CI(I_);
-                s.zn[j][i] += s.l[j] * s.acor[i];
+                s.zn[j][i] = __builtin_fma(s.l[j], s.acor[i], s.zn[j][i]);
             });
         }
     });
@@ -846,7 +846,7 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
                 double tv[NS];
                 cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
                     constexpr int i = CI(I_);
-                    tv[i] = (-cquot) * s.zn[QMAX][i] + s.acor[i];
+                    tv[i] = __builtin_fma(-cquot, s.zn[QMAX][i], s.acor[i]);
                 });
                 xp = BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3];
             }

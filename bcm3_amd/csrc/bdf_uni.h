@@ -1,0 +1,469 @@
+// bdf_uni.h -- the CVODE BDF step of bdf_lane.h specialised for ONE trajectory per wavefront
+// (UNI launch: every value is wave-uniform).
+//
+// Same algorithm and the same floating-point operations as cvode_one_step in bdf_lane.h (the
+// two paths agree bit for bit, tests/test_popk_gpu.py); what changes is the control flow. One
+// wavefront running alone on a SIMD pays ~20-40 cycles for every branch, taken or not, but only
+// ~4 cycles for a v_cndmask and ~4 for an independent f64 op (tools/ubench, profiles/
+// r01_ubench.txt). So:
+//  * the step is instantiated per BDF order Q = 1..5 (one dispatch per attempt): no guards on
+//    the runtime order inside predict / rescale / set / complete;
+//  * short conditional work is computed unconditionally and selected (division results,
+//    tq[1]/tq[3], the order-change candidates etaqm1/etaqp1 -- independent chains the scheduler
+//    interleaves), and rescaling by eta = 1 replaces the "h changed?" branch (x * 1.0 == x);
+//  * rare events (first step after ReInit, tstop reached, failures, order changes) stay behind
+//    one branch each and reuse the generic routines of bdf_lane.h.
+#pragma once
+#include "bdf_lane.h"
+
+namespace bcm3hip {
+namespace uni {
+
+// cvRescale with eta_eff (1.0 when the step size is unchanged: exact no-op)
+template <int Q, int NS, class S>
+BDF_INL void rescale_q(S& s, double eta)
+{
+    double c = eta;
+    cfor<1, Q + 1>([&](auto j) __attribute__((always_inline)) {
+        cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] *= c; });
+        c = eta * c;
+    });
+    s.h = s.hscale * eta;
+    s.hscale = s.h;
+}
+
+template <int Q, int NS, class S>
+BDF_INL void predict_q(S& s)
+{
+    s.tn += s.h;
+    const double tc = s.tstop;
+    s.tn = (s.tstopset && (s.tn - tc) * s.h > 0.0) ? tc : s.tn;
+    cfor<1, Q + 1>([&](auto k) __attribute__((always_inline)) {
+        cfor_down<Q, CI(k)>([&](auto j) __attribute__((always_inline)) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+                s.zn[CI(j) - 1][CI(i)] += s.zn[CI(j)][CI(i)];
+            });
+        });
+    });
+}
+
+template <int Q, int NS, class S>
+BDF_INL void restore_q(S& s, double saved_t)
+{
+    s.tn = saved_t;
+    cfor<1, Q + 1>([&](auto k) __attribute__((always_inline)) {
+        cfor_down<Q, CI(k)>([&](auto j) __attribute__((always_inline)) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+                s.zn[CI(j) - 1][CI(i)] -= s.zn[CI(j)][CI(i)];
+            });
+        });
+    });
+}
+
+// cvSetBDF + cvSetTqBDF + cvSet for order Q; the qwait == 1 quantities (tq[1], tq[3]) are
+// computed unconditionally and kept only when qwait == 1.
+template <int Q, class S>
+BDF_INL double set_bdf_q(S& s)
+{
+    constexpr int q = Q;
+    double alpha0, alpha0_hat, xi_inv, xistar_inv, hsum;
+    s.l[0] = s.l[1] = xi_inv = xistar_inv = 1.0;
+    cfor<2, Q + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = 0.0; });
+    alpha0 = alpha0_hat = -1.0;
+    hsum = s.h;
+    if constexpr (q > 1) {
+        cfor<2, Q>([&](auto j) __attribute__((always_inline)) {
+            hsum += s.tau[CI(j) - 1];
+            xi_inv = fdiv(s.h, hsum);
+            alpha0 -= 1.0 / CI(j);
+            cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xi_inv, s.l[CI(i)]); });
+        });
+        alpha0 -= 1.0 / q;
+        xistar_inv = -s.l[1] - alpha0;
+        hsum += s.tau[q - 1];
+        xi_inv = fdiv(s.h, hsum);
+        alpha0_hat = -s.l[1] - xi_inv;
+        cfor_down<Q, 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xistar_inv, s.l[CI(i)]); });
+    }
+    const double A1 = 1.0 - alpha0_hat + alpha0;
+    const double A2 = __builtin_fma((double)q, A1, 1.0);
+    const double lq = s.l[q];
+    s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
+    s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
+    {
+        // qwait == 1 block of cvSetTqBDF, evaluated unconditionally
+        double tq1 = 1.0;
+        if constexpr (q > 1) {
+            const double C = fdiv(xistar_inv, lq);
+            const double A3 = alpha0 + 1.0 / q;
+            const double A4 = alpha0_hat + xi_inv;
+            const double Cpinv = fdiv(1.0 - A4 + A3, A3);
+            tq1 = fabs(C * Cpinv);
+        }
+        const double hsum2 = hsum + s.tau[q];
+        const double xi_inv2 = fdiv(s.h, hsum2);
+        const double A5 = alpha0 - 1.0 / (q + 1);
+        const double A6 = alpha0_hat - xi_inv2;
+        const double Cppinv = fdiv(1.0 - A6 + A5, A2);
+        const double tq3 = fabs(fdiv(Cppinv, xi_inv2 * (double)(q + 2) * A5));
+        const bool qw1 = (s.qwait == 1);
+        s.tq[1] = qw1 ? tq1 : s.tq[1];
+        s.tq[3] = qw1 ? tq3 : s.tq[3];
+    }
+    s.tq[4] = fdiv(CORTES, s.tq[2]);
+    const double rl1 = frcp(s.l[1]);
+    s.gamma = s.h * rl1;
+    s.gammap = (s.nst == 0) ? s.gamma : s.gammap;
+    const double gr = fdiv(s.gamma, s.gammap);
+    s.gamrat = (s.nst > 0) ? gr : 1.0;
+    return rl1;
+}
+
+// Newton iteration (bdf_lane.h newton) with the gamrat scaling and the final-norm choice as
+// selects.
+template <int NS, class S, class Model>
+BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool callSetup)
+{
+    const double tol = s.tq[4];
+    bool jbad = false;
+    int curiter = 0;
+    for (;;) {
+        double y[NS], f[NS], delta[NS];
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            y[i] = s.zn[0][i] + s.acor[i];
+        });
+        mdl.rhs(s.tn, y, f);
+        s.cnt.nfe++;
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            delta[i] = __builtin_fma(rl1, s.zn[1][i], s.acor[i]);
+            delta[i] = __builtin_fma(-s.gamma, f[i], delta[i]);
+        });
+        if (callSetup) {
+            if (jbad) convfail = CONV_BAD_J;
+            const double dgamma = fabs(fdiv(s.gamma, s.gammap) - 1.0);
+            const bool jnew = (s.nst == 0) || (s.nst > s.nstlj + CVLS_MSBJ) ||
+                              ((convfail == CONV_BAD_J) && (dgamma < CVLS_DGMAX)) || (convfail == CONV_OTHER);
+            s.cnt.nje += jnew ? 1 : 0;
+            s.nstlj = jnew ? s.nst : s.nstlj;
+            mdl.lin_setup(s.gamma, s.inv);
+            s.cnt.nsetups++;
+            s.nls_jcur = jnew;
+            s.gamrat = 1.0;
+            s.gammap = s.gamma;
+            s.crate = 1.0;
+            s.nstlp = s.nst;
+            callSetup = false;
+            curiter = 0;
+        }
+        s.cnt.nni++;
+        double b[NS], x[NS];
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            b[i] = -delta[i];
+        });
+        mdl.lin_solve(s.inv, b, x);
+        const double cg = fdiv(2.0, 1.0 + s.gamrat);
+        const double c = (s.gamrat != 1.0) ? cg : 1.0;
+        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+            constexpr int i = CI(I_);
+            x[i] *= c;
+            s.acor[i] += x[i];
+        });
+        const double del = wrms<NS>(x, s.ewt);
+        const double cr = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
+        s.crate = (curiter > 0) ? cr : s.crate;
+        const double dcon = fdiv(del * SUNMIN(1.0, s.crate), tol);
+        const double anrm = wrms<NS>(s.acor, s.ewt);
+        if (dcon <= 1.0) {
+            s.acnrm = (curiter == 0) ? del : anrm;
+            s.nls_jcur = 0;
+            return true;
+        }
+        bool fail = (curiter >= 1) && (del > RDIV * s.delp);
+        if (!fail) {
+            s.delp = del;
+            curiter++;
+            fail = (curiter >= NLS_MAXCOR);
+            if (!fail) continue;
+        }
+        if (!s.nls_jcur) {
+            callSetup = true;
+            jbad = true;
+            cfor<0, NS>([&](auto I_) __attribute__((always_inline)) { s.acor[CI(I_)] = 0.0; });
+            continue;
+        }
+        return false;
+    }
+}
+
+enum { ATTEMPT_OK = 0, ATTEMPT_CONV_FAIL = 1, ATTEMPT_ERR_FAIL = 2 };
+
+// One attempt of cvStep at order Q: rescale (eta_eff), predict, set, Newton, error test;
+// on failure the prediction is undone (cvRestore) before returning.
+template <int Q, int NS, class S, class Model>
+BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm)
+{
+    rescale_q<Q, NS>(s, eta_eff);
+    BDF_PH(2);
+    predict_q<Q, NS>(s);
+    BDF_PH(3);
+    const double rl1 = set_bdf_q<Q>(s);
+    BDF_PH(4);
+    const int convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
+    const bool callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (s.nst == 0) ||
+                           (s.nst >= s.nstlp + MSBP) || (fabs(s.gamrat - 1.0) > DGMAX);
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) { s.acor[CI(I_)] = 0.0; });
+    const bool conv = newton_u<NS>(s, mdl, rl1, convfail, callSetup);
+    BDF_PH(5);
+    dsm = s.acnrm * s.tq[2];
+    if (conv && dsm <= 1.0) return ATTEMPT_OK;
+    restore_q<Q, NS>(s, saved_t);
+    return conv ? ATTEMPT_ERR_FAIL : ATTEMPT_CONV_FAIL;
+}
+
+// cvCompleteStep + cvPrepareNextStep (+ cvComputeEtaqm1/qp1, cvChooseEta, cvSetEta) at order Q.
+// The three candidate ratios are independent chains computed together; the qwait == 0 choice
+// is made with selects.
+template <int Q, int NS, class S>
+BDF_INL void complete_q(S& s, double dsm)
+{
+    constexpr int q = Q;
+    s.nst++;
+    s.cnt.nst_total++;
+    s.hu = s.h;
+    cfor_down<Q, 2>([&](auto i) __attribute__((always_inline)) { s.tau[CI(i)] = s.tau[CI(i) - 1]; });
+    if constexpr (q == 1) s.tau[2] = (s.nst > 1) ? s.tau[1] : s.tau[2];
+    s.tau[1] = s.h;
+    cfor<0, Q + 1>([&](auto j) __attribute__((always_inline)) {
+        cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = __builtin_fma(s.l[CI(j)], s.acor[CI(i)], s.zn[CI(j)][CI(i)]); });
+    });
+    s.qwait--;
+    if constexpr (q != QMAX) {
+        const bool save = (s.qwait == 1);
+        cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+            s.zn[QMAX][CI(i)] = save ? s.acor[CI(i)] : s.zn[QMAX][CI(i)];
+        });
+        s.saved_tq5 = save ? s.tq[5] : s.saved_tq5;
+    }
+    BDF_PH(7);
+
+    if (s.etamax == 1.0) {
+        s.qwait = SUNMAX(s.qwait, 2);
+        s.qprime = q;
+        s.hprime = s.h;
+        s.eta = 1.0;
+    } else {
+        // candidates: etaq (always), etaqm1 (q > 1), etaqp1 (q < QMAX, saved_tq5 != 0)
+        const double xq = BIAS2 * dsm;
+        double xm = 0.0, xp = 0.0;
+        if constexpr (q > 1) xm = BIAS1 * wrms<NS>(s.zn[q], s.ewt) * s.tq[1];
+        bool do_p = false;
+        if constexpr (q != QMAX) {
+            do_p = (s.saved_tq5 != 0.0);
+            const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
+            double tv[NS];
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+                tv[CI(i)] = __builtin_fma(-cquot, s.zn[QMAX][CI(i)], s.acor[CI(i)]);
+            });
+            xp = BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3];
+        }
+        const double etaq = eta_from(xq, q + 1);
+        double etaqm1 = 0.0, etaqp1 = 0.0;
+        if constexpr (q > 1) etaqm1 = eta_from(xm, q);
+        if constexpr (q != QMAX) etaqp1 = do_p ? eta_from(xp, q + 2) : 0.0;
+        const bool choose = (s.qwait == 0);
+        // cvChooseEta
+        const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
+        double eta_c;
+        int qp_c = q;
+        if (etam < THRESH) {
+            eta_c = 1.0;
+        } else if (etam == etaq) {
+            eta_c = etaq;
+        } else if (etam == etaqm1) {
+            eta_c = etaqm1;
+            qp_c = q - 1;
+        } else {
+            eta_c = etaqp1;
+            qp_c = q + 1;
+        }
+        const bool to_p = choose && (qp_c == q + 1);
+        double eta = choose ? eta_c : etaq;
+        s.qprime = choose ? qp_c : q;
+        s.qwait = choose ? 2 : s.qwait;
+        cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+            s.zn[QMAX][CI(i)] = to_p ? s.acor[CI(i)] : s.zn[QMAX][CI(i)];
+        });
+        // cvSetEta (hmax_inv = 0)
+        const bool small = (eta < THRESH);
+        s.eta = small ? 1.0 : SUNMIN(eta, s.etamax);
+        s.hprime = small ? s.h : s.h * s.eta;
+    }
+    BDF_PH(8);
+    s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.acor[CI(i)] *= s.tq[2]; });
+}
+
+// CVode(..., CV_ONE_STEP) for the UNI launch: same contract as bcm3hip::cvode_one_step.
+template <int NS, class S, class Model>
+BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret)
+{
+    BDF_PH(0);
+    if (s.nst == 0) {
+        // first step after (Re)Init: rare, generic path
+        s.tretlast = tret = s.tn;
+        ewt_set<NS>(s, s.zn[0], s.ewt);
+        s.nstlj = 0;
+        s.nls_jcur = 0;
+        mdl.rhs(s.tn, s.zn[0], s.zn[1]);
+        s.cnt.nfe++;
+        if (s.tstopset) {
+            if ((s.tstop - s.tn) * (tout - s.tn) <= 0.0) return CV_ILL_INPUT;
+        }
+        double tout_hin = tout;
+        if (s.tstopset && (tout - s.tn) * (tout - s.tstop) > 0.0) tout_hin = s.tstop;
+        const int hflag = hin<NS>(s, mdl, tout_hin);
+        if (hflag != CV_SUCCESS) return hflag;
+        if (s.tstopset) {
+            if ((s.tn + s.h - s.tstop) * s.h > 0.0) s.h = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+        }
+        s.hscale = s.h;
+        s.hprime = s.h;
+        cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[1][CI(i)] *= s.h; });
+    } else {
+        const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+        const bool ret_prev = fabs(s.tn - s.tretlast) > troundoff;
+        const bool at_stop = s.tstopset && (fabs(s.tn - s.tstop) <= troundoff);
+        if (ret_prev || at_stop) {
+            if (ret_prev) {
+                s.tretlast = tret = s.tn;
+                cfor<0, NS>([&](auto i) __attribute__((always_inline)) { yout[CI(i)] = s.zn[0][CI(i)]; });
+                return CV_SUCCESS;
+            }
+            if (get_dky<NS>(s, s.tstop, yout) != CV_SUCCESS) return CV_ILL_INPUT;
+            s.tretlast = tret = s.tstop;
+            s.tstopset = 0;
+            return CV_TSTOP_RETURN;
+        }
+        const double hp2 = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+        const double eta2 = fdiv(hp2, s.h);
+        const bool clamp = s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
+        s.hprime = clamp ? hp2 : s.hprime;
+        s.eta = clamp ? eta2 : s.eta;
+        ewt_set<NS>(s, s.zn[0], s.ewt);
+    }
+    {
+        double ss = 0.0;
+        cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+            const double p = s.zn[0][CI(i)] * s.ewt[CI(i)];
+            ss = __builtin_fma(p, p, ss);
+        });
+        if (ss > (double)NS * (1.0 / (UROUND * UROUND))) {
+            s.tretlast = tret = s.tn;
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { yout[CI(i)] = s.zn[0][CI(i)]; });
+            return CV_TOO_MUCH_ACC;
+        }
+    }
+    BDF_PH(1);
+
+    // ---------------- cvStep
+    const double saved_t = s.tn;
+    int ncf = 0, nef = 0, nflag = FIRST_CALL;
+    double eta_eff = 1.0;
+    if ((s.nst > 0) && (s.hprime != s.h)) {
+        if (s.qprime != s.q) {
+            adjust_order<NS>(s, s.qprime - s.q);
+            s.q = s.qprime;
+            s.L = s.q + 1;
+            s.qwait = s.L;
+        }
+        eta_eff = s.eta;
+    }
+    double dsm = 0.0;
+    int q_done;
+    for (;;) {
+        int r;
+        switch (s.q) {
+        case 1: r = attempt_q<1, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 2: r = attempt_q<2, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 3: r = attempt_q<3, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 4: r = attempt_q<4, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        default: r = attempt_q<5, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        }
+        BDF_PH(6);
+        if (r == ATTEMPT_OK) break;
+        // failure handling (cvHandleNFlag / cvDoErrorTest), rare
+        eta_eff = 1.0;
+        s.etamax = 1.0;
+        if (r == ATTEMPT_CONV_FAIL) {
+            s.cnt.ncfn++;
+            ncf++;
+            if (ncf == MXNCF) return CV_CONV_FAILURE;
+            s.eta = ETACF;
+            nflag = PREV_CONV_FAIL;
+            eta_eff = s.eta;
+            continue;
+        }
+        nef++;
+        s.cnt.netf++;
+        nflag = PREV_ERR_FAIL;
+        if (nef == MXNEF) return CV_ERR_FAILURE;
+        if (nef <= MXNEF1) {
+            double eta = eta_from(BIAS2 * dsm, s.L);
+            eta = SUNMAX(ETAMIN, eta);
+            if (nef >= SMALL_NEF) eta = SUNMIN(eta, ETAMXF);
+            s.eta = eta;
+            eta_eff = s.eta;
+            continue;
+        }
+        s.eta = ETAMIN;
+        if (s.q > 1) {
+            adjust_order<NS>(s, -1);
+            s.L = s.q;
+            s.q--;
+            s.qwait = s.L;
+            eta_eff = s.eta;
+            continue;
+        }
+        s.h *= s.eta;
+        s.hscale = s.h;
+        s.qwait = LONG_WAIT;
+        double tv[NS];
+        mdl.rhs(s.tn, s.zn[0], tv);
+        s.cnt.nfe++;
+        cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[1][CI(i)] = s.h * tv[CI(i)]; });
+        eta_eff = 1.0;
+    }
+    q_done = s.q;
+    switch (q_done) {
+    case 1: complete_q<1, NS>(s, dsm); break;
+    case 2: complete_q<2, NS>(s, dsm); break;
+    case 3: complete_q<3, NS>(s, dsm); break;
+    case 4: complete_q<4, NS>(s, dsm); break;
+    default: complete_q<5, NS>(s, dsm); break;
+    }
+
+    // stop tests after the step (cvode.c:1395-1437)
+    const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+    if (s.tstopset && fabs(s.tn - s.tstop) <= troundoff) {
+        get_dky<NS>(s, s.tstop, yout);
+        s.tretlast = tret = s.tstop;
+        s.tstopset = 0;
+        BDF_PH(9);
+        return CV_TSTOP_RETURN;
+    }
+    const double hp2 = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+    const double eta2 = fdiv(hp2, s.h);
+    const bool clamp = s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
+    s.hprime = clamp ? hp2 : s.hprime;
+    s.eta = clamp ? eta2 : s.eta;
+    s.tretlast = tret = s.tn;
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { yout[CI(i)] = s.zn[0][CI(i)]; });
+    BDF_PH(9);
+    return CV_SUCCESS;
+}
+
+}  // namespace uni
+}  // namespace bcm3hip

@@ -21,6 +21,7 @@
 #include <cstdint>
 
 #include "bdf_lane.h"
+#include "bdf_uni.h"
 #include "popk_kernel.h"
 
 namespace bcm3hip {
@@ -101,6 +102,16 @@ BDF_INL double log_pdf_tnu4(double x, double mu, double sigma)
 // ---------------------------------------------------------------------------------------------
 // PK models (LikelihoodPopPKTrajectory.cpp:446-642)
 
+// readfirstlane of both halves: the value is (already) the same in every lane; this tells the
+// compiler so
+__device__ __forceinline__ double wave_uniform(double x)
+{
+    const long long b = __builtin_bit_cast(long long, x);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
 template <int PKT>
 struct PKTraits {
     static constexpr bool two = (PKT == BCM3HIP_PK_TWO || PKT == BCM3HIP_PK_TWO_BIPHASIC ||
@@ -138,10 +149,10 @@ struct PKLane {
             dydt[0] = -(a + ke) * y[0];
         }
         if constexpr (TR::two) {
-            dydt[1] = a * y[0] - kel * y[1] - kf * y[1] + kb * y[2];
-            dydt[2] = kf * y[1] - kb * y[2];
+            dydt[1] = __builtin_fma(kb, y[2], __builtin_fma(-kf, y[1], __builtin_fma(-kel, y[1], a * y[0])));
+            dydt[2] = __builtin_fma(kf, y[1], -(kb * y[2]));
         } else {
-            dydt[1] = a * y[0] - kel * y[1];
+            dydt[1] = __builtin_fma(-kel, y[1], a * y[0]);
         }
     }
 
@@ -158,14 +169,14 @@ struct PKLane {
     {
         const double a = cur_ka();
         const double ng = -gamma;
-        const double a00 = (-(a + ke)) * ng + 1.0;
+        const double a00 = __builtin_fma(-(a + ke), ng, 1.0);
         const double a10 = a * ng;
         if constexpr (TR::two) {
-            const double a11 = (-(kel + kf)) * ng + 1.0;
+            const double a11 = __builtin_fma(-(kel + kf), ng, 1.0);
             const double a12 = kb * ng;
             const double a21 = kf * ng;
-            const double a22 = (-kb) * ng + 1.0;
-            const double c0 = a11 * a22 - a12 * a21;  // cofactor(0,0)
+            const double a22 = __builtin_fma(-kb, ng, 1.0);
+            const double c0 = __builtin_fma(a11, a22, -(a12 * a21));  // cofactor(0,0)
             const double invdet = frcp(c0 * a00);    // det = c0*a00 + 0*a10 + 0*a20
             r.i00 = c0 * invdet;
             r.i10 = (-(a10 * a22)) * invdet;
@@ -175,7 +186,7 @@ struct PKLane {
             r.i21 = (-(a21 * a00)) * invdet;
             r.i22 = (a00 * a11) * invdet;
         } else {
-            const double a11 = (-kel) * ng + 1.0;
+            const double a11 = __builtin_fma(-kel, ng, 1.0);
             const double invdet = frcp(a00 * a11);  // a00*a11 - a01*a10, a01 = 0
             r.i00 = a11 * invdet;
             r.i10 = -a10 * invdet;
@@ -188,10 +199,10 @@ struct PKLane {
     {
         x[0] = r.i00 * b[0];
         if constexpr (TR::two) {
-            x[1] = r.i10 * b[0] + r.i11 * b[1] + r.i12 * b[2];
-            x[2] = r.i20 * b[0] + r.i21 * b[1] + r.i22 * b[2];
+            x[1] = __builtin_fma(r.i12, b[2], __builtin_fma(r.i11, b[1], r.i10 * b[0]));
+            x[2] = __builtin_fma(r.i22, b[2], __builtin_fma(r.i21, b[1], r.i20 * b[0]));
         } else {
-            x[1] = r.i10 * b[0] + r.i11 * b[1];
+            x[1] = __builtin_fma(r.i11, b[1], r.i10 * b[0]);
         }
     }
 };
@@ -220,7 +231,8 @@ BDF_INL bool check_give_treatment(double t, const uint8_t* skipped, int intermit
 // UNI (lanes_per_wave == 1): the wavefront integrates ONE trajectory and its index is made
 // wave-uniform (readfirstlane), so every value derived from it is uniform to the compiler: the
 // model data come in through scalar loads and every solver branch is a uniform (scalar) branch
-// instead of exec-mask manipulation. All 64 lanes compute the same numbers; lane 0 stores.
+// instead of exec-mask manipulation. All 64 lanes compute and store the same numbers (a
+// same-address same-value store from every lane is one well-defined store).
 template <int PKT, bool UNI>
 __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t ntraj, int lpw,
                                                         const double* __restrict__ values,
@@ -243,7 +255,6 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         g = gwave * lpw + lane;
         if (g >= ntraj) return;
     }
-    const bool writer = !UNI || lane == 0;
     const int P = m.P;
     const int64_t e = g / P;
     const int j = (int)(g - e * P);
@@ -288,6 +299,20 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         tsw = (lim < tsw) ? lim : tsw;
         mdl.ka2 = transform_var(m.transforms[ai], v[ai]);
     }
+    if constexpr (UNI) {
+        // values returned by out-of-line calls (ndtri_lower) count as divergent to the compiler;
+        // re-assert uniformity once so the whole solve stays on scalar control flow
+        mdl.ka = wave_uniform(mdl.ka);
+        mdl.ke = wave_uniform(mdl.ke);
+        mdl.kel = wave_uniform(mdl.kel);
+        mdl.kf = wave_uniform(mdl.kf);
+        mdl.kb = wave_uniform(mdl.kb);
+        mdl.ktr = wave_uniform(mdl.ktr);
+        mdl.ntr = wave_uniform(mdl.ntr);
+        mdl.lnf = wave_uniform(mdl.lnf);
+        mdl.ka2 = wave_uniform(mdl.ka2);
+        tsw = wave_uniform(tsw);
+    }
     mdl.dose = m.dose[j];
     mdl.dose_after = m.dose_after_dose_change[j];
     mdl.dose_change_time = m.dose_change_time[j];
@@ -309,7 +334,8 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     // (a non-positive discontinuity time is ignored by ODESolver::SetDiscontinuity; the
     //  host rejects such models, so next_disc > 0 here)
 
-    const double conversion = (1e6 / m.MW) / vod;
+    const double conversion = UNI ? wave_uniform((1e6 / m.MW) / vod) : (1e6 / m.MW) / vod;
+    const double sd_u = UNI ? wave_uniform(sd) : sd, sd2_u = UNI ? wave_uniform(sd2) : sd2;
     const int nsim = m.simulate_until[j];
     const double* obs = m.observed + (int64_t)j * T;
     double* tro = traj_out ? traj_out + g * (int64_t)NS * T : nullptr;
@@ -328,7 +354,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
 
     // observation term for output index i with state yi (.cpp:412-423)
     auto observe = [&](int i, const double (&yi)[NS]) __attribute__((always_inline)) {
-        if (tro && writer) {
+        if (tro) {
             cfor<0, NS>([&](auto k) __attribute__((always_inline)) { tro[CI(k) * T + i] = yi[CI(k)]; });
         }
         if (llh_done) return;
@@ -336,7 +362,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         const double yo = obs[i];
         if (!isnan(yo)) {
             const double xm = (x < 0.0) ? 0.0 : x;
-            llh += log_pdf_tnu4(x, yo, sd + sd2 * xm);
+            llh += log_pdf_tnu4(x, yo, sd_u + sd2_u * xm);
         }
         if (isnan(x)) {
             llh = -INFINITY;
@@ -344,7 +370,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         }
     };
 
-    if (tro && writer) {
+    if (tro) {
         for (int k = 0; k < NS * T; k++) tro[k] = NAN;
     }
 
@@ -382,7 +408,11 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             int current_step = 0;
             for (;;) {
                 double tret = 0.0;
-                int result = cvode_one_step<NS>(s, mdl, end_time, y, tret);
+                int result;
+                if constexpr (UNI)
+                    result = uni::cvode_one_step_u<NS>(s, mdl, end_time, y, tret);
+                else
+                    result = cvode_one_step<NS>(s, mdl, end_time, y, tret);
                 if (result < 0) {
                     status = BCM3HIP_STATUS_SOLVER_FAIL;
                     break;
@@ -447,7 +477,6 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     }
     if (status != BCM3HIP_STATUS_OK) llh = -INFINITY;
 
-    if (!writer) return;
 #ifdef BCM3_PHASES
     if (tro) cfor<0, NPHASES>([&](auto k) __attribute__((always_inline)) { tro[CI(k)] = (double)s.ph[CI(k)]; });
 #endif
