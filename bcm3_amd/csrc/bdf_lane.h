@@ -118,10 +118,10 @@ BDF_INL double fdiv(double a, double b)
     double e = __builtin_fma(-b, q, a);
     return __builtin_fma(e, r, q);
 }
-// SUNRsqrt: x <= 0 -> 0; v_rsq_f64 estimate + Goldschmidt refinement
+// SUNRsqrt: x <= 0 -> 0; v_rsq_f64 estimate + Goldschmidt refinement (branch-free: the
+// refinement runs for every x and the result is selected)
 BDF_INL double fsqrt(double x)
 {
-    if (!(x > 0.0)) return (x <= 0.0) ? 0.0 : x;  // 0 for x <= 0, NaN passes through
     double r = __builtin_amdgcn_rsq(x);
     double g = x * r, hh = 0.5 * r;
     double e = __builtin_fma(-g, hh, 0.5);
@@ -130,7 +130,16 @@ BDF_INL double fsqrt(double x)
     double d = __builtin_fma(-g, g, x);
     g = __builtin_fma(d, hh, g);
     d = __builtin_fma(-g, g, x);
-    return __builtin_fma(d, hh, g);
+    g = __builtin_fma(d, hh, g);
+    return (x > 0.0) ? g : ((x <= 0.0) ? 0.0 : x);  // 0 for x <= 0, NaN passes through
+}
+// a / b for a compile-time b with rb = 1/b correctly rounded (the value frcp(b) produces):
+// the quotient step of fdiv without the reciprocal iteration
+BDF_INL double fdiv_c(double a, double b, double rb)
+{
+    const double q = a * rb;
+    const double e = __builtin_fma(-b, q, a);
+    return __builtin_fma(e, rb, q);
 }
 
 // 1/j for j = 1..7 (the correctly rounded quotients 1.0/j)
@@ -146,27 +155,28 @@ BDF_INL double recip_int(int j)
     return r;
 }
 
-// SUNRpowerR(x, 1.0/k) = pow(x, 1/k) for k in 2..7 (sundials_math.c:40-52): x <= 0 -> 0.
-// Single-precision hardware log2/exp2 seed, two Newton steps on y^k = x in double.
-BDF_INL double root_k(double x, int k)
+// eta = 1 / (pow(bias*x, 1/k) + ADDON)  (cvode.c:2996, 3101, 3160, 3185), SUNRpowerR(x, 1/k)
+// with x <= 0 -> 0 (sundials_math.c:40-52), k in 2..7.
+// Division-free Newton iteration for z = x^(-1/k) (z <- z + z (1 - x z^k) / k) from a
+// single-precision log2/exp2 seed; eta = z / (1 + ADDON z). Two iterations reach double
+// accuracy from the ~2^-22 seed. Outside [1e-30, 1e30] (never on the solver's paths in
+// practice) the library pow is used.
+BDF_INL double eta_from(double bx, int k)
 {
-    if (!(x > 0.0)) return 0.0;
-    if (!(x > 1e-30 && x < 1e30)) return pow(x, recip_int(k));
+    if (!(bx > 1e-30 && bx < 1e30)) return frcp((bx > 0.0 ? pow(bx, recip_int(k)) : 0.0) + ADDON);
     const double rk = recip_int(k);
-    float lf = __builtin_amdgcn_logf((float)x);        // log2
-    double y = (double)__builtin_amdgcn_exp2f(lf * (float)rk);
-#pragma unroll 1
-    for (int it = 0; it < 2; it++) {
-        double p = y;  // y^(k-1), k >= 2
-        cfor<2, 7>([&](auto I) __attribute__((always_inline)) {
-            if (CI(I) < k) p *= y;
+    const float lf = __builtin_amdgcn_logf((float)bx);  // log2
+    double z = (double)__builtin_amdgcn_exp2f(-lf * (float)rk);
+    cfor<0, 2>([&](auto) __attribute__((always_inline)) {
+        double zk = z;  // z^k, k >= 2
+        cfor<2, 8>([&](auto I) __attribute__((always_inline)) {
+            if (CI(I) <= k) zk *= z;
         });
-        y = __builtin_fma(fdiv(x, p) - y, rk, y);
-    }
-    return y;
+        const double t = __builtin_fma(-bx, zk, 1.0);
+        z = __builtin_fma(z * t, rk, z);
+    });
+    return fdiv(z, __builtin_fma(ADDON, z, 1.0));
 }
-// eta = 1 / (pow(bias*x, 1/k) + ADDON)  (cvode.c:2996, 3101, 3160, 3185)
-BDF_INL double eta_from(double bx, int k) { return frcp(root_k(bx, k) + ADDON); }
 
 // SUNRpowerI for exponent 1..7 (repeated multiplication, sundials_math.c:28-38)
 BDF_INL double powI(double base, int e)
@@ -254,7 +264,7 @@ BDF_INL double wrms(const double (&x)[NS], const double (&w)[NS])
         double p = x[CI(i)] * w[CI(i)];
         s = __builtin_fma(p, p, s);
     });
-    return fsqrt(fdiv(s, (double)NS));
+    return fsqrt(fdiv_c(s, (double)NS, 1.0 / NS));
 }
 
 // cvEwtSetSV: w = 1/(rtol*|y| + atol)

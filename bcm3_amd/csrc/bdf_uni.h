@@ -3,14 +3,15 @@
 //
 // Same algorithm and the same floating-point operations as cvode_one_step in bdf_lane.h (the
 // two paths agree bit for bit, tests/test_popk_gpu.py); what changes is the control flow. One
-// wavefront running alone on a SIMD pays ~20-40 cycles for every branch, taken or not, but only
-// ~4 cycles for a v_cndmask and ~4 for an independent f64 op (tools/ubench, profiles/
-// r01_ubench.txt). So:
+// wavefront alone on a SIMD is issue bound: every VALU instruction costs ~4 cycles whether or
+// not it depends on the previous one, a branch ~20-40 cycles taken or not, a select ~4 per
+// 32-bit half (tools/ubench, profiles/r01_ubench.txt). So the instruction count is the cost:
 //  * the step is instantiated per BDF order Q = 1..5 (one dispatch per attempt): no guards on
 //    the runtime order inside predict / rescale / set / complete;
-//  * short conditional work is computed unconditionally and selected (division results,
-//    tq[1]/tq[3], the order-change candidates etaqm1/etaqp1 -- independent chains the scheduler
-//    interleaves), and rescaling by eta = 1 replaces the "h changed?" branch (x * 1.0 == x);
+//  * work of a few instructions is done unconditionally and selected (rescaling by eta = 1
+//    replaces the "h changed?" branch, x * 1.0 == x); work of tens of instructions that is
+//    needed only every q+1 steps or rarely (tq[1]/tq[3], the order-change candidates, the
+//    tstop clamp, the multi-iteration norm) sits behind one scalar branch;
 //  * rare events (first step after ReInit, tstop reached, failures, order changes) stay behind
 //    one branch each and reuse the generic routines of bdf_lane.h.
 #pragma once
@@ -60,8 +61,7 @@ BDF_INL void restore_q(S& s, double saved_t)
     });
 }
 
-// cvSetBDF + cvSetTqBDF + cvSet for order Q; the qwait == 1 quantities (tq[1], tq[3]) are
-// computed unconditionally and kept only when qwait == 1.
+// cvSetBDF + cvSetTqBDF + cvSet for order Q.
 template <int Q, class S>
 BDF_INL double set_bdf_q(S& s)
 {
@@ -90,8 +90,8 @@ BDF_INL double set_bdf_q(S& s)
     const double lq = s.l[q];
     s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
     s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
-    {
-        // qwait == 1 block of cvSetTqBDF, evaluated unconditionally
+    if (s.qwait == 1) {
+        // qwait == 1 block of cvSetTqBDF
         double tq1 = 1.0;
         if constexpr (q > 1) {
             const double C = fdiv(xistar_inv, lq);
@@ -106,9 +106,8 @@ BDF_INL double set_bdf_q(S& s)
         const double A6 = alpha0_hat - xi_inv2;
         const double Cppinv = fdiv(1.0 - A6 + A5, A2);
         const double tq3 = fabs(fdiv(Cppinv, xi_inv2 * (double)(q + 2) * A5));
-        const bool qw1 = (s.qwait == 1);
-        s.tq[1] = qw1 ? tq1 : s.tq[1];
-        s.tq[3] = qw1 ? tq3 : s.tq[3];
+        s.tq[1] = tq1;
+        s.tq[3] = tq3;
     }
     s.tq[4] = fdiv(CORTES, s.tq[2]);
     const double rl1 = frcp(s.l[1]);
@@ -119,8 +118,7 @@ BDF_INL double set_bdf_q(S& s)
     return rl1;
 }
 
-// Newton iteration (bdf_lane.h newton) with the gamrat scaling and the final-norm choice as
-// selects.
+// Newton iteration (bdf_lane.h newton) with the gamrat scaling as a select.
 template <int NS, class S, class Model>
 BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool callSetup)
 {
@@ -175,9 +173,8 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
         const double cr = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
         s.crate = (curiter > 0) ? cr : s.crate;
         const double dcon = fdiv(del * SUNMIN(1.0, s.crate), tol);
-        const double anrm = wrms<NS>(s.acor, s.ewt);
         if (dcon <= 1.0) {
-            s.acnrm = (curiter == 0) ? del : anrm;
+            s.acnrm = (curiter == 0) ? del : wrms<NS>(s.acor, s.ewt);
             s.nls_jcur = 0;
             return true;
         }
@@ -224,8 +221,6 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
 }
 
 // cvCompleteStep + cvPrepareNextStep (+ cvComputeEtaqm1/qp1, cvChooseEta, cvSetEta) at order Q.
-// The three candidate ratios are independent chains computed together; the qwait == 0 choice
-// is made with selects.
 template <int Q, int NS, class S>
 BDF_INL void complete_q(S& s, double dsm)
 {
@@ -255,47 +250,38 @@ BDF_INL void complete_q(S& s, double dsm)
         s.hprime = s.h;
         s.eta = 1.0;
     } else {
-        // candidates: etaq (always), etaqm1 (q > 1), etaqp1 (q < QMAX, saved_tq5 != 0)
-        const double xq = BIAS2 * dsm;
-        double xm = 0.0, xp = 0.0;
-        if constexpr (q > 1) xm = BIAS1 * wrms<NS>(s.zn[q], s.ewt) * s.tq[1];
-        bool do_p = false;
-        if constexpr (q != QMAX) {
-            do_p = (s.saved_tq5 != 0.0);
-            const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
-            double tv[NS];
-            cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
-                tv[CI(i)] = __builtin_fma(-cquot, s.zn[QMAX][CI(i)], s.acor[CI(i)]);
-            });
-            xp = BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3];
+        const double etaq = eta_from(BIAS2 * dsm, q + 1);
+        double eta = etaq;
+        s.qprime = q;
+        if (s.qwait == 0) {
+            // cvComputeEtaqm1 / cvComputeEtaqp1 / cvChooseEta, every q+1 steps
+            s.qwait = 2;
+            double etaqm1 = 0.0, etaqp1 = 0.0;
+            if constexpr (q > 1) etaqm1 = eta_from(BIAS1 * wrms<NS>(s.zn[q], s.ewt) * s.tq[1], q);
+            if constexpr (q != QMAX) {
+                if (s.saved_tq5 != 0.0) {
+                    const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
+                    double tv[NS];
+                    cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
+                        tv[CI(i)] = __builtin_fma(-cquot, s.zn[QMAX][CI(i)], s.acor[CI(i)]);
+                    });
+                    etaqp1 = eta_from(BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3], q + 2);
+                }
+            }
+            const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
+            if (etam < THRESH) {
+                eta = 1.0;
+            } else if (etam == etaq) {
+                eta = etaq;
+            } else if (etam == etaqm1) {
+                eta = etaqm1;
+                s.qprime = q - 1;
+            } else {
+                eta = etaqp1;
+                s.qprime = q + 1;
+                cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[QMAX][CI(i)] = s.acor[CI(i)]; });
+            }
         }
-        const double etaq = eta_from(xq, q + 1);
-        double etaqm1 = 0.0, etaqp1 = 0.0;
-        if constexpr (q > 1) etaqm1 = eta_from(xm, q);
-        if constexpr (q != QMAX) etaqp1 = do_p ? eta_from(xp, q + 2) : 0.0;
-        const bool choose = (s.qwait == 0);
-        // cvChooseEta
-        const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
-        double eta_c;
-        int qp_c = q;
-        if (etam < THRESH) {
-            eta_c = 1.0;
-        } else if (etam == etaq) {
-            eta_c = etaq;
-        } else if (etam == etaqm1) {
-            eta_c = etaqm1;
-            qp_c = q - 1;
-        } else {
-            eta_c = etaqp1;
-            qp_c = q + 1;
-        }
-        const bool to_p = choose && (qp_c == q + 1);
-        double eta = choose ? eta_c : etaq;
-        s.qprime = choose ? qp_c : q;
-        s.qwait = choose ? 2 : s.qwait;
-        cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
-            s.zn[QMAX][CI(i)] = to_p ? s.acor[CI(i)] : s.zn[QMAX][CI(i)];
-        });
         // cvSetEta (hmax_inv = 0)
         const bool small = (eta < THRESH);
         s.eta = small ? 1.0 : SUNMIN(eta, s.etamax);
@@ -347,11 +333,10 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
             s.tstopset = 0;
             return CV_TSTOP_RETURN;
         }
-        const double hp2 = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
-        const double eta2 = fdiv(hp2, s.h);
-        const bool clamp = s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
-        s.hprime = clamp ? hp2 : s.hprime;
-        s.eta = clamp ? eta2 : s.eta;
+        if (s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0)) {
+            s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+            s.eta = fdiv(s.hprime, s.h);
+        }
         ewt_set<NS>(s, s.zn[0], s.ewt);
     }
     {
@@ -454,11 +439,10 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
         BDF_PH(9);
         return CV_TSTOP_RETURN;
     }
-    const double hp2 = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
-    const double eta2 = fdiv(hp2, s.h);
-    const bool clamp = s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
-    s.hprime = clamp ? hp2 : s.hprime;
-    s.eta = clamp ? eta2 : s.eta;
+    if (s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0)) {
+        s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+        s.eta = fdiv(s.hprime, s.h);
+    }
     s.tretlast = tret = s.tn;
     cfor<0, NS>([&](auto i) __attribute__((always_inline)) { yout[CI(i)] = s.zn[0][CI(i)]; });
     BDF_PH(9);

@@ -419,6 +419,11 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                 }
                 const double t = tret;
                 current_step++;
+                // one scalar branch for the common step: nothing to output, no discontinuity,
+                // not at the end (the checks below in the reference's order otherwise)
+                const bool rare = (result != CV_SUCCESS) | (tret >= next_out) | (t >= end_time) |
+                                  (current_step == m.max_steps) | (next_disc == t);
+                if (!rare) continue;
                 while (tret >= next_out) {
                     double dky[NS];
                     if (get_dky<NS>(s, m.time[tpi], dky) != CV_SUCCESS) {
