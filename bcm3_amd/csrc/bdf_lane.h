@@ -118,8 +118,9 @@ BDF_INL double fdiv(double a, double b)
     double e = __builtin_fma(-b, q, a);
     return __builtin_fma(e, r, q);
 }
-// SUNRsqrt: x <= 0 -> 0; v_rsq_f64 estimate + Goldschmidt refinement (branch-free: the
-// refinement runs for every x and the result is selected)
+// SUNRsqrt: x <= 0 -> 0; v_rsq_f64 estimate + Goldschmidt refinement. Branch-free: the
+// refinement runs for every x (x <= 0 gives NaN there) and x <= 0 is zeroed with a bit mask,
+// NaN passes through (a select here is turned back into a branch by the compiler).
 BDF_INL double fsqrt(double x)
 {
     double r = __builtin_amdgcn_rsq(x);
@@ -131,7 +132,8 @@ BDF_INL double fsqrt(double x)
     g = __builtin_fma(d, hh, g);
     d = __builtin_fma(-g, g, x);
     g = __builtin_fma(d, hh, g);
-    return (x > 0.0) ? g : ((x <= 0.0) ? 0.0 : x);  // 0 for x <= 0, NaN passes through
+    const long long keep = (x <= 0.0) ? 0LL : -1LL;
+    return __builtin_bit_cast(double, __builtin_bit_cast(long long, g) & keep);
 }
 // a / b for a compile-time b with rb = 1/b correctly rounded (the value frcp(b) produces):
 // the quotient step of fdiv without the reciprocal iteration
@@ -214,9 +216,11 @@ BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
 #ifdef BCM3_PHASES
 #define BDF_PH(k)                          \
     do {                                   \
+        __builtin_amdgcn_sched_barrier(0); \
         const long long t_ = clock64();    \
         s.ph[k] += t_ - s.tlast;           \
         s.tlast = t_;                      \
+        __builtin_amdgcn_sched_barrier(0); \
     } while (0)
 #else
 #define BDF_PH(k) \

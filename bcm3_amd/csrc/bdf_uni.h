@@ -292,6 +292,15 @@ BDF_INL void complete_q(S& s, double dsm)
     cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.acor[CI(i)] *= s.tq[2]; });
 }
 
+// attempt at order Q and, when it passes, the completion at the same order (one dispatch on q)
+template <int Q, int NS, class S, class Model>
+BDF_INL int step_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm)
+{
+    const int r = attempt_q<Q, NS>(s, mdl, eta_eff, saved_t, nflag, dsm);
+    if (r == ATTEMPT_OK) complete_q<Q, NS>(s, dsm);
+    return r;
+}
+
 // CVode(..., CV_ONE_STEP) for the UNI launch: same contract as bcm3hip::cvode_one_step.
 template <int NS, class S, class Model>
 BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret)
@@ -367,15 +376,14 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
         eta_eff = s.eta;
     }
     double dsm = 0.0;
-    int q_done;
     for (;;) {
         int r;
         switch (s.q) {
-        case 1: r = attempt_q<1, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        case 2: r = attempt_q<2, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        case 3: r = attempt_q<3, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        case 4: r = attempt_q<4, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        default: r = attempt_q<5, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 1: r = step_q<1, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 2: r = step_q<2, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 3: r = step_q<3, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 4: r = step_q<4, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        default: r = step_q<5, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
         }
         BDF_PH(6);
         if (r == ATTEMPT_OK) break;
@@ -420,14 +428,6 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
         s.cnt.nfe++;
         cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[1][CI(i)] = s.h * tv[CI(i)]; });
         eta_eff = 1.0;
-    }
-    q_done = s.q;
-    switch (q_done) {
-    case 1: complete_q<1, NS>(s, dsm); break;
-    case 2: complete_q<2, NS>(s, dsm); break;
-    case 3: complete_q<3, NS>(s, dsm); break;
-    case 4: complete_q<4, NS>(s, dsm); break;
-    default: complete_q<5, NS>(s, dsm); break;
     }
 
     // stop tests after the step (cvode.c:1395-1437)
