@@ -377,7 +377,7 @@ BDF_INL double set_bdf(S& s)
         const double Cppinv = fdiv(1.0 - A6 + A5, A2);
         s.tq[3] = fabs(fdiv(Cppinv, xi_inv * (double)(q + 2) * A5));
     }
-    s.tq[4] = fdiv(CORTES, s.tq[2]);
+    // tq[4] = CORTES / tq[2] is used only as the Newton tolerance, folded into the test there
     // cvSet
     const double rl1 = frcp(s.l[1]);
     s.gamma = s.h * rl1;
@@ -504,8 +504,9 @@ BDF_INL void reinit(S& s, double t0, const double (&y0)[NS])
 template <int NS, class S, class Model>
 BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callSetup)
 {
-    const double tol = s.tq[4];
     bool jbad = false;
+    // 2/(1+gamrat) scaling of cvLsSolve: constant within the solve, 1 after a setup
+    double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
     int curiter = 0;
     for (;;) {
         // residual: y = zn0 + ycor; f(tn, y); res = rl1*zn1 + ycor; res += -gamma*f
@@ -535,6 +536,7 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
             s.cnt.nsetups++;
             s.nls_jcur = jnew;
             s.gamrat = 1.0;
+            cscale = 1.0;
             s.gammap = s.gamma;
             s.crate = 1.0;
             s.nstlp = s.nst;
@@ -550,7 +552,7 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
         });
         mdl.lin_solve(s.inv, b, x);
         if (s.gamrat != 1.0) {
-            const double c = fdiv(2.0, 1.0 + s.gamrat);
+            const double c = cscale;
             cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
                 constexpr int i = CI(I_);
                 x[i] *= c;
@@ -563,8 +565,8 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
         // cvNlsConvTest (cvode_nls.c:236-280)
         const double del = wrms<NS>(x, s.ewt);
         if (curiter > 0) s.crate = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
-        const double dcon = fdiv(del * SUNMIN(1.0, s.crate), tol);
-        if (dcon <= 1.0) {
+        // cvNlsConvTest: dcon = del min(1, crate) / tol <= 1 with tol = CORTES / tq[2]
+        if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
             s.acnrm = (curiter == 0) ? del : wrms<NS>(s.acor, s.ewt);
             s.nls_jcur = 0;
             return true;

@@ -89,7 +89,9 @@ BDF_INL double set_bdf_q(S& s)
     const double A2 = __builtin_fma((double)q, A1, 1.0);
     const double lq = s.l[q];
     s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
-    s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
+    // tq[5] is read only in the two steps after this one when qwait is 2 or 1 here
+    // (saved_tq5 at qwait == 1, etaqp1 at qwait == 0)
+    if (s.qwait <= 2) s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
     if (s.qwait == 1) {
         // qwait == 1 block of cvSetTqBDF
         double tq1 = 1.0;
@@ -109,7 +111,7 @@ BDF_INL double set_bdf_q(S& s)
         s.tq[1] = tq1;
         s.tq[3] = tq3;
     }
-    s.tq[4] = fdiv(CORTES, s.tq[2]);
+    // tq[4] = CORTES / tq[2] only serves as the Newton tolerance (folded into the test there)
     const double rl1 = frcp(s.l[1]);
     s.gamma = s.h * rl1;
     s.gammap = (s.nst == 0) ? s.gamma : s.gammap;
@@ -122,8 +124,9 @@ BDF_INL double set_bdf_q(S& s)
 template <int NS, class S, class Model>
 BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool callSetup)
 {
-    const double tol = s.tq[4];
     bool jbad = false;
+    // 2/(1+gamrat) scaling of cvLsSolve: constant within the solve, 1 after a setup
+    double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
     int curiter = 0;
     for (;;) {
         double y[NS], f[NS], delta[NS];
@@ -149,6 +152,7 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
             s.cnt.nsetups++;
             s.nls_jcur = jnew;
             s.gamrat = 1.0;
+            cscale = 1.0;
             s.gammap = s.gamma;
             s.crate = 1.0;
             s.nstlp = s.nst;
@@ -162,8 +166,7 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
             b[i] = -delta[i];
         });
         mdl.lin_solve(s.inv, b, x);
-        const double cg = fdiv(2.0, 1.0 + s.gamrat);
-        const double c = (s.gamrat != 1.0) ? cg : 1.0;
+        const double c = cscale;
         cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
             constexpr int i = CI(I_);
             x[i] *= c;
@@ -172,8 +175,8 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
         const double del = wrms<NS>(x, s.ewt);
         const double cr = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
         s.crate = (curiter > 0) ? cr : s.crate;
-        const double dcon = fdiv(del * SUNMIN(1.0, s.crate), tol);
-        if (dcon <= 1.0) {
+        // cvNlsConvTest: dcon = del min(1, crate) / tol <= 1 with tol = CORTES / tq[2]
+        if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
             s.acnrm = (curiter == 0) ? del : wrms<NS>(s.acor, s.ewt);
             s.nls_jcur = 0;
             return true;
@@ -301,52 +304,60 @@ BDF_INL int step_q(S& s, const Model& mdl, double eta_eff, double saved_t, int n
     return r;
 }
 
-// CVode(..., CV_ONE_STEP) for the UNI launch: same contract as bcm3hip::cvode_one_step.
+// CVode(..., CV_ONE_STEP) for the UNI launch: same contract as bcm3hip::cvode_one_step, except
+// that a successful step does not copy zn[0] to yout (the caller reads s.zn[0]).
 template <int NS, class S, class Model>
 BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret)
 {
     BDF_PH(0);
-    if (s.nst == 0) {
-        // first step after (Re)Init: rare, generic path
-        s.tretlast = tret = s.tn;
-        ewt_set<NS>(s, s.zn[0], s.ewt);
-        s.nstlj = 0;
-        s.nls_jcur = 0;
-        mdl.rhs(s.tn, s.zn[0], s.zn[1]);
-        s.cnt.nfe++;
-        if (s.tstopset) {
-            if ((s.tstop - s.tn) * (tout - s.tn) <= 0.0) return CV_ILL_INPUT;
-        }
-        double tout_hin = tout;
-        if (s.tstopset && (tout - s.tn) * (tout - s.tstop) > 0.0) tout_hin = s.tstop;
-        const int hflag = hin<NS>(s, mdl, tout_hin);
-        if (hflag != CV_SUCCESS) return hflag;
-        if (s.tstopset) {
-            if ((s.tn + s.h - s.tstop) * s.h > 0.0) s.h = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
-        }
-        s.hscale = s.h;
-        s.hprime = s.h;
-        cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[1][CI(i)] *= s.h; });
-    } else {
+    {
+        // one scalar branch for the common entry (cvode.c:1251-1310): not the first step after
+        // (Re)Init, tn was not returned before, tstop is neither reached nor within the next step
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+        const bool first = (s.nst == 0);
         const bool ret_prev = fabs(s.tn - s.tretlast) > troundoff;
         const bool at_stop = s.tstopset && (fabs(s.tn - s.tstop) <= troundoff);
-        if (ret_prev || at_stop) {
-            if (ret_prev) {
+        const bool clamp = s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
+        if (first | ret_prev | at_stop | clamp) {
+            if (first) {
                 s.tretlast = tret = s.tn;
-                cfor<0, NS>([&](auto i) __attribute__((always_inline)) { yout[CI(i)] = s.zn[0][CI(i)]; });
-                return CV_SUCCESS;
+                ewt_set<NS>(s, s.zn[0], s.ewt);
+                s.nstlj = 0;
+                s.nls_jcur = 0;
+                mdl.rhs(s.tn, s.zn[0], s.zn[1]);
+                s.cnt.nfe++;
+                if (s.tstopset) {
+                    if ((s.tstop - s.tn) * (tout - s.tn) <= 0.0) return CV_ILL_INPUT;
+                }
+                double tout_hin = tout;
+                if (s.tstopset && (tout - s.tn) * (tout - s.tstop) > 0.0) tout_hin = s.tstop;
+                const int hflag = hin<NS>(s, mdl, tout_hin);
+                if (hflag != CV_SUCCESS) return hflag;
+                if (s.tstopset) {
+                    if ((s.tn + s.h - s.tstop) * s.h > 0.0) s.h = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+                }
+                s.hscale = s.h;
+                s.hprime = s.h;
+                cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[1][CI(i)] *= s.h; });
+            } else {
+                if (ret_prev) {
+                    s.tretlast = tret = s.tn;
+                    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { yout[CI(i)] = s.zn[0][CI(i)]; });
+                    return CV_SUCCESS;
+                }
+                if (at_stop) {
+                    if (get_dky<NS>(s, s.tstop, yout) != CV_SUCCESS) return CV_ILL_INPUT;
+                    s.tretlast = tret = s.tstop;
+                    s.tstopset = 0;
+                    return CV_TSTOP_RETURN;
+                }
+                s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+                s.eta = fdiv(s.hprime, s.h);
+                ewt_set<NS>(s, s.zn[0], s.ewt);
             }
-            if (get_dky<NS>(s, s.tstop, yout) != CV_SUCCESS) return CV_ILL_INPUT;
-            s.tretlast = tret = s.tstop;
-            s.tstopset = 0;
-            return CV_TSTOP_RETURN;
+        } else {
+            ewt_set<NS>(s, s.zn[0], s.ewt);
         }
-        if (s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0)) {
-            s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
-            s.eta = fdiv(s.hprime, s.h);
-        }
-        ewt_set<NS>(s, s.zn[0], s.ewt);
     }
     {
         double ss = 0.0;
@@ -365,15 +376,14 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
     // ---------------- cvStep
     const double saved_t = s.tn;
     int ncf = 0, nef = 0, nflag = FIRST_CALL;
-    double eta_eff = 1.0;
-    if ((s.nst > 0) && (s.hprime != s.h)) {
-        if (s.qprime != s.q) {
-            adjust_order<NS>(s, s.qprime - s.q);
-            s.q = s.qprime;
-            s.L = s.q + 1;
-            s.qwait = s.L;
-        }
-        eta_eff = s.eta;
+    // cvAdjustParams when the step size changed; rescaling by eta_eff = 1 is a no-op
+    const bool adj = (s.nst > 0) & (s.hprime != s.h);
+    double eta_eff = adj ? s.eta : 1.0;
+    if (adj & (s.qprime != s.q)) {
+        adjust_order<NS>(s, s.qprime - s.q);
+        s.q = s.qprime;
+        s.L = s.q + 1;
+        s.qwait = s.L;
     }
     double dsm = 0.0;
     for (;;) {
@@ -432,19 +442,20 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
 
     // stop tests after the step (cvode.c:1395-1437)
     const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
-    if (s.tstopset && fabs(s.tn - s.tstop) <= troundoff) {
-        get_dky<NS>(s, s.tstop, yout);
-        s.tretlast = tret = s.tstop;
-        s.tstopset = 0;
-        BDF_PH(9);
-        return CV_TSTOP_RETURN;
-    }
-    if (s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0)) {
+    const bool reached = fabs(s.tn - s.tstop) <= troundoff;
+    if (s.tstopset & (reached | ((s.tn + s.hprime - s.tstop) * s.h > 0.0))) {
+        if (reached) {
+            get_dky<NS>(s, s.tstop, yout);
+            s.tretlast = tret = s.tstop;
+            s.tstopset = 0;
+            BDF_PH(9);
+            return CV_TSTOP_RETURN;
+        }
         s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
         s.eta = fdiv(s.hprime, s.h);
     }
+    // yout = zn[0] on CV_SUCCESS is left to the caller (needed only on its rare path)
     s.tretlast = tret = s.tn;
-    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { yout[CI(i)] = s.zn[0][CI(i)]; });
     BDF_PH(9);
     return CV_SUCCESS;
 }

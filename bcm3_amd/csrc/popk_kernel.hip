@@ -424,6 +424,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                 const bool rare = (result != CV_SUCCESS) | (tret >= next_out) | (t >= end_time) |
                                   (current_step == m.max_steps) | (next_disc == t);
                 if (!rare) continue;
+                if (result == CV_SUCCESS) cfor<0, NS>([&](auto k) __attribute__((always_inline)) { y[CI(k)] = s.zn[0][CI(k)]; });
                 while (tret >= next_out) {
                     double dky[NS];
                     if (get_dky<NS>(s, m.time[tpi], dky) != CV_SUCCESS) {
