@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("BCM3HIP_LIB") or os.path.join(_HERE, "lib", "libbcm3h
 PK_TYPES = {"one": 0, "two": 1, "one_biphasic": 2, "two_biphasic": 3, "one_transit": 4, "two_transit": 5}
 ANALYTIC_BANANA, ANALYTIC_CIRCULAR = 1, 2
 OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES, OPT_TIMING_LOG = 1, 2, 3
+PRIOR_UNIFORM, PRIOR_NORMAL = 0, 1
 
 
 class PopPKModel(C.Structure):
@@ -78,6 +79,12 @@ def lib() -> C.CDLL:
     L.bcm3hip_close.argtypes = [vp]
     L.bcm3hip_set_option.argtypes = [vp, C.c_int, i64]
     L.bcm3hip_num_variables.argtypes = [vp]
+    u64 = C.c_uint64
+    L.bcm3hip_ptmh_propose.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, i64, u64, u64, vp]
+    L.bcm3hip_ptmh_accept.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp, i64,
+                                      u64, u64, vp]
+    L.bcm3hip_pt_exchange_local.argtypes = [C.c_int, C.c_int, i64, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp,
+                                            u64, u64, vp]
     L.bcm3hip_kernel_time_log.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(i64), C.POINTER(C.c_double)]
     L.bcm3hip_eval_batch.argtypes = [vp, sz, sz, vp, vp, vp]
     L.bcm3hip_eval_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
@@ -184,3 +191,27 @@ class Context:
             self.close()
         except Exception:
             pass
+
+
+def _u64(x: int) -> int:
+    return int(x) & ((1 << 64) - 1)
+
+
+def ptmh_propose(C, d, kind, p0, p1, scale, temps, values, prop, lprior_prop, chain0, seed, it, stream=None):
+    """bcm3hip_ptmh_propose on device pointers (ints)."""
+    check(lib().bcm3hip_ptmh_propose(C, d, kind, p0, p1, scale, temps, values, prop, lprior_prop, chain0,
+                                     _u64(seed), _u64(it), stream), "ptmh_propose")
+
+
+def ptmh_accept(C, d, temps, prop, lprior_prop, llh_prop, learning_rate, values, lprior, llh, lpp, accept_out,
+                accepted, chain0, seed, it, stream=None):
+    """bcm3hip_ptmh_accept on device pointers (ints; accept_out / accepted may be None)."""
+    check(lib().bcm3hip_ptmh_accept(C, d, temps, prop, lprior_prop, llh_prop, learning_rate, values, lprior, llh, lpp,
+                                    accept_out, accepted, chain0, _u64(seed), _u64(it), stream), "ptmh_accept")
+
+
+def pt_exchange_local(C, d, g0, start, wrap_local, temps, values, llh, lprior, lpp, acc_mask, accepted, seed, rnd,
+                      stream=None):
+    """bcm3hip_pt_exchange_local on device pointers (ints; acc_mask / accepted may be None)."""
+    check(lib().bcm3hip_pt_exchange_local(C, d, g0, start, int(wrap_local), temps, values, llh, lprior, lpp,
+                                          acc_mask, accepted, _u64(seed), _u64(rnd), stream), "pt_exchange_local")

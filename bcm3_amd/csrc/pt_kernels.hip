@@ -1,0 +1,225 @@
+// pt_kernels.hip -- the sampler side of one PT-MH iteration as three small HIP kernels, so that
+// an iteration is propose -> batched likelihood -> accept -> exchange with everything in HBM and
+// no host round trip:
+//   ptmh_propose_kernel   SamplerPTChain::MutateMove proposal + PriorIndependence::EvaluateLogPDF
+//                         (src/sampler/SamplerPTChain.cpp:217-279, src/sampler/PriorIndependence.cpp:129-157,
+//                          src/sampler/UnivariateMarginal.cpp:326-345)
+//   ptmh_accept_kernel    TestSample + the state update (SamplerPTChain.cpp:280-313, 465-481)
+//   pt_exchange_kernel    SamplerPT::DoExchangeMove / SamplerPTChain::ExchangeMove for the pairs inside
+//                         one rank's slice of the temperature ladder (SamplerPT.cpp:277-298,
+//                         SamplerPTChain.cpp:328-381); pairs that straddle ranks are exchanged by the
+//                         host over RCCL (bcm3_amd/pt.py).
+// Random numbers are counter based (splitmix64 of seed, iteration, chain, slot), so a chain's
+// stream does not depend on how chains are distributed over ranks or blocks.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/bcm3hip.h"
+
+namespace bcm3hip {
+namespace {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// uniform in [0, 1) from 53 random bits
+__device__ __forceinline__ double u01(uint64_t z) { return (double)(z >> 11) * (1.0 / 9007199254740992.0); }
+
+// key for (seed, iteration, chain, slot); slot < 2^16
+__device__ __forceinline__ uint64_t rng_key(uint64_t seed, uint64_t iter, uint64_t chain, uint64_t slot)
+{
+    return splitmix64(splitmix64(seed) ^ (iter * 0x100000001B3ull) ^ (chain * 0xC2B2AE3D27D4EB4Full) ^
+                      (slot * 0x165667B19E3779F9ull));
+}
+
+// standard normal by Box-Muller from two counter-based uniforms
+__device__ __forceinline__ double normal01(uint64_t seed, uint64_t iter, uint64_t chain, uint64_t slot)
+{
+    const double u1 = 1.0 - u01(rng_key(seed, iter, chain, 2 * slot));  // (0, 1]
+    const double u2 = u01(rng_key(seed, iter, chain, 2 * slot + 1));
+    return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+__global__ void ptmh_propose_kernel(int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0,
+                                    const double* __restrict__ p1, const double* __restrict__ scale,
+                                    const double* __restrict__ temps, const double* __restrict__ values,
+                                    double* __restrict__ prop, double* __restrict__ lprior_prop, int64_t chain0,
+                                    uint64_t seed, uint64_t iter)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const uint64_t gc = (uint64_t)(chain0 + c);
+    const bool t0 = temps[c] == 0.0;
+    double lp = 0.0;
+    for (int i = 0; i < d; i++) {
+        double x;
+        if (t0) {
+            // PriorIndependence::Sample: uniform a + u (b - a), normal mu + sigma z
+            if (kind[i] == BCM3HIP_PRIOR_UNIFORM)
+                x = p0[i] + u01(rng_key(seed, iter, gc, 0x8000 + i)) * (p1[i] - p0[i]);
+            else
+                x = p0[i] + p1[i] * normal01(seed, iter, gc, 0x4000 + i);
+        } else {
+            x = values[(int64_t)c * d + i] + scale[i] * normal01(seed, iter, gc, i);
+        }
+        prop[(int64_t)c * d + i] = x;
+        // UnivariateMarginal::EvaluateLogPDF
+        double l;
+        if (kind[i] == BCM3HIP_PRIOR_UNIFORM) {
+            l = (x < p0[i] || x > p1[i]) ? -INFINITY : -log(p1[i] - p0[i]);
+        } else {
+            const double s = p1[i];
+            const double dx = x - p0[i];
+            l = log(1.0 / sqrt(2.0 * s * s * 3.141592653589793)) - dx * dx * (1.0 / (2.0 * s * s));
+        }
+        lp += l;
+    }
+    lprior_prop[c] = lp;
+}
+
+__global__ void ptmh_accept_kernel(int C, int d, const double* __restrict__ temps, const double* __restrict__ prop,
+                                   const double* __restrict__ lprior_prop, const double* __restrict__ llh_prop,
+                                   double learning_rate, double* __restrict__ values, double* __restrict__ lprior,
+                                   double* __restrict__ llh, double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
+                                   unsigned long long* __restrict__ accepted, int64_t chain0, uint64_t seed,
+                                   uint64_t iter)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double T = temps[c];
+    const double nl = llh_prop[c] * learning_rate;  // Sampler::EvaluateLikelihood
+    const double nq = lprior_prop[c];
+    bool acc;
+    double npp;
+    if (T == 0.0) {
+        // sample from the prior, always accepted; 0 * -inf avoided (SamplerPTChain.cpp:231-237)
+        acc = true;
+        npp = (nl == -INFINITY) ? nq : nq + T * nl;
+    } else {
+        npp = nq + T * nl;
+        acc = false;
+        if (npp > -INFINITY) {
+            double tp = exp(npp - lpp[c]);
+            tp = (tp < 1.0) ? tp : 1.0;  // std::min((Real)1.0, tp): NaN -> 1
+            acc = u01(rng_key(seed, iter, (uint64_t)(chain0 + c), 0xC000)) < tp;
+        }
+    }
+    if (acc) {
+        for (int i = 0; i < d; i++) values[(int64_t)c * d + i] = prop[(int64_t)c * d + i];
+        lprior[c] = nq;
+        llh[c] = nl;
+        lpp[c] = npp;
+    }
+    if (acc_out) acc_out[c] = acc ? 1 : 0;
+    if (accepted && acc) atomicAdd(accepted, 1ull);
+}
+
+// one ExchangeMove between local chains i1 and i2 of the slice (global index of i1 = g1)
+__device__ void exchange_pair(int d, int i1, int i2, int64_t g1, const double* temps, double* values, double* llh,
+                              double* lprior, double* lpp, uint8_t* acc_mask, unsigned long long* accepted,
+                              uint64_t seed, uint64_t round)
+{
+    const double t1 = temps[i1], t2 = temps[i2];
+    const double p1 = (t1 == 0.0) ? lprior[i2] : t1 * llh[i2] + lprior[i2];
+    const double p2 = (t2 == 0.0) ? lprior[i1] : t2 * llh[i1] + lprior[i1];
+    double tp = exp((p1 + p2) - (lpp[i1] + lpp[i2]));
+    tp = (tp < 1.0) ? tp : 1.0;  // std::min((Real)1.0, tp): a NaN probability becomes 1
+    // bcm3_amd.pt.exchange_uniform(seed, round, g1)
+    const uint64_t key = splitmix64(splitmix64(seed) ^ (round * 0x100000001B3ull) ^ ((uint64_t)g1 * 0xC2B2AE3D27D4EB4Full));
+    const bool swap = u01(key) < tp;
+    if (swap) {
+        for (int k = 0; k < d; k++) {
+            const double a = values[(int64_t)i1 * d + k];
+            values[(int64_t)i1 * d + k] = values[(int64_t)i2 * d + k];
+            values[(int64_t)i2 * d + k] = a;
+        }
+        const double l = llh[i1];
+        llh[i1] = llh[i2];
+        llh[i2] = l;
+        const double q = lprior[i1];
+        lprior[i1] = lprior[i2];
+        lprior[i2] = q;
+        lpp[i1] = p1;
+        lpp[i2] = p2;
+        if (accepted) atomicAdd(accepted, 1ull);
+    }
+    if (acc_mask) acc_mask[i1] = swap ? 1 : 0;
+}
+
+// local pairs of one round: first chains i (local index) with (g0 + i - start) even and i + 1 < C,
+// then -- single rank only -- the wrap pair (C-1, 0) after them (the reference loops in order)
+__global__ void pt_exchange_kernel(int C, int d, int64_t g0, int start, int wrap_local, const double* temps,
+                                   double* values, double* llh, double* lprior, double* lpp, uint8_t* acc_mask,
+                                   unsigned long long* accepted, uint64_t seed, uint64_t round)
+{
+    const int par = (int)(((g0 - start) % 2 + 2) % 2);  // local i is a first chain iff (i + par) even
+    const int first = par;                              // smallest such i
+    for (int p = threadIdx.x;; p += blockDim.x) {
+        const int i = first + 2 * p;
+        if (i + 1 >= C) break;
+        exchange_pair(d, i, i + 1, g0 + i, temps, values, llh, lprior, lpp, acc_mask, accepted, seed, round);
+    }
+    __syncthreads();
+    if (wrap_local && threadIdx.x == 0) {
+        exchange_pair(d, C - 1, 0, g0 + C - 1, temps, values, llh, lprior, lpp, acc_mask, accepted, seed, round);
+    }
+}
+
+}  // namespace
+}  // namespace bcm3hip
+
+using namespace bcm3hip;
+
+extern "C" {
+
+int bcm3hip_ptmh_propose(int C, int d, const int32_t* prior_kind, const double* prior_p0, const double* prior_p1,
+                         const double* scale, const double* temps, const double* values, double* prop,
+                         double* lprior_prop, int64_t chain0, uint64_t seed, uint64_t iter, void* stream)
+{
+    if (C < 0 || d <= 0 || (C > 0 && (!prior_kind || !prior_p0 || !prior_p1 || !scale || !temps || !values || !prop ||
+                                      !lprior_prop)))
+        return BCM3HIP_ERR_ARG;
+    if (C == 0) return 0;
+    hipLaunchKernelGGL(ptmh_propose_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d, prior_kind,
+                       prior_p0, prior_p1, scale, temps, values, prop, lprior_prop, chain0, seed, iter);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_accept(int C, int d, const double* temps, const double* prop, const double* lprior_prop,
+                        const double* llh_prop, double learning_rate, double* values, double* lprior, double* llh,
+                        double* lpp, uint8_t* accept_out, uint64_t* accepted, int64_t chain0, uint64_t seed,
+                        uint64_t iter, void* stream)
+{
+    if (C < 0 || d <= 0 ||
+        (C > 0 && (!temps || !prop || !lprior_prop || !llh_prop || !values || !lprior || !llh || !lpp)))
+        return BCM3HIP_ERR_ARG;
+    if (C == 0) return 0;
+    hipLaunchKernelGGL(ptmh_accept_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d, temps, prop,
+                       lprior_prop, llh_prop, learning_rate, values, lprior, llh, lpp, accept_out,
+                       (unsigned long long*)accepted, chain0, seed, iter);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_pt_exchange_local(int C, int d, int64_t g0, int start, int wrap_local, const double* temps,
+                              double* values, double* llh, double* lprior, double* lpp, uint8_t* acc_mask,
+                              uint64_t* accepted, uint64_t seed, uint64_t round, void* stream)
+{
+    if (C < 0 || d <= 0 || (start != 0 && start != 1) ||
+        (C > 0 && (!temps || !values || !llh || !lprior || !lpp)))
+        return BCM3HIP_ERR_ARG;
+    if (C < 2 && !wrap_local) return 0;
+    if (C == 0) return 0;
+    hipLaunchKernelGGL(pt_exchange_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, C, d, g0, start, wrap_local,
+                       temps, values, llh, lprior, lpp, acc_mask, (unsigned long long*)accepted, seed, round);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+}  // extern "C"

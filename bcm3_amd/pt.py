@@ -109,7 +109,7 @@ class PTExchange:
         p1 = _proposed(t1, llh2, lp2)
         p2 = _proposed(t2, llh1, lp1)
         tp = torch.exp((p1 + p2) - (lpp1 + lpp2))
-        tp = torch.minimum(torch.ones_like(tp), tp)
+        tp = torch.where(tp < 1.0, tp, torch.ones_like(tp))  # std::min(1.0, tp): NaN -> 1
         u = exchange_uniforms_tensor(self.seed, self.round, pair_idx)
         return u < tp, p1, p2
 

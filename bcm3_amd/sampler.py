@@ -12,9 +12,10 @@ Restates, for the sampler's hot loop only (SURVEY.md §8 a):
   UnivariateMarginal::EvaluateLogPDF uniform / normal (src/sampler/UnivariateMarginal.cpp:326-345).
 
 The reference evaluates the C chains' likelihoods one per task-manager thread; here all C
-proposals go to the GPU in one bcm3_likelihood_evaluate_batch_device launch. The proposal is a
-fixed diagonal Gaussian random walk (the reference's adaptive proposals, src/sampler/Proposal*.cpp,
-are outside the hot-path scope; SURVEY.md §8 f).
+proposals go to the GPU in one bcm3_likelihood_evaluate_batch_device launch, between the
+propose / accept kernels of bcm3_amd/csrc/pt_kernels.hip. The proposal is a fixed diagonal
+Gaussian random walk (the reference's adaptive proposals, src/sampler/Proposal*.cpp, are outside
+the hot-path scope; SURVEY.md §8 f).
 """
 from __future__ import annotations
 
@@ -84,57 +85,99 @@ class DevicePrior:
 
 
 class PTMHDevice:
-    """C chains of one rank: state tensors in HBM, one batched likelihood launch per mutate."""
+    """C chains of one rank, state in HBM; one iteration = exchange kernel (+ RCCL for the pairs
+    that straddle ranks) -> propose kernel -> batched likelihood launch -> accept kernel, all on
+    torch's current stream (include/bcm3hip.h: bcm3hip_pt_exchange_local, bcm3hip_ptmh_propose,
+    bcm3hip_ptmh_accept). No host synchronisation inside an iteration."""
+
+    INIT_ITER = (1 << 63) - 1  # RNG iteration index reserved for the initial prior draw
 
     def __init__(self, likelihood, prior: DevicePrior, temperatures, rank=0, world=1, seed=0, device="cuda",
-                 learning_rate: float = 1.0, exploration_steps: int = 1):
+                 learning_rate: float = 1.0, exploration_steps: int = 1, group=None):
+        from . import _hip
+        self._hip = _hip
+        _hip.lib()  # fails loudly without the HIP library
         self.ll, self.prior = likelihood, prior
         self.dev = torch.device(device)
-        self.ex = PTExchange(temperatures, rank=rank, world=world, seed=seed, device=self.dev)
+        self.ex = PTExchange(temperatures, rank=rank, world=world, seed=seed, device=self.dev, group=group)
         self.C, self.d = self.ex.C, prior.d
+        self.Ctot, self.rank, self.world = self.ex.Ctot, rank, world
+        self.g0 = rank * self.C
         self.T = self.ex.T
-        self.lr = learning_rate
+        self.lr = float(learning_rate)
+        self.seed = int(seed)
         self.exploration_steps = exploration_steps
-        self.gen = torch.Generator(device=self.dev)
-        self.gen.manual_seed(seed * 1000003 + rank)
-        self.values = prior.sample(self.C, self.gen)
-        self.lprior = prior.log_pdf(self.values)
-        self.llh = self._eval(self.values)
-        self.lpp = self.ex.lpowerposterior(self.llh, self.lprior)
-        self.status = torch.zeros(self.C, dtype=torch.int32, device=self.dev)
+        self.iter = 0
+        self.round = 0
+        C, d, dev = self.C, self.d, self.dev
+        self.kind = torch.where(prior.is_uniform, 0, 1).to(torch.int32)
+        self.p0 = torch.where(prior.is_uniform, prior.a, prior.mu).contiguous()
+        self.p1 = torch.where(prior.is_uniform, prior.b, prior.sigma).contiguous()
+        self.scale = prior.scale.contiguous()
+        self.values = torch.empty((C, d), dtype=torch.float64, device=dev)
+        self.prop = torch.empty((C, d), dtype=torch.float64, device=dev)
+        self.lprior = torch.empty(C, dtype=torch.float64, device=dev)
+        self.lprior_prop = torch.empty(C, dtype=torch.float64, device=dev)
+        self.llh = torch.empty(C, dtype=torch.float64, device=dev)
+        self.llh_prop = torch.empty(C, dtype=torch.float64, device=dev)
+        self.status = torch.empty(C, dtype=torch.int32, device=dev)
+        self.lpp = torch.empty(C, dtype=torch.float64, device=dev)
+        self.accepted_mutate = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.accepted_exchange = torch.zeros(1, dtype=torch.int64, device=dev)
         self.attempted_mutate = 0
-        self.accepted_mutate = torch.zeros((), dtype=torch.int64, device=self.dev)
+        self.attempted_exchange = 0
+        # initial state: every chain draws from the prior (the propose kernel at T = 0)
+        zeros = torch.zeros(C, dtype=torch.float64, device=dev)
+        _hip.ptmh_propose(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(), self.scale.data_ptr(),
+                          zeros.data_ptr(), self.values.data_ptr(), self.values.data_ptr(), self.lprior.data_ptr(),
+                          self.g0, self.seed, self.INIT_ITER, self._stream())
+        self._eval(self.values, self.llh)
+        self.llh.mul_(self.lr)
+        self.lpp.copy_(self.ex.lpowerposterior(self.llh, self.lprior))
 
-    def _eval(self, x: torch.Tensor) -> torch.Tensor:
-        x = x.contiguous()
-        out = torch.empty(x.shape[0], dtype=torch.float64, device=self.dev)
-        status = torch.empty(x.shape[0], dtype=torch.int32, device=self.dev)
-        stream = torch.cuda.current_stream(self.dev).cuda_stream if self.dev.type == "cuda" else None
-        self.ll.evaluate_batch_device(x.shape[0], x.data_ptr(), out.data_ptr(), status.data_ptr(), stream)
-        return out * self.lr if self.lr != 1.0 else out
+    def _stream(self):
+        return torch.cuda.current_stream(self.dev).cuda_stream
+
+    def _eval(self, x: torch.Tensor, out: torch.Tensor):
+        self.ll.evaluate_batch_device(self.C, x.data_ptr(), out.data_ptr(), self.status.data_ptr(), self._stream())
+
+    def exchange(self):
+        """DoExchangeMove round (SamplerPT.cpp:277-298): local pairs on the GPU, boundary pairs
+        over RCCL point-to-point."""
+        if self.Ctot < 2:
+            return
+        start = self.round % 2
+        wrap_local = self.world == 1 and (self.Ctot - 1 - start) % 2 == 0
+        self._hip.pt_exchange_local(self.C, self.d, self.g0, start, wrap_local, self.T.data_ptr(),
+                                    self.values.data_ptr(), self.llh.data_ptr(), self.lprior.data_ptr(),
+                                    self.lpp.data_ptr(), None, self.accepted_exchange.data_ptr(), self.seed,
+                                    self.round, self._stream())
+        n_local = sum(1 for i in range(self.C - 1) if (self.g0 + i - start) % 2 == 0) + int(wrap_local)
+        self.attempted_exchange += n_local
+        if self.world > 1 and (self.g0 + self.C - 1 - start) % 2 == 0:
+            acc = torch.zeros(self.C, dtype=torch.bool, device=self.dev)
+            self.ex.round = self.round
+            self.ex._cross(self.values, self.llh, self.lprior, self.lpp, acc)
+            self.accepted_exchange += acc[self.C - 1:].to(torch.int64)
+            self.attempted_exchange += 1
+        self.round += 1
 
     def mutate(self):
-        C = self.C
-        t0 = self.T == 0.0
-        step = torch.randn((C, self.d), dtype=torch.float64, device=self.dev, generator=self.gen) * self.prior.scale
-        prop = torch.where(t0[:, None], self.prior.sample(C, self.gen), self.values + step)
-        new_lprior = self.prior.log_pdf(prop)
-        new_llh = self._eval(prop)
-        # T == 0: lpp = lprior (also when llh == -inf, .cpp:231-237); T > 0: lprior + T * llh (.cpp:284)
-        new_lpp = torch.where(t0, new_lprior, new_lprior + self.T * new_llh)
-        u = torch.rand(C, dtype=torch.float64, device=self.dev, generator=self.gen)
-        tp = torch.clamp(torch.exp(new_lpp - self.lpp), max=1.0)
-        accept = t0 | ((new_lpp > -math.inf) & (u < tp))
-        self.values = torch.where(accept[:, None], prop, self.values)
-        self.lprior = torch.where(accept, new_lprior, self.lprior)
-        self.llh = torch.where(accept, new_llh, self.llh)
-        self.lpp = torch.where(accept, new_lpp, self.lpp)
+        """DoMutateMove (SamplerPT.cpp:308-319): all chains' proposals in one likelihood launch."""
+        h, C, d, st = self._hip, self.C, self.d, self._stream()
+        h.ptmh_propose(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(), self.scale.data_ptr(),
+                       self.T.data_ptr(), self.values.data_ptr(), self.prop.data_ptr(), self.lprior_prop.data_ptr(),
+                       self.g0, self.seed, self.iter, st)
+        self._eval(self.prop, self.llh_prop)
+        h.ptmh_accept(C, d, self.T.data_ptr(), self.prop.data_ptr(), self.lprior_prop.data_ptr(),
+                      self.llh_prop.data_ptr(), self.lr, self.values.data_ptr(), self.lprior.data_ptr(),
+                      self.llh.data_ptr(), self.lpp.data_ptr(), None, self.accepted_mutate.data_ptr(), self.g0,
+                      self.seed, self.iter, st)
         self.attempted_mutate += C
-        self.accepted_mutate += accept.sum()
+        self.iter += 1
 
     def iteration(self):
         """One DeterministicEvenOdd iteration (SamplerPT.cpp:203-212)."""
-        if self.ex.Ctot > 1:
-            self.ex.step(self.values, self.llh, self.lprior, self.lpp)
+        self.exchange()
         for _ in range(self.exploration_steps):
             self.mutate()

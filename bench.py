@@ -174,7 +174,9 @@ def main():
     if rank == 0 and args.throughput_batch > 0:
         # extra (not the headline): one large batch of proposals, to show the chip-filling rate
         n = args.throughput_batch
-        x = prior.sample(n, loop.gen).contiguous()
+        gen = torch.Generator(device=device)
+        gen.manual_seed(args.seed + 1)
+        x = prior.sample(n, gen).contiguous()
         out = torch.empty(n, dtype=torch.float64, device=device)
         stream = torch.cuda.current_stream(device).cuda_stream
         ll.evaluate_batch_device(n, x.data_ptr(), out.data_ptr(), None, stream)

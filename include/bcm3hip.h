@@ -145,6 +145,30 @@ int bcm3hip_last_kernel_ms(bcm3hip_ctx* ctx, float* ms);
  * the number of launches, then clears the log. Lets a timed loop run without host syncs. */
 int bcm3hip_kernel_time_log(bcm3hip_ctx* ctx, double* total_ms, int64_t* launches, double* max_ms);
 
+/* ---- PT-MH iteration kernels (device buffers, asynchronous on `stream`, current device) ----
+ * One sampler iteration of C chains of d variables = bcm3hip_pt_exchange_local (+ cross-rank
+ * pairs on the host over RCCL), then bcm3hip_ptmh_propose -> bcm3hip_eval_batch_device ->
+ * bcm3hip_ptmh_accept. Random numbers are counter based: splitmix64 of (seed, iter, global chain
+ * index chain0 + c, slot). Replaces SamplerPT::DoMutateMove / DoExchangeMove's per-chain loops
+ * (src/sampler/SamplerPT.cpp:277-319, src/sampler/SamplerPTChain.cpp:217-381). */
+enum { BCM3HIP_PRIOR_UNIFORM = 0, BCM3HIP_PRIOR_NORMAL = 1 };
+/* prior_kind[d], prior_p0[d] (lower | mu), prior_p1[d] (upper | sigma), scale[d] random-walk sd,
+ * temps[C], values[C*d] -> prop[C*d], lprior_prop[C]. T == 0 chains draw from the prior. */
+int bcm3hip_ptmh_propose(int C, int d, const int32_t* prior_kind, const double* prior_p0, const double* prior_p1,
+                         const double* scale, const double* temps, const double* values, double* prop,
+                         double* lprior_prop, int64_t chain0, uint64_t seed, uint64_t iter, void* stream);
+/* TestSample + state update with llh_prop from the likelihood launch (times learning_rate);
+ * accept_out[C] (may be NULL), *accepted += number accepted (may be NULL). */
+int bcm3hip_ptmh_accept(int C, int d, const double* temps, const double* prop, const double* lprior_prop,
+                        const double* llh_prop, double learning_rate, double* values, double* lprior, double* llh,
+                        double* lpp, uint8_t* accept_out, uint64_t* accepted, int64_t chain0, uint64_t seed,
+                        uint64_t iter, void* stream);
+/* Exchange round `round` (start = round % 2) for the pairs inside chains [g0, g0+C) of the ladder;
+ * wrap_local: also the pair (C-1, 0) (single-rank ladder). acc_mask[C] marks accepted first chains. */
+int bcm3hip_pt_exchange_local(int C, int d, int64_t g0, int start, int wrap_local, const double* temps,
+                              double* values, double* llh, double* lprior, double* lpp, uint8_t* acc_mask,
+                              uint64_t* accepted, uint64_t seed, uint64_t round, void* stream);
+
 /* Parity/diagnostic batch (host buffers, any output may be NULL):
  * patient_llh[n*P], traj[n*P*N*T] (states at output times, NaN where not simulated),
  * stats[n*P]. PopPK contexts only. */

@@ -27,12 +27,12 @@ def exchange_round(chains, temps, rnd, seed, uniform):
         p1 = c2["lprior"] if t1 == 0.0 else t1 * c2["llh"] + c2["lprior"]
         p2 = c1["lprior"] if t2 == 0.0 else t2 * c1["llh"] + c1["lprior"]
         x = (p1 + p2) - (c1["lpp"] + c2["lpp"])
-        if math.isnan(x):
-            tp = float("nan")
-        elif x >= 0.0:
+        # tp = std::min((Real)1.0, exp(x)) == (exp(x) < 1 ? exp(x) : 1): a NaN x gives 1
+        if math.isnan(x) or x >= 0.0:
             tp = 1.0
         else:
-            tp = min(1.0, math.exp(x))
+            tp = math.exp(x)
+            tp = tp if tp < 1.0 else 1.0
         alpha = uniform(seed, rnd, ci)
         acc = alpha < tp
         if acc:
