@@ -38,7 +38,7 @@ BDF_INL void predict_q(S& s)
 {
     s.tn += s.h;
     const double tc = s.tstop;
-    s.tn = (s.tstopset && (s.tn - tc) * s.h > 0.0) ? tc : s.tn;
+    s.tn = ((s.tstopset != 0) & ((s.tn - tc) * s.h > 0.0)) ? tc : s.tn;
     cfor<1, Q + 1>([&](auto k) __attribute__((always_inline)) {
         cfor_down<Q, CI(k)>([&](auto j) __attribute__((always_inline)) {
             cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
@@ -144,8 +144,8 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
         if (callSetup) {
             if (jbad) convfail = CONV_BAD_J;
             const double dgamma = fabs(fdiv(s.gamma, s.gammap) - 1.0);
-            const bool jnew = (s.nst == 0) || (s.nst > s.nstlj + CVLS_MSBJ) ||
-                              ((convfail == CONV_BAD_J) && (dgamma < CVLS_DGMAX)) || (convfail == CONV_OTHER);
+            const bool jnew = (s.nst == 0) | (s.nst > s.nstlj + CVLS_MSBJ) |
+                              ((convfail == CONV_BAD_J) & (dgamma < CVLS_DGMAX)) | (convfail == CONV_OTHER);
             s.cnt.nje += jnew ? 1 : 0;
             s.nstlj = jnew ? s.nst : s.nstlj;
             mdl.lin_setup(s.gamma, s.inv);
@@ -181,7 +181,7 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
             s.nls_jcur = 0;
             return true;
         }
-        bool fail = (curiter >= 1) && (del > RDIV * s.delp);
+        bool fail = (curiter >= 1) & (del > RDIV * s.delp);
         if (!fail) {
             s.delp = del;
             curiter++;
@@ -211,14 +211,14 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
     BDF_PH(3);
     const double rl1 = set_bdf_q<Q>(s);
     BDF_PH(4);
-    const int convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
-    const bool callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (s.nst == 0) ||
-                           (s.nst >= s.nstlp + MSBP) || (fabs(s.gamrat - 1.0) > DGMAX);
+    const int convfail = ((nflag == FIRST_CALL) | (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
+    const bool callSetup = (nflag == PREV_CONV_FAIL) | (nflag == PREV_ERR_FAIL) | (s.nst == 0) |
+                           (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);
     cfor<0, NS>([&](auto I_) __attribute__((always_inline)) { s.acor[CI(I_)] = 0.0; });
     const bool conv = newton_u<NS>(s, mdl, rl1, convfail, callSetup);
     BDF_PH(5);
     dsm = s.acnrm * s.tq[2];
-    if (conv && dsm <= 1.0) return ATTEMPT_OK;
+    if (conv & (dsm <= 1.0)) return ATTEMPT_OK;
     restore_q<Q, NS>(s, saved_t);
     return conv ? ATTEMPT_ERR_FAIL : ATTEMPT_CONV_FAIL;
 }
@@ -316,8 +316,8 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         const bool first = (s.nst == 0);
         const bool ret_prev = fabs(s.tn - s.tretlast) > troundoff;
-        const bool at_stop = s.tstopset && (fabs(s.tn - s.tstop) <= troundoff);
-        const bool clamp = s.tstopset && ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
+        const bool at_stop = (s.tstopset != 0) & (fabs(s.tn - s.tstop) <= troundoff);
+        const bool clamp = (s.tstopset != 0) & ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
         if (first | ret_prev | at_stop | clamp) {
             if (first) {
                 s.tretlast = tret = s.tn;
@@ -443,7 +443,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
     // stop tests after the step (cvode.c:1395-1437)
     const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
     const bool reached = fabs(s.tn - s.tstop) <= troundoff;
-    if (s.tstopset & (reached | ((s.tn + s.hprime - s.tstop) * s.h > 0.0))) {
+    if ((s.tstopset != 0) & (reached | ((s.tn + s.hprime - s.tstop) * s.h > 0.0))) {
         if (reached) {
             get_dky<NS>(s, s.tstop, yout);
             s.tretlast = tret = s.tstop;
