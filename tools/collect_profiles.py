@@ -1,0 +1,48 @@
+"""Copy the round-end evidence from gpurun_out/<tag> into profiles/ (tracked).
+
+    python tools/collect_profiles.py r01
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    src = os.path.join(ROOT, "gpurun_out", tag)
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    copies = {
+        os.path.join(src, "kt", "kt_kernel_stats.csv"): f"{tag}_kernel_stats.csv",
+        os.path.join(src, "bench.json"): f"{tag}_bench.json",
+        os.path.join(src, "ubench_lat.txt"): f"{tag}_ubench_lat.txt",
+        os.path.join(src, "ubench_branch.txt"): f"{tag}_ubench_branch.txt",
+        os.path.join(src, "probe.log"): f"{tag}_lpw_sweep.txt",
+        os.path.join(src, "pytest_gpu.log"): f"{tag}_pytest_gpu.log",
+    }
+    for a, b in copies.items():
+        if os.path.exists(a):
+            shutil.copy(a, os.path.join(dst, b))
+            print("copied", b)
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), src, dst, tag, "256"], check=True,
+                   stdout=subprocess.DEVNULL)
+    # second SQ pass
+    import collections
+    import csv
+    p = os.path.join(src, "pmc_sq2", "pmc_counter_collection.csv")
+    if os.path.exists(p):
+        agg = collections.defaultdict(list)
+        for r in csv.DictReader(open(p)):
+            if "popk_traj_kernel" in r["Kernel_Name"]:
+                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        with open(os.path.join(dst, f"{tag}_pmc_sq2.json"), "w") as f:
+            json.dump({k: sum(v) / len(v) for k, v in agg.items()}, f, indent=1)
+        print("wrote", f"{tag}_pmc_sq2.json")
+
+
+if __name__ == "__main__":
+    main()
