@@ -259,13 +259,14 @@ static int ensure_traj_scratch(bcm3hip_ctx* c, size_t n)
     return 0;
 }
 
-// Measured on MI355X (profiles/r01_lpw_sweep.txt): the lane kernel runs best with about one
-// wavefront per CU -- a second wave on the same CU competes for the instruction cache -- so pack
-// trajectories into lanes only once there are more of them than CUs.
+// Measured on MI355X (profiles/r01_lpw_sweep.txt): one trajectory per wavefront (the UNI
+// solver) is fastest up to ~4k trajectories (16 waves per CU); beyond that packing 16+
+// trajectories per wavefront (lane solver, ~1k wavefronts in flight) gives the highest rate.
 static int auto_lanes_per_wave(size_t ntraj)
 {
-    int lpw = 1;
-    while (lpw < 64 && ntraj > (size_t)lpw * 256) lpw *= 2;
+    if (ntraj <= 4608) return 1;
+    int lpw = 16;
+    while (lpw < 64 && ntraj > (size_t)lpw * 1024) lpw *= 2;
     return lpw;
 }
 

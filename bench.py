@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--throughput-batch", type=int, default=16384,
                     help="extra: evals/s of one large batch (0 = skip); not the headline value")
+    ap.add_argument("--extras", type=int, default=1, help="extra: P=64 and circular workloads (0 = skip)")
     return ap.parse_args()
 
 
@@ -112,6 +113,43 @@ def cpu_baseline(budget_s: float, seed: int):
     return {"value": n / el, "unit": "log-likelihood evals/sec", "cores": cores, "kind": kind,
             "sample": f"{n} uniform prior draws of the C3 PopPK problem in batches of {batch}, "
                       f"{cores} threads, {el:.1f} s ({'oracle/_ref/libbcm3ref.so: reference CVODE 5.3.0 sources' if kind == 'reference' else 'oracle/liboracle.so restatement'})"}
+
+
+def _rate(ll, n, x, device, reps=3):
+    import torch
+    from bcm3_amd import _hip
+    out = torch.empty(n, dtype=torch.float64, device=device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    ll.evaluate_batch_device(n, x.data_ptr(), out.data_ptr(), None, stream)
+    torch.cuda.synchronize()
+    ll.set_option(_hip.OPT_TIMING_LOG, 1)
+    for _ in range(reps):
+        ll.evaluate_batch_device(n, x.data_ptr(), out.data_ptr(), None, stream)
+    tt, nl, _ = ll.kernel_time_log()
+    ll.set_option(_hip.OPT_TIMING_LOG, 0)
+    return tt / nl
+
+
+def extra_workloads(device, seed):
+    """Secondary lines (not the headline): the P=64 population variant of C3 (256 chains x 64
+    patient trajectories per launch) and config C2 (circular ridge, 256 chains)."""
+    import torch
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.sampler import DevicePrior, load_prior
+    out = {}
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed + 2)
+    for name, tag, n in (("p64", "popk_p64_256chains", 256), ("circular", "circular_256chains", 256)):
+        lik, pri = os.path.join(GOLDEN, f"{name}_likelihood.xml"), os.path.join(GOLDEN, f"{name}_prior.xml")
+        ll = Likelihood(lik, pri, device=device.index or 0)
+        x = DevicePrior(load_prior(pri), device).sample(n, gen).contiguous()
+        ms = _rate(ll, n, x, device)
+        rec = {"chains": n, "kernel_ms": ms, "evals_per_s": n / (ms * 1e-3)}
+        if name == "p64":
+            rec["trajectories_per_s"] = 64 * n / (ms * 1e-3)
+        out[tag] = rec
+        ll.close()
+    return out
 
 
 def main():
@@ -188,6 +226,9 @@ def main():
         tt, nl, _ = ll.kernel_time_log()
         ll.set_option(_hip.OPT_TIMING_LOG, 0)
         extra["throughput_batch"] = {"n": n, "kernel_ms": tt / nl, "evals_per_s": n / (tt / nl * 1e-3)}
+
+    if rank == 0 and args.extras:
+        extra.update(extra_workloads(device, args.seed))
 
     if world > 1:
         dist.barrier()
