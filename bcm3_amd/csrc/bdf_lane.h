@@ -259,6 +259,7 @@ struct BdfState {
 #ifdef BCM3_PHASES
     long long ph[NPHASES];
     long long tlast;
+    int qh[QMAX + 1];  // successful steps per order
 #endif
 };
 

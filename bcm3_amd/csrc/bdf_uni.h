@@ -301,6 +301,9 @@ BDF_INL int step_q(S& s, const Model& mdl, double eta_eff, double saved_t, int n
 {
     const int r = attempt_q<Q, NS>(s, mdl, eta_eff, saved_t, nflag, dsm);
     if (r == ATTEMPT_OK) complete_q<Q, NS>(s, dsm);
+#ifdef BCM3_PHASES
+    if (r == ATTEMPT_OK) s.qh[Q]++;
+#endif
     return r;
 }
 

@@ -349,6 +349,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     s.nst = 0;
 #ifdef BCM3_PHASES
     cfor<0, NPHASES>([&](auto k) __attribute__((always_inline)) { s.ph[CI(k)] = 0; });
+    cfor<0, QMAX + 1>([&](auto k) __attribute__((always_inline)) { s.qh[CI(k)] = 0; });
     s.tlast = clock64();
 #endif
 
@@ -485,6 +486,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
 
 #ifdef BCM3_PHASES
     if (tro) cfor<0, NPHASES>([&](auto k) __attribute__((always_inline)) { tro[CI(k)] = (double)s.ph[CI(k)]; });
+    if (tro) cfor<1, QMAX + 1>([&](auto k) __attribute__((always_inline)) { tro[NPHASES + CI(k) - 1] = (double)s.qh[CI(k)]; });
 #endif
     if (logp_direct) logp_direct[e] = 0.0 + llh;  // P == 1: logp = 0 + patient term
     if (patient_llh) patient_llh[g] = llh;

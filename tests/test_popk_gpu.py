@@ -78,7 +78,8 @@ def test_p64_population(orc):
                                      "two_transit"])
 @pytest.mark.parametrize("rule", ["daily", "intermittent1", "intermittent2", "intermittent3", "skipped",
                                   "dose_change", "interval12"])
-def test_all_models_and_dosing_rules(orc, pk_type, rule):
+@pytest.mark.parametrize("lpw", [64, 1])
+def test_all_models_and_dosing_rules(orc, pk_type, rule, lpw):
     kw = dict(P=2, T_days=6)
     if rule.startswith("intermittent"):
         kw["intermittent"] = int(rule[-1])
@@ -90,7 +91,7 @@ def test_all_models_and_dosing_rules(orc, pk_type, rule):
     elif rule == "interval12":
         kw["interval"] = 12.0
     prob, lo, hi = H.make_problem(pk_type, **kw)
-    ctx = H.gpu_context(prob)
+    ctx = H.gpu_context(prob, lanes_per_wave=lpw)  # lane solver and one-trajectory-per-wave solver
     vals = H.draws(lo, hi, 256, 91)
     g = ctx.eval(vals, detail=True)
     o = orc.popk_eval(prob, vals, nthreads=8)

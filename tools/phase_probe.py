@@ -38,6 +38,8 @@ def main():
     for k, name in enumerate(NAMES):
         print(f"  {name:24s} {per[k]:8.0f}  {100 * per[k] / per.sum():5.1f}%")
     print("stats means:", {k: float(g["stats"][k].mean()) for k in g["stats"].dtype.names})
+    qh = g["traj"].reshape(n, -1)[:, len(NAMES):len(NAMES) + 5].sum(axis=0)
+    print("successful steps by order q=1..5 (UNI solver):", (qh / qh.sum()).round(3).tolist())
 
 
 if __name__ == "__main__":
