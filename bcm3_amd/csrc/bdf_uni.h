@@ -120,75 +120,88 @@ BDF_INL double set_bdf_q(S& s)
     return rl1;
 }
 
-// Newton iteration (bdf_lane.h newton) with the gamrat scaling as a select.
+// One Newton correction (residual, optional setup, solve, update): the body shared by the
+// first and the later iterations of newton_u.
+template <int NS, class S, class Model>
+BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& cscale, bool setup, bool jbad,
+                                 int convfail)
+{
+    double y[NS], f[NS], delta[NS];
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = CI(I_);
+        y[i] = s.zn[0][i] + s.acor[i];
+    });
+    mdl.rhs(s.tn, y, f);
+    s.cnt.nfe++;
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = CI(I_);
+        delta[i] = __builtin_fma(rl1, s.zn[1][i], s.acor[i]);
+        delta[i] = __builtin_fma(-s.gamma, f[i], delta[i]);
+    });
+    if (setup) {
+        // cvNlsLSetup -> cvLsSetup (cvode_ls.c:1415-1500)
+        if (jbad) convfail = CONV_BAD_J;
+        const double dgamma = fabs(fdiv(s.gamma, s.gammap) - 1.0);
+        const bool jnew = (s.nst == 0) | (s.nst > s.nstlj + CVLS_MSBJ) |
+                          ((convfail == CONV_BAD_J) & (dgamma < CVLS_DGMAX)) | (convfail == CONV_OTHER);
+        s.cnt.nje += jnew ? 1 : 0;
+        s.nstlj = jnew ? s.nst : s.nstlj;
+        mdl.lin_setup(s.gamma, s.inv);
+        s.cnt.nsetups++;
+        s.nls_jcur = jnew;
+        s.gamrat = 1.0;
+        cscale = 1.0;
+        s.gammap = s.gamma;
+        s.crate = 1.0;
+        s.nstlp = s.nst;
+    }
+    s.cnt.nni++;
+    double b[NS], x[NS];
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = CI(I_);
+        b[i] = -delta[i];
+    });
+    mdl.lin_solve(s.inv, b, x);
+    cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
+        constexpr int i = CI(I_);
+        x[i] *= cscale;
+        s.acor[i] += x[i];
+    });
+    return wrms<NS>(x, s.ewt);
+}
+
+// Newton iteration of cvNls (bdf_lane.h newton; sunnonlinsol_newton.c:183-322, cvNlsConvTest
+// cvode_nls.c:236-280) with the first iteration peeled: ~70 % of the steps converge there, and
+// it needs neither the convergence-rate update nor the divergence test.
 template <int NS, class S, class Model>
 BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool callSetup)
 {
     bool jbad = false;
     // 2/(1+gamrat) scaling of cvLsSolve: constant within the solve, 1 after a setup
     double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
-    int curiter = 0;
     for (;;) {
-        double y[NS], f[NS], delta[NS];
-        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
-            constexpr int i = CI(I_);
-            y[i] = s.zn[0][i] + s.acor[i];
-        });
-        mdl.rhs(s.tn, y, f);
-        s.cnt.nfe++;
-        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
-            constexpr int i = CI(I_);
-            delta[i] = __builtin_fma(rl1, s.zn[1][i], s.acor[i]);
-            delta[i] = __builtin_fma(-s.gamma, f[i], delta[i]);
-        });
-        if (callSetup) {
-            if (jbad) convfail = CONV_BAD_J;
-            const double dgamma = fabs(fdiv(s.gamma, s.gammap) - 1.0);
-            const bool jnew = (s.nst == 0) | (s.nst > s.nstlj + CVLS_MSBJ) |
-                              ((convfail == CONV_BAD_J) & (dgamma < CVLS_DGMAX)) | (convfail == CONV_OTHER);
-            s.cnt.nje += jnew ? 1 : 0;
-            s.nstlj = jnew ? s.nst : s.nstlj;
-            mdl.lin_setup(s.gamma, s.inv);
-            s.cnt.nsetups++;
-            s.nls_jcur = jnew;
-            s.gamrat = 1.0;
-            cscale = 1.0;
-            s.gammap = s.gamma;
-            s.crate = 1.0;
-            s.nstlp = s.nst;
-            callSetup = false;
-            curiter = 0;
-        }
-        s.cnt.nni++;
-        double b[NS], x[NS];
-        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
-            constexpr int i = CI(I_);
-            b[i] = -delta[i];
-        });
-        mdl.lin_solve(s.inv, b, x);
-        const double c = cscale;
-        cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
-            constexpr int i = CI(I_);
-            x[i] *= c;
-            s.acor[i] += x[i];
-        });
-        const double del = wrms<NS>(x, s.ewt);
-        const double cr = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
-        s.crate = (curiter > 0) ? cr : s.crate;
+        // iteration 0 (crate as left by the previous step)
+        double del = newton_correction<NS>(s, mdl, rl1, cscale, callSetup, jbad, convfail);
         // cvNlsConvTest: dcon = del min(1, crate) / tol <= 1 with tol = CORTES / tq[2]
         if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
-            s.acnrm = (curiter == 0) ? del : wrms<NS>(s.acor, s.ewt);
+            s.acnrm = del;
             s.nls_jcur = 0;
             return true;
         }
-        bool fail = (curiter >= 1) & (del > RDIV * s.delp);
-        if (!fail) {
+        s.delp = del;
+        // iterations 1 .. NLS_MAXCOR-1
+        for (int it = 1; it < NLS_MAXCOR; it++) {
+            del = newton_correction<NS>(s, mdl, rl1, cscale, false, false, convfail);
+            s.crate = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
+            if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
+                s.acnrm = wrms<NS>(s.acor, s.ewt);
+                s.nls_jcur = 0;
+                return true;
+            }
+            if (del > RDIV * s.delp) break;  // diverging
             s.delp = del;
-            curiter++;
-            fail = (curiter >= NLS_MAXCOR);
-            if (!fail) continue;
         }
-        if (!s.nls_jcur) {
+        if (!s.nls_jcur) {  // retry once with a fresh Jacobian (jbad)
             callSetup = true;
             jbad = true;
             cfor<0, NS>([&](auto I_) __attribute__((always_inline)) { s.acor[CI(I_)] = 0.0; });
