@@ -90,26 +90,28 @@ BDF_INL double set_bdf_q(S& s)
     const double lq = s.l[q];
     s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
     // tq[5] is read only in the two steps after this one when qwait is 2 or 1 here
-    // (saved_tq5 at qwait == 1, etaqp1 at qwait == 0)
-    if (s.qwait <= 2) s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
-    if (s.qwait == 1) {
-        // qwait == 1 block of cvSetTqBDF
-        double tq1 = 1.0;
-        if constexpr (q > 1) {
-            const double C = fdiv(xistar_inv, lq);
-            const double A3 = alpha0 + 1.0 / q;
-            const double A4 = alpha0_hat + xi_inv;
-            const double Cpinv = fdiv(1.0 - A4 + A3, A3);
-            tq1 = fabs(C * Cpinv);
+    // (saved_tq5 at qwait == 1, etaqp1 at qwait == 0); tq[1], tq[3] only at qwait == 1
+    if (s.qwait <= 2) {
+        s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
+        if (s.qwait == 1) {
+            // qwait == 1 block of cvSetTqBDF
+            double tq1 = 1.0;
+            if constexpr (q > 1) {
+                const double C = fdiv(xistar_inv, lq);
+                const double A3 = alpha0 + 1.0 / q;
+                const double A4 = alpha0_hat + xi_inv;
+                const double Cpinv = fdiv(1.0 - A4 + A3, A3);
+                tq1 = fabs(C * Cpinv);
+            }
+            const double hsum2 = hsum + s.tau[q];
+            const double xi_inv2 = fdiv(s.h, hsum2);
+            const double A5 = alpha0 - 1.0 / (q + 1);
+            const double A6 = alpha0_hat - xi_inv2;
+            const double Cppinv = fdiv(1.0 - A6 + A5, A2);
+            const double tq3 = fabs(fdiv(Cppinv, xi_inv2 * (double)(q + 2) * A5));
+            s.tq[1] = tq1;
+            s.tq[3] = tq3;
         }
-        const double hsum2 = hsum + s.tau[q];
-        const double xi_inv2 = fdiv(s.h, hsum2);
-        const double A5 = alpha0 - 1.0 / (q + 1);
-        const double A6 = alpha0_hat - xi_inv2;
-        const double Cppinv = fdiv(1.0 - A6 + A5, A2);
-        const double tq3 = fabs(fdiv(Cppinv, xi_inv2 * (double)(q + 2) * A5));
-        s.tq[1] = tq1;
-        s.tq[3] = tq3;
     }
     // tq[4] = CORTES / tq[2] only serves as the Newton tolerance (folded into the test there)
     const double rl1 = frcp(s.l[1]);
@@ -118,6 +120,24 @@ BDF_INL double set_bdf_q(S& s)
     const double gr = fdiv(s.gamma, s.gammap);
     s.gamrat = (s.nst > 0) ? gr : 1.0;
     return rl1;
+}
+
+// eta_from of bdf_lane.h (same operations) with the range check as one scalar branch
+BDF_INL double eta_from_u(double bx, int k)
+{
+    if (!((bx > 1e-30) & (bx < 1e30))) return frcp((bx > 0.0 ? pow(bx, recip_int(k)) : 0.0) + ADDON);
+    const double rk = recip_int(k);
+    const float lf = __builtin_amdgcn_logf((float)bx);
+    double z = (double)__builtin_amdgcn_exp2f(-lf * (float)rk);
+    cfor<0, 2>([&](auto) __attribute__((always_inline)) {
+        double zk = z;
+        cfor<2, 8>([&](auto I) __attribute__((always_inline)) {
+            if (CI(I) <= k) zk *= z;
+        });
+        const double t = __builtin_fma(-bx, zk, 1.0);
+        z = __builtin_fma(z * t, rk, z);
+    });
+    return fdiv(z, __builtin_fma(ADDON, z, 1.0));
 }
 
 // One Newton correction (residual, optional setup, solve, update): the body shared by the
@@ -266,14 +286,14 @@ BDF_INL void complete_q(S& s, double dsm)
         s.hprime = s.h;
         s.eta = 1.0;
     } else {
-        const double etaq = eta_from(BIAS2 * dsm, q + 1);
+        const double etaq = eta_from_u(BIAS2 * dsm, q + 1);
         double eta = etaq;
         s.qprime = q;
         if (s.qwait == 0) {
             // cvComputeEtaqm1 / cvComputeEtaqp1 / cvChooseEta, every q+1 steps
             s.qwait = 2;
             double etaqm1 = 0.0, etaqp1 = 0.0;
-            if constexpr (q > 1) etaqm1 = eta_from(BIAS1 * wrms<NS>(s.zn[q], s.ewt) * s.tq[1], q);
+            if constexpr (q > 1) etaqm1 = eta_from_u(BIAS1 * wrms<NS>(s.zn[q], s.ewt) * s.tq[1], q);
             if constexpr (q != QMAX) {
                 if (s.saved_tq5 != 0.0) {
                     const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
@@ -281,7 +301,7 @@ BDF_INL void complete_q(S& s, double dsm)
                     cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
                         tv[CI(i)] = __builtin_fma(-cquot, s.zn[QMAX][CI(i)], s.acor[CI(i)]);
                     });
-                    etaqp1 = eta_from(BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3], q + 2);
+                    etaqp1 = eta_from_u(BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3], q + 2);
                 }
             }
             const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
