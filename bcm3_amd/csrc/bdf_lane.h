@@ -266,10 +266,12 @@ struct BdfState {
 template <int NS>
 BDF_INL double wrms(const double (&x)[NS], const double (&w)[NS])
 {
+    // sum of rounded squares in component order (the lane-vector solver sums the same way)
     double s = 0.0;
     cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
-        double p = x[CI(i)] * w[CI(i)];
-        s = __builtin_fma(p, p, s);
+        const double p = x[CI(i)] * w[CI(i)];
+        const double p2 = p * p;
+        s = (CI(i) == 0) ? p2 : s + p2;
     });
     return fsqrt(fdiv_c(s, (double)NS, 1.0 / NS));
 }
@@ -716,7 +718,7 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
             constexpr int i = CI(I_);
             const double p = s.zn[0][i] * s.ewt[i];
-            ss = __builtin_fma(p, p, ss);
+            ss = (i == 0) ? p * p : ss + p * p;
         });
         if (ss > (double)NS * (1.0 / (UROUND * UROUND))) {
             s.tretlast = tret = s.tn;

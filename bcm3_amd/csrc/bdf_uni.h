@@ -399,7 +399,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
         double ss = 0.0;
         cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
             const double p = s.zn[0][CI(i)] * s.ewt[CI(i)];
-            ss = __builtin_fma(p, p, ss);
+            ss = (CI(i) == 0) ? p * p : ss + p * p;
         });
         if (ss > (double)NS * (1.0 / (UROUND * UROUND))) {
             s.tretlast = tret = s.tn;

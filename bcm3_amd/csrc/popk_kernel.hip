@@ -135,25 +135,45 @@ struct PKLane {
         return ka;
     }
 
-    BDF_INL void rhs(double t, const double (&y)[NS], double (&dydt)[NS]) const
+    // The PK systems are linear, dy/dt = A(ka) y + u(t) e0 (RHS_*, .cpp:446-560): A's entries
+    // (a(i, j)) and the transit input u are evaluated once per call; every product of the
+    // matrix-vector sum is an fma in the fixed order j = 0, 1, 2 -- including the structural
+    // zeros -- so the one-trajectory-per-wavefront solver, which forms the same sums across
+    // lanes, produces identical bits.
+    BDF_INL double a(int i, int j) const
     {
-        double a = cur_ka();
+        const double k = cur_ka();
+        if constexpr (TR::two) {
+            const double m[3][3] = {{-(k + ke), 0.0, 0.0}, {k, -(kel + kf), kb}, {0.0, kf, -kb}};
+            return m[i][j];
+        } else {
+            const double m[2][2] = {{-(k + ke), 0.0}, {k, -kel}};
+            return m[i][j];
+        }
+    }
+
+    // transit absorption input (.cpp:568-592), 0 for the other models
+    BDF_INL double input(double t) const
+    {
         if constexpr (TR::transit) {
             double d = dose;
             if (t >= dose_change_time) d = dose_after;
-            double tst = t - last_treatment;
-            double transit = exp((ntr * log(ktr * tst) - ktr * tst) - lnf);
-            transit = ktr * transit * d;
-            dydt[0] = transit - (a + ke) * y[0];
-        } else {
-            dydt[0] = -(a + ke) * y[0];
+            const double tst = t - last_treatment;
+            const double transit = exp((ntr * log(ktr * tst) - ktr * tst) - lnf);
+            return ktr * transit * d;
         }
-        if constexpr (TR::two) {
-            dydt[1] = __builtin_fma(kb, y[2], __builtin_fma(-kf, y[1], __builtin_fma(-kel, y[1], a * y[0])));
-            dydt[2] = __builtin_fma(kf, y[1], -(kb * y[2]));
-        } else {
-            dydt[1] = __builtin_fma(-kel, y[1], a * y[0]);
-        }
+        return 0.0;
+    }
+
+    BDF_INL void rhs(double t, const double (&y)[NS], double (&dydt)[NS]) const
+    {
+        cfor<0, NS>([&](auto I) __attribute__((always_inline)) {
+            constexpr int i = CI(I);
+            double f = a(i, 0) * y[0];
+            cfor<1, NS>([&](auto J) __attribute__((always_inline)) { f = __builtin_fma(a(i, CI(J)), y[CI(J)], f); });
+            dydt[i] = f;
+        });
+        if constexpr (TR::transit) dydt[0] = dydt[0] + input(t);
     }
 
     // Jacobian (CalculateJacobian_*, .cpp:457-642) is constant within a dosing segment, so the
@@ -195,15 +215,20 @@ struct PKLane {
         }
     }
 
+    // x = A^-1 b with the full row sums (structural zeros included, see rhs)
+    BDF_INL static double inv_at(const Inv& r, int i, int j)
+    {
+        const double m[3][3] = {{r.i00, 0.0, 0.0}, {r.i10, r.i11, r.i12}, {r.i20, r.i21, r.i22}};
+        return m[i][j];
+    }
     BDF_INL void lin_solve(const Inv& r, const double (&b)[NS], double (&x)[NS]) const
     {
-        x[0] = r.i00 * b[0];
-        if constexpr (TR::two) {
-            x[1] = __builtin_fma(r.i12, b[2], __builtin_fma(r.i11, b[1], r.i10 * b[0]));
-            x[2] = __builtin_fma(r.i22, b[2], __builtin_fma(r.i21, b[1], r.i20 * b[0]));
-        } else {
-            x[1] = __builtin_fma(r.i11, b[1], r.i10 * b[0]);
-        }
+        cfor<0, NS>([&](auto I) __attribute__((always_inline)) {
+            constexpr int i = CI(I);
+            double v = inv_at(r, i, 0) * b[0];
+            cfor<1, NS>([&](auto J) __attribute__((always_inline)) { v = __builtin_fma(inv_at(r, i, CI(J)), b[CI(J)], v); });
+            x[i] = v;
+        });
     }
 };
 
