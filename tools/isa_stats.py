@@ -13,7 +13,7 @@ CSRC = os.path.join(ROOT, "bcm3_amd", "csrc")
 
 
 def build_asm(out="/tmp/popk_kernel.s"):
-    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-ffp-contract=off", "-mllvm", "-simplifycfg-sink-common=false",
+    subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S", "-ffp-contract=off", "-mllvm", "-simplifycfg-sink-common=false", "-mllvm", "-structurizecfg-skip-uniform-regions",
                     "-o", out, os.path.join(CSRC, "popk_kernel.hip")], check=True)
     return out
 
