@@ -140,6 +140,26 @@ BDF_INL double eta_from_u(double bx, int k)
     return fdiv(z, __builtin_fma(ADDON, z, 1.0));
 }
 
+// Step-size ratios below THRESH are discarded (cvSetEta: eta = 1), so an eta candidate only has
+// to be computed exactly when it can reach THRESH. eta = 1 / (bx^(1/k) + ADDON) >= THRESH needs
+// bx <= (1/THRESH - ADDON)^k; above that bound (with a 1e-9 relative margin, far wider than the
+// few-ulp error of eta_from) the candidate is replaced by 0, which every later use (the
+// THRESH test, the max over candidates and the equality tests of cvChooseEta) treats exactly
+// like the true value < THRESH.
+constexpr double eta_cut(int k)
+{
+    double c = 1.0;
+    for (int i = 0; i < k; i++) c *= (1.0 / THRESH - ADDON);
+    return c * (1.0 + 1e-9);
+}
+template <int K>
+BDF_INL double eta_candidate(double bx)
+{
+    constexpr double cut = eta_cut(K);
+    if (bx > cut) return 0.0;
+    return eta_from_u(bx, K);
+}
+
 // One Newton correction (residual, optional setup, solve, update): the body shared by the
 // first and the later iterations of newton_u.
 template <int NS, class S, class Model>
@@ -286,14 +306,14 @@ BDF_INL void complete_q(S& s, double dsm)
         s.hprime = s.h;
         s.eta = 1.0;
     } else {
-        const double etaq = eta_from_u(BIAS2 * dsm, q + 1);
+        const double etaq = eta_candidate<q + 1>(BIAS2 * dsm);
         double eta = etaq;
         s.qprime = q;
         if (s.qwait == 0) {
             // cvComputeEtaqm1 / cvComputeEtaqp1 / cvChooseEta, every q+1 steps
             s.qwait = 2;
             double etaqm1 = 0.0, etaqp1 = 0.0;
-            if constexpr (q > 1) etaqm1 = eta_from_u(BIAS1 * wrms<NS>(s.zn[q], s.ewt) * s.tq[1], q);
+            if constexpr (q > 1) etaqm1 = eta_candidate<q>(BIAS1 * wrms<NS>(s.zn[q], s.ewt) * s.tq[1]);
             if constexpr (q != QMAX) {
                 if (s.saved_tq5 != 0.0) {
                     const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
@@ -301,7 +321,7 @@ BDF_INL void complete_q(S& s, double dsm)
                     cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
                         tv[CI(i)] = __builtin_fma(-cquot, s.zn[QMAX][CI(i)], s.acor[CI(i)]);
                     });
-                    etaqp1 = eta_from_u(BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3], q + 2);
+                    etaqp1 = eta_candidate<q + 2>(BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3]);
                 }
             }
             const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
@@ -342,19 +362,27 @@ BDF_INL int step_q(S& s, const Model& mdl, double eta_eff, double saved_t, int n
 
 // CVode(..., CV_ONE_STEP) for the UNI launch: same contract as bcm3hip::cvode_one_step, except
 // that a successful step does not copy zn[0] to yout (the caller reads s.zn[0]).
+// hot: the previous call returned CV_SUCCESS and nothing changed the solver since. The entry
+// tests are then known: nst > 0, tretlast == tn, the tstop tests of the step's end (same
+// expressions, same values) found tstop neither reached nor inside the next step, or already
+// applied the clamp (hprime, eta) that the entry test would recompute identically.
 template <int NS, class S, class Model>
-BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret)
+BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret, bool hot)
 {
     BDF_PH(0);
     {
         // one scalar branch for the common entry (cvode.c:1251-1310): not the first step after
         // (Re)Init, tn was not returned before, tstop is neither reached nor within the next step
-        const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
-        const bool first = (s.nst == 0);
-        const bool ret_prev = fabs(s.tn - s.tretlast) > troundoff;
-        const bool at_stop = (s.tstopset != 0) & (fabs(s.tn - s.tstop) <= troundoff);
-        const bool clamp = (s.tstopset != 0) & ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
-        if (first | ret_prev | at_stop | clamp) {
+        bool rare_entry = false, first = false, ret_prev = false, at_stop = false;
+        if (!hot) {
+            const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+            first = (s.nst == 0);
+            ret_prev = fabs(s.tn - s.tretlast) > troundoff;
+            at_stop = (s.tstopset != 0) & (fabs(s.tn - s.tstop) <= troundoff);
+            const bool clamp = (s.tstopset != 0) & ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
+            rare_entry = first | ret_prev | at_stop | clamp;
+        }
+        if (rare_entry) {
             if (first) {
                 s.tretlast = tret = s.tn;
                 ewt_set<NS>(s, s.zn[0], s.ewt);

@@ -432,11 +432,12 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             s.tstop = next_disc;
             s.tstopset = 1;
             int current_step = 0;
+            bool hot = false;  // previous step was a plain CV_SUCCESS (uni::cvode_one_step_u)
             for (;;) {
                 double tret = 0.0;
                 int result;
                 if constexpr (UNI)
-                    result = uni::cvode_one_step_u<NS>(s, mdl, end_time, y, tret);
+                    result = uni::cvode_one_step_u<NS>(s, mdl, end_time, y, tret, hot);
                 else
                     result = cvode_one_step<NS>(s, mdl, end_time, y, tret);
                 if (result < 0) {
@@ -449,6 +450,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                 // not at the end (the checks below in the reference's order otherwise)
                 const bool rare = (result != CV_SUCCESS) | (tret >= next_out) | (t >= end_time) |
                                   (current_step == m.max_steps) | (next_disc == t);
+                hot = !rare;
                 if (!rare) continue;
                 if (result == CV_SUCCESS) cfor<0, NS>([&](auto k) __attribute__((always_inline)) { y[CI(k)] = s.zn[0][CI(k)]; });
                 while (tret >= next_out) {
