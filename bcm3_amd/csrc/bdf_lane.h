@@ -72,6 +72,14 @@ enum { CV_SUCCESS = 0, CV_TSTOP_RETURN = 1, CV_TOO_MUCH_ACC = -2, CV_ERR_FAILURE
        CV_CONV_FAILURE = -4, CV_ILL_INPUT = -22, CV_BAD_T = -26, CV_TOO_CLOSE = -27 };
 
 #define BDF_INL __device__ __forceinline__
+// branch-layout hints for the UNI solver (hot path falls through; rare work out of line)
+#ifdef BCM3_NO_EXPECT
+#define BDF_LIKELY(x) (x)
+#define BDF_UNLIKELY(x) (x)
+#else
+#define BDF_LIKELY(x) __builtin_expect(!!(x), 1)
+#define BDF_UNLIKELY(x) __builtin_expect(!!(x), 0)
+#endif
 
 // compile-time index loops: f(IC<j>{}) for j = B..E-1 (cfor) or j = B down to E (cfor_down)
 template <int V>
@@ -255,6 +263,7 @@ struct BdfState {
     int q, qprime, qwait, L;
     int nst, nstlp, nstlj;
     int nls_jcur;
+    int check_tolsf;  // 0: the too-much-accuracy test cannot fire (rtol >= 1e-10, atol >= 0)
     BdfCounters cnt;
 #ifdef BCM3_PHASES
     long long ph[NPHASES];

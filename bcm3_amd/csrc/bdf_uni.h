@@ -156,7 +156,7 @@ template <int K>
 BDF_INL double eta_candidate(double bx)
 {
     constexpr double cut = eta_cut(K);
-    if (bx > cut) return 0.0;
+    if (BDF_LIKELY(bx > cut)) return 0.0;
     return eta_from_u(bx, K);
 }
 
@@ -178,7 +178,7 @@ BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& csc
         delta[i] = __builtin_fma(rl1, s.zn[1][i], s.acor[i]);
         delta[i] = __builtin_fma(-s.gamma, f[i], delta[i]);
     });
-    if (setup) {
+    if (BDF_UNLIKELY(setup)) {
         // cvNlsLSetup -> cvLsSetup (cvode_ls.c:1415-1500)
         if (jbad) convfail = CONV_BAD_J;
         const double dgamma = fabs(fdiv(s.gamma, s.gammap) - 1.0);
@@ -223,7 +223,7 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
         // iteration 0 (crate as left by the previous step)
         double del = newton_correction<NS>(s, mdl, rl1, cscale, callSetup, jbad, convfail);
         // cvNlsConvTest: dcon = del min(1, crate) / tol <= 1 with tol = CORTES / tq[2]
-        if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
+        if (BDF_LIKELY(del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES)) {
             s.acnrm = del;
             s.nls_jcur = 0;
             return true;
@@ -258,7 +258,8 @@ enum { ATTEMPT_OK = 0, ATTEMPT_CONV_FAIL = 1, ATTEMPT_ERR_FAIL = 2 };
 template <int Q, int NS, class S, class Model>
 BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm)
 {
-    rescale_q<Q, NS>(s, eta_eff);
+    // h == hscale holds between steps, so eta_eff == 1 leaves zn, h and hscale as they are
+    if (BDF_UNLIKELY(eta_eff != 1.0)) rescale_q<Q, NS>(s, eta_eff);
     BDF_PH(2);
     predict_q<Q, NS>(s);
     BDF_PH(3);
@@ -271,7 +272,7 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
     const bool conv = newton_u<NS>(s, mdl, rl1, convfail, callSetup);
     BDF_PH(5);
     dsm = s.acnrm * s.tq[2];
-    if (conv & (dsm <= 1.0)) return ATTEMPT_OK;
+    if (BDF_LIKELY(conv & (dsm <= 1.0))) return ATTEMPT_OK;
     restore_q<Q, NS>(s, saved_t);
     return conv ? ATTEMPT_ERR_FAIL : ATTEMPT_CONV_FAIL;
 }
@@ -300,7 +301,7 @@ BDF_INL void complete_q(S& s, double dsm)
     }
     BDF_PH(7);
 
-    if (s.etamax == 1.0) {
+    if (BDF_UNLIKELY(s.etamax == 1.0)) {
         s.qwait = SUNMAX(s.qwait, 2);
         s.qprime = q;
         s.hprime = s.h;
@@ -353,7 +354,7 @@ template <int Q, int NS, class S, class Model>
 BDF_INL int step_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm)
 {
     const int r = attempt_q<Q, NS>(s, mdl, eta_eff, saved_t, nflag, dsm);
-    if (r == ATTEMPT_OK) complete_q<Q, NS>(s, dsm);
+    if (BDF_LIKELY(r == ATTEMPT_OK)) complete_q<Q, NS>(s, dsm);
 #ifdef BCM3_PHASES
     if (r == ATTEMPT_OK) s.qh[Q]++;
 #endif
@@ -374,7 +375,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
         // one scalar branch for the common entry (cvode.c:1251-1310): not the first step after
         // (Re)Init, tn was not returned before, tstop is neither reached nor within the next step
         bool rare_entry = false, first = false, ret_prev = false, at_stop = false;
-        if (!hot) {
+        if (BDF_UNLIKELY(!hot)) {
             const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
             first = (s.nst == 0);
             ret_prev = fabs(s.tn - s.tretlast) > troundoff;
@@ -382,7 +383,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
             const bool clamp = (s.tstopset != 0) & ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
             rare_entry = first | ret_prev | at_stop | clamp;
         }
-        if (rare_entry) {
+        if (BDF_UNLIKELY(rare_entry)) {
             if (first) {
                 s.tretlast = tret = s.tn;
                 ewt_set<NS>(s, s.zn[0], s.ewt);
@@ -423,7 +424,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
             ewt_set<NS>(s, s.zn[0], s.ewt);
         }
     }
-    {
+    if (BDF_UNLIKELY(s.check_tolsf)) {
         double ss = 0.0;
         cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
             const double p = s.zn[0][CI(i)] * s.ewt[CI(i)];
@@ -443,7 +444,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
     // cvAdjustParams when the step size changed; rescaling by eta_eff = 1 is a no-op
     const bool adj = (s.nst > 0) & (s.hprime != s.h);
     double eta_eff = adj ? s.eta : 1.0;
-    if (adj & (s.qprime != s.q)) {
+    if (BDF_UNLIKELY(adj & (s.qprime != s.q))) {
         adjust_order<NS>(s, s.qprime - s.q);
         s.q = s.qprime;
         s.L = s.q + 1;
@@ -460,7 +461,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
         default: r = step_q<5, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
         }
         BDF_PH(6);
-        if (r == ATTEMPT_OK) break;
+        if (BDF_LIKELY(r == ATTEMPT_OK)) break;
         // failure handling (cvHandleNFlag / cvDoErrorTest), rare
         eta_eff = 1.0;
         s.etamax = 1.0;
@@ -507,7 +508,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
     // stop tests after the step (cvode.c:1395-1437)
     const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
     const bool reached = fabs(s.tn - s.tstop) <= troundoff;
-    if ((s.tstopset != 0) & (reached | ((s.tn + s.hprime - s.tstop) * s.h > 0.0))) {
+    if (BDF_UNLIKELY((s.tstopset != 0) & (reached | ((s.tn + s.hprime - s.tstop) * s.h > 0.0)))) {
         if (reached) {
             get_dky<NS>(s, s.tstop, yout);
             s.tretlast = tret = s.tstop;
