@@ -46,6 +46,7 @@ struct bcm3hip_ctx {
     bcm3hip_traj_stats* stats = nullptr;
     size_t cap_stats = 0;
     int lanes_per_wave = 0;  // 0 = auto (auto_lanes_per_wave)
+    int uni_solver = 0;      // BCM3HIP_OPT_UNI_SOLVER
     int block_waves = 1;
 };
 
@@ -245,6 +246,10 @@ int bcm3hip_set_option(bcm3hip_ctx* c, int option, int64_t value)
         c->log_timing = value != 0;
         c->log_used = 0;
         return 0;
+    case BCM3HIP_OPT_UNI_SOLVER:
+        if (value != 0 && value != 1) return BCM3HIP_ERR_ARG;
+        c->uni_solver = (int)value;
+        return 0;
     default: return BCM3HIP_ERR_ARG;
     }
 }
@@ -292,7 +297,7 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
         if (r) return r;
         e = launch_popk(c->pm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, dtraj, dstats,
                         c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
-                        c->block_waves, s, e0, e1);
+                        c->block_waves, c->uni_solver, s, e0, e1);
     } else {
         e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     }

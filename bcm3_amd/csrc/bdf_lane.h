@@ -81,6 +81,16 @@ enum { CV_SUCCESS = 0, CV_TSTOP_RETURN = 1, CV_TOO_MUCH_ACC = -2, CV_ERR_FAILURE
 #define BDF_UNLIKELY(x) __builtin_expect(!!(x), 0)
 #endif
 
+// readfirstlane of both halves: the value is (already) the same in every lane, or only lane 0's
+// value is wanted; the result is uniform to the compiler
+BDF_INL double wave_uniform(double x)
+{
+    const long long b = __builtin_bit_cast(long long, x);
+    const int lo = __builtin_amdgcn_readfirstlane((int)b);
+    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
 // compile-time index loops: f(IC<j>{}) for j = B..E-1 (cfor) or j = B down to E (cfor_down)
 template <int V>
 struct IC {

@@ -1,0 +1,626 @@
+// bdf_vec.h -- the one-trajectory-per-wavefront BDF step (bdf_uni.h) with the solver's state
+// VECTORS spread across lanes: lane i holds component i of zn[0..5], ewt, acor (lanes >= NS
+// carry don't-care values). Every component-wise operation of the step -- predict, rescale,
+// the Nordsieck update, the Newton residual / update, the error weights -- is then ONE VALU
+// instruction instead of NS; the scalars of the step (tn, h, l, tq, gamma, eta, counters) stay
+// wave-uniform exactly as in bdf_uni.h and share its code (set_bdf_q, eta_candidate).
+//
+// Cross-lane work is the two small contractions of the linear PK systems and the norms:
+//   * matrix-vector products (RHS  A y, solve  A^-1 b): the column j of the matrix lives in
+//     the lanes (lane i: a(i, j)) and y_j is broadcast to every lane with one DPP row_newbcast
+//     move, f = a(:,0) y0 -> fma(a(:,1), y1, f) -> fma(a(:,2), y2, f): the same products and
+//     fma order as the scalar model (PKLane::rhs / lin_solve), so the bits agree;
+//   * weighted RMS norms: squares in lanes, the sum ((p0^2 + p1^2) + p2^2) from broadcasts in
+//     component order, made wave-uniform with readfirstlane (wrms of bdf_lane.h sums the same
+//     rounded squares in the same order).
+// Results are bit-identical to bdf_uni.h and bdf_lane.h (tests/test_popk_gpu.py runs all three).
+#pragma once
+#include "bdf_uni.h"
+
+namespace bcm3hip {
+namespace vec {
+
+BDF_INL int lane_id() { return (int)(threadIdx.x & 63); }
+
+// value of lane J of this 16-lane row in every lane (v_mov_b64_dpp row_newbcast:J)
+template <int J>
+BDF_INL double bc(double v)
+{
+    return __builtin_amdgcn_update_dpp(v, v, 0x150 + J, 0xf, 0xf, false);
+}
+
+// component k (lane k) as a uniform value
+BDF_INL double comp(double v, int k)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)b, k);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// lane vector from NS uniform values (lane i <- a[i]; lanes >= NS get a[NS-1])
+template <int NS>
+BDF_INL double from_array(const double (&a)[NS])
+{
+    const int ln = lane_id();
+    double r = a[NS - 1];
+    cfor_down<NS - 2, 0>([&](auto i) __attribute__((always_inline)) { r = (ln == CI(i)) ? a[CI(i)] : r; });
+    return r;
+}
+template <int NS>
+BDF_INL void to_array(double v, double (&a)[NS])
+{
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { a[CI(i)] = comp(v, CI(i)); });
+}
+
+// sum over the components in component order ((c0 + c1) + c2), uniform
+template <int NS>
+BDF_INL double lane_sum(double p)
+{
+    double s = bc<0>(p) + bc<1>(p);
+    if constexpr (NS == 3) s = s + bc<2>(p);
+    return wave_uniform(s);
+}
+
+// N_VWrmsNorm (wrms of bdf_lane.h)
+template <int NS>
+BDF_INL double wrms(double x, double w)
+{
+    const double p = x * w;
+    return fsqrt(fdiv_c(vec::lane_sum<NS>(p * p), (double)NS, 1.0 / NS));
+}
+
+// y = M x for M held as lane columns (lane i of col[j] = m(i, j))
+template <int NS>
+BDF_INL double matvec(const double (&col)[NS], double x)
+{
+    double r = col[0] * bc<0>(x);
+    cfor<1, NS>([&](auto j) __attribute__((always_inline)) { r = __builtin_fma(col[CI(j)], bc<CI(j)>(x), r); });
+    return r;
+}
+
+template <int NS>
+struct VecState {
+    double rtol, atol;
+    double zn[QMAX + 1];  // lane i: component i
+    double ewt, acor;
+    double acol[NS];  // columns of the RHS matrix A(ka) (constant between ReInits)
+    double icol[NS];  // columns of (I - gamma J)^-1 (lin_setup)
+    double tau[QMAX + 2], tq[6], l[QMAX + 1];
+    double tn, h, hprime, eta, hscale, hu, tretlast;
+    double gamma, gammap, gamrat, crate, delp, acnrm, etamax, saved_tq5;
+    double tstop;
+    int tstopset;
+    int q, qprime, qwait, L;
+    int nst, nstlp, nstlj;
+    int nls_jcur;
+    int check_tolsf;
+    BdfCounters cnt;
+#ifdef BCM3_PHASES
+    long long ph[NPHASES];
+    long long tlast;
+    int qh[QMAX + 1];
+#endif
+};
+
+template <class S>
+BDF_INL void ewt_set(S& s)
+{
+    s.ewt = frcp(__builtin_fma(s.rtol, fabs(s.zn[0]), s.atol));
+}
+
+template <int Q, class S>
+BDF_INL void rescale_q(S& s, double eta)
+{
+    double c = eta;
+    cfor<1, Q + 1>([&](auto j) __attribute__((always_inline)) {
+        s.zn[CI(j)] *= c;
+        c = eta * c;
+    });
+    s.h = s.hscale * eta;
+    s.hscale = s.h;
+}
+
+template <int Q, class S>
+BDF_INL void predict_q(S& s)
+{
+    s.tn += s.h;
+    const double tc = s.tstop;
+    s.tn = ((s.tstopset != 0) & ((s.tn - tc) * s.h > 0.0)) ? tc : s.tn;
+    cfor<1, Q + 1>([&](auto k) __attribute__((always_inline)) {
+        cfor_down<Q, CI(k)>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j) - 1] += s.zn[CI(j)]; });
+    });
+}
+
+template <int Q, class S>
+BDF_INL void restore_q(S& s, double saved_t)
+{
+    s.tn = saved_t;
+    cfor<1, Q + 1>([&](auto k) __attribute__((always_inline)) {
+        cfor_down<Q, CI(k)>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j) - 1] -= s.zn[CI(j)]; });
+    });
+}
+
+// cvIncreaseBDF / cvDecreaseBDF / cvAdjustOrder (bdf_lane.h increase_bdf, decrease_bdf)
+template <class S>
+BDF_INL void increase_bdf(S& s)
+{
+    double alpha0, alpha1, prod, xi, xiold, hsum, A1;
+    double l[QMAX + 1];
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = 0.0; });
+    l[2] = alpha1 = prod = xiold = 1.0;
+    alpha0 = -1.0;
+    hsum = s.hscale;
+    cfor<1, QMAX - 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) < s.q) {
+            hsum += s.tau[CI(j) + 1];
+            xi = fdiv(hsum, s.hscale);
+            prod *= xi;
+            alpha0 -= 1.0 / (CI(j) + 1);
+            alpha1 += frcp(xi);
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xiold, l[CI(i) - 1]); });
+            xiold = xi;
+        }
+    });
+    A1 = fdiv(-alpha0 - alpha1, prod);
+    const double znL = A1 * s.zn[QMAX];
+    cfor<2, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) == s.q + 1)
+            s.zn[CI(j)] = znL;
+        else if (CI(j) <= s.q)
+            s.zn[CI(j)] = __builtin_fma(l[CI(j)], znL, s.zn[CI(j)]);
+    });
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
+}
+
+template <class S>
+BDF_INL void decrease_bdf(S& s)
+{
+    double l[QMAX + 1];
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = 0.0; });
+    l[2] = 1.0;
+    double hsum = 0.0;
+    cfor<1, QMAX - 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q - 2) {
+            hsum += s.tau[CI(j)];
+            const double xi = fdiv(hsum, s.hscale);
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xi, l[CI(i) - 1]); });
+        }
+    });
+    // zn[q] by a select chain starting from a constant (see sel in bdf_lane.h)
+    double znq = 0.0;
+    cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { znq = (s.q == CI(j)) ? s.zn[CI(j)] : znq; });
+    cfor<2, QMAX>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) < s.q) s.zn[CI(j)] = __builtin_fma(-l[CI(j)], znq, s.zn[CI(j)]);
+    });
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
+}
+
+template <class S>
+BDF_INL void adjust_order(S& s, int deltaq)
+{
+    if ((s.q == 2) && (deltaq != 1)) return;
+    if (deltaq == 1)
+        vec::increase_bdf(s);
+    else if (deltaq == -1)
+        vec::decrease_bdf(s);
+}
+
+// CVodeGetDky(t, 0) into a lane vector
+template <class S>
+BDF_INL int get_dky(const S& s, double t, double& dky)
+{
+    double tfuzz = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.hu));
+    if (s.hu < 0.0) tfuzz = -tfuzz;
+    const double tp = s.tn - s.hu - tfuzz;
+    const double tn1 = s.tn + tfuzz;
+    if ((t - tp) * (t - tn1) > 0.0) return CV_BAD_T;
+    const double sv = fdiv(t - s.tn, s.h);
+    double c[QMAX + 1];
+    c[0] = 1.0;
+    cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { c[CI(j)] = c[CI(j) - 1] * sv; });
+    dky = 0.0;
+    cfor_down<QMAX, 0>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q) dky = __builtin_fma(c[CI(j)], s.zn[CI(j)], dky);
+    });
+    return CV_SUCCESS;
+}
+template <int NS, class S>
+BDF_INL int get_dky_array(const S& s, double t, double (&dky)[NS])
+{
+    double v;
+    const int r = vec::get_dky(s, t, v);
+    if (r == CV_SUCCESS) vec::to_array<NS>(v, dky);
+    return r;
+}
+
+// CVodeReInit; also refreshes the RHS matrix columns (the dosing callbacks that precede a ReInit
+// may switch the absorption rate)
+template <int NS, class S, class Model>
+BDF_INL void reinit(S& s, const Model& mdl, double t0, const double (&y0)[NS])
+{
+    s.tn = t0;
+    s.q = 1;
+    s.L = 2;
+    s.qwait = 2;
+    s.etamax = ETAMX1;
+    s.hu = 0.0;
+    s.zn[0] = vec::from_array<NS>(y0);
+    mdl.rhs_columns(s.acol);
+    s.nst = 0;
+    s.nstlp = 0;
+    s.cnt.nreinit++;
+}
+
+// cvHin (bdf_lane.h hin)
+template <int NS, class S, class Model>
+BDF_INL int hin(S& s, const Model& mdl, double tout)
+{
+    const double tdiff = tout - s.tn;
+    if (tdiff == 0.0) return CV_TOO_CLOSE;
+    const int sign = (tdiff > 0.0) ? 1 : -1;
+    const double tdist = fabs(tdiff);
+    const double tround = UROUND * SUNMAX(fabs(s.tn), fabs(tout));
+    if (tdist < 2.0 * tround) return CV_TOO_CLOSE;
+    const double hlb = HLB_FACTOR * tround;
+    // cvUpperBoundH0: max over components in component order
+    double t1 = frcp(s.ewt);
+    t1 = __builtin_fma(HUB_FACTOR, fabs(s.zn[0]), t1);
+    const double r = fdiv(fabs(s.zn[1]), t1);
+    double hub_inv = bc<0>(r);
+    cfor<1, NS>([&](auto i) __attribute__((always_inline)) {
+        const double ri = bc<CI(i)>(r);
+        hub_inv = (ri > hub_inv) ? ri : hub_inv;
+    });
+    hub_inv = wave_uniform(hub_inv);
+    double hub = HUB_FACTOR * tdist;
+    if (hub * hub_inv > 1.0) hub = frcp(hub_inv);
+    double hg = fsqrt(hlb * hub);
+    if (hub < hlb) {
+        s.h = (sign == -1) ? -hg : hg;
+        return CV_SUCCESS;
+    }
+    double hnew = hg;
+#pragma unroll 1
+    for (int count1 = 1; count1 <= MAX_ITERS; count1++) {
+        const double hgs = hg * sign;
+        const double yy = __builtin_fma(hgs, s.zn[1], s.zn[0]);
+        double tv = mdl.rhs_v(s.tn + hgs, yy, s.acol);
+        s.cnt.nfe++;
+        const double a = frcp(hgs);
+        tv = a * (tv - s.zn[1]);
+        const double yddnrm = vec::wrms<NS>(tv, s.ewt);
+        hnew = (yddnrm * hub * hub > 2.0) ? fsqrt(fdiv(2.0, yddnrm)) : fsqrt(hg * hub);
+        if (count1 == MAX_ITERS) break;
+        const double hrat = fdiv(hnew, hg);
+        if ((hrat > 0.5) && (hrat < 2.0)) break;
+        if ((count1 > 1) && (hrat > 2.0)) {
+            hnew = hg;
+            break;
+        }
+        hg = hnew;
+    }
+    double h0 = H_BIAS * hnew;
+    if (h0 < hlb) h0 = hlb;
+    if (h0 > hub) h0 = hub;
+    if (sign == -1) h0 = -h0;
+    s.h = h0;
+    return CV_SUCCESS;
+}
+
+// one Newton correction (uni::newton_correction)
+template <int NS, class S, class Model>
+BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& cscale, bool setup, bool jbad,
+                                 int convfail)
+{
+    const double y = s.zn[0] + s.acor;
+    const double f = mdl.rhs_v(s.tn, y, s.acol);
+    s.cnt.nfe++;
+    double delta = __builtin_fma(rl1, s.zn[1], s.acor);
+    delta = __builtin_fma(-s.gamma, f, delta);
+    if (BDF_UNLIKELY(setup)) {
+        if (jbad) convfail = CONV_BAD_J;
+        const double dgamma = fabs(fdiv(s.gamma, s.gammap) - 1.0);
+        const bool jnew = (s.nst == 0) | (s.nst > s.nstlj + CVLS_MSBJ) |
+                          ((convfail == CONV_BAD_J) & (dgamma < CVLS_DGMAX)) | (convfail == CONV_OTHER);
+        s.cnt.nje += jnew ? 1 : 0;
+        s.nstlj = jnew ? s.nst : s.nstlj;
+        mdl.lin_setup_v(s.gamma, s.icol);
+        s.cnt.nsetups++;
+        s.nls_jcur = jnew;
+        s.gamrat = 1.0;
+        cscale = 1.0;
+        s.gammap = s.gamma;
+        s.crate = 1.0;
+        s.nstlp = s.nst;
+    }
+    s.cnt.nni++;
+    double x = vec::matvec<NS>(s.icol, -delta);
+    x *= cscale;
+    s.acor += x;
+    return vec::wrms<NS>(x, s.ewt);
+}
+
+// Newton iteration, first iteration peeled (uni::newton_u)
+template <int NS, class S, class Model>
+BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callSetup)
+{
+    bool jbad = false;
+    double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
+    for (;;) {
+        double del = vec::newton_correction<NS>(s, mdl, rl1, cscale, callSetup, jbad, convfail);
+        if (BDF_LIKELY(del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES)) {
+            s.acnrm = del;
+            s.nls_jcur = 0;
+            return true;
+        }
+        s.delp = del;
+        for (int it = 1; it < NLS_MAXCOR; it++) {
+            del = vec::newton_correction<NS>(s, mdl, rl1, cscale, false, false, convfail);
+            s.crate = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
+            if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
+                s.acnrm = vec::wrms<NS>(s.acor, s.ewt);
+                s.nls_jcur = 0;
+                return true;
+            }
+            if (del > RDIV * s.delp) break;
+            s.delp = del;
+        }
+        if (!s.nls_jcur) {
+            callSetup = true;
+            jbad = true;
+            s.acor = 0.0;
+            continue;
+        }
+        return false;
+    }
+}
+
+template <int Q, int NS, class S, class Model>
+BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm)
+{
+    if (BDF_UNLIKELY(eta_eff != 1.0)) vec::rescale_q<Q>(s, eta_eff);
+    BDF_PH(2);
+    vec::predict_q<Q>(s);
+    BDF_PH(3);
+    const double rl1 = uni::set_bdf_q<Q>(s);
+    BDF_PH(4);
+    const int convfail = ((nflag == FIRST_CALL) | (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
+    const bool callSetup = (nflag == PREV_CONV_FAIL) | (nflag == PREV_ERR_FAIL) | (s.nst == 0) |
+                           (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);
+    s.acor = 0.0;
+    const bool conv = vec::newton<NS>(s, mdl, rl1, convfail, callSetup);
+    BDF_PH(5);
+    dsm = s.acnrm * s.tq[2];
+    if (BDF_LIKELY(conv & (dsm <= 1.0))) return uni::ATTEMPT_OK;
+    vec::restore_q<Q>(s, saved_t);
+    return conv ? uni::ATTEMPT_ERR_FAIL : uni::ATTEMPT_CONV_FAIL;
+}
+
+template <int Q, int NS, class S>
+BDF_INL void complete_q(S& s, double dsm)
+{
+    constexpr int q = Q;
+    s.nst++;
+    s.cnt.nst_total++;
+    s.hu = s.h;
+    cfor_down<Q, 2>([&](auto i) __attribute__((always_inline)) { s.tau[CI(i)] = s.tau[CI(i) - 1]; });
+    if constexpr (q == 1) s.tau[2] = (s.nst > 1) ? s.tau[1] : s.tau[2];
+    s.tau[1] = s.h;
+    cfor<0, Q + 1>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j)] = __builtin_fma(s.l[CI(j)], s.acor, s.zn[CI(j)]); });
+    s.qwait--;
+    if constexpr (q != QMAX) {
+        const bool save = (s.qwait == 1);
+        s.zn[QMAX] = save ? s.acor : s.zn[QMAX];
+        s.saved_tq5 = save ? s.tq[5] : s.saved_tq5;
+    }
+    BDF_PH(7);
+
+    if (BDF_UNLIKELY(s.etamax == 1.0)) {
+        s.qwait = SUNMAX(s.qwait, 2);
+        s.qprime = q;
+        s.hprime = s.h;
+        s.eta = 1.0;
+    } else {
+        const double etaq = uni::eta_candidate<q + 1>(BIAS2 * dsm);
+        double eta = etaq;
+        s.qprime = q;
+        if (s.qwait == 0) {
+            s.qwait = 2;
+            double etaqm1 = 0.0, etaqp1 = 0.0;
+            if constexpr (q > 1) etaqm1 = uni::eta_candidate<q>(BIAS1 * vec::wrms<NS>(s.zn[q], s.ewt) * s.tq[1]);
+            if constexpr (q != QMAX) {
+                if (s.saved_tq5 != 0.0) {
+                    const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
+                    const double tv = __builtin_fma(-cquot, s.zn[QMAX], s.acor);
+                    etaqp1 = uni::eta_candidate<q + 2>(BIAS3 * vec::wrms<NS>(tv, s.ewt) * s.tq[3]);
+                }
+            }
+            const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
+            if (etam < THRESH) {
+                eta = 1.0;
+            } else if (etam == etaq) {
+                eta = etaq;
+            } else if (etam == etaqm1) {
+                eta = etaqm1;
+                s.qprime = q - 1;
+            } else {
+                eta = etaqp1;
+                s.qprime = q + 1;
+                s.zn[QMAX] = s.acor;
+            }
+        }
+        const bool small = (eta < THRESH);
+        s.eta = small ? 1.0 : SUNMIN(eta, s.etamax);
+        s.hprime = small ? s.h : s.h * s.eta;
+    }
+    BDF_PH(8);
+    s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
+    s.acor *= s.tq[2];
+}
+
+template <int Q, int NS, class S, class Model>
+BDF_INL int step_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm)
+{
+    const int r = vec::attempt_q<Q, NS>(s, mdl, eta_eff, saved_t, nflag, dsm);
+    if (BDF_LIKELY(r == uni::ATTEMPT_OK)) vec::complete_q<Q, NS>(s, dsm);
+#ifdef BCM3_PHASES
+    if (r == uni::ATTEMPT_OK) s.qh[Q]++;
+#endif
+    return r;
+}
+
+// CVode(..., CV_ONE_STEP), same contract as uni::cvode_one_step_u (yout: uniform components)
+template <int NS, class S, class Model>
+BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret, bool hot)
+{
+    BDF_PH(0);
+    {
+        bool rare_entry = false, first = false, ret_prev = false, at_stop = false;
+        if (BDF_UNLIKELY(!hot)) {
+            const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+            first = (s.nst == 0);
+            ret_prev = fabs(s.tn - s.tretlast) > troundoff;
+            at_stop = (s.tstopset != 0) & (fabs(s.tn - s.tstop) <= troundoff);
+            const bool clamp = (s.tstopset != 0) & ((s.tn + s.hprime - s.tstop) * s.h > 0.0);
+            rare_entry = first | ret_prev | at_stop | clamp;
+        }
+        if (BDF_UNLIKELY(rare_entry)) {
+            if (first) {
+                s.tretlast = tret = s.tn;
+                vec::ewt_set(s);
+                s.nstlj = 0;
+                s.nls_jcur = 0;
+                s.zn[1] = mdl.rhs_v(s.tn, s.zn[0], s.acol);
+                s.cnt.nfe++;
+                if (s.tstopset) {
+                    if ((s.tstop - s.tn) * (tout - s.tn) <= 0.0) return CV_ILL_INPUT;
+                }
+                double tout_hin = tout;
+                if (s.tstopset && (tout - s.tn) * (tout - s.tstop) > 0.0) tout_hin = s.tstop;
+                const int hflag = vec::hin<NS>(s, mdl, tout_hin);
+                if (hflag != CV_SUCCESS) return hflag;
+                if (s.tstopset) {
+                    if ((s.tn + s.h - s.tstop) * s.h > 0.0) s.h = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+                }
+                s.hscale = s.h;
+                s.hprime = s.h;
+                s.zn[1] *= s.h;
+            } else {
+                if (ret_prev) {
+                    s.tretlast = tret = s.tn;
+                    vec::to_array<NS>(s.zn[0], yout);
+                    return CV_SUCCESS;
+                }
+                if (at_stop) {
+                    double v;
+                    if (vec::get_dky(s, s.tstop, v) != CV_SUCCESS) return CV_ILL_INPUT;
+                    vec::to_array<NS>(v, yout);
+                    s.tretlast = tret = s.tstop;
+                    s.tstopset = 0;
+                    return CV_TSTOP_RETURN;
+                }
+                s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+                s.eta = fdiv(s.hprime, s.h);
+                vec::ewt_set(s);
+            }
+        } else {
+            vec::ewt_set(s);
+        }
+    }
+    if (BDF_UNLIKELY(s.check_tolsf)) {
+        const double p = s.zn[0] * s.ewt;
+        const double ss = vec::lane_sum<NS>(p * p);
+        if (ss > (double)NS * (1.0 / (UROUND * UROUND))) {
+            s.tretlast = tret = s.tn;
+            vec::to_array<NS>(s.zn[0], yout);
+            return CV_TOO_MUCH_ACC;
+        }
+    }
+    BDF_PH(1);
+
+    const double saved_t = s.tn;
+    int ncf = 0, nef = 0, nflag = FIRST_CALL;
+    const bool adj = (s.nst > 0) & (s.hprime != s.h);
+    double eta_eff = adj ? s.eta : 1.0;
+    if (BDF_UNLIKELY(adj & (s.qprime != s.q))) {
+        vec::adjust_order(s, s.qprime - s.q);
+        s.q = s.qprime;
+        s.L = s.q + 1;
+        s.qwait = s.L;
+    }
+    double dsm = 0.0;
+    for (;;) {
+        int r;
+        switch (s.q) {
+        case 1: r = vec::step_q<1, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 2: r = vec::step_q<2, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 3: r = vec::step_q<3, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        case 4: r = vec::step_q<4, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        default: r = vec::step_q<5, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+        }
+        BDF_PH(6);
+        if (BDF_LIKELY(r == uni::ATTEMPT_OK)) break;
+        eta_eff = 1.0;
+        s.etamax = 1.0;
+        if (r == uni::ATTEMPT_CONV_FAIL) {
+            s.cnt.ncfn++;
+            ncf++;
+            if (ncf == MXNCF) return CV_CONV_FAILURE;
+            s.eta = ETACF;
+            nflag = PREV_CONV_FAIL;
+            eta_eff = s.eta;
+            continue;
+        }
+        nef++;
+        s.cnt.netf++;
+        nflag = PREV_ERR_FAIL;
+        if (nef == MXNEF) return CV_ERR_FAILURE;
+        if (nef <= MXNEF1) {
+            double eta = eta_from(BIAS2 * dsm, s.L);
+            eta = SUNMAX(ETAMIN, eta);
+            if (nef >= SMALL_NEF) eta = SUNMIN(eta, ETAMXF);
+            s.eta = eta;
+            eta_eff = s.eta;
+            continue;
+        }
+        s.eta = ETAMIN;
+        if (s.q > 1) {
+            vec::adjust_order(s, -1);
+            s.L = s.q;
+            s.q--;
+            s.qwait = s.L;
+            eta_eff = s.eta;
+            continue;
+        }
+        s.h *= s.eta;
+        s.hscale = s.h;
+        s.qwait = LONG_WAIT;
+        const double tv = mdl.rhs_v(s.tn, s.zn[0], s.acol);
+        s.cnt.nfe++;
+        s.zn[1] = s.h * tv;
+        eta_eff = 1.0;
+    }
+
+    const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+    const bool reached = fabs(s.tn - s.tstop) <= troundoff;
+    if (BDF_UNLIKELY((s.tstopset != 0) & (reached | ((s.tn + s.hprime - s.tstop) * s.h > 0.0)))) {
+        if (reached) {
+            double v;
+            vec::get_dky(s, s.tstop, v);
+            vec::to_array<NS>(v, yout);
+            s.tretlast = tret = s.tstop;
+            s.tstopset = 0;
+            BDF_PH(9);
+            return CV_TSTOP_RETURN;
+        }
+        s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+        s.eta = fdiv(s.hprime, s.h);
+    }
+    s.tretlast = tret = s.tn;
+    BDF_PH(9);
+    return CV_SUCCESS;
+}
+
+}  // namespace vec
+}  // namespace bcm3hip

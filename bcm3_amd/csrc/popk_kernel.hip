@@ -19,9 +19,11 @@
 
 #include <cmath>
 #include <cstdint>
+#include <type_traits>
 
 #include "bdf_lane.h"
 #include "bdf_uni.h"
+#include "bdf_vec.h"
 #include "popk_kernel.h"
 
 namespace bcm3hip {
@@ -101,16 +103,6 @@ BDF_INL double log_pdf_tnu4(double x, double mu, double sigma)
 
 // ---------------------------------------------------------------------------------------------
 // PK models (LikelihoodPopPKTrajectory.cpp:446-642)
-
-// readfirstlane of both halves: the value is (already) the same in every lane; this tells the
-// compiler so
-__device__ __forceinline__ double wave_uniform(double x)
-{
-    const long long b = __builtin_bit_cast(long long, x);
-    const int lo = __builtin_amdgcn_readfirstlane((int)b);
-    const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
-}
 
 template <int PKT>
 struct PKTraits {
@@ -230,6 +222,38 @@ struct PKLane {
             x[i] = v;
         });
     }
+
+    // ---- lane-vector forms for bdf_vec.h (lane i = component i; same products, same order)
+    // columns of A: lane i of c[j] = a(i, j)
+    BDF_INL void rhs_columns(double (&c)[NS]) const
+    {
+        cfor<0, NS>([&](auto J) __attribute__((always_inline)) {
+            constexpr int j = CI(J);
+            double col[NS];
+            cfor<0, NS>([&](auto I) __attribute__((always_inline)) { col[CI(I)] = a(CI(I), j); });
+            c[j] = vec::from_array<NS>(col);
+        });
+    }
+    BDF_INL double rhs_v(double t, double y, const double (&acol)[NS]) const
+    {
+        double f = vec::matvec<NS>(acol, y);
+        if constexpr (TR::transit) {
+            const double u = input(t);
+            f = (vec::lane_id() == 0) ? f + u : f;
+        }
+        return f;
+    }
+    BDF_INL void lin_setup_v(double gamma, double (&icol)[NS]) const
+    {
+        Inv r;
+        lin_setup(gamma, r);
+        cfor<0, NS>([&](auto J) __attribute__((always_inline)) {
+            constexpr int j = CI(J);
+            double col[NS];
+            cfor<0, NS>([&](auto I) __attribute__((always_inline)) { col[CI(I)] = inv_at(r, CI(I), j); });
+            icol[j] = vec::from_array<NS>(col);
+        });
+    }
 };
 
 // CheckGiveTreatment (.cpp:644-671)
@@ -258,7 +282,12 @@ BDF_INL bool check_give_treatment(double t, const uint8_t* skipped, int intermit
 // model data come in through scalar loads and every solver branch is a uniform (scalar) branch
 // instead of exec-mask manipulation. All 64 lanes compute and store the same numbers (a
 // same-address same-value store from every lane is one well-defined store).
-template <int PKT, bool UNI>
+// MODE: POPK_LANES (lanes_per_wave trajectories per wavefront, bdf_lane.h), POPK_UNI (one
+// trajectory per wavefront, scalar state: bdf_uni.h), POPK_VEC (one trajectory per wavefront,
+// state vectors across lanes: bdf_vec.h). All three give the same bits.
+enum { POPK_LANES = 0, POPK_UNI = 1, POPK_VEC = 2 };
+
+template <int PKT, int MODE>
 __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t ntraj, int lpw,
                                                         const double* __restrict__ values,
                                                         double* __restrict__ logp_direct,
@@ -269,6 +298,8 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
 {
     using TR = PKTraits<PKT>;
     constexpr int NS = TR::NS;
+    constexpr bool UNI = (MODE != POPK_LANES);
+    constexpr bool VEC = (MODE == POPK_VEC);
     const int lane = threadIdx.x & 63;
     int64_t g;
     if constexpr (UNI) {
@@ -369,7 +400,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     bool llh_done = false;  // NaN concentration seen: llh = -inf, stop accumulating
     int status = BCM3HIP_STATUS_OK;
 
-    BdfState<NS, typename PKLane<PKT>::Inv> s;
+    std::conditional_t<VEC, vec::VecState<NS>, BdfState<NS, typename PKLane<PKT>::Inv>> s;
     s.cnt = BdfCounters{0, 0, 0, 0, 0, 0, 0, 0};
     s.nst = 0;
 #ifdef BCM3_PHASES
@@ -430,7 +461,10 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             s.tstopset = 0;
             double y[NS];
             cfor<0, NS>([&](auto k) __attribute__((always_inline)) { y[CI(k)] = y0[CI(k)]; });
-            reinit<NS>(s, 0.0, y);
+            if constexpr (VEC)
+                vec::reinit<NS>(s, mdl, 0.0, y);
+            else
+                reinit<NS>(s, 0.0, y);
             s.tstop = next_disc;
             s.tstopset = 1;
             int current_step = 0;
@@ -438,7 +472,9 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             for (;;) {
                 double tret = 0.0;
                 int result;
-                if constexpr (UNI)
+                if constexpr (VEC)
+                    result = vec::cvode_one_step<NS>(s, mdl, end_time, y, tret, hot);
+                else if constexpr (UNI)
                     result = uni::cvode_one_step_u<NS>(s, mdl, end_time, y, tret, hot);
                 else
                     result = cvode_one_step<NS>(s, mdl, end_time, y, tret);
@@ -454,10 +490,20 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                                   (current_step == m.max_steps) | (next_disc == t);
                 hot = !rare;
                 if (BDF_LIKELY(!rare)) continue;
-                if (result == CV_SUCCESS) cfor<0, NS>([&](auto k) __attribute__((always_inline)) { y[CI(k)] = s.zn[0][CI(k)]; });
+                if (result == CV_SUCCESS) {
+                    if constexpr (VEC)
+                        vec::to_array<NS>(s.zn[0], y);
+                    else
+                        cfor<0, NS>([&](auto k) __attribute__((always_inline)) { y[CI(k)] = s.zn[0][CI(k)]; });
+                }
                 while (tret >= next_out) {
                     double dky[NS];
-                    if (get_dky<NS>(s, m.time[tpi], dky) != CV_SUCCESS) {
+                    int dr;
+                    if constexpr (VEC)
+                        dr = vec::get_dky_array<NS>(s, m.time[tpi], dky);
+                    else
+                        dr = get_dky<NS>(s, m.time[tpi], dky);
+                    if (dr != CV_SUCCESS) {
                         status = BCM3HIP_STATUS_SOLVER_FAIL;
                         break;
                     }
@@ -504,7 +550,10 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                         }
                         next_disc = current_dose_time;
                     }
-                    reinit<NS>(s, t, y);
+                    if constexpr (VEC)
+                        vec::reinit<NS>(s, mdl, t, y);
+                    else
+                        reinit<NS>(s, t, y);
                     s.tstop = next_disc;
                     s.tstopset = 1;
                 }
@@ -562,8 +611,8 @@ __global__ void copy_status_kernel(int64_t n, const int32_t* __restrict__ src, i
 
 hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
                        double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
-                       bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, hipStream_t stream,
-                       hipEvent_t ev_start, hipEvent_t ev_stop)
+                       bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, int uni_solver,
+                       hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop)
 {
     const int64_t ntraj = n * (int64_t)m.P;
     if (ntraj == 0) return hipSuccess;
@@ -574,14 +623,18 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
     dim3 grid((unsigned)nblocks), block(64 * bw);
     const bool direct = (m.P == 1);
     const bool uni = (lpw == 1) && ntraj < (int64_t)1 << 30;
+    const bool vec_state = uni && (uni_solver == 0);
     double* logp_direct = direct ? logp : nullptr;
     if (ev_start) hipEventRecord(ev_start, stream);
 #define LAUNCH(PKT)                                                                                           \
-    if (uni)                                                                                                  \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, true>), grid, block, 0, stream, m, ntraj, lpw, values,        \
+    if (vec_state)                                                                                            \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC>), grid, block, 0, stream, m, ntraj, lpw, values,    \
+                           logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out);         \
+    else if (uni)                                                                                             \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_UNI>), grid, block, 0, stream, m, ntraj, lpw, values,    \
                            logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out);         \
     else                                                                                                      \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, false>), grid, block, 0, stream, m, ntraj, lpw, values,       \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_LANES>), grid, block, 0, stream, m, ntraj, lpw, values,  \
                            logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out)
     switch (m.pk_type) {
     case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;

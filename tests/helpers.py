@@ -31,10 +31,14 @@ def problem_fields(prob: O.PopPKProblem) -> dict:
     return {k: getattr(prob, k) for k in keys}
 
 
-def gpu_context(prob: O.PopPKProblem, lanes_per_wave: int = 64):
+def gpu_context(prob: O.PopPKProblem, lanes_per_wave: int = 64, uni_solver: int = 0):
+    """lanes_per_wave 1: one trajectory per wavefront, uni_solver 0 = lane-vector state
+    (bdf_vec.h), 1 = scalar state (bdf_uni.h); > 1: lane solver (bdf_lane.h)."""
     from bcm3_amd import _hip
     ctx = _hip.Context.popk(problem_fields(prob))
     ctx.set_option(_hip.OPT_LANES_PER_WAVE, lanes_per_wave)
+    if uni_solver:  # (0 is the library default)
+        ctx.set_option(_hip.OPT_UNI_SOLVER, uni_solver)
     return ctx
 
 

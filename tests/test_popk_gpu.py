@@ -78,8 +78,7 @@ def test_p64_population(orc):
                                      "two_transit"])
 @pytest.mark.parametrize("rule", ["daily", "intermittent1", "intermittent2", "intermittent3", "skipped",
                                   "dose_change", "interval12"])
-@pytest.mark.parametrize("lpw", [64, 1])
-def test_all_models_and_dosing_rules(orc, pk_type, rule, lpw):
+def test_all_models_and_dosing_rules(orc, pk_type, rule):
     kw = dict(P=2, T_days=6)
     if rule.startswith("intermittent"):
         kw["intermittent"] = int(rule[-1])
@@ -91,12 +90,25 @@ def test_all_models_and_dosing_rules(orc, pk_type, rule, lpw):
     elif rule == "interval12":
         kw["interval"] = 12.0
     prob, lo, hi = H.make_problem(pk_type, **kw)
-    ctx = H.gpu_context(prob, lanes_per_wave=lpw)  # lane solver and one-trajectory-per-wave solver
     vals = H.draws(lo, hi, 256, 91)
-    g = ctx.eval(vals, detail=True)
     o = orc.popk_eval(prob, vals, nthreads=8)
-    _check(prob, g, o)
-    ctx.close()
+    # the three solver layouts: one trajectory per wavefront with the state vectors across lanes
+    # (default), the same with scalar state, and 64 trajectories per wavefront (lane solver).
+    # The oracle envelope is checked on the first; the other two must agree with it bit for bit
+    # (log-likelihoods, every interpolated output, every solver counter).
+    ref = None
+    for lpw, uni_solver in ((1, 0), (1, 1), (64, 0)):
+        ctx = H.gpu_context(prob, lanes_per_wave=lpw, uni_solver=uni_solver)
+        g = ctx.eval(vals, detail=True)
+        ctx.close()
+        if ref is None:
+            _check(prob, g, o)
+            ref = g
+            continue
+        assert np.array_equal(g["logp"], ref["logp"]), (lpw, uni_solver)
+        assert np.array_equal(g["traj"], ref["traj"], equal_nan=True), (lpw, uni_solver)
+        for k in ref["stats"].dtype.names:
+            assert np.array_equal(g["stats"][k], ref["stats"][k]), (lpw, uni_solver, k)
 
 
 def test_max_steps_failures_give_minus_inf(orc):
@@ -133,11 +145,13 @@ def test_lanes_per_wave_invariant(c3):
     prob, ctx = c3
     vals = H.S.prior_draws(1, 300, 12)
     ref, _ = ctx.eval(vals)
-    for lpw in (1, 7, 32):
+    for lpw, uni_solver in ((1, 0), (1, 1), (7, 0), (32, 0)):
         ctx.set_option(_hip.OPT_LANES_PER_WAVE, lpw)
+        ctx.set_option(_hip.OPT_UNI_SOLVER, uni_solver)
         got, _ = ctx.eval(vals)
-        assert np.array_equal(got, ref), lpw
+        assert np.array_equal(got, ref), (lpw, uni_solver)
     ctx.set_option(_hip.OPT_LANES_PER_WAVE, 64)
+    ctx.set_option(_hip.OPT_UNI_SOLVER, 0)
 
 
 def test_empty_batch(c3):
