@@ -22,11 +22,13 @@ namespace vec {
 
 BDF_INL int lane_id() { return (int)(threadIdx.x & 63); }
 
-// value of lane J of this 16-lane row in every lane (v_mov_b64_dpp row_newbcast:J)
+// value of lane J of this 16-lane row in every lane (v_mov_b64_dpp row_newbcast:J). Every lane
+// is written (full row and bank masks), so the mov form needs no tied "old" operand -- no copy
+// of the source before each broadcast
 template <int J>
 BDF_INL double bc(double v)
 {
-    return __builtin_amdgcn_update_dpp(v, v, 0x150 + J, 0xf, 0xf, false);
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, false);
 }
 
 // component k (lane k) as a uniform value
@@ -79,7 +81,18 @@ BDF_INL double matvec(const double (&col)[NS], double x)
     return r;
 }
 
-template <int NS>
+// per-trajectory solver statistics only when the caller asked for them: without, the counters
+// compile to nothing (they would hold 8 SGPRs and a scalar add per event on the hot path)
+struct NoCount {
+    BDF_INL NoCount operator++(int) { return *this; }
+    BDF_INL NoCount& operator+=(int) { return *this; }
+    BDF_INL operator int() const { return 0; }
+};
+struct NoCounters {
+    NoCount nst_total, nfe, nni, nsetups, nje, netf, ncfn, nreinit;
+};
+
+template <int NS, bool STATS = true>
 struct VecState {
     double rtol, atol;
     double zn[QMAX + 1];  // lane i: component i
@@ -95,7 +108,7 @@ struct VecState {
     int nst, nstlp, nstlj;
     int nls_jcur;
     int check_tolsf;
-    BdfCounters cnt;
+    std::conditional_t<STATS, BdfCounters, NoCounters> cnt;
 #ifdef BCM3_PHASES
     long long ph[NPHASES];
     long long tlast;
@@ -470,9 +483,110 @@ BDF_INL int step_q(S& s, const Model& mdl, double eta_eff, double saved_t, int n
     return r;
 }
 
-// CVode(..., CV_ONE_STEP), same contract as uni::cvode_one_step_u (yout: uniform components)
+// The attempt loop of cvStep (cvode.c:2082-2174) from a given first attempt result onward:
+// r == PENDING runs the attempt at the current order, otherwise r / dsm are the outcome of the
+// first attempt (made by fast_run). Then the end of CVode's ONE_STEP return (tstop handling).
+constexpr int ATTEMPT_PENDING = -1;
+
+// end of CVode after a successful step (cvode.c:1249-1270): tstop reached / clamp the next h
+template <int NS, class S>
+BDF_INL int finish_step(S& s, double (&yout)[NS], double& tret)
+{
+    const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+    const bool reached = fabs(s.tn - s.tstop) <= troundoff;
+    if (BDF_UNLIKELY((s.tstopset != 0) & (reached | ((s.tn + s.hprime - s.tstop) * s.h > 0.0)))) {
+        if (reached) {
+            double v;
+            vec::get_dky(s, s.tstop, v);
+            vec::to_array<NS>(v, yout);
+            s.tretlast = tret = s.tstop;
+            s.tstopset = 0;
+            BDF_PH(9);
+            return CV_TSTOP_RETURN;
+        }
+        s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+        s.eta = fdiv(s.hprime, s.h);
+    }
+    s.tretlast = tret = s.tn;
+    BDF_PH(9);
+    return CV_SUCCESS;
+}
+
 template <int NS, class S, class Model>
-BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret, bool hot)
+BDF_INL int attempt_loop(S& s, const Model& mdl, double (&yout)[NS], double& tret, double saved_t, double eta_eff,
+                         int r, double dsm)
+{
+    int ncf = 0, nef = 0, nflag = FIRST_CALL;
+    for (;;) {
+        if (r == ATTEMPT_PENDING) {
+            switch (s.q) {
+            case 1: r = vec::step_q<1, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+            case 2: r = vec::step_q<2, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+            case 3: r = vec::step_q<3, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+            case 4: r = vec::step_q<4, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+            default: r = vec::step_q<5, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
+            }
+        }
+        BDF_PH(6);
+        if (BDF_LIKELY(r == uni::ATTEMPT_OK)) break;
+        const int failed = r;
+        r = ATTEMPT_PENDING;
+        eta_eff = 1.0;
+        s.etamax = 1.0;
+        if (failed == uni::ATTEMPT_CONV_FAIL) {
+            s.cnt.ncfn++;
+            ncf++;
+            if (ncf == MXNCF) return CV_CONV_FAILURE;
+            s.eta = ETACF;
+            nflag = PREV_CONV_FAIL;
+            eta_eff = s.eta;
+            continue;
+        }
+        nef++;
+        s.cnt.netf++;
+        nflag = PREV_ERR_FAIL;
+        if (nef == MXNEF) return CV_ERR_FAILURE;
+        if (nef <= MXNEF1) {
+            double eta = eta_from(BIAS2 * dsm, s.L);
+            eta = SUNMAX(ETAMIN, eta);
+            if (nef >= SMALL_NEF) eta = SUNMIN(eta, ETAMXF);
+            s.eta = eta;
+            eta_eff = s.eta;
+            continue;
+        }
+        s.eta = ETAMIN;
+        if (s.q > 1) {
+            vec::adjust_order(s, -1);
+            s.L = s.q;
+            s.q--;
+            s.qwait = s.L;
+            eta_eff = s.eta;
+            continue;
+        }
+        s.h *= s.eta;
+        s.hscale = s.h;
+        s.qwait = LONG_WAIT;
+        const double tv = mdl.rhs_v(s.tn, s.zn[0], s.acol);
+        s.cnt.nfe++;
+        s.zn[1] = s.h * tv;
+        eta_eff = 1.0;
+    }
+    return vec::finish_step<NS>(s, yout, tret);
+}
+
+// The step is split so that the attempt loop (5 order-specialised steps) is instantiated once in
+// the driver: cvode_entry and fast_run either finish the CVode call themselves or return
+// NEED_ATTEMPTS with the arguments of attempt_loop in a Pending record.
+constexpr int NEED_ATTEMPTS = 1000;
+struct Pending {
+    double saved_t, eta_eff, dsm;
+    int r;
+};
+
+// CVode(..., CV_ONE_STEP) up to the attempt loop, same contract as uni::cvode_one_step_u
+// (yout: uniform components); cvode_entry + attempt_loop == one CVode call
+template <int NS, class S, class Model>
+BDF_INL int cvode_entry(S& s, const Model& mdl, double tout, double (&yout)[NS], double& tret, bool hot, Pending& pd)
 {
     BDF_PH(0);
     {
@@ -539,87 +653,55 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
     }
     BDF_PH(1);
 
-    const double saved_t = s.tn;
-    int ncf = 0, nef = 0, nflag = FIRST_CALL;
+    pd.saved_t = s.tn;
     const bool adj = (s.nst > 0) & (s.hprime != s.h);
-    double eta_eff = adj ? s.eta : 1.0;
+    pd.eta_eff = adj ? s.eta : 1.0;
     if (BDF_UNLIKELY(adj & (s.qprime != s.q))) {
         vec::adjust_order(s, s.qprime - s.q);
         s.q = s.qprime;
         s.L = s.q + 1;
         s.qwait = s.L;
     }
-    double dsm = 0.0;
-    for (;;) {
-        int r;
-        switch (s.q) {
-        case 1: r = vec::step_q<1, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        case 2: r = vec::step_q<2, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        case 3: r = vec::step_q<3, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        case 4: r = vec::step_q<4, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        default: r = vec::step_q<5, NS>(s, mdl, eta_eff, saved_t, nflag, dsm); break;
-        }
-        BDF_PH(6);
-        if (BDF_LIKELY(r == uni::ATTEMPT_OK)) break;
-        eta_eff = 1.0;
-        s.etamax = 1.0;
-        if (r == uni::ATTEMPT_CONV_FAIL) {
-            s.cnt.ncfn++;
-            ncf++;
-            if (ncf == MXNCF) return CV_CONV_FAILURE;
-            s.eta = ETACF;
-            nflag = PREV_CONV_FAIL;
-            eta_eff = s.eta;
-            continue;
-        }
-        nef++;
-        s.cnt.netf++;
-        nflag = PREV_ERR_FAIL;
-        if (nef == MXNEF) return CV_ERR_FAILURE;
-        if (nef <= MXNEF1) {
-            double eta = eta_from(BIAS2 * dsm, s.L);
-            eta = SUNMAX(ETAMIN, eta);
-            if (nef >= SMALL_NEF) eta = SUNMIN(eta, ETAMXF);
-            s.eta = eta;
-            eta_eff = s.eta;
-            continue;
-        }
-        s.eta = ETAMIN;
-        if (s.q > 1) {
-            vec::adjust_order(s, -1);
-            s.L = s.q;
-            s.q--;
-            s.qwait = s.L;
-            eta_eff = s.eta;
-            continue;
-        }
-        s.h *= s.eta;
-        s.hscale = s.h;
-        s.qwait = LONG_WAIT;
-        const double tv = mdl.rhs_v(s.tn, s.zn[0], s.acol);
-        s.cnt.nfe++;
-        s.zn[1] = s.h * tv;
-        eta_eff = 1.0;
-    }
+    pd.r = ATTEMPT_PENDING;
+    pd.dsm = 0.0;
+    return NEED_ATTEMPTS;
+}
 
-    const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
-    const bool reached = fabs(s.tn - s.tstop) <= troundoff;
-    if (BDF_UNLIKELY((s.tstopset != 0) & (reached | ((s.tn + s.hprime - s.tstop) * s.h > 0.0)))) {
-        if (reached) {
-            double v;
-            vec::get_dky(s, s.tstop, v);
-            vec::to_array<NS>(v, yout);
-            s.tretlast = tret = s.tstop;
-            s.tstopset = 0;
-            BDF_PH(9);
-            return CV_TSTOP_RETURN;
+// Consecutive plain steps at order Q, as the driver would run them one cvode_one_step(hot) call
+// at a time, with the per-step bookkeeping of the general path folded into ONE exit test:
+// a step stays in the loop only when the general path would have (1) found no tstop event in
+// finish_step (tstop neither reached nor within the next step), (2) handed the driver a
+// CV_SUCCESS that triggers nothing there (no output time or end time passed, step budget not
+// exhausted, no discontinuity at t), and (3) next entered cvode_one_step hot with no order change
+// pending. Preconditions (checked by the caller): the last step was such a hot CV_SUCCESS, q == Q,
+// qprime == Q, nst > 0, check_tolsf == 0, tstopset and tstop == next_disc. tlim = min(next
+// output time, end time). Returns the result of the last step exactly as cvode_one_step would;
+// the driver counts that step, the loop counts the others in current_step.
+template <int Q, int NS, class S, class Model>
+BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, double tlim, int& current_step,
+                     int max_steps, Pending& pd)
+{
+    for (;;) {
+        vec::ewt_set(s);
+        const double saved_t = s.tn;
+        const double eta_eff = (s.hprime != s.h) ? s.eta : 1.0;
+        double dsm;
+        const int r = vec::step_q<Q, NS>(s, mdl, eta_eff, saved_t, FIRST_CALL, dsm);
+        if (BDF_UNLIKELY(r != uni::ATTEMPT_OK)) {
+            // failed first attempt: the attempt loop takes over from here
+            s.tretlast = saved_t;
+            pd.saved_t = saved_t;
+            pd.eta_eff = eta_eff;
+            pd.r = r;
+            pd.dsm = dsm;
+            return NEED_ATTEMPTS;
         }
-        s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
-        s.eta = fdiv(s.hprime, s.h);
+        const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+        const bool quiet = (fabs(s.tn - s.tstop) > troundoff) & !((s.tn + s.hprime - s.tstop) * s.h > 0.0) &
+                           (s.tn < tlim) & (s.qprime == Q) & (current_step + 1 != max_steps);
+        if (BDF_UNLIKELY(!quiet)) return vec::finish_step<NS>(s, yout, tret);
+        current_step++;
     }
-    s.tretlast = tret = s.tn;
-    BDF_PH(9);
-    return CV_SUCCESS;
 }
 
 }  // namespace vec

@@ -287,7 +287,7 @@ BDF_INL bool check_give_treatment(double t, const uint8_t* skipped, int intermit
 // state vectors across lanes: bdf_vec.h). All three give the same bits.
 enum { POPK_LANES = 0, POPK_UNI = 1, POPK_VEC = 2 };
 
-template <int PKT, int MODE>
+template <int PKT, int MODE, bool STATS>
 __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t ntraj, int lpw,
                                                         const double* __restrict__ values,
                                                         double* __restrict__ logp_direct,
@@ -355,9 +355,11 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         tsw = (lim < tsw) ? lim : tsw;
         mdl.ka2 = transform_var(m.transforms[ai], v[ai]);
     }
-    if constexpr (UNI) {
+    if constexpr (UNI && !VEC) {
         // values returned by out-of-line calls (ndtri_lower) count as divergent to the compiler;
-        // re-assert uniformity once so the whole solve stays on scalar control flow
+        // re-assert uniformity once so the whole solve stays on scalar control flow (the VEC
+        // solver keeps them in VGPRs: its control flow depends on them only through norms made
+        // uniform by lane_sum, and 20 fewer live SGPRs cut its SGPR spilling)
         mdl.ka = wave_uniform(mdl.ka);
         mdl.ke = wave_uniform(mdl.ke);
         mdl.kel = wave_uniform(mdl.kel);
@@ -400,8 +402,8 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     bool llh_done = false;  // NaN concentration seen: llh = -inf, stop accumulating
     int status = BCM3HIP_STATUS_OK;
 
-    std::conditional_t<VEC, vec::VecState<NS>, BdfState<NS, typename PKLane<PKT>::Inv>> s;
-    s.cnt = BdfCounters{0, 0, 0, 0, 0, 0, 0, 0};
+    std::conditional_t<VEC, vec::VecState<NS, STATS>, BdfState<NS, typename PKLane<PKT>::Inv>> s;
+    s.cnt = {};
     s.nst = 0;
 #ifdef BCM3_PHASES
     cfor<0, NPHASES>([&](auto k) __attribute__((always_inline)) { s.ph[CI(k)] = 0; });
@@ -472,9 +474,28 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             for (;;) {
                 double tret = 0.0;
                 int result;
-                if constexpr (VEC)
-                    result = vec::cvode_one_step<NS>(s, mdl, end_time, y, tret, hot);
-                else if constexpr (UNI)
+                if constexpr (VEC) {
+                    // after a plain step: run the following plain steps of the same order in
+                    // vec::fast_run (same results, one exit test per step)
+                    const bool fast = hot & (s.qprime == s.q) & (s.check_tolsf == 0) & (s.tstopset != 0) &
+                                      (s.tstop == next_disc);
+                    vec::Pending pd;
+                    if (BDF_LIKELY(fast)) {
+                        const double tlim = (next_out < end_time) ? next_out : end_time;
+                        const int ms = m.max_steps;
+                        switch (s.q) {
+                        case 1: result = vec::fast_run<1, NS>(s, mdl, y, tret, tlim, current_step, ms, pd); break;
+                        case 2: result = vec::fast_run<2, NS>(s, mdl, y, tret, tlim, current_step, ms, pd); break;
+                        case 3: result = vec::fast_run<3, NS>(s, mdl, y, tret, tlim, current_step, ms, pd); break;
+                        case 4: result = vec::fast_run<4, NS>(s, mdl, y, tret, tlim, current_step, ms, pd); break;
+                        default: result = vec::fast_run<5, NS>(s, mdl, y, tret, tlim, current_step, ms, pd); break;
+                        }
+                    } else {
+                        result = vec::cvode_entry<NS>(s, mdl, end_time, y, tret, hot, pd);
+                    }
+                    if (result == vec::NEED_ATTEMPTS)
+                        result = vec::attempt_loop<NS>(s, mdl, y, tret, pd.saved_t, pd.eta_eff, pd.r, pd.dsm);
+                } else if constexpr (UNI)
                     result = uni::cvode_one_step_u<NS>(s, mdl, end_time, y, tret, hot);
                 else
                     result = cvode_one_step<NS>(s, mdl, end_time, y, tret);
@@ -569,7 +590,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     if (logp_direct) logp_direct[e] = 0.0 + llh;  // P == 1: logp = 0 + patient term
     if (patient_llh) patient_llh[g] = llh;
     if (traj_status) traj_status[g] = status;
-    if (stats_out) {
+    if (STATS && stats_out) {
         bcm3hip_traj_stats st;
         st.nst = s.cnt.nst_total;
         st.nfe = s.cnt.nfe;
@@ -627,14 +648,17 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
     double* logp_direct = direct ? logp : nullptr;
     if (ev_start) hipEventRecord(ev_start, stream);
 #define LAUNCH(PKT)                                                                                           \
-    if (vec_state)                                                                                            \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC>), grid, block, 0, stream, m, ntraj, lpw, values,    \
-                           logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out);         \
+    if (vec_state && !stats_out)                                                                              \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, false>), grid, block, 0, stream, m, ntraj, lpw,     \
+                           values, logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, nullptr);   \
+    else if (vec_state)                                                                                       \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, true>), grid, block, 0, stream, m, ntraj, lpw,      \
+                           values, logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out); \
     else if (uni)                                                                                             \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_UNI>), grid, block, 0, stream, m, ntraj, lpw, values,    \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_UNI, true>), grid, block, 0, stream, m, ntraj, lpw, values, \
                            logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out);         \
     else                                                                                                      \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_LANES>), grid, block, 0, stream, m, ntraj, lpw, values,  \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_LANES, true>), grid, block, 0, stream, m, ntraj, lpw, values,  \
                            logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out)
     switch (m.pk_type) {
     case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;
