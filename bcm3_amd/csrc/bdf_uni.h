@@ -89,10 +89,10 @@ BDF_INL double set_bdf_q(S& s)
     const double A2 = __builtin_fma((double)q, A1, 1.0);
     const double lq = s.l[q];
     s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
-    // tq[5] is read only in the two steps after this one when qwait is 2 or 1 here
-    // (saved_tq5 at qwait == 1, etaqp1 at qwait == 0); tq[1], tq[3] only at qwait == 1
-    if (s.qwait <= 2) {
-        s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
+    // tq[5] unconditionally as cvSetTqBDF does (qwait <= 2, when it is read, holds in almost every
+    // step, so a branch around it costs more than it saves); tq[1], tq[3] only at qwait == 1
+    s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
+    {
         if (s.qwait == 1) {
             // qwait == 1 block of cvSetTqBDF
             double tq1 = 1.0;

@@ -55,21 +55,28 @@ BDF_INL void to_array(double v, double (&a)[NS])
     cfor<0, NS>([&](auto i) __attribute__((always_inline)) { a[CI(i)] = comp(v, CI(i)); });
 }
 
-// sum over the components in component order ((c0 + c1) + c2), uniform
+// sum over the components in component order ((c0 + c1) + c2), in every lane of row 0
 template <int NS>
-BDF_INL double lane_sum(double p)
+BDF_INL double lane_sum_v(double p)
 {
     double s = bc<0>(p) + bc<1>(p);
     if constexpr (NS == 3) s = s + bc<2>(p);
-    return wave_uniform(s);
+    return s;
+}
+// ... made uniform
+template <int NS>
+BDF_INL double lane_sum(double p)
+{
+    return wave_uniform(lane_sum_v<NS>(p));
 }
 
-// N_VWrmsNorm (wrms of bdf_lane.h)
+// N_VWrmsNorm (wrms of bdf_lane.h); the quotient and square root run on the lane value and only
+// the norm is made uniform (a uniform operand pair would need a copy back into VGPRs first)
 template <int NS>
 BDF_INL double wrms(double x, double w)
 {
     const double p = x * w;
-    return fsqrt(fdiv_c(vec::lane_sum<NS>(p * p), (double)NS, 1.0 / NS));
+    return wave_uniform(fsqrt(fdiv_c(vec::lane_sum_v<NS>(p * p), (double)NS, 1.0 / NS)));
 }
 
 // y = M x for M held as lane columns (lane i of col[j] = m(i, j))
@@ -321,6 +328,79 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
     return CV_SUCCESS;
 }
 
+// cvSetBDF + cvSetTqBDF + cvSet for order Q (uni::set_bdf_q) without the qwait == 1 block of
+// cvSetTqBDF: tq[1] and tq[3] are read only by the order-change candidates, which run in the
+// completion of the same step exactly when qwait was 1 here, so tq_13 computes them there from
+// the intermediates kept in TqCtx (no per-step branch on qwait in the attempt)
+struct TqCtx {
+    double alpha0, alpha0_hat, xi_inv, xistar_inv, hsum2, lq, A2;  // hsum2: before complete shifts tau
+};
+
+template <int Q, class S>
+BDF_INL double set_bdf_q(S& s, TqCtx& c)
+{
+    constexpr int q = Q;
+    double alpha0, alpha0_hat, xi_inv, xistar_inv, hsum;
+    s.l[0] = s.l[1] = xi_inv = xistar_inv = 1.0;
+    cfor<2, Q + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = 0.0; });
+    alpha0 = alpha0_hat = -1.0;
+    hsum = s.h;
+    if constexpr (q > 1) {
+        cfor<2, Q>([&](auto j) __attribute__((always_inline)) {
+            hsum += s.tau[CI(j) - 1];
+            xi_inv = fdiv(s.h, hsum);
+            alpha0 -= 1.0 / CI(j);
+            cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xi_inv, s.l[CI(i)]); });
+        });
+        alpha0 -= 1.0 / q;
+        xistar_inv = -s.l[1] - alpha0;
+        hsum += s.tau[q - 1];
+        xi_inv = fdiv(s.h, hsum);
+        alpha0_hat = -s.l[1] - xi_inv;
+        cfor_down<Q, 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xistar_inv, s.l[CI(i)]); });
+    }
+    const double A1 = 1.0 - alpha0_hat + alpha0;
+    const double A2 = __builtin_fma((double)q, A1, 1.0);
+    const double lq = s.l[q];
+    s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
+    s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
+    c.alpha0 = alpha0;
+    c.alpha0_hat = alpha0_hat;
+    c.xi_inv = xi_inv;
+    c.xistar_inv = xistar_inv;
+    c.hsum2 = hsum + s.tau[q];
+    c.lq = lq;
+    c.A2 = A2;
+    const double rl1 = frcp(s.l[1]);
+    s.gamma = s.h * rl1;
+    s.gammap = (s.nst == 0) ? s.gamma : s.gammap;
+    const double gr = fdiv(s.gamma, s.gammap);
+    s.gamrat = (s.nst > 0) ? gr : 1.0;
+    return rl1;
+}
+
+// the qwait == 1 block of cvSetTqBDF (uni::set_bdf_q), from the same operands
+template <int Q, class S>
+BDF_INL void tq_13(S& s, const TqCtx& c)
+{
+    constexpr int q = Q;
+    double tq1 = 1.0;
+    if constexpr (q > 1) {
+        const double C = fdiv(c.xistar_inv, c.lq);
+        const double A3 = c.alpha0 + 1.0 / q;
+        const double A4 = c.alpha0_hat + c.xi_inv;
+        const double Cpinv = fdiv(1.0 - A4 + A3, A3);
+        tq1 = fabs(C * Cpinv);
+    }
+    const double xi_inv2 = fdiv(s.h, c.hsum2);
+    const double A5 = c.alpha0 - 1.0 / (q + 1);
+    const double A6 = c.alpha0_hat - xi_inv2;
+    const double Cppinv = fdiv(1.0 - A6 + A5, c.A2);
+    const double tq3 = fabs(fdiv(Cppinv, xi_inv2 * (double)(q + 2) * A5));
+    s.tq[1] = tq1;
+    s.tq[3] = tq3;
+}
+
 // one Newton correction (uni::newton_correction)
 template <int NS, class S, class Model>
 BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& cscale, bool setup, bool jbad,
@@ -354,15 +434,14 @@ BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& csc
     return vec::wrms<NS>(x, s.ewt);
 }
 
-// Newton iteration, first iteration peeled (uni::newton_u)
+// Newton iteration (uni::newton_u) after its first correction del (made by attempt_q)
 template <int NS, class S, class Model>
-BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callSetup)
+BDF_INL bool newton_rest(S& s, const Model& mdl, double rl1, int convfail, bool callSetup, double cscale, double del)
 {
     bool jbad = false;
-    double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
-    for (;;) {
-        double del = vec::newton_correction<NS>(s, mdl, rl1, cscale, callSetup, jbad, convfail);
-        if (BDF_LIKELY(del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES)) {
+    for (bool first = true;; first = false) {
+        if (!first) del = vec::newton_correction<NS>(s, mdl, rl1, cscale, callSetup, jbad, convfail);
+        if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
             s.acnrm = del;
             s.nls_jcur = 0;
             return true;
@@ -389,20 +468,34 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
     }
 }
 
+// One attempt at order Q (uni::attempt_q). The usual outcome -- Newton converges on its first
+// correction and the error test passes -- is decided by ONE branch on both tests (the local
+// error dsm = acnrm tq[2] of a first-iteration convergence is del tq[2]); anything else goes on
+// through newton_rest, which repeats the convergence test on the same del.
 template <int Q, int NS, class S, class Model>
-BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm)
+BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm, TqCtx& tc)
 {
     if (BDF_UNLIKELY(eta_eff != 1.0)) vec::rescale_q<Q>(s, eta_eff);
     BDF_PH(2);
     vec::predict_q<Q>(s);
     BDF_PH(3);
-    const double rl1 = uni::set_bdf_q<Q>(s);
+    const double rl1 = vec::set_bdf_q<Q>(s, tc);
     BDF_PH(4);
     const int convfail = ((nflag == FIRST_CALL) | (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
     const bool callSetup = (nflag == PREV_CONV_FAIL) | (nflag == PREV_ERR_FAIL) | (s.nst == 0) |
                            (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);
     s.acor = 0.0;
-    const bool conv = vec::newton<NS>(s, mdl, rl1, convfail, callSetup);
+    double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
+    const double del = vec::newton_correction<NS>(s, mdl, rl1, cscale, callSetup, false, convfail);
+    const double dsm1 = del * s.tq[2];
+    if (BDF_LIKELY((del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) & (dsm1 <= 1.0))) {
+        s.acnrm = del;
+        s.nls_jcur = 0;
+        dsm = dsm1;
+        BDF_PH(5);
+        return uni::ATTEMPT_OK;
+    }
+    const bool conv = vec::newton_rest<NS>(s, mdl, rl1, convfail, callSetup, cscale, del);
     BDF_PH(5);
     dsm = s.acnrm * s.tq[2];
     if (BDF_LIKELY(conv & (dsm <= 1.0))) return uni::ATTEMPT_OK;
@@ -410,8 +503,10 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
     return conv ? uni::ATTEMPT_ERR_FAIL : uni::ATTEMPT_CONV_FAIL;
 }
 
-template <int Q, int NS, class S>
-BDF_INL void complete_q(S& s, double dsm)
+// FAST: called from fast_run, where the step's first attempt passed, so etamax is the value the
+// previous completion set (ETAMX2 / ETAMX3) or ReInit's ETAMX1 -- never 1
+template <int Q, int NS, bool FAST, class S>
+BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc)
 {
     constexpr int q = Q;
     s.nst++;
@@ -429,7 +524,7 @@ BDF_INL void complete_q(S& s, double dsm)
     }
     BDF_PH(7);
 
-    if (BDF_UNLIKELY(s.etamax == 1.0)) {
+    if (BDF_UNLIKELY(!FAST && (s.etamax == 1.0))) {
         s.qwait = SUNMAX(s.qwait, 2);
         s.qprime = q;
         s.hprime = s.h;
@@ -440,6 +535,7 @@ BDF_INL void complete_q(S& s, double dsm)
         s.qprime = q;
         if (s.qwait == 0) {
             s.qwait = 2;
+            vec::tq_13<q>(s, tc);  // qwait was 1 in this step's set_bdf_q
             double etaqm1 = 0.0, etaqp1 = 0.0;
             if constexpr (q > 1) etaqm1 = uni::eta_candidate<q>(BIAS1 * vec::wrms<NS>(s.zn[q], s.ewt) * s.tq[1]);
             if constexpr (q != QMAX) {
@@ -472,11 +568,12 @@ BDF_INL void complete_q(S& s, double dsm)
     s.acor *= s.tq[2];
 }
 
-template <int Q, int NS, class S, class Model>
+template <int Q, int NS, bool FAST = false, class S, class Model>
 BDF_INL int step_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm)
 {
-    const int r = vec::attempt_q<Q, NS>(s, mdl, eta_eff, saved_t, nflag, dsm);
-    if (BDF_LIKELY(r == uni::ATTEMPT_OK)) vec::complete_q<Q, NS>(s, dsm);
+    TqCtx tc;
+    const int r = vec::attempt_q<Q, NS>(s, mdl, eta_eff, saved_t, nflag, dsm, tc);
+    if (BDF_LIKELY(r == uni::ATTEMPT_OK)) vec::complete_q<Q, NS, FAST>(s, dsm, tc);
 #ifdef BCM3_PHASES
     if (r == uni::ATTEMPT_OK) s.qh[Q]++;
 #endif
@@ -686,7 +783,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         const double saved_t = s.tn;
         const double eta_eff = (s.hprime != s.h) ? s.eta : 1.0;
         double dsm;
-        const int r = vec::step_q<Q, NS>(s, mdl, eta_eff, saved_t, FIRST_CALL, dsm);
+        const int r = vec::step_q<Q, NS, true>(s, mdl, eta_eff, saved_t, FIRST_CALL, dsm);
         if (BDF_UNLIKELY(r != uni::ATTEMPT_OK)) {
             // failed first attempt: the attempt loop takes over from here
             s.tretlast = saved_t;
