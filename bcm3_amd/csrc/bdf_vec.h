@@ -505,8 +505,9 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
 
 // FAST: called from fast_run, where the step's first attempt passed, so etamax is the value the
 // previous completion set (ETAMX2 / ETAMX3) or ReInit's ETAMX1 -- never 1
-template <int Q, int NS, bool FAST, class S>
-BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc)
+// cvCompleteStep (complete_head_q) + cvPrepareNextStep (complete_eta_q)
+template <int Q, class S>
+BDF_INL void complete_head_q(S& s)
 {
     constexpr int q = Q;
     s.nst++;
@@ -523,7 +524,12 @@ BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc)
         s.saved_tq5 = save ? s.tq[5] : s.saved_tq5;
     }
     BDF_PH(7);
+}
 
+template <int Q, int NS, bool FAST, class S>
+BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
+{
+    constexpr int q = Q;
     if (BDF_UNLIKELY(!FAST && (s.etamax == 1.0))) {
         s.qwait = SUNMAX(s.qwait, 2);
         s.qprime = q;
@@ -566,6 +572,13 @@ BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc)
     BDF_PH(8);
     s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
     s.acor *= s.tq[2];
+}
+
+template <int Q, int NS, bool FAST, class S>
+BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc)
+{
+    vec::complete_head_q<Q>(s);
+    vec::complete_eta_q<Q, NS, FAST>(s, dsm, tc);
 }
 
 template <int Q, int NS, bool FAST = false, class S, class Model>
@@ -783,7 +796,8 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         const double saved_t = s.tn;
         const double eta_eff = (s.hprime != s.h) ? s.eta : 1.0;
         double dsm;
-        const int r = vec::step_q<Q, NS, true>(s, mdl, eta_eff, saved_t, FIRST_CALL, dsm);
+        TqCtx tc;
+        const int r = vec::attempt_q<Q, NS>(s, mdl, eta_eff, saved_t, FIRST_CALL, dsm, tc);
         if (BDF_UNLIKELY(r != uni::ATTEMPT_OK)) {
             // failed first attempt: the attempt loop takes over from here
             s.tretlast = saved_t;
@@ -793,6 +807,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             pd.dsm = dsm;
             return NEED_ATTEMPTS;
         }
+        vec::complete_q<Q, NS, true>(s, dsm, tc);
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         const bool quiet = (fabs(s.tn - s.tstop) > troundoff) & !((s.tn + s.hprime - s.tstop) * s.h > 0.0) &
                            (s.tn < tlim) & (s.qprime == Q) & (current_step + 1 != max_steps);
