@@ -475,12 +475,19 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                 double tret = 0.0;
                 int result;
                 if constexpr (VEC) {
-                    // after a plain step: run the following plain steps of the same order in
-                    // vec::fast_run (same results, one exit test per step)
-                    const bool fast = hot & (s.qprime == s.q) & (s.check_tolsf == 0) & (s.tstopset != 0) &
-                                      (s.tstop == next_disc);
+                    // after a plain step: run the following plain steps in vec::fast_run (same
+                    // results, one exit test per step); an order change the last step decided is
+                    // made here first, as cvode_entry would (it always comes with hprime != h)
+                    const bool fast = hot & ((s.qprime == s.q) | (s.hprime != s.h)) & (s.check_tolsf == 0) &
+                                      (s.tstopset != 0) & (s.tstop == next_disc);
                     vec::Pending pd;
                     if (BDF_LIKELY(fast)) {
+                        if (BDF_UNLIKELY(s.qprime != s.q)) {
+                            vec::adjust_order(s, s.qprime - s.q);
+                            s.q = s.qprime;
+                            s.L = s.q + 1;
+                            s.qwait = s.L;
+                        }
                         const double tlim = (next_out < end_time) ? next_out : end_time;
                         const int ms = m.max_steps;
                         switch (s.q) {
