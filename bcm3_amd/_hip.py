@@ -19,6 +19,8 @@ PK_TYPES = {"one": 0, "two": 1, "one_biphasic": 2, "two_biphasic": 3, "one_trans
 ANALYTIC_BANANA, ANALYTIC_CIRCULAR = 1, 2
 OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES, OPT_TIMING_LOG, OPT_UNI_SOLVER = 1, 2, 3, 4
 PRIOR_UNIFORM, PRIOR_NORMAL = 0, 1
+PROPOSAL_GLOBAL_COVARIANCE, PROPOSAL_GAUSSIAN_MIXTURE = 0, 1
+PROPOSAL_KMAX = 16
 
 
 class PopPKModel(C.Structure):
@@ -47,6 +49,15 @@ class AnalyticModel(C.Structure):
 class TrajStats(C.Structure):
     """bcm3hip_traj_stats"""
     _fields_ = [(k, C.c_int32) for k in ("nst", "nfe", "nni", "nsetups", "nje", "netf", "ncfn", "nreinit")]
+
+
+class Proposal(C.Structure):
+    """bcm3hip_proposal (device pointers)"""
+    _fields_ = [("kind", C.c_int32), ("kmax", C.c_int32), ("t_dof", C.c_double),
+                ("target_acceptance", C.c_double), ("scaling_learning_rate", C.c_double),
+                ("scaling_ema_period", C.c_double)] + \
+               [(k, C.c_void_p) for k in ("lower", "upper", "ncomp", "weights", "mean", "chol", "logc", "scale",
+                                          "ema", "selected", "work")]
 
 
 STATS_DTYPE = np.dtype([(k, np.int32) for k in ("nst", "nfe", "nni", "nsetups", "nje", "netf", "ncfn", "nreinit")])
@@ -85,6 +96,11 @@ def lib() -> C.CDLL:
                                       u64, u64, vp]
     L.bcm3hip_pt_exchange_local.argtypes = [C.c_int, C.c_int, i64, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp,
                                             u64, u64, vp]
+    L.bcm3hip_ptmh_propose_adaptive.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp,
+                                                C.POINTER(Proposal), i64, u64, u64, vp]
+    L.bcm3hip_ptmh_accept_adaptive.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_double, vp, vp, vp, vp,
+                                               vp, vp, C.POINTER(Proposal), i64, u64, u64, vp]
+    L.bcm3hip_history_add.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp]
     L.bcm3hip_kernel_time_log.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(i64), C.POINTER(C.c_double)]
     L.bcm3hip_eval_batch.argtypes = [vp, sz, sz, vp, vp, vp]
     L.bcm3hip_eval_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
@@ -215,3 +231,28 @@ def pt_exchange_local(C, d, g0, start, wrap_local, temps, values, llh, lprior, l
     """bcm3hip_pt_exchange_local on device pointers (ints; acc_mask / accepted may be None)."""
     check(lib().bcm3hip_pt_exchange_local(C, d, g0, start, int(wrap_local), temps, values, llh, lprior, lpp,
                                           acc_mask, accepted, _u64(seed), _u64(rnd), stream), "pt_exchange_local")
+
+
+def ptmh_propose_adaptive(C, d, kind, p0, p1, temps, values, prop, lprior_prop, log_mh, proposal: Proposal, chain0,
+                          seed, it, stream=None):
+    """bcm3hip_ptmh_propose_adaptive on device pointers (ints) and a Proposal of device pointers."""
+    check(lib().bcm3hip_ptmh_propose_adaptive(C, d, kind, p0, p1, temps, values, prop, lprior_prop, log_mh,
+                                              C_byref(proposal), chain0, _u64(seed), _u64(it), stream),
+          "ptmh_propose_adaptive")
+
+
+def ptmh_accept_adaptive(C, d, temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values, lprior, llh, lpp,
+                         accept_out, accepted, proposal: Proposal, chain0, seed, it, stream=None):
+    """bcm3hip_ptmh_accept_adaptive on device pointers (ints; accept_out / accepted may be None)."""
+    check(lib().bcm3hip_ptmh_accept_adaptive(C, d, temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values,
+                                             lprior, llh, lpp, accept_out, accepted, C_byref(proposal), chain0,
+                                             _u64(seed), _u64(it), stream), "ptmh_accept_adaptive")
+
+
+def history_add(C, d, H, subsampling, temps, values, mask, history, counters, stream=None):
+    """bcm3hip_history_add on device pointers (ints; mask may be None)."""
+    check(lib().bcm3hip_history_add(C, d, H, subsampling, temps, values, mask, history, counters, stream),
+          "history_add")
+
+
+C_byref = C.byref

@@ -1,0 +1,588 @@
+// proposal_kernels.hip -- the adaptive proposals of SamplerPTChain::MutateMove (one_block blocking,
+// src/sampler/SamplerPTChain.cpp:241-310) as HIP kernels over all chains of a rank, with the
+// proposal state resident in HBM (bcm3hip_proposal, include/bcm3hip.h):
+//
+//   ptmh_propose_adaptive_kernel  Proposal::Update, GetNewSample (+ ReflectOnBounds), the prior of
+//                                 the new point and CalculateMHRatio, for
+//       global_covariance  ProposalGlobalCovariance (ProposalGlobalCovariance.cpp:20-47) with the
+//                          base Proposal::Update (Proposal.cpp:197-208);
+//       gaussian_mixture   ProposalGaussianMixture (ProposalGaussianMixture.cpp:20-99): component
+//                          chosen by the responsibilities of the current point (GMM.cpp:172-186),
+//                          per-component scale adaptation, MH ratio of the mixture densities;
+//     T == 0 chains draw from the prior (SamplerPTChain.cpp:221-240);
+//   ptmh_accept_adaptive_kernel   TestSample with the MH ratio (SamplerPTChain.cpp:465-481), the
+//                                 state update and Proposal::NotifyAccepted (Proposal.cpp:210-220,
+//                                 ProposalGaussianMixture.cpp:91-103);
+//   history_add_kernel            SampleHistory::AddSample (SampleHistory.cpp:32-45) after a mutate
+//                                 move (SamplerPTChain.cpp:309) or an exchange move (:374-379).
+//
+// One thread per chain: the per-chain work is O(K d^2) sequential triangular algebra on small
+// matrices (d = 12 for the PopPK configs), a few microseconds against the millisecond likelihood
+// launch between propose and accept. Arithmetic follows the reference's expressions in order
+// (sequential sums, no contraction: the library is built with -ffp-contract=off), so
+// tests/proposal_reference.py restates it operation for operation.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "../../include/bcm3hip.h"
+#include "ctr_rng.h"
+
+namespace bcm3hip {
+namespace {
+
+using rng::normal01;
+using rng::rng_key;
+using rng::u01;
+
+// MathFunctions.h:67-82 (boost::math::log1p -> log1p)
+__device__ double logsum2(double loga, double logb)
+{
+    if (logb > loga) {
+        const double t = loga;
+        loga = logb;
+        logb = t;
+    }
+    if (loga == -INFINITY) return loga;
+    const double diff = logb - loga;
+    if (diff < -500) return loga;
+    return loga + log1p(exp(diff));
+}
+
+// Proposal::ReflectOnBounds (Proposal.cpp:384-397); bounded to 4096 reflections (a proposal that
+// far outside is then folded in one step -- never reached by proposals within ~10^3 ranges)
+__device__ double reflect(double x, double lb, double ub)
+{
+    for (int it = 0; it < 4096; it++) {
+        if (x < lb)
+            x = lb + (lb - x);
+        else if (x > ub)
+            x = ub - (x - ub);
+        else
+            return x;
+    }
+    const double w = ub - lb;
+    double r = fmod(x - lb, 2.0 * w);
+    if (r < 0.0) r += 2.0 * w;
+    return (r <= w) ? lb + r : ub - (r - w);
+}
+
+// L s = v in place (Eigen matrixL().solveInPlace): forward substitution, sequential sums
+__device__ __forceinline__ void lower_solve(int d, const double* L, double* v)
+{
+    for (int i = 0; i < d; i++)
+    {
+        double acc = 0.0;
+        for (int j = 0; j < i; j++) acc += L[i * d + j] * v[j];
+        v[i] = (v[i] - acc) / L[i * d + i];
+    }
+}
+
+__device__ __forceinline__ double dot(int d, const double* a)
+{
+    double s = 0.0;
+    for (int i = 0; i < d; i++) s += a[i] * a[i];
+    return s;
+}
+
+// GMM::CalculateResponsibilities (GMM.cpp:172-186) with GMM::LogPdfMVN (:392-398) and
+// logsum(VectorReal) (MathFunctions.h:84-92)
+__device__ __forceinline__ void responsibilities(int K, int d, const double* x, const double* mean,
+                                                 const double* chol, const double* logc, const double* w, double* r,
+                                                 double* tmp)
+{
+    for (int k = 0; k < K; k++)
+    {
+        for (int i = 0; i < d; i++) tmp[i] = x[i] - mean[k * d + i];
+        lower_solve(d, chol + (int64_t)k * d * d, tmp);
+        r[k] = (logc[k] - 0.5 * dot(d, tmp)) + log(w[k]);
+    }
+    double m = r[0];
+    for (int k = 0; k < K; k++) m = (r[k] > m) ? r[k] : m;
+    double sum = 0.0;
+    for (int k = 0; k < K; k++) sum += exp(r[k] - m);
+    const double lsum = log(sum) + m;
+    double tot = 0.0;
+    for (int k = 0; k < K; k++)
+    {
+        r[k] = exp(r[k] - lsum);
+        tot += r[k];
+    }
+    for (int k = 0; k < K; k++) r[k] = r[k] / tot;
+}
+
+// RNG::GetGamma(k, theta) (RNG.cpp:84-111), Marsaglia-Tsang, normals by Box-Muller
+__device__ double gamma_draw(double k, double theta, uint64_t seed, uint64_t iter, uint64_t gc)
+{
+    double scale_u = 1.0;
+    if (k < 1.0) {
+        const double u = u01(rng_key(seed, iter, gc, rng::KEY_GAMMA_SMALLK));
+        scale_u = pow(u, 1.0 / k);
+        k = 1.0 + k;
+    }
+    const double dd = k - 0.33333333333333333333333333333333;
+    const double c = 0.33333333333333333333333333333333 / sqrt(dd);
+    int ni = 0, ui = 0;
+    double v = 1.0;
+    while (ni < 0x800 && ui < 0x800) {
+        double x;
+        do {
+            x = normal01(seed, iter, gc, rng::SLOT_GAMMA_NORMAL + ni);
+            ni++;
+            v = 1.0 + c * x;
+        } while (v <= 0.0 && ni < 0x800);
+        v = v * v * v;
+        const double u = u01(rng_key(seed, iter, gc, rng::KEY_GAMMA_UNIFORM + ui));
+        ui++;
+        if (u < 1 - 0.0331 * x * x * x * x) break;
+        if (log(u) < 0.5 * x * x + dd * (1 - v + log(v))) break;
+    }
+    return theta * dd * v * scale_u;
+}
+
+__device__ double prior_logpdf(int kind, double p0, double p1, double x)
+{
+    // UnivariateMarginal::EvaluateLogPDF (UnivariateMarginal.cpp:326-345)
+    if (kind == BCM3HIP_PRIOR_UNIFORM) return (x < p0 || x > p1) ? -INFINITY : -log(p1 - p0);
+    const double s = p1;
+    const double dx = x - p0;
+    return log(1.0 / sqrt(2.0 * s * s * 3.141592653589793)) - dx * dx * (1.0 / (2.0 * s * s));
+}
+
+// one chain of ptmh_propose_adaptive (see the file header); v, t: [d], rf, rr: [K] scratch
+__device__ __forceinline__ void propose_chain(int c, int d, const int32_t* __restrict__ kind,
+                                              const double* __restrict__ p0, const double* __restrict__ p1,
+                                              const double* __restrict__ temps, const double* __restrict__ values,
+                                              double* __restrict__ prop, double* __restrict__ lprior_prop,
+                                              double* __restrict__ log_mh, const bcm3hip_proposal& P, uint64_t gc,
+                                              uint64_t seed, uint64_t iter, double* v, double* t, double* rf,
+                                              double* rr)
+{
+    const double* cur = values + (int64_t)c * d;
+    double* nxt = prop + (int64_t)c * d;
+    double lmh = 0.0;
+    if (temps[c] == 0.0) {
+        // PriorIndependence::Sample: uniform a + u (b - a), normal mu + sigma z
+        for (int i = 0; i < d; i++) {
+            if (kind[i] == BCM3HIP_PRIOR_UNIFORM)
+                nxt[i] = p0[i] + u01(rng_key(seed, iter, gc, rng::KEY_PRIOR_UNIFORM + i)) * (p1[i] - p0[i]);
+            else
+                nxt[i] = p0[i] + p1[i] * normal01(seed, iter, gc, rng::SLOT_PRIOR_NORMAL + i);
+        }
+    } else {
+        const int Km = P.kmax;
+        int K = (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) ? P.ncomp[c] : 1;
+        K = (K < 1) ? 1 : ((K > Km) ? Km : K);
+        double* scale = P.scale + (int64_t)c * Km;
+        double* ema = P.ema + (int64_t)c * Km;
+        const double* mean = P.mean + (int64_t)c * Km * d;
+        const double* chol = P.chol + (int64_t)c * Km * d * d;
+        const double* logc = P.logc + (int64_t)c * Km;
+        const double* w = P.weights + (int64_t)c * Km;
+        const double slr = P.scaling_learning_rate;
+        const double target = P.target_acceptance;
+        int sel;
+        if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
+            // ProposalGaussianMixture::Update: only the component used last
+            const int last = P.selected[c];
+            if (last != -1) {
+                const double lrate = 1.0 + u01(rng_key(seed, iter, gc, rng::KEY_UPDATE)) * slr * K;
+                if (ema[last] < target / (1.0 - slr)) {
+                    scale[last] /= lrate;
+                    scale[last] = (scale[last] > 1e-4) ? scale[last] : 1e-4;
+                } else if (ema[last] > (1 + slr) * target) {
+                    scale[last] *= lrate;
+                    scale[last] = (scale[last] < 10.0) ? scale[last] : 10.0;
+                }
+            }
+            // the current point's values in v (read once)
+            for (int i = 0; i < d; i++) v[i] = cur[i];
+            responsibilities(K, d, v, mean, chol, logc, w, rf, t);
+            // RNG::Sample (RNG.cpp:41-56)
+            const double u = u01(rng_key(seed, iter, gc, rng::KEY_SELECT));
+            double acc = 0.0;
+            sel = K - 1;
+            bool found = false;
+            for (int k = 0; k < K; k++)
+            {
+                acc += rf[k];
+                if (!found && u < acc) {
+                    sel = k;
+                    found = true;
+                }
+            }
+        } else {
+            // Proposal::Update (base class)
+            const double lrate = 1.0 + u01(rng_key(seed, iter, gc, rng::KEY_UPDATE)) * slr;
+            if (ema[0] < 0.952381 * target) {
+                scale[0] /= lrate;
+                scale[0] = (scale[0] > 1e-4) ? scale[0] : 1e-4;
+            } else if (ema[0] > 1.05 * target) {
+                scale[0] *= lrate;
+                scale[0] = (scale[0] < 10.0) ? scale[0] : 10.0;
+            }
+            sel = 0;
+        }
+        double t_scale = 1.0;
+        if (P.t_dof > 0.0) {
+            const double wg = gamma_draw(0.5 * P.t_dof, 0.5 * P.t_dof, seed, iter, gc);
+            t_scale = 1.0 / sqrt(wg);  // bcm3::rsqrt (MathFunctions.h:35-48) to full precision
+        }
+        // x = L z, x *= t_scale * scale, new = x + current, reflected on the prior bounds
+        const double* Ls = chol + (int64_t)sel * d * d;
+        for (int i = 0; i < d; i++) t[i] = normal01(seed, iter, gc, i);
+        const double f = t_scale * scale[sel];
+        for (int i = 0; i < d; i++)
+        {
+            double x = 0.0;
+            for (int j = 0; j < i + 1; j++) x += Ls[i * d + j] * t[j];
+            v[i] = reflect(x * f + cur[i], P.lower[i], P.upper[i]);
+        }
+        if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
+            // ProposalGaussianMixture::CalculateMHRatio; v holds the new point, t is scratch
+            responsibilities(K, d, v, mean, chol, logc, w, rr, t);
+            double fwd = -INFINITY, rev = -INFINITY;
+            for (int k = 0; k < K; k++)
+            {
+                const double* Lk = chol + (int64_t)k * d * d;
+                const double sk = scale[k];
+                // forward: L s = (new - cur) / s_k; reverse: L s = -(new - cur) / s_k = -s
+                for (int i = 0; i < d; i++) t[i] = (v[i] - cur[i]) / sk;
+                lower_solve(d, Lk, t);
+                const double base = -log(sk * sk) + logc[k];
+                const double q = 0.5 * dot(d, t);  // the reverse solution is -t: same square sum
+                fwd = logsum2(fwd, (base - q) + log(rf[k]));
+                rev = logsum2(rev, (base - q) + log(rr[k]));
+            }
+            lmh = rev - fwd;
+        }
+        for (int i = 0; i < d; i++) nxt[i] = v[i];
+        P.selected[c] = sel;
+    }
+    double lp = 0.0;
+    for (int i = 0; i < d; i++) lp += prior_logpdf(kind[i], p0[i], p1[i], nxt[i]);
+    lprior_prop[c] = lp;
+    log_mh[c] = lmh;
+}
+
+// ---- one wavefront per chain, lane i = variable i (d <= 64) ----
+// The same arithmetic as propose_chain, element for element: the triangular solve runs in its
+// column form (after s_j is known, every row i > j adds L_ij s_j), which accumulates each row's
+// sum in the same j order as the row form; sums over variables / components run sequentially
+// over lanes (readlane chains), so the results are those of the thread-per-chain kernel.
+
+__device__ __forceinline__ double lane_bcast(double x, int j)  // x of lane j (j wave-uniform)
+{
+    const long long b = __builtin_bit_cast(long long, x);
+    const int lo = __builtin_amdgcn_readlane((int)b, j);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), j);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// lane i (< d) holds v_i and row i of L (Lrow); returns s_i of L s = v
+__device__ __forceinline__ double wave_lower_solve(int d, const double* Lrow, double v, int lane)
+{
+    double acc = 0.0, s = 0.0;
+    for (int j = 0; j < d; j++) {
+        if (lane == j) s = (v - acc) / Lrow[j];
+        const double sj = lane_bcast(s, j);
+        if (lane > j && lane < d) acc += Lrow[j] * sj;
+    }
+    return s;
+}
+
+// sum_{i<n} x_i in lane order (uniform result)
+__device__ __forceinline__ double wave_seq_sum(int n, double x)
+{
+    double s = 0.0;
+    for (int i = 0; i < n; i++) s += lane_bcast(x, i);
+    return s;
+}
+
+// responsibilities of the point x (lane i = x_i); lane k of the result = r_k
+__device__ __forceinline__ double wave_responsibilities(int K, int d, double x, const double* mean,
+                                                        const double* chol, const double* logc, const double* w,
+                                                        int lane)
+{
+    double r = 0.0;
+    for (int k = 0; k < K; k++) {
+        const double t0 = (lane < d) ? x - mean[k * d + lane] : 0.0;
+        const double t = wave_lower_solve(d, chol + (int64_t)k * d * d + (int64_t)((lane < d) ? lane : 0) * d, t0,
+                                          lane);
+        const double rk = (logc[k] - 0.5 * wave_seq_sum(d, (lane < d) ? t * t : 0.0)) + log(w[k]);
+        r = (lane == k) ? rk : r;
+    }
+    double m = lane_bcast(r, 0);
+    for (int k = 1; k < K; k++) {
+        const double rk = lane_bcast(r, k);
+        m = (rk > m) ? rk : m;
+    }
+    double sum = 0.0;
+    for (int k = 0; k < K; k++) sum += exp(lane_bcast(r, k) - m);
+    const double lsum = log(sum) + m;
+    const double e = exp(r - lsum);
+    const double tot = wave_seq_sum(K, e);
+    return e / tot;
+}
+
+__global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
+    int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0, const double* __restrict__ p1,
+    const double* __restrict__ temps, const double* __restrict__ values, double* __restrict__ prop,
+    double* __restrict__ lprior_prop, double* __restrict__ log_mh, bcm3hip_proposal P, int64_t chain0,
+    uint64_t seed, uint64_t iter)
+{
+    const int lane = threadIdx.x & 63;
+    const int c = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    if (c >= C) return;
+    const uint64_t gc = (uint64_t)(chain0 + c);
+    const bool on = lane < d;
+    const int li = on ? lane : 0;
+    const double cur = values[(int64_t)c * d + li];
+    double nxt;
+    double lmh = 0.0;
+    if (temps[c] == 0.0) {
+        if (kind[li] == BCM3HIP_PRIOR_UNIFORM)
+            nxt = p0[li] + u01(rng_key(seed, iter, gc, rng::KEY_PRIOR_UNIFORM + li)) * (p1[li] - p0[li]);
+        else
+            nxt = p0[li] + p1[li] * normal01(seed, iter, gc, rng::SLOT_PRIOR_NORMAL + li);
+    } else {
+        const int Km = P.kmax;
+        int K = (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) ? P.ncomp[c] : 1;
+        K = (K < 1) ? 1 : ((K > Km) ? Km : K);
+        double* scale = P.scale + (int64_t)c * Km;
+        double* ema = P.ema + (int64_t)c * Km;
+        const double* mean = P.mean + (int64_t)c * Km * d;
+        const double* chol = P.chol + (int64_t)c * Km * d * d;
+        const double* logc = P.logc + (int64_t)c * Km;
+        const double* w = P.weights + (int64_t)c * Km;
+        const double slr = P.scaling_learning_rate;
+        const double target = P.target_acceptance;
+        int sel;
+        double rf = 0.0;
+        // the scale Update changes (component upd, new value sc): kept in registers, since other
+        // lanes read it after lane 0's store
+        int upd = -1;
+        double sc = 0.0;
+        if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
+            const int last = P.selected[c];
+            if (last != -1) {
+                const double lrate = 1.0 + u01(rng_key(seed, iter, gc, rng::KEY_UPDATE)) * slr * K;
+                sc = scale[last];
+                if (ema[last] < target / (1.0 - slr)) {
+                    sc /= lrate;
+                    sc = (sc > 1e-4) ? sc : 1e-4;
+                } else if (ema[last] > (1 + slr) * target) {
+                    sc *= lrate;
+                    sc = (sc < 10.0) ? sc : 10.0;
+                }
+                if (lane == 0) scale[last] = sc;
+                upd = last;
+            }
+            rf = wave_responsibilities(K, d, cur, mean, chol, logc, w, lane);
+            const double u = u01(rng_key(seed, iter, gc, rng::KEY_SELECT));
+            double acc = 0.0;
+            sel = K - 1;
+            for (int k = 0; k < K; k++) {
+                acc += lane_bcast(rf, k);
+                if (u < acc) {
+                    sel = k;
+                    break;
+                }
+            }
+        } else {
+            const double lrate = 1.0 + u01(rng_key(seed, iter, gc, rng::KEY_UPDATE)) * slr;
+            sc = scale[0];
+            if (ema[0] < 0.952381 * target) {
+                sc /= lrate;
+                sc = (sc > 1e-4) ? sc : 1e-4;
+            } else if (ema[0] > 1.05 * target) {
+                sc *= lrate;
+                sc = (sc < 10.0) ? sc : 10.0;
+            }
+            if (lane == 0) scale[0] = sc;
+            upd = 0;
+            sel = 0;
+        }
+        double t_scale = 1.0;
+        if (P.t_dof > 0.0) {
+            const double wg = gamma_draw(0.5 * P.t_dof, 0.5 * P.t_dof, seed, iter, gc);
+            t_scale = 1.0 / sqrt(wg);
+        }
+        const double* Ls = chol + (int64_t)sel * d * d + (int64_t)li * d;
+        const double z = normal01(seed, iter, gc, li);
+        const double f = t_scale * ((sel == upd) ? sc : scale[sel]);
+        double x = 0.0;
+        for (int j = 0; j < d; j++) {
+            const double zj = lane_bcast(z, j);
+            if (j <= lane) x += Ls[j] * zj;
+        }
+        nxt = reflect(x * f + cur, P.lower[li], P.upper[li]);
+        if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
+            const double rr = wave_responsibilities(K, d, nxt, mean, chol, logc, w, lane);
+            double fwd = -INFINITY, rev = -INFINITY;
+            for (int k = 0; k < K; k++) {
+                const double sk = (k == upd) ? sc : scale[k];
+                const double t0 = on ? (nxt - cur) / sk : 0.0;
+                const double t = wave_lower_solve(d, chol + (int64_t)k * d * d + (int64_t)li * d, t0, lane);
+                const double base = -log(sk * sk) + logc[k];
+                const double q = 0.5 * wave_seq_sum(d, on ? t * t : 0.0);
+                fwd = logsum2(fwd, (base - q) + log(lane_bcast(rf, k)));
+                rev = logsum2(rev, (base - q) + log(lane_bcast(rr, k)));
+            }
+            lmh = rev - fwd;
+        }
+        if (lane == 0) P.selected[c] = sel;
+    }
+    if (on) prop[(int64_t)c * d + lane] = nxt;
+    const double lp = wave_seq_sum(d, on ? prior_logpdf(kind[li], p0[li], p1[li], nxt) : 0.0);
+    if (lane == 0) {
+        lprior_prop[c] = lp;
+        log_mh[c] = lmh;
+    }
+}
+
+// generic path (d > 64): one thread per chain, its vectors in the global work buffer
+__global__ void __launch_bounds__(64) ptmh_propose_adaptive_kernel(
+    int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0, const double* __restrict__ p1,
+    const double* __restrict__ temps, const double* __restrict__ values, double* __restrict__ prop,
+    double* __restrict__ lprior_prop, double* __restrict__ log_mh, bcm3hip_proposal P, int64_t chain0,
+    uint64_t seed, uint64_t iter)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const int Km = P.kmax;
+    double* work = P.work + (int64_t)c * (2 * Km + 2 * d);
+    propose_chain(c, d, kind, p0, p1, temps, values, prop, lprior_prop, log_mh, P, (uint64_t)(chain0 + c), seed,
+                  iter, work + 2 * Km, work + 2 * Km + d, work, work + Km);
+}
+
+__global__ void ptmh_accept_adaptive_kernel(int C, int d, const double* __restrict__ temps,
+                                            const double* __restrict__ prop, const double* __restrict__ lprior_prop,
+                                            const double* __restrict__ llh_prop, const double* __restrict__ log_mh,
+                                            double learning_rate, double* __restrict__ values,
+                                            double* __restrict__ lprior, double* __restrict__ llh,
+                                            double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
+                                            unsigned long long* __restrict__ accepted, bcm3hip_proposal P,
+                                            int64_t chain0, uint64_t seed, uint64_t iter)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    const double T = temps[c];
+    const double nl = llh_prop[c] * learning_rate;  // Sampler::EvaluateLikelihood
+    const double nq = lprior_prop[c];
+    bool acc;
+    double npp;
+    if (T == 0.0) {
+        acc = true;
+        npp = (nl == -INFINITY) ? nq : nq + T * nl;
+    } else {
+        npp = nq + T * nl;
+        acc = false;
+        if (npp > -INFINITY) {
+            double tp = npp - lpp[c];
+            tp = exp(tp + log_mh[c]);
+            tp = (tp < 1.0) ? tp : 1.0;  // std::min((Real)1.0, tp): NaN -> 1
+            acc = u01(rng_key(seed, iter, (uint64_t)(chain0 + c), rng::KEY_ACCEPT)) < tp;
+        }
+        // NotifyAccepted (EMA of the acceptance of the component that proposed)
+        const int sel = P.selected[c];
+        double* ema = P.ema + (int64_t)c * P.kmax + sel;
+        const double alpha = 2.0 / (P.scaling_ema_period + 1);
+        *ema += ((acc ? 1.0 : 0.0) - *ema) * alpha;
+    }
+    if (acc) {
+        for (int i = 0; i < d; i++) values[(int64_t)c * d + i] = prop[(int64_t)c * d + i];
+        lprior[c] = nq;
+        llh[c] = nl;
+        lpp[c] = npp;
+    }
+    if (acc_out) acc_out[c] = acc ? 1 : 0;
+    if (accepted && acc) atomicAdd(accepted, 1ull);
+}
+
+// SampleHistory::AddSample for the chains with T != 0 (and mask[c] != 0 when a mask is given):
+// every `subsampling`-th call stores the values as float in slot n % H of the chain's ring
+__global__ void history_add_kernel(int C, int d, int H, int subsampling, const double* __restrict__ temps,
+                                   const double* __restrict__ values, const uint8_t* __restrict__ mask,
+                                   float* __restrict__ hist, int64_t* __restrict__ counters)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    if (temps[c] == 0.0 || (mask && !mask[c])) return;
+    int64_t* n = counters + 2 * (int64_t)c;
+    n[1]++;
+    if (n[1] == subsampling) {
+        const int64_t ix = n[0] % H;
+        for (int i = 0; i < d; i++) hist[((int64_t)c * H + ix) * d + i] = (float)values[(int64_t)c * d + i];
+        n[0]++;
+        n[1] = 0;
+    }
+}
+
+bool proposal_ok(const bcm3hip_proposal* P, int C, int d)
+{
+    if (!P || P->kmax < 1 || P->kmax > BCM3HIP_PROPOSAL_KMAX) return false;
+    if (P->kind != BCM3HIP_PROPOSAL_GLOBAL_COVARIANCE && P->kind != BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) return false;
+    if (!(P->scaling_ema_period > 0.0) || !(P->t_dof >= 0.0)) return false;
+    if (C > 0 && (!P->lower || !P->upper || !P->ncomp || !P->weights || !P->mean || !P->chol || !P->logc ||
+                  !P->scale || !P->ema || !P->selected || !P->work))
+        return false;
+    return true;
+}
+
+}  // namespace
+}  // namespace bcm3hip
+
+using namespace bcm3hip;
+
+extern "C" {
+
+int bcm3hip_ptmh_propose_adaptive(int C, int d, const int32_t* prior_kind, const double* prior_p0,
+                                  const double* prior_p1, const double* temps, const double* values, double* prop,
+                                  double* lprior_prop, double* log_mh, const bcm3hip_proposal* proposal,
+                                  int64_t chain0, uint64_t seed, uint64_t iter, void* stream)
+{
+    if (C < 0 || d <= 0 || !proposal_ok(proposal, C, d) ||
+        (C > 0 && (!prior_kind || !prior_p0 || !prior_p1 || !temps || !values || !prop || !lprior_prop || !log_mh)))
+        return BCM3HIP_ERR_ARG;
+    if (C == 0) return 0;
+    // one wavefront per chain (lanes over variables) up to 64 variables, beyond one thread per chain
+    if (d <= 64)
+        hipLaunchKernelGGL(ptmh_propose_wave_kernel, dim3(C), dim3(64), 0, (hipStream_t)stream, C, d, prior_kind,
+                           prior_p0, prior_p1, temps, values, prop, lprior_prop, log_mh, *proposal, chain0, seed, iter);
+    else
+        hipLaunchKernelGGL(ptmh_propose_adaptive_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C,
+                           d, prior_kind, prior_p0, prior_p1, temps, values, prop, lprior_prop, log_mh, *proposal,
+                           chain0, seed, iter);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double* prop, const double* lprior_prop,
+                                 const double* llh_prop, const double* log_mh, double learning_rate, double* values,
+                                 double* lprior, double* llh, double* lpp, uint8_t* accept_out, uint64_t* accepted,
+                                 const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed, uint64_t iter,
+                                 void* stream)
+{
+    if (C < 0 || d <= 0 || !proposal_ok(proposal, C, d) ||
+        (C > 0 && (!temps || !prop || !lprior_prop || !llh_prop || !log_mh || !values || !lprior || !llh || !lpp)))
+        return BCM3HIP_ERR_ARG;
+    if (C == 0) return 0;
+    hipLaunchKernelGGL(ptmh_accept_adaptive_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d,
+                       temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values, lprior, llh, lpp, accept_out,
+                       (unsigned long long*)accepted, *proposal, chain0, seed, iter);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_history_add(int C, int d, int H, int subsampling, const double* temps, const double* values,
+                        const uint8_t* mask, float* history, int64_t* counters, void* stream)
+{
+    if (C < 0 || d <= 0 || H <= 0 || subsampling <= 0 || (C > 0 && (!temps || !values || !history || !counters)))
+        return BCM3HIP_ERR_ARG;
+    if (C == 0) return 0;
+    hipLaunchKernelGGL(history_add_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d, H,
+                       subsampling, temps, values, mask, history, counters);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+}  // extern "C"

@@ -9,44 +9,23 @@
 //                         one rank's slice of the temperature ladder (SamplerPT.cpp:277-298,
 //                         SamplerPTChain.cpp:328-381); pairs that straddle ranks are exchanged by the
 //                         host over RCCL (bcm3_amd/pt.py).
-// Random numbers are counter based (splitmix64 of seed, iteration, chain, slot), so a chain's
-// stream does not depend on how chains are distributed over ranks or blocks.
+// Random numbers are counter based (ctr_rng.h), so a chain's stream does not depend on how chains
+// are distributed over ranks or blocks.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <cstdint>
 
 #include "../../include/bcm3hip.h"
+#include "ctr_rng.h"
 
 namespace bcm3hip {
 namespace {
 
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
-{
-    x += 0x9E3779B97F4A7C15ull;
-    uint64_t z = x;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-// uniform in [0, 1) from 53 random bits
-__device__ __forceinline__ double u01(uint64_t z) { return (double)(z >> 11) * (1.0 / 9007199254740992.0); }
-
-// key for (seed, iteration, chain, slot); slot < 2^16
-__device__ __forceinline__ uint64_t rng_key(uint64_t seed, uint64_t iter, uint64_t chain, uint64_t slot)
-{
-    return splitmix64(splitmix64(seed) ^ (iter * 0x100000001B3ull) ^ (chain * 0xC2B2AE3D27D4EB4Full) ^
-                      (slot * 0x165667B19E3779F9ull));
-}
-
-// standard normal by Box-Muller from two counter-based uniforms
-__device__ __forceinline__ double normal01(uint64_t seed, uint64_t iter, uint64_t chain, uint64_t slot)
-{
-    const double u1 = 1.0 - u01(rng_key(seed, iter, chain, 2 * slot));  // (0, 1]
-    const double u2 = u01(rng_key(seed, iter, chain, 2 * slot + 1));
-    return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
-}
+using rng::normal01;
+using rng::rng_key;
+using rng::splitmix64;
+using rng::u01;
 
 __global__ void ptmh_propose_kernel(int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0,
                                     const double* __restrict__ p1, const double* __restrict__ scale,
@@ -64,9 +43,9 @@ __global__ void ptmh_propose_kernel(int C, int d, const int32_t* __restrict__ ki
         if (t0) {
             // PriorIndependence::Sample: uniform a + u (b - a), normal mu + sigma z
             if (kind[i] == BCM3HIP_PRIOR_UNIFORM)
-                x = p0[i] + u01(rng_key(seed, iter, gc, 0x8000 + i)) * (p1[i] - p0[i]);
+                x = p0[i] + u01(rng_key(seed, iter, gc, rng::KEY_PRIOR_UNIFORM + i)) * (p1[i] - p0[i]);
             else
-                x = p0[i] + p1[i] * normal01(seed, iter, gc, 0x4000 + i);
+                x = p0[i] + p1[i] * normal01(seed, iter, gc, rng::SLOT_PRIOR_NORMAL + i);
         } else {
             x = values[(int64_t)c * d + i] + scale[i] * normal01(seed, iter, gc, i);
         }
@@ -109,7 +88,7 @@ __global__ void ptmh_accept_kernel(int C, int d, const double* __restrict__ temp
         if (npp > -INFINITY) {
             double tp = exp(npp - lpp[c]);
             tp = (tp < 1.0) ? tp : 1.0;  // std::min((Real)1.0, tp): NaN -> 1
-            acc = u01(rng_key(seed, iter, (uint64_t)(chain0 + c), 0xC000)) < tp;
+            acc = u01(rng_key(seed, iter, (uint64_t)(chain0 + c), rng::KEY_ACCEPT)) < tp;
         }
     }
     if (acc) {

@@ -1,0 +1,215 @@
+"""Adaptive MCMC proposals with their state in HBM (one_block blocking).
+
+Host side of bcm3_amd/csrc/proposal_kernels.hip (include/bcm3hip.h: bcm3hip_proposal). Restates
+for the device sampler:
+
+* the proposal state a chain's Proposal object holds -- ProposalGlobalCovariance
+  (src/sampler/ProposalGlobalCovariance.cpp) and ProposalGaussianMixture
+  (src/sampler/ProposalGaussianMixture.cpp) with the base Proposal (src/sampler/Proposal.cpp):
+  Cholesky factors, log normalisers, adaptive scales and acceptance-rate EMAs per chain;
+* Proposal::Initialize / InitializeImpl (Proposal.cpp:33-140, ProposalGlobalCovariance.cpp:64-104,
+  ProposalGaussianMixture.cpp:125-254) -- the infrequent adaptation step, run here with torch on
+  the device (batched covariance and Cholesky over all chains of the rank);
+* SampleHistory (src/sampler/SampleHistory.cpp) as a per-chain float ring buffer in HBM.
+
+Adaptation of gaussian_mixture fits a single Gaussian component to the history (mean and the
+(n-1)-normalised covariance). The reference fits mixtures with 1-13 components by EM and keeps the
+lowest AIC (ProposalGaussianMixture.cpp:157-189; src/stats/GMM.cpp); that fit is outside the
+hot-path scope. Mixtures fitted elsewhere are loaded with set_mixture().
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+from . import _hip
+
+KINDS = {"global_covariance": _hip.PROPOSAL_GLOBAL_COVARIANCE, "gaussian_mixture": _hip.PROPOSAL_GAUSSIAN_MIXTURE}
+
+
+def target_acceptance_rate(d: int) -> float:
+    """Proposal::Initialize (Proposal.cpp:45-53)."""
+    return {1: 0.44, 2: 0.35, 3: 0.3}.get(d, 0.234)
+
+
+def log_normaliser(chol: torch.Tensor) -> torch.Tensor:
+    """-sum_j log L_jj - d/2 log(2 pi) over the last two dims (ProposalGlobalCovariance.cpp:96-101,
+    GMM::Set)."""
+    d = chol.shape[-1]
+    det = torch.log(torch.diagonal(chol, dim1=-2, dim2=-1)).sum(dim=-1)
+    return -det - 0.5 * d * math.log(2.0 * math.pi)
+
+
+class DeviceProposal:
+    """Per-chain proposal state of C chains (rank-local) for d variables."""
+
+    def __init__(self, kind: str, prior, temps: torch.Tensor, kmax: int = 1, t_dof: float = 0.0):
+        if kind not in KINDS:
+            raise ValueError(f"Unknown proposal type \"{kind}\"")
+        if not 1 <= kmax <= _hip.PROPOSAL_KMAX:
+            raise ValueError(f"kmax must be in 1..{_hip.PROPOSAL_KMAX}")
+        if kind == "global_covariance":
+            kmax = 1
+        dev = temps.device
+        self.kind, self.kmax, self.t_dof = kind, int(kmax), float(t_dof)
+        self.C, self.d = int(temps.numel()), prior.d
+        self.temps = temps
+        C, d, K = self.C, self.d, self.kmax
+        f64 = dict(dtype=torch.float64, device=dev)
+        inf = torch.full((d,), math.inf, **f64)
+        # Prior::GetLowerBound / GetUpperBound (UnivariateMarginal.cpp:627-647)
+        self.lower = torch.where(prior.is_uniform, prior.a, -inf).contiguous()
+        self.upper = torch.where(prior.is_uniform, prior.b, inf).contiguous()
+        # EvaluateMarginalMean / Variance (UnivariateMarginal.cpp:448-540)
+        self.prior_mean = torch.where(prior.is_uniform, 0.5 * (prior.b + prior.a), prior.mu)
+        width = prior.b - prior.a
+        self.prior_var = torch.where(prior.is_uniform, (width * width) / 12.0, prior.sigma * prior.sigma)
+        self.target = target_acceptance_rate(d)
+        self.ncomp = torch.ones(C, dtype=torch.int32, device=dev)
+        self.weights = torch.zeros((C, K), **f64)
+        self.mean = torch.zeros((C, K, d), **f64)
+        self.chol = torch.zeros((C, K, d, d), **f64)
+        self.logc = torch.zeros((C, K), **f64)
+        self.scale = torch.zeros((C, K), **f64)
+        self.ema = torch.zeros((C, K), **f64)
+        self.selected = torch.full((C,), -1, dtype=torch.int32, device=dev)
+        self.work = torch.zeros((C, 2 * K + 2 * d), **f64)
+        self.reset_from_prior(torch.ones(C, dtype=torch.bool, device=dev))
+        self.struct = _hip.Proposal(
+            kind=KINDS[kind], kmax=K, t_dof=self.t_dof, target_acceptance=self.target,
+            scaling_learning_rate=0.05, scaling_ema_period=1000.0,
+            lower=self.lower.data_ptr(), upper=self.upper.data_ptr(), ncomp=self.ncomp.data_ptr(),
+            weights=self.weights.data_ptr(), mean=self.mean.data_ptr(), chol=self.chol.data_ptr(),
+            logc=self.logc.data_ptr(), scale=self.scale.data_ptr(), ema=self.ema.data_ptr(),
+            selected=self.selected.data_ptr(), work=self.work.data_ptr())
+
+    # ---- InitializeImpl without usable history: a single Gaussian from the prior's moments
+    def reset_from_prior(self, chains: torch.Tensor):
+        d = self.d
+        L = torch.diag_embed(torch.sqrt(self.prior_var))  # llt of a diagonal matrix
+        self._set_single(chains, self.prior_mean.expand(self.C, d), L.expand(self.C, d, d))
+        self._reset_scales(chains, initial=True)
+
+    def _set_single(self, chains, mean, L):
+        m = chains.view(-1, 1)
+        self.ncomp.copy_(torch.where(chains, torch.ones_like(self.ncomp), self.ncomp))
+        w = torch.zeros_like(self.weights)
+        w[:, 0] = 1.0
+        self.weights.copy_(torch.where(m, w, self.weights))
+        newmean = torch.zeros_like(self.mean)
+        newmean[:, 0] = mean
+        self.mean.copy_(torch.where(m.view(-1, 1, 1), newmean, self.mean))
+        newchol = torch.zeros_like(self.chol)
+        newchol[:, 0] = L
+        # unused slots keep an identity factor so that no kernel path can divide by zero
+        for k in range(1, self.kmax):
+            newchol[:, k] = torch.eye(self.d, dtype=torch.float64, device=self.chol.device)
+        self.chol.copy_(torch.where(m.view(-1, 1, 1, 1), newchol, self.chol))
+        self.logc.copy_(torch.where(m, log_normaliser(self.chol), self.logc))
+
+    def _reset_scales(self, chains, initial: bool):
+        m = chains.view(-1, 1)
+        if self.kind == "gaussian_mixture":
+            # ProposalGaussianMixture::InitializeImpl (:250-251), at every (re)initialisation
+            s = torch.full_like(self.scale, 2.38 / math.sqrt(self.d))
+            e = torch.full_like(self.ema, self.target)
+        elif initial:
+            # Proposal() constructor (Proposal.cpp:26-29): adaptive_scale 1, acceptance EMA 0.23
+            s = torch.ones_like(self.scale)
+            e = torch.full_like(self.ema, 0.23)
+        else:
+            return  # ProposalGlobalCovariance keeps its adaptive scale across adaptations
+        self.scale.copy_(torch.where(m, s, self.scale))
+        self.ema.copy_(torch.where(m, e, self.ema))
+        # selected_component is set once, in the constructor (ProposalGaussianMixture.cpp:10-14); a
+        # refit keeps it unless it no longer names a component
+        stale = (self.selected >= self.ncomp) if not initial else torch.ones_like(chains)
+        self.selected.copy_(torch.where(chains & stale, torch.full_like(self.selected, -1), self.selected))
+
+    def set_mixture(self, chain: int, weights, means, covariances):
+        """Load a fitted mixture for one chain (ProposalGaussianMixture after GMM::Set)."""
+        if self.kind != "gaussian_mixture":
+            raise ValueError("set_mixture needs a gaussian_mixture proposal")
+        w = torch.as_tensor(weights, dtype=torch.float64, device=self.chol.device)
+        K = int(w.numel())
+        if not 1 <= K <= self.kmax:
+            raise ValueError(f"{K} components do not fit kmax={self.kmax}")
+        mu = torch.as_tensor(means, dtype=torch.float64, device=self.chol.device).reshape(K, self.d)
+        cov = torch.as_tensor(covariances, dtype=torch.float64, device=self.chol.device).reshape(K, self.d, self.d)
+        L, info = torch.linalg.cholesky_ex(cov)
+        if bool((info != 0).any()):
+            raise ValueError("component covariance is not positive definite")
+        self.ncomp[chain] = K
+        self.weights[chain].zero_()
+        self.weights[chain, :K] = w
+        self.mean[chain].zero_()
+        self.mean[chain, :K] = mu
+        eye = torch.eye(self.d, dtype=torch.float64, device=self.chol.device)
+        self.chol[chain] = eye
+        self.chol[chain, :K] = L
+        self.logc[chain] = log_normaliser(self.chol[chain])
+        self.scale[chain] = 2.38 / math.sqrt(self.d)
+        self.ema[chain] = self.target
+        self.selected[chain] = -1
+
+    # ---- Proposal::Initialize from the sample history (AdaptProposal, SamplerPTChain.cpp:120-200)
+    def adapt(self, history: torch.Tensor, counters: torch.Tensor):
+        """history [C][H][d] float32 ring, counters [C][2] (bcm3hip_history_add). Chains at T == 0
+        are not adapted (SamplerPTChain::AdaptProposal returns early)."""
+        C, H, d = history.shape
+        n = torch.clamp(counters[:, 0], max=H)
+        active = self.temps != 0.0
+        fit = active & (n >= 2)
+        if bool(fit.any()):
+            idx = torch.arange(H, device=history.device).view(1, H, 1)
+            valid = (idx < n.view(C, 1, 1)).to(torch.float64)
+            x = history.to(torch.float64) * valid
+            cnt = n.to(torch.float64).clamp(min=2.0).view(C, 1)
+            mean = x.sum(dim=1) / cnt
+            xc = (history.to(torch.float64) - mean.view(C, 1, d)) * valid
+            cov = xc.transpose(1, 2) @ xc / (cnt.view(C, 1, 1) - 1.0)
+            # diagonal at least 1e-6 of the prior variance (ProposalGlobalCovariance.cpp:83-87)
+            diag = torch.diagonal(cov, dim1=-2, dim2=-1)
+            floor = 1e-6 * self.prior_var
+            cov = cov + torch.diag_embed(torch.clamp(floor - diag, min=0.0))
+            L, info = torch.linalg.cholesky_ex(cov)
+            ok = fit & (info == 0)
+            # (global_covariance never reads the mean: its random walk is symmetric)
+            self._set_single(ok, mean, torch.where(ok.view(C, 1, 1), L, self.chol[:, 0]))
+            fit = ok
+        # chains without a usable history (or a failed factorisation) restart from the prior
+        rest = active & ~fit
+        if bool(rest.any()):
+            L = torch.diag_embed(torch.sqrt(self.prior_var))
+            self._set_single(rest, self.prior_mean.expand(C, d), L.expand(C, d, d))
+        self._reset_scales(active, initial=False)
+
+
+class SampleHistory:
+    """Per-chain float ring buffer in HBM (SampleHistory.cpp:14-45)."""
+
+    def __init__(self, C: int, d: int, size: int, subsampling: int, device):
+        self.C, self.d, self.H, self.sub = C, d, int(size), int(subsampling)
+        self.samples = torch.zeros((C, self.H, d), dtype=torch.float32, device=device)
+        self.counters = torch.zeros((C, 2), dtype=torch.int64, device=device)
+
+    def add(self, temps: torch.Tensor, values: torch.Tensor, mask: Optional[torch.Tensor] = None, stream=None):
+        _hip.history_add(self.C, self.d, self.H, self.sub, temps.data_ptr(), values.data_ptr(),
+                         None if mask is None else mask.data_ptr(), self.samples.data_ptr(),
+                         self.counters.data_ptr(), stream)
+
+
+def history_geometry(adapt_proposal_samples: int, use_every_nth: int, exploration_steps: int, num_chains: int,
+                     max_history_size: int):
+    """History size and subsampling (SamplerPT::Initialize, SamplerPT.cpp:113-123)."""
+    expected = adapt_proposal_samples * use_every_nth
+    if num_chains > 1:
+        expected *= exploration_steps + 1
+    sub = 1
+    size = expected
+    if size > max_history_size:
+        sub = (expected + max_history_size - 1) // max_history_size
+        size = expected // sub
+    return max(size, 1), sub

@@ -11,11 +11,15 @@ Restates, for the sampler's hot loop only (SURVEY.md §8 a):
 * PriorIndependence::EvaluateLogPDF (src/sampler/PriorIndependence.cpp:129-157) with
   UnivariateMarginal::EvaluateLogPDF uniform / normal (src/sampler/UnivariateMarginal.cpp:326-345).
 
+* the per-block proposal of MutateMove (SamplerPTChain.cpp:241-310) with its state in HBM:
+  gaussian_mixture (the reference's default proposal_type) or global_covariance, with the scale
+  adaptation, MH ratio and sample history (bcm3_amd/proposal.py, csrc/proposal_kernels.hip), and the
+  periodic proposal adaptation of SamplerPT::Run (SamplerPT.cpp:229-248).
+
 The reference evaluates the C chains' likelihoods one per task-manager thread; here all C
 proposals go to the GPU in one bcm3_likelihood_evaluate_batch_device launch, between the
-propose / accept kernels of bcm3_amd/csrc/pt_kernels.hip. The proposal is a fixed diagonal
-Gaussian random walk (the reference's adaptive proposals, src/sampler/Proposal*.cpp, are outside
-the hot-path scope; SURVEY.md §8 f).
+propose / accept kernels. proposal="random_walk" keeps a fixed diagonal Gaussian random walk
+(bcm3_amd/csrc/pt_kernels.hip) for comparisons.
 """
 from __future__ import annotations
 
@@ -26,6 +30,7 @@ from typing import List, Optional
 
 import torch
 
+from .proposal import DeviceProposal, SampleHistory, history_geometry
 from .pt import PTExchange
 
 
@@ -93,7 +98,10 @@ class PTMHDevice:
     INIT_ITER = (1 << 63) - 1  # RNG iteration index reserved for the initial prior draw
 
     def __init__(self, likelihood, prior: DevicePrior, temperatures, rank=0, world=1, seed=0, device="cuda",
-                 learning_rate: float = 1.0, exploration_steps: int = 1, group=None):
+                 learning_rate: float = 1.0, exploration_steps: int = 1, group=None,
+                 proposal: str = "gaussian_mixture", t_dof: float = 0.0, kmax: int = 1,
+                 adapt_proposal_samples: int = 2000, adapt_proposal_times: int = 2, max_history_size: int = 2000,
+                 use_every_nth: int = 1):
         from . import _hip
         self._hip = _hip
         _hip.lib()  # fails loudly without the HIP library
@@ -126,6 +134,20 @@ class PTMHDevice:
         self.accepted_exchange = torch.zeros(1, dtype=torch.int64, device=dev)
         self.attempted_mutate = 0
         self.attempted_exchange = 0
+        # proposals (ptmhsampler.proposal_type) and the sample history that adapts them
+        self.proposal_type = proposal
+        self.adaptive = proposal != "random_walk"
+        self.use_every_nth = int(use_every_nth)
+        self.adapt_samples, self.adapt_times = int(adapt_proposal_samples), int(adapt_proposal_times)
+        self.adaptations_done = 0
+        self.samples_done = 0
+        if self.adaptive:
+            self.proposal = DeviceProposal(proposal, prior, self.T, kmax=kmax, t_dof=t_dof)
+            H, sub = history_geometry(self.adapt_samples, self.use_every_nth, exploration_steps, self.Ctot,
+                                      max_history_size)
+            self.history = SampleHistory(C, d, H, sub, dev)
+            self.log_mh = torch.zeros(C, dtype=torch.float64, device=dev)
+            self._masks = {start: self._exchange_masks(start) for start in (0, 1)}
         # initial state: every chain draws from the prior (the propose kernel at T = 0)
         zeros = torch.zeros(C, dtype=torch.float64, device=dev)
         _hip.ptmh_propose(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(), self.scale.data_ptr(),
@@ -160,11 +182,35 @@ class PTMHDevice:
             self.ex._cross(self.values, self.llh, self.lprior, self.lpp, acc)
             self.accepted_exchange += acc[self.C - 1:].to(torch.int64)
             self.attempted_exchange += 1
+        if self.adaptive:
+            # ExchangeMove adds the (possibly swapped) state of both chains of a pair to their
+            # histories (SamplerPTChain.cpp:374-379)
+            for mask in self._masks[start]:
+                self.history.add(self.T, self.values, mask, self._stream())
         self.round += 1
+
+    def _exchange_masks(self, start: int):
+        return [None if m is None else torch.tensor(m, dtype=torch.uint8, device=self.dev)
+                for m in exchange_participants(self.C, self.g0, self.Ctot, self.world, start)]
 
     def mutate(self):
         """DoMutateMove (SamplerPT.cpp:308-319): all chains' proposals in one likelihood launch."""
         h, C, d, st = self._hip, self.C, self.d, self._stream()
+        if self.adaptive:
+            P = self.proposal.struct
+            h.ptmh_propose_adaptive(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(),
+                                    self.T.data_ptr(), self.values.data_ptr(), self.prop.data_ptr(),
+                                    self.lprior_prop.data_ptr(), self.log_mh.data_ptr(), P, self.g0, self.seed,
+                                    self.iter, st)
+            self._eval(self.prop, self.llh_prop)
+            h.ptmh_accept_adaptive(C, d, self.T.data_ptr(), self.prop.data_ptr(), self.lprior_prop.data_ptr(),
+                                   self.llh_prop.data_ptr(), self.log_mh.data_ptr(), self.lr, self.values.data_ptr(),
+                                   self.lprior.data_ptr(), self.llh.data_ptr(), self.lpp.data_ptr(), None,
+                                   self.accepted_mutate.data_ptr(), P, self.g0, self.seed, self.iter, st)
+            self.history.add(self.T, self.values, None, st)  # SamplerPTChain.cpp:309
+            self.attempted_mutate += C
+            self.iter += 1
+            return
         h.ptmh_propose(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(), self.scale.data_ptr(),
                        self.T.data_ptr(), self.values.data_ptr(), self.prop.data_ptr(), self.lprior_prop.data_ptr(),
                        self.g0, self.seed, self.iter, st)
@@ -176,8 +222,52 @@ class PTMHDevice:
         self.attempted_mutate += C
         self.iter += 1
 
-    def iteration(self):
-        """One DeterministicEvenOdd iteration (SamplerPT.cpp:203-212)."""
+    def iteration(self, last: bool = False):
+        """One DeterministicEvenOdd iteration (SamplerPT.cpp:203-212), then the proposal adaptation
+        every adapt_proposal_samples samples, at most adapt_proposal_times times and not after the
+        last sample (SamplerPT.cpp:226-248)."""
         self.exchange()
         for _ in range(self.exploration_steps):
             self.mutate()
+        si = self.samples_done
+        self.samples_done += 1
+        if self.adaptive and (si + 1) % self.use_every_nth == 0:
+            sample_ix = si // self.use_every_nth
+            if (self.adapt_samples > 0 and (sample_ix + 1) % self.adapt_samples == 0 and not last
+                    and self.adaptations_done < self.adapt_times):
+                self.adapt_proposal()
+
+    def adapt_proposal(self):
+        """SamplerPTChain::AdaptProposal for every chain of the rank (T == 0 chains excepted)."""
+        self.proposal.adapt(self.history.samples, self.history.counters)
+        self.adaptations_done += 1
+
+    def run(self, num_samples: int):
+        """SamplerPT::Run's loop over num_samples * use_every_nth iterations."""
+        total = num_samples * self.use_every_nth
+        for si in range(total):
+            self.iteration(last=(si + 1 == total))
+
+def exchange_participants(C: int, g0: int, Ctot: int, world: int, start: int):
+    """Chains of the rank owning global chains [g0, g0+C) that are in a pair in an exchange round
+    with this start (SamplerPT.cpp:279-298), as one list of flags per pair set; [None] when every
+    chain is in exactly one pair. A chain in two pairs (the wrap pair of an odd single-rank ladder)
+    appears in two lists, so its history receives both samples as in the reference."""
+    if Ctot < 2:
+        return []
+    local = [False] * C
+    for i in range(C - 1):
+        if (g0 + i - start) % 2 == 0:
+            local[i] = local[i + 1] = True
+    extra = [False] * C
+    if world == 1:
+        if (Ctot - 1 - start) % 2 == 0:  # wrap pair (C-1, 0)
+            extra[C - 1] = extra[0] = True
+    else:
+        if (g0 + C - 1 - start) % 2 == 0:  # the last chain pairs with the next rank's first
+            extra[C - 1] = True
+        if ((g0 - 1) % Ctot - start) % 2 == 0:  # the first chain pairs with the previous rank's last
+            extra[0] = True
+    if all(a != b for a, b in zip(local, extra)):
+        return [None]
+    return [m for m in (local, extra) if any(m)]

@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chains", type=int, default=256, help="tempered chains per GPU")
     ap.add_argument("--lanes-per-wave", type=int, default=0, help="0 = auto")
+    ap.add_argument("--proposal", default="gaussian_mixture",
+                    help="ptmhsampler.proposal_type: gaussian_mixture (reference default) | global_covariance | "
+                         "random_walk")
     ap.add_argument("--seed", type=int, default=20251016)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--throughput-batch", type=int, default=16384,
@@ -177,7 +180,7 @@ def main():
     C = args.chains
     prior = DevicePrior(load_prior(PRIOR_XML), device)
     loop = PTMHDevice(ll, prior, temperature_ladder(C * world), rank=rank, world=world, seed=args.seed,
-                      device=device)
+                      device=device, proposal=args.proposal)
 
     for _ in range(args.warmup):
         loop.iteration()
@@ -262,6 +265,7 @@ def main():
             "global_chains": C * world,
             "lanes_per_wave": args.lanes_per_wave or "auto",
             "parallelism": f"chains sharded over {world} rank(s); PT swap = RCCL neighbour send/recv",
+            "proposal": args.proposal,
         },
         "roofline": {
             "bound": "hbm",

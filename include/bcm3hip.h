@@ -172,6 +172,51 @@ int bcm3hip_pt_exchange_local(int C, int d, int64_t g0, int start, int wrap_loca
                               double* values, double* llh, double* lprior, double* lpp, uint8_t* acc_mask,
                               uint64_t* accepted, uint64_t seed, uint64_t round, void* stream);
 
+/* ---- Adaptive proposals (one_block blocking), state resident in device memory ----
+ * Replace SamplerPTChain::MutateMove's per-block Proposal::Update / GetNewSample /
+ * CalculateMHRatio / NotifyAccepted (src/sampler/SamplerPTChain.cpp:241-310) for
+ * ProposalGlobalCovariance (src/sampler/ProposalGlobalCovariance.cpp:20-47) and
+ * ProposalGaussianMixture (src/sampler/ProposalGaussianMixture.cpp:20-103), and
+ * SampleHistory::AddSample (src/sampler/SampleHistory.cpp:32-45). All pointers in the struct are
+ * device pointers; per-chain arrays are indexed by the rank-local chain c in [0, C). */
+enum { BCM3HIP_PROPOSAL_GLOBAL_COVARIANCE = 0, BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE = 1 };
+enum { BCM3HIP_PROPOSAL_KMAX = 16 };
+typedef struct {
+    int32_t kind;                 /* BCM3HIP_PROPOSAL_* (ptmhsampler.proposal_type) */
+    int32_t kmax;                 /* component slots per chain, 1..BCM3HIP_PROPOSAL_KMAX */
+    double t_dof;                 /* ptmhsampler.proposal_t_dof, 0 = normal proposals */
+    double target_acceptance;     /* Proposal::Initialize: 0.44 / 0.35 / 0.3 / 0.234 by d */
+    double scaling_learning_rate; /* 0.05 (Proposal.cpp:22) */
+    double scaling_ema_period;    /* 1000 (Proposal.cpp:21) */
+    const double* lower;          /* [d] prior bounds for ReflectOnBounds (-inf / +inf if unbounded) */
+    const double* upper;          /* [d] */
+    int32_t* ncomp;               /* [C] mixture components in use (1 for global_covariance) */
+    double* weights;              /* [C][kmax] mixture weights */
+    double* mean;                 /* [C][kmax][d] component means */
+    double* chol;                 /* [C][kmax][d][d] lower Cholesky factors, row-major */
+    double* logc;                 /* [C][kmax] -sum log L_jj - d/2 log(2 pi) */
+    double* scale;                /* [C][kmax] adaptive scales */
+    double* ema;                  /* [C][kmax] acceptance-rate EMAs */
+    int32_t* selected;            /* [C] component of the last proposal, -1 before the first */
+    double* work;                 /* [C][2*kmax + 2*d] scratch */
+} bcm3hip_proposal;
+/* As bcm3hip_ptmh_propose, with the proposal's scale update, the mixture component choice and
+ * log_mh[C] = log Metropolis-Hastings ratio (0 for global_covariance). */
+int bcm3hip_ptmh_propose_adaptive(int C, int d, const int32_t* prior_kind, const double* prior_p0,
+                                  const double* prior_p1, const double* temps, const double* values, double* prop,
+                                  double* lprior_prop, double* log_mh, const bcm3hip_proposal* proposal,
+                                  int64_t chain0, uint64_t seed, uint64_t iter, void* stream);
+/* As bcm3hip_ptmh_accept, with log_mh added to the transition and the acceptance EMA update. */
+int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double* prop, const double* lprior_prop,
+                                 const double* llh_prop, const double* log_mh, double learning_rate, double* values,
+                                 double* lprior, double* llh, double* lpp, uint8_t* accept_out, uint64_t* accepted,
+                                 const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed, uint64_t iter,
+                                 void* stream);
+/* SampleHistory::AddSample for chains with T != 0 and (mask == NULL or mask[c] != 0):
+ * history[C][H][d] float ring, counters[C][2] = {samples stored, calls since the last store}. */
+int bcm3hip_history_add(int C, int d, int H, int subsampling, const double* temps, const double* values,
+                        const uint8_t* mask, float* history, int64_t* counters, void* stream);
+
 /* Parity/diagnostic batch (host buffers, any output may be NULL):
  * patient_llh[n*P], traj[n*P*N*T] (states at output times, NaN where not simulated),
  * stats[n*P]. PopPK contexts only. */

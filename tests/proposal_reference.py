@@ -1,0 +1,254 @@
+"""TEST INFRASTRUCTURE ONLY -- Python restatement of bcm3_amd/csrc/proposal_kernels.hip (same
+counter-based random numbers, same operation order), itself a restatement of the reference's
+Proposal::Update / NotifyAccepted (src/sampler/Proposal.cpp:197-220), ProposalGlobalCovariance
+(src/sampler/ProposalGlobalCovariance.cpp:20-47), ProposalGaussianMixture
+(src/sampler/ProposalGaussianMixture.cpp:20-103), GMM::CalculateResponsibilities
+(src/stats/GMM.cpp:172-186), RNG::GetGamma / Sample (src/utils/RNG.cpp:41-111),
+Proposal::ReflectOnBounds (Proposal.cpp:384-397), TestSample (SamplerPTChain.cpp:465-481) and
+SampleHistory::AddSample (src/sampler/SampleHistory.cpp:32-45)."""
+import math
+
+import numpy as np
+
+from ptmh_reference import normal01, rng_key, u01
+
+GLOBAL_COVARIANCE, GAUSSIAN_MIXTURE = 0, 1
+SLOT_PRIOR_NORMAL, SLOT_GAMMA_NORMAL = 0x2000, 0x3000
+KEY_PRIOR_UNIFORM, KEY_GAMMA_UNIFORM, KEY_GAMMA_SMALLK = 0x8000, 0x9000, 0x9800
+KEY_UPDATE, KEY_SELECT, KEY_ACCEPT = 0xA000, 0xA001, 0xC000
+
+
+def _u(seed, it, gc, k):
+    return float(u01(rng_key(seed, it, gc, k)))
+
+
+def _n(seed, it, gc, s):
+    return float(normal01(seed, it, gc, s))
+
+
+def logsum2(a, b):
+    if b > a:
+        a, b = b, a
+    if a == -math.inf:
+        return a
+    diff = b - a
+    if diff < -500:
+        return a
+    return a + math.log1p(math.exp(diff))
+
+
+def reflect(x, lb, ub):
+    for _ in range(4096):
+        if x < lb:
+            x = lb + (lb - x)
+        elif x > ub:
+            x = ub - (x - ub)
+        else:
+            return x
+    w = ub - lb
+    r = math.fmod(x - lb, 2.0 * w)
+    if r < 0.0:
+        r += 2.0 * w
+    return lb + r if r <= w else ub - (r - w)
+
+
+def lower_solve(L, v):
+    d = len(v)
+    v = list(v)
+    for i in range(d):
+        acc = 0.0
+        for j in range(i):
+            acc += L[i][j] * v[j]
+        v[i] = (v[i] - acc) / L[i][i]
+    return v
+
+
+def dot(a):
+    s = 0.0
+    for x in a:
+        s += x * x
+    return s
+
+
+def responsibilities(x, mean, chol, logc, w):
+    K = len(w)
+    r = []
+    for k in range(K):
+        t = lower_solve(chol[k], [x[i] - mean[k][i] for i in range(len(x))])
+        r.append((logc[k] - 0.5 * dot(t)) + math.log(w[k]))
+    m = r[0]
+    for k in range(1, K):
+        m = r[k] if r[k] > m else m
+    s = 0.0
+    for k in range(K):
+        s += math.exp(r[k] - m)
+    lsum = math.log(s) + m
+    tot = 0.0
+    for k in range(K):
+        r[k] = math.exp(r[k] - lsum)
+        tot += r[k]
+    return [rk / tot for rk in r]
+
+
+def gamma_draw(k, theta, seed, it, gc):
+    scale_u = 1.0
+    if k < 1.0:
+        u = _u(seed, it, gc, KEY_GAMMA_SMALLK)
+        scale_u = u ** (1.0 / k)
+        k = 1.0 + k
+    dd = k - 0.33333333333333333333333333333333
+    c = 0.33333333333333333333333333333333 / math.sqrt(dd)
+    ni = ui = 0
+    v = 1.0
+    while ni < 0x800 and ui < 0x800:
+        while True:
+            x = _n(seed, it, gc, SLOT_GAMMA_NORMAL + ni)
+            ni += 1
+            v = 1.0 + c * x
+            if not (v <= 0.0 and ni < 0x800):
+                break
+        v = v * v * v
+        u = _u(seed, it, gc, KEY_GAMMA_UNIFORM + ui)
+        ui += 1
+        if u < 1 - 0.0331 * x * x * x * x:
+            break
+        if math.log(u) < 0.5 * x * x + dd * (1 - v + math.log(v)):
+            break
+    return theta * dd * v * scale_u
+
+
+def prior_logpdf(kind, p0, p1, x):
+    if kind == 0:
+        return -math.inf if (x < p0 or x > p1) else -math.log(p1 - p0)
+    s = p1
+    dx = x - p0
+    return math.log(1.0 / math.sqrt(2.0 * s * s * 3.141592653589793)) - dx * dx * (1.0 / (2.0 * s * s))
+
+
+def propose(P, kind, p0, p1, temps, values, chain0, seed, it):
+    """P: dict of numpy arrays (copies of the DeviceProposal state), updated in place like the
+    kernel (scale, selected). Returns prop, lprior_prop, log_mh."""
+    C, d = values.shape
+    prop = np.empty_like(values)
+    lprior = np.zeros(C)
+    lmh = np.zeros(C)
+    slr, target = 0.05, P["target"]
+    for c in range(C):
+        gc = chain0 + c
+        cur = [float(v) for v in values[c]]
+        nxt = [0.0] * d
+        if temps[c] == 0.0:
+            for i in range(d):
+                if kind[i] == 0:
+                    nxt[i] = p0[i] + _u(seed, it, gc, KEY_PRIOR_UNIFORM + i) * (p1[i] - p0[i])
+                else:
+                    nxt[i] = p0[i] + p1[i] * _n(seed, it, gc, SLOT_PRIOR_NORMAL + i)
+        else:
+            gmm = P["kind"] == GAUSSIAN_MIXTURE
+            K = int(P["ncomp"][c]) if gmm else 1
+            scale = P["scale"][c]
+            ema = P["ema"][c]
+            mean = P["mean"][c].tolist()
+            chol = P["chol"][c].tolist()
+            logc = P["logc"][c].tolist()
+            w = P["weights"][c].tolist()
+            if gmm:
+                last = int(P["selected"][c])
+                if last != -1:
+                    lrate = 1.0 + _u(seed, it, gc, KEY_UPDATE) * slr * K
+                    if ema[last] < target / (1.0 - slr):
+                        scale[last] = max(scale[last] / lrate, 1e-4)
+                    elif ema[last] > (1 + slr) * target:
+                        scale[last] = min(scale[last] * lrate, 10.0)
+                rf = responsibilities(cur, mean[:K], chol[:K], logc[:K], w[:K])
+                u = _u(seed, it, gc, KEY_SELECT)
+                acc = 0.0
+                sel = K - 1
+                for k in range(K):
+                    acc += rf[k]
+                    if u < acc:
+                        sel = k
+                        break
+            else:
+                lrate = 1.0 + _u(seed, it, gc, KEY_UPDATE) * slr
+                if ema[0] < 0.952381 * target:
+                    scale[0] = max(scale[0] / lrate, 1e-4)
+                elif ema[0] > 1.05 * target:
+                    scale[0] = min(scale[0] * lrate, 10.0)
+                sel = 0
+            t_scale = 1.0
+            if P["t_dof"] > 0.0:
+                t_scale = 1.0 / math.sqrt(gamma_draw(0.5 * P["t_dof"], 0.5 * P["t_dof"], seed, it, gc))
+            z = [_n(seed, it, gc, i) for i in range(d)]
+            f = t_scale * float(scale[sel])
+            Ls = chol[sel]
+            v = [0.0] * d
+            for i in range(d):
+                x = 0.0
+                for j in range(i + 1):
+                    x += Ls[i][j] * z[j]
+                v[i] = x * f
+            nxt = [reflect(v[i] + cur[i], P["lower"][i], P["upper"][i]) for i in range(d)]
+            if gmm:
+                rr = responsibilities(nxt, mean[:K], chol[:K], logc[:K], w[:K])
+                fwd = rev = -math.inf
+                for k in range(K):
+                    sk = float(scale[k])
+                    vv = [(nxt[i] - cur[i]) / sk for i in range(d)]
+                    s1 = lower_solve(chol[k], vv)
+                    s2 = lower_solve(chol[k], [-x for x in vv])
+                    base = -math.log(sk * sk) + logc[k]
+                    fwd = logsum2(fwd, (base - 0.5 * dot(s1)) + math.log(rf[k]))
+                    rev = logsum2(rev, (base - 0.5 * dot(s2)) + math.log(rr[k]))
+                lmh[c] = rev - fwd
+            P["selected"][c] = sel
+        prop[c] = nxt
+        lp = 0.0
+        for i in range(d):
+            lp += prior_logpdf(kind[i], p0[i], p1[i], nxt[i])
+        lprior[c] = lp
+    return prop, lprior, lmh
+
+
+def accept(P, temps, prop, lprior_prop, llh_prop, log_mh, lr, values, lprior, llh, lpp, chain0, seed, it):
+    """In place (state arrays and P["ema"]); returns the accept mask."""
+    C = len(temps)
+    out = np.zeros(C, dtype=bool)
+    alpha = 2.0 / (1000.0 + 1)
+    for c in range(C):
+        T = temps[c]
+        nl = llh_prop[c] * lr
+        nq = lprior_prop[c]
+        if T == 0.0:
+            a = True
+            npp = nq if nl == -math.inf else nq + T * nl
+        else:
+            npp = nq + T * nl
+            a = False
+            if npp > -math.inf:
+                tp = npp - lpp[c]
+                with np.errstate(over="ignore", invalid="ignore"):
+                    tp = float(np.exp(tp + log_mh[c]))
+                tp = tp if tp < 1.0 else 1.0
+                a = _u(seed, it, chain0 + c, KEY_ACCEPT) < tp
+            sel = int(P["selected"][c])
+            e = P["ema"][c, sel]
+            P["ema"][c, sel] = e + ((1.0 if a else 0.0) - e) * alpha
+        if a:
+            values[c] = prop[c]
+            lprior[c], llh[c], lpp[c] = nq, nl, npp
+        out[c] = a
+    return out
+
+
+def history_add(temps, values, mask, hist, counters, sub):
+    C, H, d = hist.shape
+    for c in range(C):
+        if temps[c] == 0.0 or (mask is not None and not mask[c]):
+            continue
+        counters[c, 1] += 1
+        if counters[c, 1] == sub:
+            ix = counters[c, 0] % H
+            hist[c, ix] = values[c].astype(np.float32)
+            counters[c, 0] += 1
+            counters[c, 1] = 0

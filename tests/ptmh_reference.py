@@ -49,7 +49,7 @@ def propose(kind, p0, p1, scale, temps, values, chain0, seed, it):
                 if kind[i] == 0:
                     x = p0[i] + float(u01(rng_key(seed, it, gc, 0x8000 + i))) * (p1[i] - p0[i])
                 else:
-                    x = p0[i] + p1[i] * float(normal01(seed, it, gc, 0x4000 + i))
+                    x = p0[i] + p1[i] * float(normal01(seed, it, gc, 0x2000 + i))
             else:
                 x = values[c, i] + scale[i] * float(normal01(seed, it, gc, i))
             prop[c, i] = x

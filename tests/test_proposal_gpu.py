@@ -1,0 +1,198 @@
+"""GPU tests of the adaptive proposal kernels (bcm3_amd/csrc/proposal_kernels.hip) against their
+Python restatement (tests/proposal_reference.py), and of the device sampler with them."""
+import math
+import os
+
+import numpy as np
+import pytest
+
+import helpers as H
+import proposal_reference as R
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _prior(name="c3_prior.xml"):
+    from bcm3_amd.sampler import DevicePrior, load_prior
+    return DevicePrior(load_prior(os.path.join(H.GOLDEN, name)), "cuda")
+
+
+def _prior_arrays(prior):
+    kind = torch.where(prior.is_uniform, 0, 1).to(torch.int32)
+    p0 = torch.where(prior.is_uniform, prior.a, prior.mu).contiguous()
+    p1 = torch.where(prior.is_uniform, prior.b, prior.sigma).contiguous()
+    return kind, p0, p1
+
+
+def _state(P):
+    return {"kind": P.struct.kind, "t_dof": P.t_dof, "target": P.target, "ncomp": P.ncomp.cpu().numpy(),
+            "weights": P.weights.cpu().numpy(), "mean": P.mean.cpu().numpy(), "chol": P.chol.cpu().numpy(),
+            "logc": P.logc.cpu().numpy(), "scale": P.scale.cpu().numpy().copy(), "ema": P.ema.cpu().numpy().copy(),
+            "selected": P.selected.cpu().numpy().copy(), "lower": P.lower.cpu().numpy(),
+            "upper": P.upper.cpu().numpy()}
+
+
+def _random_mixtures(P, rng, K):
+    d = P.d
+    for c in range(P.C):
+        w = rng.uniform(0.2, 1.0, K)
+        w /= w.sum()
+        mu = P.prior_mean.cpu().numpy() + rng.normal(0, 0.3, (K, d)) * np.sqrt(P.prior_var.cpu().numpy())
+        cov = []
+        for _ in range(K):
+            A = rng.normal(0, 1, (d, d)) * np.sqrt(P.prior_var.cpu().numpy())[:, None] * 0.2
+            cov.append(A @ A.T + np.diag(0.05 * P.prior_var.cpu().numpy()))
+        P.set_mixture(c, w, mu, np.array(cov))
+
+
+def _check_propose(kind, K, t_dof, its=(0, 7, 2**40), prior_xml="c3_prior.xml", C=48):
+    from bcm3_amd import _hip
+    from bcm3_amd.proposal import DeviceProposal
+    from bcm3_amd.pt import temperature_ladder
+    prior = _prior(prior_xml)
+    kd, p0, p1 = _prior_arrays(prior)
+    d = prior.d
+    temps = torch.tensor(temperature_ladder(C), dtype=torch.float64, device="cuda")
+    P = DeviceProposal(kind, prior, temps, kmax=max(K, 1), t_dof=t_dof)
+    rng = np.random.default_rng(11 + K)
+    if kind == "gaussian_mixture" and K > 1:
+        _random_mixtures(P, rng, K)
+    # some chains have proposed before (Update runs on them), with EMAs on both sides of target
+    P.selected[::2] = 0
+    P.ema.copy_(torch.tensor(rng.uniform(0.1, 0.4, P.ema.shape), device="cuda"))
+    gen = torch.Generator(device="cuda")
+    gen.manual_seed(3)
+    values = prior.sample(C, gen)
+    prop = torch.empty_like(values)
+    lp = torch.empty(C, dtype=torch.float64, device="cuda")
+    lmh = torch.empty(C, dtype=torch.float64, device="cuda")
+    for it in its:
+        ref = _state(P)
+        _hip.ptmh_propose_adaptive(C, d, kd.data_ptr(), p0.data_ptr(), p1.data_ptr(), temps.data_ptr(),
+                                   values.data_ptr(), prop.data_ptr(), lp.data_ptr(), lmh.data_ptr(), P.struct, 128,
+                                   77, it)
+        torch.cuda.synchronize()
+        rp, rl, rm = R.propose(ref, kd.cpu().numpy(), p0.cpu().numpy(), p1.cpu().numpy(), temps.cpu().numpy(),
+                               values.cpu().numpy(), 128, 77, it)
+        # (heavy-tailed t steps of ~1e3 prior widths fold an ulp of pow/sqrt into ~1e-12 absolute)
+        np.testing.assert_allclose(prop.cpu().numpy(), rp, rtol=1e-12, atol=1e-11)
+        assert np.array_equal(P.selected.cpu().numpy(), ref["selected"])
+        np.testing.assert_allclose(P.scale.cpu().numpy(), ref["scale"], rtol=1e-14)
+        got = lp.cpu().numpy()
+        assert np.array_equal(np.isinf(got), np.isinf(rl))
+        np.testing.assert_allclose(got[np.isfinite(rl)], rl[np.isfinite(rl)], rtol=1e-12)
+        np.testing.assert_allclose(lmh.cpu().numpy(), rm, rtol=1e-9, atol=1e-11)
+        # proposals reflect on the prior bounds: every uniform marginal stays inside
+        assert np.all(np.isfinite(got))
+        values.copy_(prop)
+    return P
+
+
+def test_propose_global_covariance():
+    _check_propose("global_covariance", 1, 0.0)
+
+
+def test_propose_gaussian_mixture_single():
+    P = _check_propose("gaussian_mixture", 1, 0.0)
+    assert float(P.ema.abs().sum()) > 0
+
+
+@pytest.mark.parametrize("K", [2, 3])
+def test_propose_gaussian_mixture_components(K):
+    _check_propose("gaussian_mixture", K, 0.0)
+
+
+@pytest.mark.parametrize("t_dof", [0.5, 5.0])
+def test_propose_t_distributed(t_dof):
+    _check_propose("gaussian_mixture", 2, t_dof)
+
+
+@pytest.mark.parametrize("kind", ["gaussian_mixture", "global_covariance"])
+def test_propose_many_variables(kind):
+    """d = 138 (the P = 64 PopPK variant): the thread-per-chain kernel beyond 64 variables."""
+    _check_propose(kind, 2 if kind == "gaussian_mixture" else 1, 0.0, its=(0, 3), prior_xml="p64_prior.xml", C=6)
+
+
+def test_accept_adaptive_matches_reference():
+    from bcm3_amd import _hip
+    from bcm3_amd.proposal import DeviceProposal
+    from bcm3_amd.pt import temperature_ladder
+    prior = _prior()
+    C, d = 200, prior.d
+    temps = torch.tensor(temperature_ladder(C), dtype=torch.float64, device="cuda")
+    P = DeviceProposal("gaussian_mixture", prior, temps, kmax=2)
+    rng = np.random.default_rng(5)
+    P.selected.copy_(torch.tensor(rng.integers(0, 2, C), dtype=torch.int32, device="cuda"))
+    values = torch.tensor(rng.normal(size=(C, d)), device="cuda")
+    prop = torch.tensor(rng.normal(size=(C, d)), device="cuda")
+    lprior = torch.tensor(rng.normal(size=C), device="cuda")
+    llh = torch.tensor(rng.normal(size=C) * 10, device="cuda")
+    lpp = lprior + temps * llh
+    lprior_prop = torch.tensor(rng.normal(size=C), device="cuda")
+    llh_prop = torch.tensor(rng.normal(size=C) * 10, device="cuda")
+    llh_prop[5] = -math.inf
+    lprior_prop[7] = -math.inf
+    log_mh = torch.tensor(rng.normal(size=C), device="cuda")
+    ref = _state(P)
+    rv, rq, rl, rp = (values.cpu().numpy(), lprior.cpu().numpy(), llh.cpu().numpy(), lpp.cpu().numpy())
+    racc = R.accept(ref, temps.cpu().numpy(), prop.cpu().numpy(), lprior_prop.cpu().numpy(),
+                    llh_prop.cpu().numpy(), log_mh.cpu().numpy(), 0.7, rv, rq, rl, rp, 9, 21, 4)
+    acc = torch.zeros(C, dtype=torch.uint8, device="cuda")
+    n_acc = torch.zeros(1, dtype=torch.int64, device="cuda")
+    _hip.ptmh_accept_adaptive(C, d, temps.data_ptr(), prop.data_ptr(), lprior_prop.data_ptr(), llh_prop.data_ptr(),
+                              log_mh.data_ptr(), 0.7, values.data_ptr(), lprior.data_ptr(), llh.data_ptr(),
+                              lpp.data_ptr(), acc.data_ptr(), n_acc.data_ptr(), P.struct, 9, 21, 4)
+    torch.cuda.synchronize()
+    assert np.array_equal(acc.cpu().numpy().astype(bool), racc)
+    assert int(n_acc.item()) == int(racc.sum())
+    np.testing.assert_array_equal(values.cpu().numpy(), rv)
+    np.testing.assert_array_equal(lpp.cpu().numpy(), rp)
+    np.testing.assert_allclose(P.ema.cpu().numpy(), ref["ema"], rtol=1e-15)
+
+
+def test_history_ring_matches_reference():
+    from bcm3_amd.proposal import SampleHistory
+    rng = np.random.default_rng(9)
+    C, d, Hs, sub = 6, 3, 4, 2
+    temps = torch.tensor([0.0, 0.1, 0.2, 0.5, 0.8, 1.0], dtype=torch.float64, device="cuda")
+    hist = SampleHistory(C, d, Hs, sub, "cuda")
+    rh = np.zeros((C, Hs, d), dtype=np.float32)
+    rc = np.zeros((C, 2), dtype=np.int64)
+    for step in range(13):
+        vals = torch.tensor(rng.normal(size=(C, d)), device="cuda")
+        mask = None if step % 3 else torch.tensor([1, 0, 1, 1, 0, 1], dtype=torch.uint8, device="cuda")
+        hist.add(temps, vals, mask)
+        R.history_add(temps.cpu().numpy(), vals.cpu().numpy(), None if mask is None else mask.cpu().numpy(), rh, rc,
+                      sub)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(hist.samples.cpu().numpy(), rh)
+    np.testing.assert_array_equal(hist.counters.cpu().numpy(), rc)
+    assert rc[0, 0] == 0  # T == 0 chain keeps no history
+
+
+@pytest.mark.parametrize("proposal", ["gaussian_mixture", "global_covariance"])
+def test_sampler_adaptive_proposals(proposal):
+    """Circular ridge (config C2) with the reference's proposals: the run stays finite, the scale
+    adaptation steers the acceptance of the posterior chain toward the target, and the proposal
+    adapts from the sample history."""
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.pt import temperature_ladder
+    from bcm3_amd.sampler import DevicePrior, PTMHDevice, load_prior
+    prior = DevicePrior(load_prior(os.path.join(H.GOLDEN, "circular_prior.xml")), "cuda")
+    ll = Likelihood(os.path.join(H.GOLDEN, "circular_likelihood.xml"), os.path.join(H.GOLDEN, "circular_prior.xml"),
+                    device=0)
+    C = 16
+    s = PTMHDevice(ll, prior, temperature_ladder(C), seed=5, proposal=proposal, adapt_proposal_samples=100,
+                   adapt_proposal_times=1)
+    s.run(300)
+    torch.cuda.synchronize()
+    assert s.adaptations_done == 1
+    assert torch.isfinite(s.lpp).all()
+    assert torch.isfinite(s.proposal.chol).all()
+    ema = s.proposal.ema.cpu().numpy()
+    # the posterior chain's acceptance EMA has moved toward the d = 2 target of 0.35
+    assert 0.05 < ema[-1, 0] < 0.8
+    n = s.history.counters.cpu().numpy()
+    assert n[0, 0] == 0 and n[1:, 0].min() > 0
