@@ -30,7 +30,7 @@ class PopPKModel(C.Structure):
         ("num_pk_pop_params", C.c_int32), ("d", C.c_int32), ("P", C.c_int32), ("T", C.c_int32),
         ("sd_ix", C.c_int32), ("n_transit_ix", C.c_int32), ("transit_time_ix", C.c_int32),
         ("biphasic_time_ix", C.c_int32), ("absorption2_ix", C.c_int32), ("max_steps", C.c_int32),
-        ("pad_", C.c_int32),
+        ("param_map", C.c_int32),
         ("rtol", C.c_double), ("atol", C.c_double), ("MW", C.c_double), ("fixed_vod", C.c_double),
         ("fixed_kf", C.c_double), ("fixed_kb", C.c_double),
         ("transforms", C.c_void_p), ("time", C.c_void_p), ("observed", C.c_void_p), ("dose", C.c_void_p),
@@ -142,9 +142,7 @@ class Context:
                   "dose_change_time": np.float64, "intermittent": np.int32, "skipped_days": np.uint8,
                   "simulate_until": np.int32}
         for name, _ in PopPKModel._fields_:
-            if name == "pad_":
-                continue
-            v = model_fields[name]
+            v = model_fields.get(name, 0) if name == "param_map" else model_fields[name]
             if name in arrays:
                 a = np.ascontiguousarray(v, dtype=arrays[name])
                 keep.append(a)

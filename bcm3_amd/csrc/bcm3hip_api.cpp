@@ -132,7 +132,19 @@ int bcm3hip_open_popk(int device, const bcm3hip_popk_model* m, bcm3hip_ctx** out
     const bool biphasic = m->pk_type == BCM3HIP_PK_ONE_BIPHASIC || m->pk_type == BCM3HIP_PK_TWO_BIPHASIC;
     if (m->N != (two ? 3 : 2)) return BCM3HIP_ERR_MODEL;
     if (m->d <= 0 || m->P <= 0 || m->T < 0 || m->sd_ix < 0 || m->sd_ix + 1 >= m->d) return BCM3HIP_ERR_MODEL;
-    if (m->num_pk_params + m->num_pk_pop_params * m->P + 1 >= m->d) return BCM3HIP_ERR_MODEL;
+    if (m->param_map == BCM3HIP_PARAM_MAP_POPULATION) {
+        if (m->num_pk_params + m->num_pk_pop_params * m->P + 1 >= m->d) return BCM3HIP_ERR_MODEL;
+    } else if (m->param_map == BCM3HIP_PARAM_MAP_SINGLE) {
+        // one patient; the variables read by fixed index (LikelihoodPharmacokineticTrajectory.cpp:226-259)
+        int need = std::isnan(m->fixed_vod) ? 4 : 3;
+        if (two && std::isnan(m->fixed_kf)) need = 6;
+        if (biphasic) need = 8;
+        if (m->P != 1 || m->d < need) return BCM3HIP_ERR_MODEL;
+        if (biphasic && (m->biphasic_time_ix != 6 || m->absorption2_ix != 7)) return BCM3HIP_ERR_MODEL;
+    } else {
+        return BCM3HIP_ERR_MODEL;
+    }
+    if (transit && (m->n_transit_ix >= m->d || m->transit_time_ix >= m->d)) return BCM3HIP_ERR_MODEL;
     if (transit && (m->n_transit_ix < 0 || m->transit_time_ix < 0)) return BCM3HIP_ERR_MODEL;
     if (biphasic && (m->biphasic_time_ix < 0 || m->absorption2_ix < 0)) return BCM3HIP_ERR_MODEL;
     for (int j = 0; j < m->P; j++) {
@@ -163,6 +175,7 @@ int bcm3hip_open_popk(int device, const bcm3hip_popk_model* m, bcm3hip_ctx** out
     pm.biphasic_time_ix = m->biphasic_time_ix;
     pm.absorption2_ix = m->absorption2_ix;
     pm.max_steps = m->max_steps;
+    pm.param_map = m->param_map;
     pm.rtol = m->rtol;
     pm.atol = m->atol;
     pm.MW = m->MW;

@@ -53,7 +53,10 @@ std::string option_get(const OptionsMap& vm, const std::string& key, const std::
     return it == vm.end() ? def : it->second;
 }
 
-std::vector<std::string> LikelihoodFactory::SupportedTypes() { return {"pop_pk_trajectory", "banana", "circular"}; }
+std::vector<std::string> LikelihoodFactory::SupportedTypes()
+{
+    return {"pop_pk_trajectory", "pharmacokinetic_trajectory", "banana", "circular"};
+}
 
 std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::string& fn,
                                                                  std::shared_ptr<const VariableSet> varset,
@@ -87,12 +90,14 @@ std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::strin
     }
     if (type == "pop_pk_trajectory") {
         ll = std::make_shared<LikelihoodPopPKTrajectory>(sampling_threads, evaluation_threads);
+    } else if (type == "pharmacokinetic_trajectory") {
+        ll = std::make_shared<LikelihoodPharmacokineticTrajectory>(sampling_threads, evaluation_threads);
     } else if (type == "banana") {
         ll = std::make_shared<TestLikelihoodBanana>(sampling_threads, evaluation_threads);
     } else if (type == "circular") {
         ll = std::make_shared<TestLikelihoodCircular>(sampling_threads, evaluation_threads);
     } else {
-        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, banana, circular)",
+        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, banana, circular)",
                  type.c_str());
         return ll;
     }

@@ -328,6 +328,205 @@ bool LikelihoodPopPKTrajectory::CheckEvaluable()
 }
 
 // ---------------------------------------------------------------------------------------------
+// LikelihoodPharmacokineticTrajectory
+
+static int32_t pk_type_code(const std::string& t)
+{
+    // SetPKModelType (LikelihoodPharmacokineticTrajectory.cpp:66-83), after its string mapping
+    if (t == "one") return BCM3HIP_PK_ONE;
+    if (t == "two") return BCM3HIP_PK_TWO;
+    if (t == "one_biphasic_uptake" || t == "two_biphasic_uptake") return BCM3HIP_PK_TWO_BIPHASIC;
+    if (t == "one_transit") return BCM3HIP_PK_ONE_TRANSIT;
+    if (t == "two_transit") return BCM3HIP_PK_TWO_TRANSIT;
+    return -1;
+}
+
+static Real molecular_weight(const std::string& drug)
+{
+    if (drug == "lapatinib") return 581.06;
+    if (drug == "dacomitinib") return 469.95;
+    if (drug == "afatinib") return 485.94;
+    if (drug == "trametinib") return 615.404;
+    if (drug == "mirdametinib") return 482.19;
+    if (drug == "selumetinib") return 457.68;
+    return NaN;
+}
+
+// LikelihoodPharmacokineticTrajectory::Initialize (.cpp:85-213). The reference opens "pkdata.nc";
+// this build reads the same arrays from a JSON sidecar (pkdata_file attribute, default
+// "pkdata.json"), as for pop_pk_trajectory.
+bool LikelihoodPharmacokineticTrajectory::Initialize(std::shared_ptr<const VariableSet> vs,
+                                                     const XmlNode& likelihood_node, const OptionsMap& vm)
+{
+    varset = vs;
+    std::string trial, pk_type_str, pkdata_file;
+    try {
+        const XmlNode* modelnode = likelihood_node.child("pk_model");
+        if (!modelnode) throw XmlError{"No such node (pk_model)"};
+        drug = modelnode->get("drug");
+        pk_type_str = modelnode->get("type");
+        trial = modelnode->get("trial");
+        patient_id = modelnode->has_attr("patient") ? modelnode->get("patient") : std::string();
+        pkdata_file = modelnode->has_attr("pkdata_file") ? modelnode->get("pkdata_file") : std::string("pkdata.json");
+        fixed_vod = modelnode->get_double("volume_of_distribution", NaN);
+        fixed_periphery_fwd = modelnode->get_double("k_periphery_fwd", NaN);
+        fixed_periphery_bwd = modelnode->get_double("k_periphery_bwd", NaN);
+    } catch (XmlError& e) {
+        LOGERROR("Error parsing likelihood file: %s", e.what.c_str());
+        return false;
+    }
+    const std::string use_patient = option_get(vm, "pk.patient", "");
+    if (!use_patient.empty()) patient_id = use_patient;
+    if (patient_id.empty()) {
+        LOGERROR("Patient ID has not been specified in either the likelihood or as command-line option.");
+        return false;
+    }
+    const int32_t pk_type = pk_type_code(pk_type_str);
+    if (pk_type < 0) {
+        LOGERROR("Invalid PK model type");
+        return false;
+    }
+
+    std::string path = pkdata_file;
+    if (!file_exists(path)) {
+        std::string alt = option_get(vm, "likelihood_dir", ".") + "/" + pkdata_file;
+        if (file_exists(alt)) path = alt;
+    }
+    Json data;
+    try {
+        data = json_load(path);
+    } catch (JsonError& e) {
+        LOGERROR("Failed to open data file %s: %s", pkdata_file.c_str(), e.what.c_str());
+        return false;
+    }
+    const Json* g = data.find(trial);
+    if (!g) {
+        LOGERROR("Group \"%s\" not found in %s", trial.c_str(), path.c_str());
+        return false;
+    }
+    bool result = true;
+    auto var = [&](const std::string& name) -> const Json* {
+        const Json* v = g->find(name);
+        if (!v) {
+            LOGERROR("Variable \"%s\" not found in group \"%s\"", name.c_str(), trial.c_str());
+            result = false;
+        }
+        return v;
+    };
+    const Json* jt = var("time");
+    const Json* jp = var("patients");
+    const Json* jc = var(drug + "_plasma_concentration");
+    const Json* jd = var(drug + "_dose");
+    const Json* jda = var(drug + "_dose_after_dose_change");
+    const Json* jdt = var(drug + "_dose_change_time");
+    const Json* jdi = var(drug + "_dosing_interval");
+    const Json* jin = var(drug + "_intermittent");
+    const Json* jti = var("treatment_interruptions");
+    if (!result) return false;
+    size_t pix = jp->arr.size();
+    for (size_t j = 0; j < jp->arr.size(); j++) {
+        const Json& p = jp->arr[j];
+        const std::string id = p.type == Json::String ? p.str : std::to_string((long)p.num);
+        if (id == patient_id) {
+            pix = j;
+            break;
+        }
+    }
+    if (pix == jp->arr.size()) {
+        LOGERROR("Cannot find patient \"%s\" in data file", patient_id.c_str());
+        return false;
+    }
+    const size_t T = jt->arr.size();
+    time.resize(T);
+    observed.resize(T);
+    skipped_days.assign(29, 0);
+    try {
+        for (size_t i = 0; i < T; i++) {
+            time[i] = jt->arr[i].as_double();
+            observed[i] = jc->arr.at(pix).arr.at(i).as_double();
+        }
+        dose = {jd->arr.at(pix).as_double()};
+        dose_after_dose_change = {jda->arr.at(pix).as_double()};
+        dose_change_time = {jdt->arr.at(pix).as_double()};
+        dosing_interval = {jdi->arr.at(pix).as_double()};
+        // `intermittent` is read as a bool here (.cpp:183-185)
+        intermittent = {jin->arr.at(pix).as_double() != 0.0 ? 1 : 0};
+        for (int i = 0; i < 29; i++)
+            if (jti->arr.at(pix).arr.at(i).as_double() != 0.0) skipped_days[i] = 1;
+    } catch (std::out_of_range&) {
+        LOGERROR("PK data arrays have inconsistent dimensions");
+        return false;
+    } catch (JsonError& e) {
+        LOGERROR("PK data: %s", e.what.c_str());
+        return false;
+    }
+    simulate_until = {(int32_t)T};  // every time point (SolveReturnSolution over `time`, .cpp:311)
+    MW = molecular_weight(drug);
+
+    transforms.resize(varset->GetNumVariables());
+    for (size_t i = 0; i < transforms.size(); i++) transforms[i] = (int32_t)varset->GetVariableTransform(i);
+    auto ix = [&](const char* n) -> int32_t {
+        size_t i = varset->GetVariableIndex(n, false);
+        return i == std::numeric_limits<size_t>::max() ? -1 : (int32_t)i;
+    };
+    const bool two = pk_type == BCM3HIP_PK_TWO || pk_type == BCM3HIP_PK_TWO_BIPHASIC || pk_type == BCM3HIP_PK_TWO_TRANSIT;
+    const bool biphasic = pk_type == BCM3HIP_PK_ONE_BIPHASIC || pk_type == BCM3HIP_PK_TWO_BIPHASIC;
+    model = bcm3hip_popk_model{};
+    model.pk_type = pk_type;
+    model.N = two ? 3 : 2;
+    model.num_pk_params = 0;  // (no variable-count check: it is compiled out in the reference, .cpp:118-150)
+    model.num_pk_pop_params = 0;
+    model.d = (int32_t)varset->GetNumVariables();
+    model.P = 1;
+    model.T = (int32_t)T;
+    model.sd_ix = ix("standard_deviation");
+    model.n_transit_ix = ix("n_transit");
+    model.transit_time_ix = ix("mean_transit_time");
+    model.biphasic_time_ix = biphasic ? 6 : -1;  // fixed indices (.cpp:252-253)
+    model.absorption2_ix = biphasic ? 7 : -1;
+    model.max_steps = 2000;
+    model.param_map = BCM3HIP_PARAM_MAP_SINGLE;
+    // SetTolerance(1e-6f, dose * 1e-6f) (.cpp:205)
+    model.rtol = (double)1e-6f;
+    model.atol = dose[0] * (double)1e-6f;
+    model.MW = std::isnan(MW) ? 1.0 : MW;
+    model.fixed_vod = fixed_vod;
+    model.fixed_kf = fixed_periphery_fwd;
+    model.fixed_kb = fixed_periphery_bwd;
+    model.transforms = transforms.data();
+    model.time = time.data();
+    model.observed = observed.data();
+    model.dose = dose.data();
+    model.dosing_interval = dosing_interval.data();
+    model.dose_after_dose_change = dose_after_dose_change.data();
+    model.dose_change_time = dose_change_time.data();
+    model.intermittent = intermittent.data();
+    model.skipped_days = skipped_days.data();
+    model.simulate_until = simulate_until.data();
+    if (model.sd_ix < 0) {
+        LOGERROR("Could not find variable \"standard_deviation\"");
+        return false;
+    }
+    if (!OpenDevice(vm)) return false;
+    if (option_get(vm, "backend", "") == "none") return true;
+    int r = bcm3hip_open_popk(device, &model, &ctx);
+    if (r != 0) {
+        LOGERROR("Opening the PK GPU context failed: %s", bcm3hip_error_string(r));
+        return false;
+    }
+    return true;
+}
+
+bool LikelihoodPharmacokineticTrajectory::CheckEvaluable()
+{
+    if (std::isnan(MW)) {
+        LOGERROR("Unknown drug \"%s\"", drug.c_str());
+        return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------------
 // TestLikelihoodBanana::Initialize (TestLikelihoodBanana.cpp:13-39)
 bool TestLikelihoodBanana::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& node, const OptionsMap& vm)
 {

@@ -1,11 +1,14 @@
 // LikelihoodGPU.h -- MI355X-backed implementations of the reference's likelihood types on the
 // hot path, behind the bcm3::Likelihood interface:
 //   pop_pk_trajectory  LikelihoodPopPKTrajectory (src/likelihoods/LikelihoodPopPKTrajectory.h:10-115)
+//   pharmacokinetic_trajectory  LikelihoodPharmacokineticTrajectory
+//                      (src/likelihoods/LikelihoodPharmacokineticTrajectory.h; one patient, same solver)
 //   banana             TestLikelihoodBanana      (src/likelihoods/TestLikelihoodBanana.cpp)
 //   circular           TestLikelihoodCircular    (src/likelihoods/TestLikelihoodCircular.cpp)
 // Each owns one libbcm3hip context (include/bcm3hip.h) on the configured device. There is no
 // CPU fallback: without a GPU, Initialize fails.
 #pragma once
+#include <cmath>
 #include <mutex>
 #include <set>
 
@@ -72,6 +75,29 @@ private:
     std::vector<int32_t> intermittent, simulate_until, transforms;
     std::vector<uint8_t> skipped_days;
     Real MW;
+    bcm3hip_popk_model model{};
+};
+
+// One patient's trajectory (LikelihoodPharmacokineticTrajectory.cpp:85-340): the PopPK kernel with
+// the single-patient parameter map (BCM3HIP_PARAM_MAP_SINGLE)
+class LikelihoodPharmacokineticTrajectory : public LikelihoodGPUBase {
+public:
+    LikelihoodPharmacokineticTrajectory(size_t sampling_threads, size_t evaluation_threads) {}
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+    bool PostInitialize() override { return true; }
+    const std::string& GetPatientID() const { return patient_id; }
+    const bcm3hip_popk_model& GetDeviceModel() const { return model; }
+
+protected:
+    bool CheckEvaluable() override;
+
+private:
+    std::string drug, patient_id;
+    Real fixed_vod = NAN, fixed_periphery_fwd = NAN, fixed_periphery_bwd = NAN, MW = NAN;
+    std::vector<Real> time, observed, dose, dosing_interval, dose_after_dose_change, dose_change_time;
+    std::vector<int32_t> intermittent, simulate_until, transforms;
+    std::vector<uint8_t> skipped_days;
     bcm3hip_popk_model model{};
 };
 

@@ -57,10 +57,15 @@ int bcm3_likelihood_create_ex(const char* likelihood_xml, const char* prior_xml,
 int bcm3_likelihood_popk_model(const bcm3_likelihood* h, void* model)
 {
     if (!h || !model) return -1;
-    auto* p = dynamic_cast<bcm3::LikelihoodPopPKTrajectory*>(h->ll.get());
-    if (!p) return -2;
-    *(bcm3hip_popk_model*)model = p->GetDeviceModel();
-    return 0;
+    if (auto* p = dynamic_cast<bcm3::LikelihoodPopPKTrajectory*>(h->ll.get())) {
+        *(bcm3hip_popk_model*)model = p->GetDeviceModel();
+        return 0;
+    }
+    if (auto* p = dynamic_cast<bcm3::LikelihoodPharmacokineticTrajectory*>(h->ll.get())) {
+        *(bcm3hip_popk_model*)model = p->GetDeviceModel();
+        return 0;
+    }
+    return -2;
 }
 
 void bcm3_likelihood_destroy(bcm3_likelihood* h) { delete h; }

@@ -11,7 +11,7 @@ namespace bcm3hip {
 // Same fields as bcm3hip_popk_model, with device pointers.
 struct PopPKDevModel {
     int32_t pk_type, N, num_pk_params, num_pk_pop_params, d, P, T, sd_ix;
-    int32_t n_transit_ix, transit_time_ix, biphasic_time_ix, absorption2_ix, max_steps;
+    int32_t n_transit_ix, transit_time_ix, biphasic_time_ix, absorption2_ix, max_steps, param_map;
     double rtol, atol, MW, fixed_vod, fixed_kf, fixed_kb;
     const int32_t* transforms;
     const double* time;

@@ -323,10 +323,19 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     const double sd = transform_var(m.transforms[sdix], v[sdix]);
     const double sd2 = transform_var(m.transforms[sdix + 1], v[sdix + 1]);
     PKLane<PKT> mdl;
-    mdl.ka = fastpow10(quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
-    mdl.ke = transform_var(m.transforms[1], v[1]);
+    // single-patient likelihood (LikelihoodPharmacokineticTrajectory.cpp:226-259): the rates are the
+    // transformed variables; the population likelihood draws ka and CL per patient (.cpp:283-286)
+    const bool single = (m.param_map == BCM3HIP_PARAM_MAP_SINGLE);
     const double vod = isnan(m.fixed_vod) ? transform_var(m.transforms[3], v[3]) : m.fixed_vod;
-    mdl.kel = fastpow10(quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / vod;
+    if (single) {
+        mdl.ka = transform_var(m.transforms[0], v[0]);
+        mdl.ke = transform_var(m.transforms[1], v[1]);
+        mdl.kel = transform_var(m.transforms[2], v[2]) / vod;
+    } else {
+        mdl.ka = fastpow10(quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
+        mdl.ke = transform_var(m.transforms[1], v[1]);
+        mdl.kel = fastpow10(quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / vod;
+    }
     mdl.kf = mdl.kb = 0.0;
     if constexpr (TR::two) {
         if (isnan(m.fixed_kf)) {
@@ -352,7 +361,9 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         const int bi = m.biphasic_time_ix, ai = m.absorption2_ix;
         tsw = transform_var(m.transforms[bi], v[bi]);
         const double lim = interval - 1e-2;
-        tsw = (lim < tsw) ? lim : tsw;
+        // (the population likelihood keeps the switch inside the dosing interval, .cpp:303-305;
+        //  the single-patient one does not, LikelihoodPharmacokineticTrajectory.cpp:253)
+        tsw = (!single && lim < tsw) ? lim : tsw;
         mdl.ka2 = transform_var(m.transforms[ai], v[ai]);
     }
     if constexpr (UNI && !VEC) {
@@ -423,7 +434,9 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             const double xm = (x < 0.0) ? 0.0 : x;
             llh += log_pdf_tnu4(x, yo, sd_u + sd2_u * xm);
         }
-        if (isnan(x)) {
+        // population likelihood: a NaN concentration ends the patient at -inf (.cpp:418-421); the
+        // single-patient likelihood has no such rule, NaN reaches the caller as in the reference
+        if (isnan(x) && !single) {
             llh = -INFINITY;
             llh_done = true;
         }

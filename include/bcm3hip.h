@@ -60,6 +60,14 @@ enum {
 /* VariableSet::TransformVariable codes (src/sampler/VariableSet.cpp:97-124). */
 enum { BCM3HIP_TF_NONE = 0, BCM3HIP_TF_LOG = 1, BCM3HIP_TF_LOG10 = 2, BCM3HIP_TF_LOGIT = 3 };
 
+/* Parameter maps (values -> PK rate constants) of the two CVODE PK likelihoods:
+ * POPULATION = LikelihoodPopPKTrajectory::EvaluateLogProbability (.cpp:263-310): non-centred random
+ *   effects per patient, NaN concentrations give -inf;
+ * SINGLE = LikelihoodPharmacokineticTrajectory::EvaluateLogProbability
+ *   (src/likelihoods/LikelihoodPharmacokineticTrajectory.cpp:215-262): the rates are the
+ *   (transformed) variables themselves, biphasic time / absorption at variables 6 / 7, P = 1. */
+enum { BCM3HIP_PARAM_MAP_POPULATION = 0, BCM3HIP_PARAM_MAP_SINGLE = 1 };
+
 /* Flat PopPK model: everything LikelihoodPopPKTrajectory::Initialize derives from
  * likelihood.xml + prior.xml + the pkdata file (.cpp:50-252). Host pointers; the arrays are
  * copied to device memory by bcm3hip_open_popk and need not outlive the call. */
@@ -77,7 +85,7 @@ typedef struct {
     int32_t biphasic_time_ix;  /* "biphasic_uptake_time" or -1 */
     int32_t absorption2_ix;    /* "mean_absorption2" or -1 */
     int32_t max_steps;         /* 2000 (ODESolverCVODE.cpp:45) */
-    int32_t pad_;
+    int32_t param_map;         /* BCM3HIP_PARAM_MAP_*: which likelihood's parameter map */
     double rtol;               /* (double)1e-6f */
     double atol;               /* min dose * (double)1e-6f */
     double MW;                 /* molecular weight of the drug */

@@ -62,7 +62,7 @@ class OrcPopPKModel(C.Structure):
         ("num_pk_pop_params", C.c_int32), ("d", C.c_int32), ("P", C.c_int32), ("T", C.c_int32),
         ("sd_ix", C.c_int32), ("n_transit_ix", C.c_int32), ("transit_time_ix", C.c_int32),
         ("biphasic_time_ix", C.c_int32), ("absorption2_ix", C.c_int32), ("max_steps", C.c_int32),
-        ("pad_", C.c_int32),
+        ("param_map", C.c_int32),
         ("rtol", C.c_double), ("atol", C.c_double), ("MW", C.c_double), ("fixed_vod", C.c_double),
         ("fixed_kf", C.c_double), ("fixed_kb", C.c_double),
         ("transforms", C.POINTER(C.c_int32)), ("time", C.POINTER(C.c_double)),
@@ -116,6 +116,7 @@ class PopPKProblem:
     skipped_days: np.ndarray
     simulate_until: np.ndarray
     variables: List[Variable] = field(default_factory=list)
+    param_map: int = 0  # 0 LikelihoodPopPKTrajectory, 1 LikelihoodPharmacokineticTrajectory
 
     def to_c(self):
         keep = []
@@ -127,7 +128,8 @@ class PopPKProblem:
 
         m = OrcPopPKModel()
         for k in ("pk_type", "N", "num_pk_params", "num_pk_pop_params", "d", "P", "T", "sd_ix",
-                  "n_transit_ix", "transit_time_ix", "biphasic_time_ix", "absorption2_ix", "max_steps"):
+                  "n_transit_ix", "transit_time_ix", "biphasic_time_ix", "absorption2_ix", "max_steps",
+                  "param_map"):
             setattr(m, k, int(getattr(self, k)))
         for k in ("rtol", "atol", "MW", "fixed_vod", "fixed_kf", "fixed_kb"):
             setattr(m, k, float(getattr(self, k)))
@@ -214,6 +216,50 @@ def build_problem(pkdata: dict, trial: str, drug: str, pk_type_str: str, variabl
         transforms=np.array([v.transform for v in variables], dtype=np.int32), time=time,
         observed=obs, dose=dose, dosing_interval=di, dose_after_dose_change=dadc, dose_change_time=dct,
         intermittent=inter, skipped_days=ti, simulate_until=sim_until, variables=list(variables))
+
+
+def build_single_problem(pkdata: dict, trial: str, drug: str, pk_type_str: str, variables: List[Variable],
+                         patient: str, fixed_vod=math.nan, fixed_kf=math.nan, fixed_kb=math.nan) -> PopPKProblem:
+    """Restates LikelihoodPharmacokineticTrajectory::Initialize (src/likelihoods/
+    LikelihoodPharmacokineticTrajectory.cpp:85-213) for one patient of a pkdata dict: no
+    variable-count check (compiled out, .cpp:118-150), every time point simulated, tolerances
+    SetTolerance(1e-6f, dose * 1e-6f) with the patient's dose (.cpp:205), biphasic switch time
+    and second absorption rate at variables 6 and 7 (.cpp:252-253)."""
+    g = pkdata[trial]
+    pk_type = PK_TYPES[pk_type_str]
+    names = [v.name for v in variables]
+    patients = [str(p) for p in g["patients"]]
+    if patient not in patients:
+        raise ValueError(f'Cannot find patient "{patient}" in data file')
+    j = patients.index(patient)
+    time = np.array(g["time"], dtype=np.float64)
+    T = len(time)
+
+    def f(x):
+        return math.nan if x is None else float(x)
+
+    obs = np.array([f(v) for v in g[drug + "_plasma_concentration"][j]], dtype=np.float64).reshape(1, T)
+    dose = np.array([f(g[drug + "_dose"][j])])
+    biphasic = pk_type in (2, 3)
+
+    def idx(name):
+        return names.index(name) if name in names else -1
+
+    return PopPKProblem(
+        pk_type=pk_type, N=NUM_STATES[pk_type], num_pk_params=0, num_pk_pop_params=0, d=len(variables), P=1,
+        T=T, sd_ix=idx("standard_deviation"), n_transit_ix=idx("n_transit"),
+        transit_time_ix=idx("mean_transit_time"), biphasic_time_ix=6 if biphasic else -1,
+        absorption2_ix=7 if biphasic else -1, max_steps=2000,
+        rtol=_f32(1e-6), atol=float(dose[0]) * _f32(1e-6), MW=MOLECULAR_WEIGHT[drug],
+        fixed_vod=fixed_vod, fixed_kf=fixed_kf, fixed_kb=fixed_kb,
+        transforms=np.array([v.transform for v in variables], dtype=np.int32), time=time, observed=obs,
+        dose=dose, dosing_interval=np.array([f(g[drug + "_dosing_interval"][j])]),
+        dose_after_dose_change=np.array([f(g[drug + "_dose_after_dose_change"][j])]),
+        dose_change_time=np.array([f(g[drug + "_dose_change_time"][j])]),
+        # read as a bool (.cpp:183-185)
+        intermittent=np.array([1 if g[drug + "_intermittent"][j] else 0], dtype=np.int32),
+        skipped_days=np.array(g["treatment_interruptions"][j], dtype=np.uint8).reshape(1, 29),
+        simulate_until=np.array([T], dtype=np.int32), variables=list(variables), param_map=1)
 
 
 class Oracle:

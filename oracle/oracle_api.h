@@ -36,7 +36,8 @@ typedef struct {
     int32_t biphasic_time_ix;
     int32_t absorption2_ix;
     int32_t max_steps;
-    int32_t pad_;
+    int32_t param_map; /* 0 population (LikelihoodPopPKTrajectory), 1 single patient
+                          (LikelihoodPharmacokineticTrajectory) */
     double rtol;
     double atol;
     double MW;

@@ -285,11 +285,19 @@ static void eval_range(job* jb)
             pd.dose_change_time = m->dose_change_time[j];
             pd.intermittent = m->intermittent[j];
             pd.skipped_days = m->skipped_days + 29 * j;
-            /* parameter map (.cpp:283-310) */
-            pd.ka = fastpow10(orc_quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
-            pd.ke = orc_transform(m->transforms[1], v[1]);
+            /* parameter map: population (LikelihoodPopPKTrajectory.cpp:283-310) or single patient
+             * (LikelihoodPharmacokineticTrajectory.cpp:226-259) */
+            const int single = (m->param_map == 1);
             pd.vod = isnan(m->fixed_vod) ? orc_transform(m->transforms[3], v[3]) : m->fixed_vod;
-            pd.kel = fastpow10(orc_quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / pd.vod;
+            if (single) {
+                pd.ka = orc_transform(m->transforms[0], v[0]);
+                pd.ke = orc_transform(m->transforms[1], v[1]);
+                pd.kel = orc_transform(m->transforms[2], v[2]) / pd.vod;
+            } else {
+                pd.ka = fastpow10(orc_quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
+                pd.ke = orc_transform(m->transforms[1], v[1]);
+                pd.kel = fastpow10(orc_quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / pd.vod;
+            }
             if (is_two(m->pk_type)) {
                 if (isnan(m->fixed_kf)) {
                     pd.kf = orc_transform(m->transforms[4], v[4]);
@@ -306,7 +314,9 @@ static void eval_range(job* jb)
             if (is_biphasic(m->pk_type)) {
                 pd.tsw = orc_transform(m->transforms[m->biphasic_time_ix], v[m->biphasic_time_ix]);
                 double lim = pd.dosing_interval - 1e-2;
-                pd.tsw = (lim < pd.tsw) ? lim : pd.tsw; /* std::min(a,b) = (b < a) ? b : a */
+                /* std::min(a,b) = (b < a) ? b : a; the single-patient likelihood does not clamp
+                 * (LikelihoodPharmacokineticTrajectory.cpp:253) */
+                if (!single) pd.tsw = (lim < pd.tsw) ? lim : pd.tsw;
                 pd.ka2 = orc_transform(m->transforms[m->absorption2_ix], v[m->absorption2_ix]);
             }
             pd.last_treatment = 0.0;
@@ -349,7 +359,7 @@ static void eval_range(job* jb)
                             double xm = (x < 0.0) ? 0.0 : x; /* std::max(x, 0.0) = (x < 0) ? 0 : x */
                             pllh += orc_log_pdf_tnu4(x, y, sd + sd2 * xm);
                         }
-                        if (isnan(x)) {
+                        if (isnan(x) && !single) { /* (.cpp:418-421; no such rule in the single-patient one) */
                             pllh = -INFINITY;
                             break;
                         }

@@ -27,7 +27,8 @@ def problem_fields(prob: O.PopPKProblem) -> dict:
     keys = ("pk_type", "N", "num_pk_params", "num_pk_pop_params", "d", "P", "T", "sd_ix", "n_transit_ix",
             "transit_time_ix", "biphasic_time_ix", "absorption2_ix", "max_steps", "rtol", "atol", "MW",
             "fixed_vod", "fixed_kf", "fixed_kb", "transforms", "time", "observed", "dose", "dosing_interval",
-            "dose_after_dose_change", "dose_change_time", "intermittent", "skipped_days", "simulate_until")
+            "dose_after_dose_change", "dose_change_time", "intermittent", "skipped_days", "simulate_until",
+            "param_map")
     return {k: getattr(prob, k) for k in keys}
 
 
@@ -106,3 +107,42 @@ def make_problem(pk_type_str: str, P: int = 2, T_days: int = 7, intermittent=0, 
 def draws(lo, hi, n, seed):
     rng = np.random.default_rng(seed)
     return lo + (hi - lo) * rng.random((n, len(lo)))
+
+
+def make_single_problem(pk_type_str: str, T_days: int = 7, intermittent=0, skipped=(), dose_change=None, seed: int = 5,
+                        interval: float = 24.0, patient: str = "p1"):
+    """One patient of make_problem's data for the single-patient likelihood (pharmacokinetic_trajectory):
+    variables by the reference's fixed indices (LikelihoodPharmacokineticTrajectory.cpp:221-253)."""
+    rng = np.random.default_rng(seed)
+    times = [0.0, 1.0, 2.0, 4.0, 8.0] + [24.0 * d for d in range(1, T_days + 1)]
+    T = len(times)
+    pk_type = O.PK_TYPES[pk_type_str]
+    v = [("k_absorption", -1.5, 0.0, True), ("k_excretion", -3.0, -1.5, True), ("clearance", 0.5, 1.5, True),
+         ("volume_of_distribution", 1.5, 2.5, True)]
+    if pk_type in (1, 3, 5):
+        v += [("k_periphery_fwd", -2.5, -1.0, True), ("k_periphery_bwd", -2.5, -1.0, True)]
+    else:
+        v += [("unused4", 0.0, 1.0, False), ("unused5", 0.0, 1.0, False)]
+    if pk_type in (2, 3):
+        v += [("biphasic_uptake_time", 0.0, 1.2, True), ("mean_absorption2", -1.5, -0.5, True)]
+    if pk_type in (4, 5):
+        v += [("n_transit", 0.0, 1.0, True), ("mean_transit_time", 0.0, 0.7, True)]
+    v += [("standard_deviation", -1.0, 1.0, True), ("standard_deviation_proportional", -2.0, -0.7, True)]
+    variables = [O.Variable(n, lo, hi, O.TF_LOG10 if ls else O.TF_NONE) for n, lo, hi, ls in v]
+    nan = None
+    obs = [[nan] + [float(x) for x in rng.uniform(50, 2000, T - 1)] for _ in range(2)]
+    ti = [[1 if d in skipped else 0 for d in range(29)] for _ in range(2)]
+    pk = {"TRIAL": {
+        "time": times, "patients": ["p0", "p1"],
+        "lapatinib_plasma_concentration": obs,
+        "lapatinib_dose": [1000.0, 1250.0],
+        "lapatinib_dose_after_dose_change": [nan if dose_change is None else dose_change[0]] * 2,
+        "lapatinib_dose_change_time": [nan if dose_change is None else dose_change[1]] * 2,
+        "lapatinib_dosing_interval": [interval] * 2,
+        "lapatinib_intermittent": [intermittent] * 2,
+        "treatment_interruptions": ti,
+    }}
+    prob = O.build_single_problem(pk, "TRIAL", "lapatinib", pk_type_str, variables, patient)
+    lo = np.array([x.lower for x in variables])
+    hi = np.array([x.upper for x in variables])
+    return prob, lo, hi, pk
