@@ -100,6 +100,8 @@ def lib() -> C.CDLL:
                                                 C.POINTER(Proposal), i64, u64, u64, vp]
     L.bcm3hip_ptmh_accept_adaptive.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_double, vp, vp, vp, vp,
                                                vp, vp, C.POINTER(Proposal), i64, u64, u64, vp]
+    L.bcm3hip_pt_exchange_pair.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp,
+                                           u64, u64, vp]
     L.bcm3hip_history_add.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp]
     L.bcm3hip_kernel_time_log.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(i64), C.POINTER(C.c_double)]
     L.bcm3hip_eval_batch.argtypes = [vp, sz, sz, vp, vp, vp]
@@ -245,6 +247,12 @@ def ptmh_accept_adaptive(C, d, temps, prop, lprior_prop, llh_prop, log_mh, learn
     check(lib().bcm3hip_ptmh_accept_adaptive(C, d, temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values,
                                              lprior, llh, lpp, accept_out, accepted, C_byref(proposal), chain0,
                                              _u64(seed), _u64(it), stream), "ptmh_accept_adaptive")
+
+
+def pt_exchange_pair(C, d, i1, i2, g1, temps, values, llh, lprior, lpp, acc_out, accepted, seed, rnd, stream=None):
+    """bcm3hip_pt_exchange_pair on device pointers (ints; acc_out / accepted may be None)."""
+    check(lib().bcm3hip_pt_exchange_pair(C, d, i1, i2, g1, temps, values, llh, lprior, lpp, acc_out, accepted,
+                                         _u64(seed), _u64(rnd), stream), "pt_exchange_pair")
 
 
 def history_add(C, d, H, subsampling, temps, values, mask, history, counters, stream=None):

@@ -102,7 +102,7 @@ __global__ void ptmh_accept_kernel(int C, int d, const double* __restrict__ temp
 }
 
 // one ExchangeMove between local chains i1 and i2 of the slice (global index of i1 = g1)
-__device__ void exchange_pair(int d, int i1, int i2, int64_t g1, const double* temps, double* values, double* llh,
+__device__ bool exchange_pair(int d, int i1, int i2, int64_t g1, const double* temps, double* values, double* llh,
                               double* lprior, double* lpp, uint8_t* acc_mask, unsigned long long* accepted,
                               uint64_t seed, uint64_t round)
 {
@@ -131,6 +131,7 @@ __device__ void exchange_pair(int d, int i1, int i2, int64_t g1, const double* t
         if (accepted) atomicAdd(accepted, 1ull);
     }
     if (acc_mask) acc_mask[i1] = swap ? 1 : 0;
+    return swap;
 }
 
 // local pairs of one round: first chains i (local index) with (g0 + i - start) even and i + 1 < C,
@@ -150,6 +151,17 @@ __global__ void pt_exchange_kernel(int C, int d, int64_t g0, int start, int wrap
     if (wrap_local && threadIdx.x == 0) {
         exchange_pair(d, C - 1, 0, g0 + C - 1, temps, values, llh, lprior, lpp, acc_mask, accepted, seed, round);
     }
+}
+
+// one pair (stochastic_random swapping, SamplerPT.cpp:300-305): local chains i1, i2, uniform keyed by
+// the global index g1 of the first
+__global__ void pt_exchange_pair_kernel(int d, int i1, int i2, int64_t g1, const double* temps, double* values,
+                                        double* llh, double* lprior, double* lpp, uint8_t* acc_out,
+                                        unsigned long long* accepted, uint64_t seed, uint64_t round)
+{
+    if (threadIdx.x != 0) return;
+    const bool a = exchange_pair(d, i1, i2, g1, temps, values, llh, lprior, lpp, nullptr, accepted, seed, round);
+    if (acc_out) *acc_out = a ? 1 : 0;
 }
 
 }  // namespace
@@ -198,6 +210,18 @@ int bcm3hip_pt_exchange_local(int C, int d, int64_t g0, int start, int wrap_loca
     if (C == 0) return 0;
     hipLaunchKernelGGL(pt_exchange_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, C, d, g0, start, wrap_local,
                        temps, values, llh, lprior, lpp, acc_mask, (unsigned long long*)accepted, seed, round);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_pt_exchange_pair(int C, int d, int i1, int i2, int64_t g1, const double* temps, double* values,
+                             double* llh, double* lprior, double* lpp, uint8_t* acc_out, uint64_t* accepted,
+                             uint64_t seed, uint64_t round, void* stream)
+{
+    if (C < 2 || d <= 0 || i1 < 0 || i2 < 0 || i1 >= C || i2 >= C || i1 == i2 || !temps || !values || !llh ||
+        !lprior || !lpp)
+        return BCM3HIP_ERR_ARG;
+    hipLaunchKernelGGL(pt_exchange_pair_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d, i1, i2, g1, temps,
+                       values, llh, lprior, lpp, acc_out, (unsigned long long*)accepted, seed, round);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

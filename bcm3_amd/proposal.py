@@ -202,10 +202,10 @@ class SampleHistory:
 
 
 def history_geometry(adapt_proposal_samples: int, use_every_nth: int, exploration_steps: int, num_chains: int,
-                     max_history_size: int):
+                     max_history_size: int, deterministic: bool = True):
     """History size and subsampling (SamplerPT::Initialize, SamplerPT.cpp:113-123)."""
     expected = adapt_proposal_samples * use_every_nth
-    if num_chains > 1:
+    if num_chains > 1 and deterministic:
         expected *= exploration_steps + 1
     sub = 1
     size = expected

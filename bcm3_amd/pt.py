@@ -44,6 +44,23 @@ def exchange_uniform(seed: int, rnd: int, pair: int) -> float:
     return (z >> 11) * (1.0 / 9007199254740992.0)
 
 
+# salts of the stochastic swapping schemes' draws (SamplerPT::Run, SamplerPT.cpp:195-202, 300-305):
+# the reference draws both from its global ranlux48 stream; here they are counter based too
+_MOVE_SALT = 0x6D6F76655F747970
+_PAIR_SALT = 0x706169725F696478
+
+
+def move_uniform(seed: int, iteration: int) -> float:
+    """Uniform deciding exchange (< exchange_probability) vs mutate in a stochastic scheme."""
+    return exchange_uniform(seed ^ _MOVE_SALT, iteration, 0)
+
+
+def random_pair(seed: int, rnd: int, Ctot: int) -> int:
+    """stochastic_random: first chain ci of the pair (ci, ci + 1), uniform in [0, Ctot - 2]
+    (rng.GetUnsignedInt(chains.size() - 2), SamplerPT.cpp:301)."""
+    return min(int(exchange_uniform(seed ^ _PAIR_SALT, rnd, 0) * (Ctot - 1)), Ctot - 2)
+
+
 def _t_splitmix64(x: torch.Tensor) -> torch.Tensor:
     # int64 tensors with two's-complement wraparound; >> emulated as a logical shift
     def lsr(v, k):
@@ -149,6 +166,57 @@ class PTExchange:
             self._cross(values, llh, lprior, lpp, acc_mask)
         self.round += 1
         return acc_mask
+
+    def step_single(self, values: torch.Tensor, llh: torch.Tensor, lprior: torch.Tensor, lpp: torch.Tensor, ci: int):
+        """One stochastic_random exchange of the global pair (ci, ci + 1) in place (SamplerPT.cpp:300-305);
+        ranks owning neither chain do nothing. Returns the accept flag (a 1-element tensor) on the
+        ranks that own a chain of the pair, else None."""
+        C, g0, dev = self.C, self.rank * self.C, self.device
+        l1, l2 = ci - g0, ci + 1 - g0
+        a = None
+        gl = torch.tensor([ci], dtype=torch.int64, device=dev)
+        if 0 <= l1 and l2 < C:
+            i1 = torch.tensor([l1], dtype=torch.int64, device=dev)
+            i2 = torch.tensor([l2], dtype=torch.int64, device=dev)
+            a, p1, p2 = self._accept(self.T[i1], self.T[i2], llh[i1], llh[i2], lprior[i1], lprior[i2], lpp[i1],
+                                     lpp[i2], gl)
+            self._apply_local(values, llh, lprior, lpp, i1, i2, a, p1, p2)
+        elif self.world > 1 and l1 == C - 1:
+            o = self._exchange_record(values, llh, lprior, lpp, C - 1, (self.rank + 1) % self.world)
+            d = values.shape[1]
+            a, p1, _ = self._accept(self.T[C - 1:C], o[d + 3:d + 4], llh[C - 1:C], o[d:d + 1], lprior[C - 1:C],
+                                    o[d + 1:d + 2], lpp[C - 1:C], o[d + 2:d + 3], gl)
+            self._take(values, llh, lprior, lpp, C - 1, o, a, p1)
+        elif self.world > 1 and l2 == 0:
+            q = self._exchange_record(values, llh, lprior, lpp, 0, (self.rank - 1) % self.world)
+            d = values.shape[1]
+            a, _, p2 = self._accept(q[d + 3:d + 4], self.T[0:1], q[d:d + 1], llh[0:1], q[d + 1:d + 2], lprior[0:1],
+                                    q[d + 2:d + 3], lpp[0:1], gl)
+            self._take(values, llh, lprior, lpp, 0, q, a, p2)
+        if a is not None and 0 <= l1:
+            self.attempted += 1
+            self.accepted = self.accepted + a.sum()
+        self.round += 1
+        return a
+
+    def _exchange_record(self, values, llh, lprior, lpp, i, peer):
+        """Send chain i's {values, llh, lprior, lpp, T} to `peer` and receive the peer's record."""
+        import torch.distributed as dist
+        d = values.shape[1]
+        mine = torch.cat([values[i], torch.stack([llh[i], lprior[i], lpp[i], self.T[i]])])
+        other = torch.empty(d + 4, dtype=torch.float64, device=self.device)
+        ops = [dist.P2POp(dist.isend, mine, peer, self.group), dist.P2POp(dist.irecv, other, peer, self.group)]
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+        return other
+
+    @staticmethod
+    def _take(values, llh, lprior, lpp, i, rec, a, p):
+        d = values.shape[1]
+        values[i] = torch.where(a, rec[:d], values[i])
+        llh[i:i + 1] = torch.where(a, rec[d:d + 1], llh[i:i + 1])
+        lprior[i:i + 1] = torch.where(a, rec[d + 1:d + 2], lprior[i:i + 1])
+        lpp[i:i + 1] = torch.where(a, p, lpp[i:i + 1])
 
     @staticmethod
     def _apply_local(values, llh, lprior, lpp, i1, i2, a, p1, p2):

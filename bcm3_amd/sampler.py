@@ -31,7 +31,7 @@ from typing import List, Optional
 import torch
 
 from .proposal import DeviceProposal, SampleHistory, history_geometry
-from .pt import PTExchange
+from .pt import PTExchange, move_uniform, random_pair
 
 
 @dataclass
@@ -101,7 +101,8 @@ class PTMHDevice:
                  learning_rate: float = 1.0, exploration_steps: int = 1, group=None,
                  proposal: str = "gaussian_mixture", t_dof: float = 0.0, kmax: int = 1,
                  adapt_proposal_samples: int = 2000, adapt_proposal_times: int = 2, max_history_size: int = 2000,
-                 use_every_nth: int = 1):
+                 use_every_nth: int = 1, swapping_scheme: str = "deterministic_even_odd",
+                 exchange_probability: float = 0.5):
         from . import _hip
         self._hip = _hip
         _hip.lib()  # fails loudly without the HIP library
@@ -134,6 +135,11 @@ class PTMHDevice:
         self.accepted_exchange = torch.zeros(1, dtype=torch.int64, device=dev)
         self.attempted_mutate = 0
         self.attempted_exchange = 0
+        # ptmhsampler.swapping_scheme / exchange_probability (SamplerPT.cpp:63-75, 163-164)
+        if swapping_scheme not in ("deterministic_even_odd", "stochastic_even_odd", "stochastic_random"):
+            raise ValueError(f"Unknown swapping scheme \"{swapping_scheme}\"")
+        self.scheme = swapping_scheme
+        self.exchange_probability = float(exchange_probability)
         # proposals (ptmhsampler.proposal_type) and the sample history that adapts them
         self.proposal_type = proposal
         self.adaptive = proposal != "random_walk"
@@ -144,7 +150,7 @@ class PTMHDevice:
         if self.adaptive:
             self.proposal = DeviceProposal(proposal, prior, self.T, kmax=kmax, t_dof=t_dof)
             H, sub = history_geometry(self.adapt_samples, self.use_every_nth, exploration_steps, self.Ctot,
-                                      max_history_size)
+                                      max_history_size, deterministic=(swapping_scheme == "deterministic_even_odd"))
             self.history = SampleHistory(C, d, H, sub, dev)
             self.log_mh = torch.zeros(C, dtype=torch.float64, device=dev)
             self._masks = {start: self._exchange_masks(start) for start in (0, 1)}
@@ -222,12 +228,49 @@ class PTMHDevice:
         self.attempted_mutate += C
         self.iter += 1
 
+    def exchange_random(self):
+        """stochastic_random DoExchangeMove (SamplerPT.cpp:300-305): one pair (ci, ci + 1), ci drawn
+        from a counter-based stream every rank computes alike; a pair inside this rank's slice
+        runs on the GPU, a pair across a slice boundary over RCCL between its two ranks."""
+        ci = random_pair(self.seed, self.round, self.Ctot)
+        l1, l2 = ci - self.g0, ci + 1 - self.g0
+        if 0 <= l1 and l2 < self.C:
+            self._hip.pt_exchange_pair(self.C, self.d, l1, l2, ci, self.T.data_ptr(), self.values.data_ptr(),
+                                       self.llh.data_ptr(), self.lprior.data_ptr(), self.lpp.data_ptr(), None,
+                                       self.accepted_exchange.data_ptr(), self.seed, self.round, self._stream())
+            self.attempted_exchange += 1
+        elif self.world > 1 and (l1 == self.C - 1 or l2 == 0):
+            self.ex.round = self.round
+            a = self.ex.step_single(self.values, self.llh, self.lprior, self.lpp, ci)
+            if l1 == self.C - 1:
+                self.accepted_exchange += a.to(torch.int64)
+                self.attempted_exchange += 1
+        if self.adaptive:
+            mine = [i for i in (l1, l2) if 0 <= i < self.C]
+            if mine:
+                mask = torch.zeros(self.C, dtype=torch.uint8, device=self.dev)
+                mask[mine] = 1
+                self.history.add(self.T, self.values, mask, self._stream())
+        self.round += 1
+
     def iteration(self, last: bool = False):
-        """One DeterministicEvenOdd iteration (SamplerPT.cpp:203-212), then the proposal adaptation
-        every adapt_proposal_samples samples, at most adapt_proposal_times times and not after the
-        last sample (SamplerPT.cpp:226-248)."""
-        self.exchange()
-        for _ in range(self.exploration_steps):
+        """One iteration of SamplerPT::Run (SamplerPT.cpp:191-219): deterministic_even_odd = an
+        exchange round then num_exploration_steps mutate moves; the stochastic schemes make an
+        exchange move with probability exchange_probability, else one mutate move; a single chain
+        only mutates. Then the proposal adaptation every adapt_proposal_samples samples, at most
+        adapt_proposal_times times and not after the last sample (SamplerPT.cpp:226-248)."""
+        if self.Ctot < 2:
+            self.mutate()
+        elif self.scheme == "deterministic_even_odd":
+            self.exchange()
+            for _ in range(self.exploration_steps):
+                self.mutate()
+        elif move_uniform(self.seed, self.samples_done) < self.exchange_probability:
+            if self.scheme == "stochastic_even_odd":
+                self.exchange()
+            else:
+                self.exchange_random()
+        else:
             self.mutate()
         si = self.samples_done
         self.samples_done += 1

@@ -225,6 +225,12 @@ int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double
 int bcm3hip_history_add(int C, int d, int H, int subsampling, const double* temps, const double* values,
                         const uint8_t* mask, float* history, int64_t* counters, void* stream);
 
+/* One exchange between local chains i1 and i2 (stochastic_random swapping, SamplerPT.cpp:300-305;
+ * g1 = global index of i1, keys the uniform); *acc_out (may be NULL) = 1 if swapped. */
+int bcm3hip_pt_exchange_pair(int C, int d, int i1, int i2, int64_t g1, const double* temps, double* values,
+                             double* llh, double* lprior, double* lpp, uint8_t* acc_out, uint64_t* accepted,
+                             uint64_t seed, uint64_t round, void* stream);
+
 /* Parity/diagnostic batch (host buffers, any output may be NULL):
  * patient_llh[n*P], traj[n*P*N*T] (states at output times, NaN where not simulated),
  * stats[n*P]. PopPK contexts only. */

@@ -42,3 +42,23 @@ def exchange_round(chains, temps, rnd, seed, uniform):
         out.append((ci, ix2, acc))
         ci += 2
     return out
+
+
+def exchange_single(chains, temps, ci, rnd, seed, uniform):
+    """stochastic_random (SamplerPT.cpp:300-305): ExchangeMove of the pair (ci, ci + 1) only."""
+    c1, c2 = chains[ci], chains[ci + 1]
+    t1, t2 = temps[ci], temps[ci + 1]
+    p1 = c2["lprior"] if t1 == 0.0 else t1 * c2["llh"] + c2["lprior"]
+    p2 = c1["lprior"] if t2 == 0.0 else t2 * c1["llh"] + c1["lprior"]
+    x = (p1 + p2) - (c1["lpp"] + c2["lpp"])
+    if math.isnan(x) or x >= 0.0:
+        tp = 1.0
+    else:
+        tp = math.exp(x)
+        tp = tp if tp < 1.0 else 1.0
+    acc = uniform(seed, rnd, ci) < tp
+    if acc:
+        for k in ("values", "llh", "lprior"):
+            c1[k], c2[k] = c2[k], c1[k]
+        c1["lpp"], c2["lpp"] = p1, p2
+    return acc

@@ -134,3 +134,85 @@ def test_sharded_gloo_matches_sequential(world, Ctot):
     # at least one cross-rank swap happened, so the P2P path was exercised
     cross = [a for pairs in log for ci, _, a in pairs if (ci + 1) % C == 0]
     assert any(cross)
+
+
+# ---- stochastic_random: one pair per exchange move (SamplerPT.cpp:300-305)
+
+def _run_oracle_single(temps, values, llh, lprior, seed, rounds):
+    chains = []
+    for i in range(len(temps)):
+        lpp = lprior[i] if temps[i] == 0.0 else lprior[i] + temps[i] * llh[i]
+        chains.append({"values": list(values[i]), "llh": float(llh[i]), "lprior": float(lprior[i]), "lpp": lpp})
+    log = []
+    for r in range(rounds):
+        ci = pt.random_pair(seed, r, len(temps))
+        log.append([(ci, ci + 1, pt_oracle.exchange_single(chains, temps, ci, r, seed, pt.exchange_uniform))])
+    return chains, log
+
+
+def _run_sharded_single(temps, values, llh, lprior, seed, rounds, rank, world):
+    ex = pt.PTExchange(temps, rank=rank, world=world, seed=seed)
+    C = ex.C
+    sl = slice(rank * C, (rank + 1) * C)
+    v = torch.tensor(values[sl]).clone()
+    l = torch.tensor(llh[sl]).clone()
+    q = torch.tensor(lprior[sl]).clone()
+    lpp = ex.lpowerposterior(l, q)
+    acc = []
+    for r in range(rounds):
+        ci = pt.random_pair(seed, r, len(temps))
+        a = ex.step_single(v, l, q, lpp, ci)
+        m = np.zeros(C, dtype=bool)
+        if a is not None and 0 <= ci - rank * C < C:
+            m[ci - rank * C] = bool(a.item())
+        acc.append(m)
+    return v.numpy(), l.numpy(), q.numpy(), lpp.numpy(), np.array(acc)
+
+
+def test_random_pair_range():
+    got = {pt.random_pair(3, r, 6) for r in range(400)}
+    assert got == {0, 1, 2, 3, 4}
+    assert all(0.0 <= pt.move_uniform(9, i) < 1.0 for i in range(100))
+
+
+def test_single_pair_single_rank_matches_sequential():
+    Ctot = 9
+    temps = pt.temperature_ladder(Ctot)
+    values, llh, lprior = _initial_state(Ctot, 4, 5)
+    chains, log = _run_oracle_single(temps, values, llh, lprior, 17, ROUNDS)
+    _compare(chains, log, _run_sharded_single(temps, values, llh, lprior, 17, ROUNDS, 0, 1), 0, Ctot)
+    assert any(a for pairs in log for _, _, a in pairs)
+
+
+def _worker_single(rank, world, port, Ctot, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        temps = pt.temperature_ladder(Ctot)
+        values, llh, lprior = _initial_state(Ctot, 3, 4321)
+        q.put((rank, _run_sharded_single(temps, values, llh, lprior, 11, 3 * ROUNDS, rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,Ctot", [(2, 8), (4, 8)])
+def test_single_pair_sharded_gloo_matches_sequential(world, Ctot):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_single, args=(r, world, port, Ctot, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    temps = pt.temperature_ladder(Ctot)
+    values, llh, lprior = _initial_state(Ctot, 3, 4321)
+    chains, log = _run_oracle_single(temps, values, llh, lprior, 11, 3 * ROUNDS)
+    C = Ctot // world
+    for r in range(world):
+        _compare(chains, log, results[r], r, C)
+    assert any(a for pairs in log for ci, _, a in pairs if (ci + 1) % C == 0)  # a cross-rank swap happened

@@ -143,3 +143,63 @@ def test_device_sampler_runs_and_accepts():
     want = torch.where(T == 0, loop.lprior, loop.lprior + T * loop.llh)
     assert torch.allclose(loop.lpp, want, rtol=0, atol=1e-9, equal_nan=True)
     assert not torch.equal(lpp0, loop.lpp)
+
+
+def test_exchange_pair_kernel_matches_sequential():
+    """stochastic_random's single-pair exchange (bcm3hip_pt_exchange_pair) vs the sequential
+    restatement of ExchangeMove, over many random pairs."""
+    from bcm3_amd import _hip
+    from bcm3_amd import pt
+    Ctot, d, seed = 12, 4, 31
+    temps = pt.temperature_ladder(Ctot)
+    rng = np.random.default_rng(2)
+    values = rng.normal(size=(Ctot, d))
+    llh = rng.normal(-40.0, 3.0, size=Ctot)
+    llh[3] = -math.inf
+    lprior = rng.normal(-4.0, 1.0, size=Ctot)
+    chains = []
+    for i in range(Ctot):
+        lpp = lprior[i] if temps[i] == 0.0 else lprior[i] + temps[i] * llh[i]
+        chains.append({"values": list(values[i]), "llh": float(llh[i]), "lprior": float(lprior[i]), "lpp": lpp})
+    T = torch.tensor(temps, dtype=torch.float64, device="cuda")
+    v = torch.tensor(values, device="cuda")
+    l = torch.tensor(llh, device="cuda")
+    q = torch.tensor(lprior, device="cuda")
+    p = torch.tensor([c["lpp"] for c in chains], device="cuda")
+    acc = torch.zeros(1, dtype=torch.uint8, device="cuda")
+    n_acc = 0
+    for r in range(200):
+        ci = pt.random_pair(seed, r, Ctot)
+        want = pt_oracle.exchange_single(chains, temps, ci, r, seed, pt.exchange_uniform)
+        _hip.pt_exchange_pair(Ctot, d, ci, ci + 1, ci, T.data_ptr(), v.data_ptr(), l.data_ptr(), q.data_ptr(),
+                              p.data_ptr(), acc.data_ptr(), None, seed, r)
+        torch.cuda.synchronize()
+        assert bool(acc.item()) == want, r
+        n_acc += want
+    assert n_acc > 0
+    for i in range(Ctot):
+        assert np.array_equal(v[i].cpu().numpy(), np.array(chains[i]["values"]))
+        a, b = p[i].item(), chains[i]["lpp"]
+        assert a == b or (math.isnan(a) and math.isnan(b))
+
+
+@pytest.mark.parametrize("scheme", ["stochastic_even_odd", "stochastic_random"])
+def test_device_sampler_stochastic_schemes(scheme):
+    from bcm3_amd import pt
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.pt import temperature_ladder
+    from bcm3_amd.sampler import DevicePrior, PTMHDevice, load_prior
+    prior = DevicePrior(load_prior(os.path.join(H.GOLDEN, "circular_prior.xml")), "cuda")
+    ll = Likelihood(os.path.join(H.GOLDEN, "circular_likelihood.xml"), os.path.join(H.GOLDEN, "circular_prior.xml"),
+                    device=0)
+    s = PTMHDevice(ll, prior, temperature_ladder(16), seed=8, swapping_scheme=scheme, exchange_probability=0.3)
+    s.run(200)
+    torch.cuda.synchronize()
+    n_ex = sum(pt.move_uniform(8, i) < 0.3 for i in range(200))
+    assert s.attempted_mutate == 16 * (200 - n_ex)
+    per_move = 8 if scheme == "stochastic_even_odd" else 1
+    assert s.attempted_exchange == per_move * n_ex
+    assert int(s.accepted_exchange.item()) > 0
+    T = s.T
+    want = torch.where(T == 0, s.lprior, s.lprior + T * s.llh)
+    assert torch.allclose(s.lpp, want, rtol=0, atol=1e-9, equal_nan=True)
