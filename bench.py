@@ -57,15 +57,17 @@ def algorithmic_bytes_per_eval(m) -> int:
 
 
 def traffic_from_profiles(tag: str, n: int):
-    """HBM bytes per launch from the committed PMC summary (tools/pmc_traffic.py), or None."""
-    path = os.path.join(PROFILES, f"r01_traffic_{tag}.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)
-        if int(t.get("n", -1)) == n:
-            return float(t["bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
-        pass
+    """HBM bytes per launch from the newest committed PMC summary (tools/pmc_traffic.py,
+    profiles/<round tag>_traffic_<tag>.json), or None."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(PROFILES, f"*_traffic_{tag}.json")), reverse=True):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+            if int(t.get("n", -1)) == n:
+                return float(t["bytes_per_launch"])
+        except (OSError, ValueError, KeyError):
+            continue
     return None
 
 
