@@ -96,7 +96,7 @@ def lib() -> C.CDLL:
                                       u64, u64, vp]
     L.bcm3hip_pt_exchange_local.argtypes = [C.c_int, C.c_int, i64, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp,
                                             u64, u64, vp]
-    L.bcm3hip_ptmh_propose_adaptive.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp,
+    L.bcm3hip_ptmh_propose_adaptive.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                                 C.POINTER(Proposal), i64, u64, u64, vp]
     L.bcm3hip_ptmh_accept_adaptive.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_double, vp, vp, vp, vp,
                                                vp, vp, C.POINTER(Proposal), i64, u64, u64, vp]
@@ -233,10 +233,10 @@ def pt_exchange_local(C, d, g0, start, wrap_local, temps, values, llh, lprior, l
                                           acc_mask, accepted, _u64(seed), _u64(rnd), stream), "pt_exchange_local")
 
 
-def ptmh_propose_adaptive(C, d, kind, p0, p1, temps, values, prop, lprior_prop, log_mh, proposal: Proposal, chain0,
-                          seed, it, stream=None):
+def ptmh_propose_adaptive(C, d, kind, p0, p1, p2, temps, values, prop, lprior_prop, log_mh, proposal: Proposal,
+                          chain0, seed, it, stream=None):
     """bcm3hip_ptmh_propose_adaptive on device pointers (ints) and a Proposal of device pointers."""
-    check(lib().bcm3hip_ptmh_propose_adaptive(C, d, kind, p0, p1, temps, values, prop, lprior_prop, log_mh,
+    check(lib().bcm3hip_ptmh_propose_adaptive(C, d, kind, p0, p1, p2, temps, values, prop, lprior_prop, log_mh,
                                               C_byref(proposal), chain0, _u64(seed), _u64(it), stream),
           "ptmh_propose_adaptive")
 

@@ -28,6 +28,7 @@
 
 #include "../../include/bcm3hip.h"
 #include "ctr_rng.h"
+#include "prior_marginal.h"
 
 namespace bcm3hip {
 namespace {
@@ -141,19 +142,11 @@ __device__ double gamma_draw(double k, double theta, uint64_t seed, uint64_t ite
     return theta * dd * v * scale_u;
 }
 
-__device__ double prior_logpdf(int kind, double p0, double p1, double x)
-{
-    // UnivariateMarginal::EvaluateLogPDF (UnivariateMarginal.cpp:326-345)
-    if (kind == BCM3HIP_PRIOR_UNIFORM) return (x < p0 || x > p1) ? -INFINITY : -log(p1 - p0);
-    const double s = p1;
-    const double dx = x - p0;
-    return log(1.0 / sqrt(2.0 * s * s * 3.141592653589793)) - dx * dx * (1.0 / (2.0 * s * s));
-}
 
 // one chain of ptmh_propose_adaptive (see the file header); v, t: [d], rf, rr: [K] scratch
 __device__ __forceinline__ void propose_chain(int c, int d, const int32_t* __restrict__ kind,
                                               const double* __restrict__ p0, const double* __restrict__ p1,
-                                              const double* __restrict__ temps, const double* __restrict__ values,
+                                              const double* __restrict__ p2, const double* __restrict__ temps, const double* __restrict__ values,
                                               double* __restrict__ prop, double* __restrict__ lprior_prop,
                                               double* __restrict__ log_mh, const bcm3hip_proposal& P, uint64_t gc,
                                               uint64_t seed, uint64_t iter, double* v, double* t, double* rf,
@@ -163,13 +156,8 @@ __device__ __forceinline__ void propose_chain(int c, int d, const int32_t* __res
     double* nxt = prop + (int64_t)c * d;
     double lmh = 0.0;
     if (temps[c] == 0.0) {
-        // PriorIndependence::Sample: uniform a + u (b - a), normal mu + sigma z
-        for (int i = 0; i < d; i++) {
-            if (kind[i] == BCM3HIP_PRIOR_UNIFORM)
-                nxt[i] = p0[i] + u01(rng_key(seed, iter, gc, rng::KEY_PRIOR_UNIFORM + i)) * (p1[i] - p0[i]);
-            else
-                nxt[i] = p0[i] + p1[i] * normal01(seed, iter, gc, rng::SLOT_PRIOR_NORMAL + i);
-        }
+        // PriorIndependence::Sample
+        for (int i = 0; i < d; i++) nxt[i] = prior::sample(kind[i], p0[i], p1[i], p2[i], seed, iter, gc, i);
     } else {
         const int Km = P.kmax;
         int K = (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) ? P.ncomp[c] : 1;
@@ -261,7 +249,7 @@ __device__ __forceinline__ void propose_chain(int c, int d, const int32_t* __res
         P.selected[c] = sel;
     }
     double lp = 0.0;
-    for (int i = 0; i < d; i++) lp += prior_logpdf(kind[i], p0[i], p1[i], nxt[i]);
+    for (int i = 0; i < d; i++) lp += prior::log_pdf(kind[i], p0[i], p1[i], p2[i], nxt[i]);
     lprior_prop[c] = lp;
     log_mh[c] = lmh;
 }
@@ -328,7 +316,7 @@ __device__ __forceinline__ double wave_responsibilities(int K, int d, double x, 
 
 __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
     int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0, const double* __restrict__ p1,
-    const double* __restrict__ temps, const double* __restrict__ values, double* __restrict__ prop,
+    const double* __restrict__ p2, const double* __restrict__ temps, const double* __restrict__ values, double* __restrict__ prop,
     double* __restrict__ lprior_prop, double* __restrict__ log_mh, bcm3hip_proposal P, int64_t chain0,
     uint64_t seed, uint64_t iter)
 {
@@ -342,10 +330,7 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
     double nxt;
     double lmh = 0.0;
     if (temps[c] == 0.0) {
-        if (kind[li] == BCM3HIP_PRIOR_UNIFORM)
-            nxt = p0[li] + u01(rng_key(seed, iter, gc, rng::KEY_PRIOR_UNIFORM + li)) * (p1[li] - p0[li]);
-        else
-            nxt = p0[li] + p1[li] * normal01(seed, iter, gc, rng::SLOT_PRIOR_NORMAL + li);
+        nxt = prior::sample(kind[li], p0[li], p1[li], p2[li], seed, iter, gc, li);
     } else {
         const int Km = P.kmax;
         int K = (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) ? P.ncomp[c] : 1;
@@ -435,7 +420,7 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
         if (lane == 0) P.selected[c] = sel;
     }
     if (on) prop[(int64_t)c * d + lane] = nxt;
-    const double lp = wave_seq_sum(d, on ? prior_logpdf(kind[li], p0[li], p1[li], nxt) : 0.0);
+    const double lp = wave_seq_sum(d, on ? prior::log_pdf(kind[li], p0[li], p1[li], p2[li], nxt) : 0.0);
     if (lane == 0) {
         lprior_prop[c] = lp;
         log_mh[c] = lmh;
@@ -445,7 +430,7 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
 // generic path (d > 64): one thread per chain, its vectors in the global work buffer
 __global__ void __launch_bounds__(64) ptmh_propose_adaptive_kernel(
     int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0, const double* __restrict__ p1,
-    const double* __restrict__ temps, const double* __restrict__ values, double* __restrict__ prop,
+    const double* __restrict__ p2, const double* __restrict__ temps, const double* __restrict__ values, double* __restrict__ prop,
     double* __restrict__ lprior_prop, double* __restrict__ log_mh, bcm3hip_proposal P, int64_t chain0,
     uint64_t seed, uint64_t iter)
 {
@@ -453,7 +438,7 @@ __global__ void __launch_bounds__(64) ptmh_propose_adaptive_kernel(
     if (c >= C) return;
     const int Km = P.kmax;
     double* work = P.work + (int64_t)c * (2 * Km + 2 * d);
-    propose_chain(c, d, kind, p0, p1, temps, values, prop, lprior_prop, log_mh, P, (uint64_t)(chain0 + c), seed,
+    propose_chain(c, d, kind, p0, p1, p2, temps, values, prop, lprior_prop, log_mh, P, (uint64_t)(chain0 + c), seed,
                   iter, work + 2 * Km, work + 2 * Km + d, work, work + Km);
 }
 
@@ -539,22 +524,25 @@ using namespace bcm3hip;
 extern "C" {
 
 int bcm3hip_ptmh_propose_adaptive(int C, int d, const int32_t* prior_kind, const double* prior_p0,
-                                  const double* prior_p1, const double* temps, const double* values, double* prop,
-                                  double* lprior_prop, double* log_mh, const bcm3hip_proposal* proposal,
-                                  int64_t chain0, uint64_t seed, uint64_t iter, void* stream)
+                                  const double* prior_p1, const double* prior_p2, const double* temps,
+                                  const double* values, double* prop, double* lprior_prop, double* log_mh,
+                                  const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed, uint64_t iter,
+                                  void* stream)
 {
     if (C < 0 || d <= 0 || !proposal_ok(proposal, C, d) ||
-        (C > 0 && (!prior_kind || !prior_p0 || !prior_p1 || !temps || !values || !prop || !lprior_prop || !log_mh)))
+        (C > 0 && (!prior_kind || !prior_p0 || !prior_p1 || !prior_p2 || !temps || !values || !prop ||
+                   !lprior_prop || !log_mh)))
         return BCM3HIP_ERR_ARG;
     if (C == 0) return 0;
     // one wavefront per chain (lanes over variables) up to 64 variables, beyond one thread per chain
     if (d <= 64)
         hipLaunchKernelGGL(ptmh_propose_wave_kernel, dim3(C), dim3(64), 0, (hipStream_t)stream, C, d, prior_kind,
-                           prior_p0, prior_p1, temps, values, prop, lprior_prop, log_mh, *proposal, chain0, seed, iter);
+                           prior_p0, prior_p1, prior_p2, temps, values, prop, lprior_prop, log_mh, *proposal, chain0,
+                           seed, iter);
     else
         hipLaunchKernelGGL(ptmh_propose_adaptive_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C,
-                           d, prior_kind, prior_p0, prior_p1, temps, values, prop, lprior_prop, log_mh, *proposal,
-                           chain0, seed, iter);
+                           d, prior_kind, prior_p0, prior_p1, prior_p2, temps, values, prop, lprior_prop, log_mh,
+                           *proposal, chain0, seed, iter);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -58,14 +58,12 @@ class DeviceProposal:
         self.temps = temps
         C, d, K = self.C, self.d, self.kmax
         f64 = dict(dtype=torch.float64, device=dev)
-        inf = torch.full((d,), math.inf, **f64)
         # Prior::GetLowerBound / GetUpperBound (UnivariateMarginal.cpp:627-647)
-        self.lower = torch.where(prior.is_uniform, prior.a, -inf).contiguous()
-        self.upper = torch.where(prior.is_uniform, prior.b, inf).contiguous()
+        self.lower = prior.lower.to(**f64).contiguous()
+        self.upper = prior.upper.to(**f64).contiguous()
         # EvaluateMarginalMean / Variance (UnivariateMarginal.cpp:448-540)
-        self.prior_mean = torch.where(prior.is_uniform, 0.5 * (prior.b + prior.a), prior.mu)
-        width = prior.b - prior.a
-        self.prior_var = torch.where(prior.is_uniform, (width * width) / 12.0, prior.sigma * prior.sigma)
+        self.prior_mean = prior.mean.to(**f64)
+        self.prior_var = prior.var.to(**f64)
         self.target = target_acceptance_rate(d)
         self.ncomp = torch.ones(C, dtype=torch.int32, device=dev)
         self.weights = torch.zeros((C, K), **f64)

@@ -34,13 +34,99 @@ from .proposal import DeviceProposal, SampleHistory, history_geometry
 from .pt import PTExchange, move_uniform, random_pair
 
 
+PRIOR_KINDS = {"uniform": 0, "normal": 1, "exponential": 2, "gamma": 3, "beta": 4, "half_cauchy": 5, "beta_prime": 6,
+               "exponential_mix": 7}
+
+
 @dataclass
 class Marginal:
-    kind: str  # "uniform" | "normal"
+    """One UnivariateMarginal (src/sampler/UnivariateMarginal.cpp:25-101): kind and its
+    parameters p = (p0, p1, p2) in the order of BCM3HIP_PRIOR_* (include/bcm3hip.h)."""
+    kind: str
     a: float = 0.0
     b: float = 0.0
     mu: float = 0.0
     sigma: float = 1.0
+    p: tuple = (0.0, 0.0, 0.0)
+
+    def bounds(self):
+        """GetLowerBound / GetUpperBound (UnivariateMarginal.cpp:627-647)."""
+        lo = self.a if self.kind == "uniform" else (
+            0.0 if self.kind in ("beta", "exponential", "gamma", "half_cauchy", "beta_prime") else -math.inf)
+        hi = self.b if self.kind == "uniform" else (1.0 if self.kind == "beta" else math.inf)
+        return lo, hi
+
+    def moments(self):
+        """EvaluateMean / EvaluateVariance (UnivariateMarginal.cpp:448-540)."""
+        p0, p1, p2 = self.p
+        k = self.kind
+        if k == "uniform":
+            d = p1 - p0
+            return 0.5 * (p1 + p0), (d * d) / 12.0
+        if k == "normal":
+            return p0, p1 * p1
+        if k == "exponential":
+            return 1.0 / p0, 1.0 / (p0 * p0)
+        if k == "gamma":
+            return p0 * p1, p0 * p1 * p1
+        if k == "beta":
+            apb = p0 + p1
+            return p0 / apb, (p0 * p1) / (apb * apb * (apb + 1))
+        if k == "half_cauchy":
+            return p0, p0 * p0
+        if k == "beta_prime":
+            mean = p2 * p0 / (p1 - 1) if p1 > 1.0 else p2
+            var = (p2 * p2 * p0 * (p0 + p1 - 1.0) / ((p1 - 2) * (p1 - 1) * (p1 - 1))) if p1 > 2.0 else p2 * p2
+            return mean, var
+        # exponential_mix
+        return p2 / p0 + (1.0 - p2) / p1, p2 * p2 / (p0 * p0) + (1.0 - p2) ** 2 / (p1 * p1)
+
+
+def _marginal(v) -> Marginal:
+    """UnivariateMarginal::Initialize (UnivariateMarginal.cpp:25-101) for one <variable>."""
+    dist = v.get("distribution")
+
+    def f(k):
+        x = v.get(k)
+        if x is None:
+            raise ValueError(f"Error parsing UnivariateMarginal: no attribute {k}")
+        return float(x)
+
+    if dist == "uniform":
+        a, b = f("lower"), f("upper")
+        if b <= a:
+            raise ValueError("Uniform distribution with upper bound less than or equal to lower bound.")
+        return Marginal("uniform", a=a, b=b, p=(a, b, 0.0))
+    if dist == "normal":
+        mu, sigma = f("mu"), f("sigma")
+        if sigma <= 0.0:
+            raise ValueError("Normal distribution with non-positive sigma.")
+        return Marginal("normal", mu=mu, sigma=sigma, p=(mu, sigma, 0.0))
+    if dist == "exponential":
+        lam = f("lambda")
+        if lam <= 0.0:
+            raise ValueError("Exponential distribution with non-positive lambda.")
+        return Marginal("exponential", p=(lam, 0.0, 0.0))
+    if dist == "gamma":
+        k, theta = f("k"), f("theta")
+        if k <= 0.0 or theta <= 0.0:
+            raise ValueError("Gamma distribution with non-positive k or theta.")
+        return Marginal("gamma", p=(k, theta, 0.0))
+    if dist == "beta":
+        a, b = f("a"), f("b")
+        if a <= 0.0 or b <= 0.0:
+            raise ValueError("Beta distribution with non-positive a or b.")
+        return Marginal("beta", p=(a, b, 0.0))
+    if dist == "half_cauchy":
+        sc = f("scale")
+        if sc <= 0.0:
+            raise ValueError("Half-Cauchy distribution with non-positive scale.")
+        return Marginal("half_cauchy", p=(sc, 0.0, 0.0))
+    if dist == "beta_prime":
+        return Marginal("beta_prime", p=(f("a"), f("b"), f("scale")))
+    if dist == "exponential_mix":
+        return Marginal("exponential_mix", p=(f("lambda"), f("lambda2"), f("mix")))
+    raise ValueError(f"Invalid distribution type \"{dist}\"")
 
 
 def load_prior(path: str) -> List[Marginal]:
@@ -48,35 +134,40 @@ def load_prior(path: str) -> List[Marginal]:
     root = ET.parse(path).getroot()
     out = []
     for v in root.iter("variable"):
-        dist = v.get("distribution")
-        if dist == "uniform":
-            m = Marginal("uniform", a=float(v.get("lower")), b=float(v.get("upper")))
-            if m.b <= m.a:
-                raise ValueError("Uniform distribution with upper bound less than or equal to lower bound.")
-        elif dist == "normal":
-            m = Marginal("normal", mu=float(v.get("mu")), sigma=float(v.get("sigma")))
-        else:
-            raise ValueError(f"prior distribution '{dist}' not supported by the device sampler")
-        out += [m] * int(v.get("repeat", "1"))
+        out += [_marginal(v)] * int(v.get("repeat", "1"))
     return out
 
 
 class DevicePrior:
+    """PriorIndependence over the marginals of a prior.xml, as device arrays: kind codes and
+    parameters for the kernels, bounds and moments for the proposals."""
+
     def __init__(self, marginals: List[Marginal], device):
         dev = torch.device(device)
         self.d = len(marginals)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.kind_codes = torch.tensor([PRIOR_KINDS[m.kind] for m in marginals], dtype=torch.int32, device=dev)
+        self.p0 = torch.tensor([m.p[0] for m in marginals], **f64)
+        self.p1 = torch.tensor([m.p[1] for m in marginals], **f64)
+        self.p2 = torch.tensor([m.p[2] for m in marginals], **f64)
+        self.lower = torch.tensor([m.bounds()[0] for m in marginals], **f64)
+        self.upper = torch.tensor([m.bounds()[1] for m in marginals], **f64)
+        self.mean = torch.tensor([m.moments()[0] for m in marginals], **f64)
+        self.var = torch.tensor([m.moments()[1] for m in marginals], **f64)
+        self.simple = all(m.kind in ("uniform", "normal") for m in marginals)
         self.is_uniform = torch.tensor([m.kind == "uniform" for m in marginals], device=dev)
-        self.a = torch.tensor([m.a for m in marginals], dtype=torch.float64, device=dev)
-        self.b = torch.tensor([m.b for m in marginals], dtype=torch.float64, device=dev)
-        self.mu = torch.tensor([m.mu for m in marginals], dtype=torch.float64, device=dev)
-        self.sigma = torch.tensor([m.sigma for m in marginals], dtype=torch.float64, device=dev)
+        self.a = torch.tensor([m.a for m in marginals], **f64)
+        self.b = torch.tensor([m.b for m in marginals], **f64)
+        self.mu = torch.tensor([m.mu for m in marginals], **f64)
+        self.sigma = torch.tensor([m.sigma for m in marginals], **f64)
         self.log_uniform = -torch.log(self.b - self.a)
         self.log_norm = torch.log(torch.rsqrt(2.0 * self.sigma * self.sigma * math.pi))
         self.inv2s2 = 1.0 / (2.0 * self.sigma * self.sigma)
         # proposal scale for the random walk: a fixed fraction of the marginal's spread
-        self.scale = torch.where(self.is_uniform, 0.02 * (self.b - self.a), 0.1 * self.sigma)
+        self.scale = 0.05 * torch.sqrt(self.var)
 
     def log_pdf(self, x: torch.Tensor) -> torch.Tensor:
+        """Uniform / normal marginals (a host check for tests; the kernels evaluate every type)."""
         inside = (x >= self.a) & (x <= self.b)
         lu = torch.where(inside, self.log_uniform, torch.full_like(x, -math.inf))
         dx = x - self.mu
@@ -84,6 +175,7 @@ class DevicePrior:
         return torch.where(self.is_uniform, lu, ln).sum(dim=1)
 
     def sample(self, n: int, gen: torch.Generator) -> torch.Tensor:
+        """Uniform / normal marginals (test inputs; T = 0 chains draw on the device)."""
         u = torch.rand((n, self.d), dtype=torch.float64, device=self.a.device, generator=gen)
         z = torch.randn((n, self.d), dtype=torch.float64, device=self.a.device, generator=gen)
         return torch.where(self.is_uniform, self.a + u * (self.b - self.a), self.mu + self.sigma * z)
@@ -102,7 +194,7 @@ class PTMHDevice:
                  proposal: str = "gaussian_mixture", t_dof: float = 0.0, kmax: int = 1,
                  adapt_proposal_samples: int = 2000, adapt_proposal_times: int = 2, max_history_size: int = 2000,
                  use_every_nth: int = 1, swapping_scheme: str = "deterministic_even_odd",
-                 exchange_probability: float = 0.5):
+                 exchange_probability: float = 0.5, initial_position_tries: int = 100):
         from . import _hip
         self._hip = _hip
         _hip.lib()  # fails loudly without the HIP library
@@ -119,10 +211,11 @@ class PTMHDevice:
         self.iter = 0
         self.round = 0
         C, d, dev = self.C, self.d, self.dev
-        self.kind = torch.where(prior.is_uniform, 0, 1).to(torch.int32)
-        self.p0 = torch.where(prior.is_uniform, prior.a, prior.mu).contiguous()
-        self.p1 = torch.where(prior.is_uniform, prior.b, prior.sigma).contiguous()
+        self.kind = prior.kind_codes.contiguous()
+        self.p0, self.p1, self.p2 = prior.p0.contiguous(), prior.p1.contiguous(), prior.p2.contiguous()
         self.scale = prior.scale.contiguous()
+        if proposal == "random_walk" and not prior.simple:
+            raise ValueError("the random-walk proposal kernel supports uniform and normal priors only")
         self.values = torch.empty((C, d), dtype=torch.float64, device=dev)
         self.prop = torch.empty((C, d), dtype=torch.float64, device=dev)
         self.lprior = torch.empty(C, dtype=torch.float64, device=dev)
@@ -154,13 +247,40 @@ class PTMHDevice:
             self.history = SampleHistory(C, d, H, sub, dev)
             self.log_mh = torch.zeros(C, dtype=torch.float64, device=dev)
             self._masks = {start: self._exchange_masks(start) for start in (0, 1)}
-        # initial state: every chain draws from the prior (the propose kernel at T = 0)
+        self._initial_positions(initial_position_tries)
+
+    def _initial_positions(self, tries: int):
+        """Starting positions (SamplerPTChain::Initialize, SamplerPTChain.cpp:188-214): every chain
+        draws from the prior until lprior + T llh > -inf, at most `tries` times. The draws are the
+        propose kernel's T = 0 path on counter streams INIT_ITER, INIT_ITER - 1, ..."""
+        C, d, dev = self.C, self.d, self.dev
         zeros = torch.zeros(C, dtype=torch.float64, device=dev)
-        _hip.ptmh_propose(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(), self.scale.data_ptr(),
-                          zeros.data_ptr(), self.values.data_ptr(), self.values.data_ptr(), self.lprior.data_ptr(),
-                          self.g0, self.seed, self.INIT_ITER, self._stream())
-        self._eval(self.values, self.llh)
-        self.llh.mul_(self.lr)
+        bad = torch.ones(C, dtype=torch.bool, device=dev)
+        self.values.zero_()
+        self.lprior.fill_(-math.inf)
+        self.llh.fill_(-math.inf)
+        for k in range(tries):
+            it = self.INIT_ITER - k
+            if self.adaptive:
+                self._hip.ptmh_propose_adaptive(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(),
+                                                self.p2.data_ptr(), zeros.data_ptr(), self.values.data_ptr(),
+                                                self.prop.data_ptr(), self.lprior_prop.data_ptr(),
+                                                self.log_mh.data_ptr(), self.proposal.struct, self.g0, self.seed, it,
+                                                self._stream())
+            else:
+                self._hip.ptmh_propose(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(),
+                                       self.scale.data_ptr(), zeros.data_ptr(), self.values.data_ptr(),
+                                       self.prop.data_ptr(), self.lprior_prop.data_ptr(), self.g0, self.seed, it,
+                                       self._stream())
+            self._eval(self.prop, self.llh_prop)
+            self.values.copy_(torch.where(bad.view(-1, 1), self.prop, self.values))
+            self.lprior.copy_(torch.where(bad, self.lprior_prop, self.lprior))
+            self.llh.copy_(torch.where(bad, self.llh_prop * self.lr, self.llh))
+            bad = ~(self.lprior + self.T * self.llh > -math.inf)
+            if not bool(bad.any()):
+                break
+        if bool(bad.any()):
+            raise RuntimeError(f"Could not find starting position with power posterior != inf after {tries} tries")
         self.lpp.copy_(self.ex.lpowerposterior(self.llh, self.lprior))
 
     def _stream(self):
@@ -205,7 +325,7 @@ class PTMHDevice:
         if self.adaptive:
             P = self.proposal.struct
             h.ptmh_propose_adaptive(C, d, self.kind.data_ptr(), self.p0.data_ptr(), self.p1.data_ptr(),
-                                    self.T.data_ptr(), self.values.data_ptr(), self.prop.data_ptr(),
+                                    self.p2.data_ptr(), self.T.data_ptr(), self.values.data_ptr(), self.prop.data_ptr(),
                                     self.lprior_prop.data_ptr(), self.log_mh.data_ptr(), P, self.g0, self.seed,
                                     self.iter, st)
             self._eval(self.prop, self.llh_prop)

@@ -162,7 +162,21 @@ int bcm3hip_kernel_time_log(bcm3hip_ctx* ctx, double* total_ms, int64_t* launche
  * bcm3hip_ptmh_accept. Random numbers are counter based: splitmix64 of (seed, iter, global chain
  * index chain0 + c, slot). Replaces SamplerPT::DoMutateMove / DoExchangeMove's per-chain loops
  * (src/sampler/SamplerPT.cpp:277-319, src/sampler/SamplerPTChain.cpp:217-381). */
-enum { BCM3HIP_PRIOR_UNIFORM = 0, BCM3HIP_PRIOR_NORMAL = 1 };
+/* UnivariateMarginal distribution types (src/sampler/UnivariateMarginal.cpp:25-101) and their
+ * parameters (p0, p1, p2): uniform (lower, upper), normal (mu, sigma), exponential (lambda),
+ * gamma (k, theta), beta (a, b), half_cauchy (scale), beta_prime (a, b, scale),
+ * exponential_mix (lambda, lambda2, mix). bcm3hip_ptmh_propose supports uniform and normal;
+ * the adaptive proposal kernels support all. */
+enum {
+    BCM3HIP_PRIOR_UNIFORM = 0,
+    BCM3HIP_PRIOR_NORMAL = 1,
+    BCM3HIP_PRIOR_EXPONENTIAL = 2,
+    BCM3HIP_PRIOR_GAMMA = 3,
+    BCM3HIP_PRIOR_BETA = 4,
+    BCM3HIP_PRIOR_HALF_CAUCHY = 5,
+    BCM3HIP_PRIOR_BETA_PRIME = 6,
+    BCM3HIP_PRIOR_EXPONENTIAL_MIX = 7
+};
 /* prior_kind[d], prior_p0[d] (lower | mu), prior_p1[d] (upper | sigma), scale[d] random-walk sd,
  * temps[C], values[C*d] -> prop[C*d], lprior_prop[C]. T == 0 chains draw from the prior. */
 int bcm3hip_ptmh_propose(int C, int d, const int32_t* prior_kind, const double* prior_p0, const double* prior_p1,
@@ -211,7 +225,8 @@ typedef struct {
 /* As bcm3hip_ptmh_propose, with the proposal's scale update, the mixture component choice and
  * log_mh[C] = log Metropolis-Hastings ratio (0 for global_covariance). */
 int bcm3hip_ptmh_propose_adaptive(int C, int d, const int32_t* prior_kind, const double* prior_p0,
-                                  const double* prior_p1, const double* temps, const double* values, double* prop,
+                                  const double* prior_p1, const double* prior_p2, const double* temps,
+                                  const double* values, double* prop,
                                   double* lprior_prop, double* log_mh, const bcm3hip_proposal* proposal,
                                   int64_t chain0, uint64_t seed, uint64_t iter, void* stream);
 /* As bcm3hip_ptmh_accept, with log_mh added to the transition and the acceptance EMA update. */

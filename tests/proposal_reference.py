@@ -117,18 +117,119 @@ def gamma_draw(k, theta, seed, it, gc):
     return theta * dd * v * scale_u
 
 
-def prior_logpdf(kind, p0, p1, x):
+def _lexp(x, lam):
+    return -math.inf if x < 0.0 else math.log(lam) - lam * x
+
+
+def prior_logpdf(kind, p0, p1, x, p2=0.0):
+    """bcm3_amd/csrc/prior_marginal.h log_pdf (UnivariateMarginal::EvaluateLogPDF)."""
     if kind == 0:
         return -math.inf if (x < p0 or x > p1) else -math.log(p1 - p0)
-    s = p1
-    dx = x - p0
-    return math.log(1.0 / math.sqrt(2.0 * s * s * 3.141592653589793)) - dx * dx * (1.0 / (2.0 * s * s))
+    if kind == 1:
+        s = p1
+        dx = x - p0
+        return math.log(1.0 / math.sqrt(2.0 * s * s * 3.141592653589793)) - dx * dx * (1.0 / (2.0 * s * s))
+    if kind == 2:
+        return _lexp(x, p0)
+    if kind == 3:
+        if x < 0.0 or x == math.inf:
+            return -math.inf
+        if p0 == 1.0:
+            return _lexp(x, 1.0 / p1)
+        return (p0 - 1.0) * math.log(x) - x / p1 - math.lgamma(p0) - p0 * math.log(p1)
+    if kind == 4:
+        if x < 0.0 or x > 1.0:
+            return -math.inf
+        return (p0 - 1.0) * math.log(x) + (p1 - 1.0) * math.log1p(-x) - (math.lgamma(p0) + math.lgamma(p1)
+                                                                           - math.lgamma(p0 + p1))
+    if kind == 5:
+        return -math.inf if x <= 0.0 else -0.45158270528945486472619522989488 - math.log(p0 + x * x / p0)
+    if kind == 6:
+        if x < 0.0:
+            return -math.inf
+        lnc = -math.log(math.exp(math.lgamma(p0) + math.lgamma(p1) - math.lgamma(p0 + p1)) * p2)
+        sx = x / p2
+        return lnc + ((p0 - 1.0) * math.log(sx) - (p0 + p1) * math.log(sx + 1.0))
+    # 7: exponential_mix
+    return logsum2(math.log(p2) + _lexp(x, p0), math.log(1.0 - p2) + _lexp(x, p1))
 
 
-def propose(P, kind, p0, p1, temps, values, chain0, seed, it):
+class _Stream:
+    def __init__(self, seed, it, gc, i):
+        self.seed, self.it, self.gc = seed, it, gc
+        self.base = 0x100000 + (i << 10)
+        self.n = self.u = 0
+
+    def uniform(self):
+        v = _u(self.seed, self.it, self.gc, 2 * (self.base + 0x200) + self.u)
+        self.u += 1
+        return v
+
+    def normal(self):
+        v = _n(self.seed, self.it, self.gc, self.base + self.n)
+        self.n += 1
+        return v
+
+
+def _gamma(k, theta, s):
+    scale_u = 1.0
+    if k < 1.0:
+        scale_u = s.uniform() ** (1.0 / k)
+        k = 1.0 + k
+    d = k - 0.33333333333333333333333333333333
+    c = 0.33333333333333333333333333333333 / math.sqrt(d)
+    v = 1.0
+    for _ in range(256):
+        tries = 0
+        while True:
+            x = s.normal()
+            v = 1.0 + c * x
+            tries += 1
+            if not (v <= 0.0 and tries < 64):
+                break
+        v = v * v * v
+        u = s.uniform()
+        if u < 1 - 0.0331 * x * x * x * x:
+            break
+        if math.log(u) < 0.5 * x * x + d * (1 - v + math.log(v)):
+            break
+    return theta * d * v * scale_u
+
+
+def _beta(a, b, s):
+    x1 = _gamma(a, 1.0, s)
+    x2 = _gamma(b, 1.0, s)
+    return x1 / (x1 + x2)
+
+
+def prior_sample(kind, p0, p1, p2, seed, it, gc, i):
+    """prior_marginal.h sample (UnivariateMarginal::Sample)."""
+    if kind == 0:
+        return p0 + _u(seed, it, gc, KEY_PRIOR_UNIFORM + i) * (p1 - p0)
+    if kind == 1:
+        return p0 + p1 * _n(seed, it, gc, SLOT_PRIOR_NORMAL + i)
+    s = _Stream(seed, it, gc, i)
+    if kind == 2:
+        return -(1.0 / p0) * math.log1p(-s.uniform())
+    if kind == 3:
+        return _gamma(p0, p1, s)
+    if kind == 4:
+        return _beta(p0, p1, s)
+    if kind == 5:
+        return abs(p0 * math.tan(3.141592653589793 * (s.uniform() - 0.5)))
+    if kind == 6:
+        x = _beta(p0, p1, s)
+        return p2 * (x / (1.0 - x))
+    p = s.uniform()
+    lam = p0 if p < p2 else p1
+    return -(1.0 / lam) * math.log1p(-s.uniform())
+
+
+def propose(P, kind, p0, p1, temps, values, chain0, seed, it, p2=None):
     """P: dict of numpy arrays (copies of the DeviceProposal state), updated in place like the
     kernel (scale, selected). Returns prop, lprior_prop, log_mh."""
     C, d = values.shape
+    p2 = np.zeros(d) if p2 is None else p2
     prop = np.empty_like(values)
     lprior = np.zeros(C)
     lmh = np.zeros(C)
@@ -139,10 +240,7 @@ def propose(P, kind, p0, p1, temps, values, chain0, seed, it):
         nxt = [0.0] * d
         if temps[c] == 0.0:
             for i in range(d):
-                if kind[i] == 0:
-                    nxt[i] = p0[i] + _u(seed, it, gc, KEY_PRIOR_UNIFORM + i) * (p1[i] - p0[i])
-                else:
-                    nxt[i] = p0[i] + p1[i] * _n(seed, it, gc, SLOT_PRIOR_NORMAL + i)
+                nxt[i] = prior_sample(kind[i], p0[i], p1[i], p2[i], seed, it, gc, i)
         else:
             gmm = P["kind"] == GAUSSIAN_MIXTURE
             K = int(P["ncomp"][c]) if gmm else 1
@@ -205,7 +303,7 @@ def propose(P, kind, p0, p1, temps, values, chain0, seed, it):
         prop[c] = nxt
         lp = 0.0
         for i in range(d):
-            lp += prior_logpdf(kind[i], p0[i], p1[i], nxt[i])
+            lp += prior_logpdf(kind[i], p0[i], p1[i], nxt[i], p2[i])
         lprior[c] = lp
     return prop, lprior, lmh
 

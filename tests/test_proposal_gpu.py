@@ -20,10 +20,7 @@ def _prior(name="c3_prior.xml"):
 
 
 def _prior_arrays(prior):
-    kind = torch.where(prior.is_uniform, 0, 1).to(torch.int32)
-    p0 = torch.where(prior.is_uniform, prior.a, prior.mu).contiguous()
-    p1 = torch.where(prior.is_uniform, prior.b, prior.sigma).contiguous()
-    return kind, p0, p1
+    return prior.kind_codes, prior.p0, prior.p1, prior.p2
 
 
 def _state(P):
@@ -51,8 +48,8 @@ def _check_propose(kind, K, t_dof, its=(0, 7, 2**40), prior_xml="c3_prior.xml", 
     from bcm3_amd import _hip
     from bcm3_amd.proposal import DeviceProposal
     from bcm3_amd.pt import temperature_ladder
-    prior = _prior(prior_xml)
-    kd, p0, p1 = _prior_arrays(prior)
+    prior = _prior(prior_xml) if isinstance(prior_xml, str) else prior_xml
+    kd, p0, p1, p2 = _prior_arrays(prior)
     d = prior.d
     temps = torch.tensor(temperature_ladder(C), dtype=torch.float64, device="cuda")
     P = DeviceProposal(kind, prior, temps, kmax=max(K, 1), t_dof=t_dof)
@@ -62,20 +59,29 @@ def _check_propose(kind, K, t_dof, its=(0, 7, 2**40), prior_xml="c3_prior.xml", 
     # some chains have proposed before (Update runs on them), with EMAs on both sides of target
     P.selected[::2] = 0
     P.ema.copy_(torch.tensor(rng.uniform(0.1, 0.4, P.ema.shape), device="cuda"))
-    gen = torch.Generator(device="cuda")
-    gen.manual_seed(3)
-    values = prior.sample(C, gen)
+    if prior.simple:
+        gen = torch.Generator(device="cuda")
+        gen.manual_seed(3)
+        values = prior.sample(C, gen)
+    else:  # inside every support: the prior moments, jittered
+        rng0 = np.random.default_rng(3)
+        m = prior.mean.cpu().numpy()
+        sd = np.sqrt(prior.var.cpu().numpy())
+        lo, hi = prior.lower.cpu().numpy(), prior.upper.cpu().numpy()
+        x = np.clip(m + 0.2 * sd * rng0.normal(size=(C, d)), np.where(np.isfinite(lo), lo + 1e-3, -np.inf),
+                    np.where(np.isfinite(hi), hi - 1e-3, np.inf))
+        values = torch.tensor(x, device="cuda")
     prop = torch.empty_like(values)
     lp = torch.empty(C, dtype=torch.float64, device="cuda")
     lmh = torch.empty(C, dtype=torch.float64, device="cuda")
     for it in its:
         ref = _state(P)
-        _hip.ptmh_propose_adaptive(C, d, kd.data_ptr(), p0.data_ptr(), p1.data_ptr(), temps.data_ptr(),
-                                   values.data_ptr(), prop.data_ptr(), lp.data_ptr(), lmh.data_ptr(), P.struct, 128,
-                                   77, it)
+        _hip.ptmh_propose_adaptive(C, d, kd.data_ptr(), p0.data_ptr(), p1.data_ptr(), p2.data_ptr(),
+                                   temps.data_ptr(), values.data_ptr(), prop.data_ptr(), lp.data_ptr(), lmh.data_ptr(),
+                                   P.struct, 128, 77, it)
         torch.cuda.synchronize()
         rp, rl, rm = R.propose(ref, kd.cpu().numpy(), p0.cpu().numpy(), p1.cpu().numpy(), temps.cpu().numpy(),
-                               values.cpu().numpy(), 128, 77, it)
+                               values.cpu().numpy(), 128, 77, it, p2=p2.cpu().numpy())
         # (heavy-tailed t steps of ~1e3 prior widths fold an ulp of pow/sqrt into ~1e-12 absolute)
         np.testing.assert_allclose(prop.cpu().numpy(), rp, rtol=1e-12, atol=1e-11)
         assert np.array_equal(P.selected.cpu().numpy(), ref["selected"])
@@ -84,8 +90,8 @@ def _check_propose(kind, K, t_dof, its=(0, 7, 2**40), prior_xml="c3_prior.xml", 
         assert np.array_equal(np.isinf(got), np.isinf(rl))
         np.testing.assert_allclose(got[np.isfinite(rl)], rl[np.isfinite(rl)], rtol=1e-12)
         np.testing.assert_allclose(lmh.cpu().numpy(), rm, rtol=1e-9, atol=1e-11)
-        # proposals reflect on the prior bounds: every uniform marginal stays inside
-        assert np.all(np.isfinite(got))
+        # proposals reflect on the prior bounds: every marginal stays inside its support
+        assert np.all(np.isfinite(got)) or not prior.simple
         values.copy_(prop)
     return P
 
@@ -196,3 +202,54 @@ def test_sampler_adaptive_proposals(proposal):
     assert 0.05 < ema[-1, 0] < 0.8
     n = s.history.counters.cpu().numpy()
     assert n[0, 0] == 0 and n[1:, 0].min() > 0
+
+
+ALL_KINDS_PRIOR = """<?xml version="1.0" encoding="utf-8"?>
+<variableset>
+  <variable name="u" distribution="uniform" lower="-1.0" upper="2.0"/>
+  <variable name="n" distribution="normal" mu="0.5" sigma="2.0"/>
+  <variable name="e" distribution="exponential" lambda="1.5"/>
+  <variable name="g" distribution="gamma" k="2.5" theta="0.7"/>
+  <variable name="g1" distribution="gamma" k="0.6" theta="2.0"/>
+  <variable name="b" distribution="beta" a="2.0" b="3.0"/>
+  <variable name="h" distribution="half_cauchy" scale="0.8"/>
+  <variable name="bp" distribution="beta_prime" a="3.0" b="4.0" scale="1.5"/>
+  <variable name="em" distribution="exponential_mix" lambda="1.0" lambda2="5.0" mix="0.3"/>
+</variableset>
+"""
+
+
+def test_prior_all_marginal_types(tmp_path):
+    """Every UnivariateMarginal type: T = 0 draws and prior log densities of the kernels vs the
+    restatement (tests/proposal_reference.py), draws inside each support."""
+    from bcm3_amd.sampler import DevicePrior, load_prior
+    path = tmp_path / "prior.xml"
+    path.write_text(ALL_KINDS_PRIOR)
+    prior = DevicePrior(load_prior(str(path)), "cuda")
+    assert prior.kind_codes.tolist() == [0, 1, 2, 3, 3, 4, 5, 6, 7]
+    P = _check_propose("global_covariance", 1, 0.0, its=(0, 9), prior_xml=prior, C=40)
+    # draws of T = 0 chains cover each marginal's support and match its moments roughly
+    from bcm3_amd import _hip
+    from bcm3_amd.pt import temperature_ladder
+    C = 4000
+    d = prior.d
+    temps = torch.zeros(C, dtype=torch.float64, device="cuda")
+    from bcm3_amd.proposal import DeviceProposal
+    Q = DeviceProposal("global_covariance", prior, temps)
+    vals = torch.zeros((C, d), dtype=torch.float64, device="cuda")
+    prop = torch.empty_like(vals)
+    lp = torch.empty(C, dtype=torch.float64, device="cuda")
+    lmh = torch.empty(C, dtype=torch.float64, device="cuda")
+    _hip.ptmh_propose_adaptive(C, d, prior.kind_codes.data_ptr(), prior.p0.data_ptr(), prior.p1.data_ptr(),
+                               prior.p2.data_ptr(), temps.data_ptr(), vals.data_ptr(), prop.data_ptr(), lp.data_ptr(),
+                               lmh.data_ptr(), Q.struct, 0, 5, 1)
+    torch.cuda.synchronize()
+    x = prop.cpu().numpy()
+    assert np.all(np.isfinite(lp.cpu().numpy()))
+    mean = prior.mean.cpu().numpy()
+    sd = np.sqrt(prior.var.cpu().numpy())
+    for i in range(d):
+        if i == 6:  # half-Cauchy: no mean; check the median = scale
+            assert abs(np.median(x[:, i]) - 0.8) < 0.08
+            continue
+        assert abs(x[:, i].mean() - mean[i]) < 5 * sd[i] / math.sqrt(C), (i, x[:, i].mean(), mean[i])
