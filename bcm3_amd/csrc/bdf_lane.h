@@ -420,7 +420,8 @@ BDF_INL void increase_bdf(S& s)
     l[2] = alpha1 = prod = xiold = 1.0;
     alpha0 = -1.0;
     hsum = s.hscale;
-    cfor<1, QMAX>([&](auto j) __attribute__((always_inline)) {
+    // j < q <= QMAX - 1: an order increase never starts from QMAX
+    cfor<1, QMAX - 1>([&](auto j) __attribute__((always_inline)) {
         if (CI(j) < s.q) {
             hsum += s.tau[CI(j) + 1];
             xi = fdiv(hsum, s.hscale);
