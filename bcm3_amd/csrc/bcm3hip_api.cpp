@@ -182,6 +182,7 @@ int bcm3hip_open_popk(int device, const bcm3hip_popk_model* m, bcm3hip_ctx** out
     pm.fixed_vod = m->fixed_vod;
     pm.fixed_kf = m->fixed_kf;
     pm.fixed_kb = m->fixed_kb;
+    pm.unity = 1.0;
     const size_t P = m->P, T = m->T;
     if ((r = upload(c, m->transforms, (size_t)m->d, &pm.transforms)) ||
         (r = upload(c, m->time, T, &pm.time)) || (r = upload(c, m->observed, P * T, &pm.observed)) ||

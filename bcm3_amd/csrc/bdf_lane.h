@@ -21,9 +21,9 @@
 //    1..QMAX with per-j guards on q. No inline-asm barriers: with one trajectory per wavefront
 //    (UNI launch) every value stays wave-uniform to the compiler and every solver branch is a
 //    scalar branch;
-//  * division / sqrt / x^(1/k) use hardware reciprocal + Newton refinement (faithfully rounded,
-//    i.e. within 1 ulp, the same order of perturbation as the reference's own FMA-contraction
-//    build differences -- see DESIGN.md "parity envelope");
+//  * division / sqrt / x^(1/k) use hardware reciprocal + one Newton refinement (within ~11 ulp;
+//    correctly rounded with -DBCM3_CORRECTLY_ROUNDED), a perturbation well inside the
+//    reference's own FMA-contraction build differences -- see DESIGN.md "parity envelope";
 //  * the model supplies a structured (I - gamma J) inverse: for constant-Jacobian models the
 //    saved Jacobian of cvLsLinSys is re-derived from the parameters instead of stored.
 #pragma once
@@ -117,51 +117,75 @@ BDF_INL void cfor_down(F&& f)
 #define SUNMIN(A, B) ((A) < (B) ? (A) : (B))
 
 // ---------------------------------------------------------------------------------------------
-// fast, faithfully rounded arithmetic
+// Fast arithmetic for the divisions, reciprocals and square roots of the BDF step. By default
+// v_rcp_f64 / v_rsq_f64 with ONE Newton (Goldschmidt) step: within ~11 ulp (tools/ubench/
+// rcp_acc.hip, sqrt_acc.hip), 5 % faster per launch at 256 draws (1.425 vs 1.505 ms, C3) and 9 %
+// at 2048 than the correctly rounded forms, which -DBCM3_CORRECTLY_ROUNDED restores (one more
+// Newton step / a residual correction; identical to the CPU's IEEE results on 4M random
+// operands). Either way the three solver forms share these functions and agree bit for bit
+// (tools/lane_diff.py); a divisor that is a compile-time constant in the order-specialised forms
+// but not in the lane form must go through fdiv_c with its folded reciprocal (tq_ra3) or a runtime
+// 1.0 (BdfState::unity), since the compiler folds v_rcp_f64 of a constant to the correctly rounded
+// value. The GPU-vs-CPU llh parity envelope (tests/parity.py) holds for both (512 C3 draws:
+// 99.6 % within 1e-8 fast, 99.4 % correctly rounded).
 
-// reciprocal: v_rcp_f64 estimate + two Newton steps
+// reciprocal
 BDF_INL double frcp(double b)
 {
     double r = __builtin_amdgcn_rcp(b);
     double e = __builtin_fma(-b, r, 1.0);
     r = __builtin_fma(e, r, r);
+#ifndef BCM3_CORRECTLY_ROUNDED
+    return r;
+#else
     e = __builtin_fma(-b, r, 1.0);
     return __builtin_fma(e, r, r);
+#endif
 }
-// a / b: v_rcp_f64 + ONE Newton step (<= 11 ulp) + one residual correction of the quotient.
-// Correctly rounded on 4M random operands over 2^-100..2^100 (tools/ubench/rcp_acc.hip), the
-// same results as with the two-step reciprocal, two instructions fewer.
+// a / b: a times the one-step reciprocal (correctly rounded: + one residual correction of the
+// quotient)
 BDF_INL double fdiv(double a, double b)
 {
     double r = __builtin_amdgcn_rcp(b);
     const double e0 = __builtin_fma(-b, r, 1.0);
     r = __builtin_fma(e0, r, r);
     const double q = a * r;
+#ifndef BCM3_CORRECTLY_ROUNDED
+    return q;
+#else
     const double e = __builtin_fma(-b, q, a);
     return __builtin_fma(e, r, q);
+#endif
 }
-// SUNRsqrt: x <= 0 -> 0; v_rsq_f64 estimate + Goldschmidt refinement. Branch-free: the
-// refinement runs for every x (x <= 0 gives NaN there) and x <= 0 is zeroed with a bit mask,
-// NaN passes through (a select here is turned back into a branch by the compiler).
+// SUNRsqrt: x <= 0 -> 0; v_rsq_f64 estimate + one Goldschmidt step (correctly rounded: + one
+// correction). Branch-free: the refinement runs for every x (x <= 0 gives NaN there) and x <= 0
+// is zeroed with a bit mask, NaN passes through (a select here is turned back into a branch by
+// the compiler).
 BDF_INL double fsqrt(double x)
 {
     double r = __builtin_amdgcn_rsq(x);
     double g = x * r, hh = 0.5 * r;
     double e = __builtin_fma(-g, hh, 0.5);
     g = __builtin_fma(g, e, g);
+#ifdef BCM3_CORRECTLY_ROUNDED
     hh = __builtin_fma(hh, e, hh);
     const double d = __builtin_fma(-g, g, x);
-    g = __builtin_fma(d, hh, g);  // one correction: correctly rounded (tools/ubench/sqrt_acc.hip)
+    g = __builtin_fma(d, hh, g);
+#endif
     const long long keep = (x <= 0.0) ? 0LL : -1LL;
     return __builtin_bit_cast(double, __builtin_bit_cast(long long, g) & keep);
 }
-// a / b for a compile-time b with rb = 1/b correctly rounded (the value frcp(b) produces):
-// the quotient step of fdiv without the reciprocal iteration
+// a / b for a compile-time b with rb = 1/b correctly rounded: a * rb (correctly rounded: + the
+// residual correction of fdiv)
 BDF_INL double fdiv_c(double a, double b, double rb)
 {
     const double q = a * rb;
+#ifndef BCM3_CORRECTLY_ROUNDED
+    return q;
+#else
     const double e = __builtin_fma(-b, q, a);
     return __builtin_fma(e, rb, q);
+#endif
 }
 
 // 1/j for j = 1..7 (the correctly rounded quotients 1.0/j)
@@ -174,6 +198,27 @@ BDF_INL double recip_int(int j)
     r = (j == 5) ? 0.2 : r;
     r = (j == 6) ? 0.16666666666666666 : r;
     r = (j == 7) ? 0.14285714285714285 : r;
+    return r;
+}
+
+// A3 of cvSetTqBDF (cvode.c:2620) depends on q alone: alpha0 + 1/q with alpha0 = -sum_{j<=q} 1/j,
+// evaluated in the same order as set_bdf. The divisor of Cpinv is therefore a compile-time
+// constant in the order-specialised solvers and a runtime value in the lane solver; dividing by
+// it through fdiv_c with the constant reciprocal keeps the three forms bit-identical (the
+// hardware reciprocal estimate differs from the compiler's folded 1.0 / A3).
+constexpr double tq_a3(int q)
+{
+    double a = -1.0;
+    for (int j = 2; j < q; j++) a -= 1.0 / j;
+    a -= 1.0 / q;
+    return a + 1.0 / q;
+}
+BDF_INL double tq_ra3(int q)
+{
+    double r = 1.0 / tq_a3(2);
+    r = (q == 3) ? 1.0 / tq_a3(3) : r;
+    r = (q == 4) ? 1.0 / tq_a3(4) : r;
+    r = (q == 5) ? 1.0 / tq_a3(5) : r;
     return r;
 }
 
@@ -262,6 +307,7 @@ struct BdfCounters {
 template <int NS, class Inv>
 struct BdfState {
     double rtol, atol;
+    double unity;  // 1.0 the compiler cannot see (see set_bdf_q in bdf_vec.h)
     double zn[QMAX + 1][NS];
     double ewt[NS], acor[NS];
     Inv inv;
@@ -389,7 +435,7 @@ BDF_INL double set_bdf(S& s)
             const double C = fdiv(xistar_inv, lq);
             const double A3 = alpha0 + recip_int(q);
             const double A4 = alpha0_hat + xi_inv;
-            const double Cpinv = fdiv(1.0 - A4 + A3, A3);
+            const double Cpinv = fdiv_c(1.0 - A4 + A3, A3, tq_ra3(q));
             s.tq[1] = fabs(C * Cpinv);
         } else {
             s.tq[1] = 1.0;

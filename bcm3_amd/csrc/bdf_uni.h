@@ -100,7 +100,7 @@ BDF_INL double set_bdf_q(S& s)
                 const double C = fdiv(xistar_inv, lq);
                 const double A3 = alpha0 + 1.0 / q;
                 const double A4 = alpha0_hat + xi_inv;
-                const double Cpinv = fdiv(1.0 - A4 + A3, A3);
+                const double Cpinv = fdiv_c(1.0 - A4 + A3, A3, 1.0 / tq_a3(q));
                 tq1 = fabs(C * Cpinv);
             }
             const double hsum2 = hsum + s.tau[q];
@@ -114,7 +114,10 @@ BDF_INL double set_bdf_q(S& s)
         }
     }
     // tq[4] = CORTES / tq[2] only serves as the Newton tolerance (folded into the test there)
-    const double rl1 = frcp(s.l[1]);
+    // at q = 2, l[1] = 1.5 is a compile-time constant here but not in the lane solver (runtime q):
+    // the compiler would fold v_rcp_f64(1.5) to the correctly rounded value while the hardware
+    // estimate (one Newton step, frcp) differs, so the operand is passed through a runtime 1.0
+    const double rl1 = frcp((q == 2) ? s.l[1] * s.unity : s.l[1]);
     s.gamma = s.h * rl1;
     s.gammap = (s.nst == 0) ? s.gamma : s.gammap;
     const double gr = fdiv(s.gamma, s.gammap);

@@ -102,6 +102,7 @@ struct NoCounters {
 template <int NS, bool STATS = true>
 struct VecState {
     double rtol, atol;
+    double unity;  // 1.0 the compiler cannot see (see set_bdf_q)
     double zn[QMAX + 1];  // lane i: component i
     double ewt, acor;
     double acol[NS];  // columns of the RHS matrix A(ka) (constant between ReInits)
@@ -371,7 +372,10 @@ BDF_INL double set_bdf_q(S& s, TqCtx& c)
     c.hsum2 = hsum + s.tau[q];
     c.lq = lq;
     c.A2 = A2;
-    const double rl1 = frcp(s.l[1]);
+    // at q = 2, l[1] = 1.5 is a compile-time constant here but not in the lane solver (runtime q):
+    // the compiler would fold v_rcp_f64(1.5) to the correctly rounded value while the hardware
+    // estimate (one Newton step, frcp) differs, so the operand is passed through a runtime 1.0
+    const double rl1 = frcp((q == 2) ? s.l[1] * s.unity : s.l[1]);
     s.gamma = s.h * rl1;
     s.gammap = (s.nst == 0) ? s.gamma : s.gammap;
     const double gr = fdiv(s.gamma, s.gammap);
@@ -389,7 +393,7 @@ BDF_INL void tq_13(S& s, const TqCtx& c)
         const double C = fdiv(c.xistar_inv, c.lq);
         const double A3 = c.alpha0 + 1.0 / q;
         const double A4 = c.alpha0_hat + c.xi_inv;
-        const double Cpinv = fdiv(1.0 - A4 + A3, A3);
+        const double Cpinv = fdiv_c(1.0 - A4 + A3, A3, 1.0 / tq_a3(q));
         tq1 = fabs(C * Cpinv);
     }
     const double xi_inv2 = fdiv(s.h, c.hsum2);

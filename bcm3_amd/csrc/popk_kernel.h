@@ -13,6 +13,7 @@ struct PopPKDevModel {
     int32_t pk_type, N, num_pk_params, num_pk_pop_params, d, P, T, sd_ix;
     int32_t n_transit_ix, transit_time_ix, biphasic_time_ix, absorption2_ix, max_steps, param_map;
     double rtol, atol, MW, fixed_vod, fixed_kf, fixed_kb;
+    double unity;  // 1.0 (a runtime value: see set_bdf_q in bdf_vec.h)
     const int32_t* transforms;
     const double* time;
     const double* observed;

@@ -468,6 +468,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             // ODESolverCVODE::Solve
             s.rtol = m.rtol;
             s.atol = m.atol;
+            s.unity = m.unity;
             // |y| ewt <= 1/rtol (1 + few ulp), so the sum of squares stays far below NS/UROUND^2
             s.check_tolsf = !((m.rtol >= 1e-10) && (m.atol >= 0.0));
             cfor<0, QMAX + 2>([&](auto k) __attribute__((always_inline)) { s.tau[CI(k)] = 0.0; });
