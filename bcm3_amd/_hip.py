@@ -40,6 +40,16 @@ class PopPKModel(C.Structure):
     ]
 
 
+class ExpmPKModel(C.Structure):
+    """bcm3hip_expm_pk_model"""
+    _fields_ = [(k, C.c_int32) for k in (
+        "d", "n_transit", "peripheral", "biphasic", "metabolite", "additive_sd_ix", "proportional_sd_ix",
+        "absorption_ix", "clearance_ix", "vod_ix", "excretion_ix", "pf_ix", "pb_ix", "mtt_ix", "direct_ix",
+        "metab_conv_ix", "n_treat", "n_obs")] + \
+        [("MW", C.c_double)] + \
+        [(k, C.c_void_p) for k in ("transforms", "treat_times", "treat_doses", "obs_times", "obs_conc")]
+
+
 class AnalyticModel(C.Structure):
     """bcm3hip_analytic_model"""
     _fields_ = [("kind", C.c_int32), ("d", C.c_int32), ("p0", C.c_double), ("p1", C.c_double),
@@ -87,6 +97,7 @@ def lib() -> C.CDLL:
     L.bcm3hip_error_string.restype = C.c_char_p
     L.bcm3hip_open_popk.argtypes = [C.c_int, C.POINTER(PopPKModel), C.POINTER(vp)]
     L.bcm3hip_open_analytic.argtypes = [C.c_int, C.POINTER(AnalyticModel), C.POINTER(vp)]
+    L.bcm3hip_open_expm_pk.argtypes = [C.c_int, C.POINTER(ExpmPKModel), C.POINTER(vp)]
     L.bcm3hip_close.argtypes = [vp]
     L.bcm3hip_set_option.argtypes = [vp, C.c_int, i64]
     L.bcm3hip_num_variables.argtypes = [vp]
@@ -108,7 +119,7 @@ def lib() -> C.CDLL:
     L.bcm3hip_eval_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
     L.bcm3hip_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float)]
     L.bcm3hip_eval_batch_detail.argtypes = [vp, sz, sz, vp, vp, vp, vp, vp, vp]
-    for f in ("bcm3hip_open_popk", "bcm3hip_open_analytic", "bcm3hip_close", "bcm3hip_set_option",
+    for f in ("bcm3hip_open_popk", "bcm3hip_open_analytic", "bcm3hip_open_expm_pk", "bcm3hip_close", "bcm3hip_set_option",
               "bcm3hip_num_variables", "bcm3hip_eval_batch", "bcm3hip_eval_batch_device",
               "bcm3hip_last_kernel_ms", "bcm3hip_eval_batch_detail"):
         getattr(L, f).restype = C.c_int
@@ -161,6 +172,25 @@ class Context:
         h = C.c_void_p()
         check(lib().bcm3hip_open_analytic(device, C.byref(m), C.byref(h)), "bcm3hip_open_analytic")
         return cls(h, d)
+
+    @classmethod
+    def expm_pk(cls, fields: dict, device: int = 0) -> "Context":
+        """bcm3hip_open_expm_pk from a dict of bcm3hip_expm_pk_model fields (arrays as sequences)."""
+        m = ExpmPKModel()
+        keep = []
+        arrays = {"transforms": np.int32, "treat_times": np.float64, "treat_doses": np.float64,
+                  "obs_times": np.float64, "obs_conc": np.float64}
+        for name, _ in ExpmPKModel._fields_:
+            v = fields[name]
+            if name in arrays:
+                a = np.ascontiguousarray(v, dtype=arrays[name])
+                keep.append(a)
+                setattr(m, name, a.ctypes.data)
+            else:
+                setattr(m, name, v)
+        h = C.c_void_p()
+        check(lib().bcm3hip_open_expm_pk(device, C.byref(m), C.byref(h)), "bcm3hip_open_expm_pk")
+        return cls(h, int(m.d))
 
     def set_option(self, opt: int, value: int):
         check(lib().bcm3hip_set_option(self.h, opt, int(value)), "bcm3hip_set_option")

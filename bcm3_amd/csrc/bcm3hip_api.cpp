@@ -19,7 +19,7 @@ using namespace bcm3hip;
 
 struct bcm3hip_ctx {
     int device = 0;
-    int kind = 0;  // 1 popk, 2 analytic
+    int kind = 0;  // 1 popk, 2 analytic, 3 expm pk
     int d = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -31,6 +31,7 @@ struct bcm3hip_ctx {
     size_t log_used = 0;
     PopPKDevModel pm{};
     AnalyticDevModel am{};
+    ExpmPKDevModel xm{};
     std::vector<void*> model_allocs;
     // grow-only scratch
     double* values = nullptr;
@@ -223,6 +224,64 @@ int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* m, bcm3hip_c
     return 0;
 }
 
+int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* m, bcm3hip_ctx** out)
+{
+    if (!m || !out) return BCM3HIP_ERR_ARG;
+    *out = nullptr;
+    const int n = 2 + (m->peripheral ? 1 : 0) + (m->metabolite ? 1 : 0) + (m->n_transit > 0 ? m->n_transit : 0);
+    if (m->n_transit < 0 || n > BCM3HIP_EXPM_NMAX || m->d <= 0) return BCM3HIP_ERR_MODEL;
+    if (m->n_treat < 1 || m->n_obs < 1 || !(m->MW > 0.0)) return BCM3HIP_ERR_MODEL;
+    auto bad = [&](int32_t ix, bool required) { return required ? (ix < 0 || ix >= m->d) : (ix >= m->d); };
+    if (bad(m->absorption_ix, true) || bad(m->clearance_ix, true) || bad(m->vod_ix, true) ||
+        bad(m->excretion_ix, false) || bad(m->additive_sd_ix, false) || bad(m->proportional_sd_ix, false) ||
+        bad(m->pf_ix, m->peripheral != 0) || bad(m->pb_ix, m->peripheral != 0) || bad(m->mtt_ix, m->n_transit > 0) ||
+        bad(m->direct_ix, m->biphasic != 0) || bad(m->metab_conv_ix, m->metabolite != 0))
+        return BCM3HIP_ERR_MODEL;
+    if (m->additive_sd_ix < 0 && m->proportional_sd_ix < 0) return BCM3HIP_ERR_MODEL;
+    for (int i = 1; i < m->n_obs; i++)
+        if (m->obs_times[i] < m->obs_times[i - 1]) return BCM3HIP_ERR_MODEL;  // PharmacoPatient.cpp:98-100
+    bcm3hip_ctx* c = new (std::nothrow) bcm3hip_ctx();
+    if (!c) return BCM3HIP_ERR_ALLOC;
+    int r = ctx_common_init(c, device);
+    if (r) {
+        bcm3hip_close(c);
+        return r;
+    }
+    c->kind = 3;
+    c->d = m->d;
+    ExpmPKDevModel& x = c->xm;
+    x.d = m->d;
+    x.n = n;
+    x.n_transit = m->n_transit;
+    x.peripheral = m->peripheral != 0;
+    x.biphasic = m->biphasic != 0;
+    x.metabolite = m->metabolite != 0;
+    x.additive_sd_ix = m->additive_sd_ix;
+    x.proportional_sd_ix = m->proportional_sd_ix;
+    x.absorption_ix = m->absorption_ix;
+    x.clearance_ix = m->clearance_ix;
+    x.vod_ix = m->vod_ix;
+    x.excretion_ix = m->excretion_ix;
+    x.pf_ix = m->pf_ix;
+    x.pb_ix = m->pb_ix;
+    x.mtt_ix = m->mtt_ix;
+    x.direct_ix = m->direct_ix;
+    x.metab_conv_ix = m->metab_conv_ix;
+    x.n_treat = m->n_treat;
+    x.n_obs = m->n_obs;
+    x.MW = m->MW;
+    if ((r = upload(c, m->transforms, (size_t)m->d, &x.transforms)) ||
+        (r = upload(c, m->treat_times, (size_t)m->n_treat, &x.treat_times)) ||
+        (r = upload(c, m->treat_doses, (size_t)m->n_treat, &x.treat_doses)) ||
+        (r = upload(c, m->obs_times, (size_t)m->n_obs, &x.obs_times)) ||
+        (r = upload(c, m->obs_conc, (size_t)m->n_obs, &x.obs_conc))) {
+        bcm3hip_close(c);
+        return r;
+    }
+    *out = c;
+    return 0;
+}
+
 int bcm3hip_close(bcm3hip_ctx* c)
 {
     if (!c) return 0;
@@ -312,6 +371,8 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
         e = launch_popk(c->pm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, dtraj, dstats,
                         c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
                         c->block_waves, c->uni_solver, s, e0, e1);
+    } else if (c->kind == 3) {
+        e = launch_expm_pk(c->xm, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     } else {
         e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     }

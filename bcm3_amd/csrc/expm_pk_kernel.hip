@@ -1,0 +1,403 @@
+// expm_pk_kernel.hip -- batched pharmaco_single likelihood on MI355X (gfx950).
+//
+// One wavefront = one evaluation (one proposal of one chain). The linear compartment model
+// dy/dt = A y is advanced from dose to dose with matrix exponentials exactly as
+// PharmacokineticModel::Solve does (src/pharmaco/PharmacokineticModel.cpp:111-177), each
+// exp(A t) by Eigen's algorithm (unsupported/Eigen/src/MatrixFunctions/MatrixExponential.h):
+// Pade degree 3/5/7/9 chosen by the 1-norm, degree 13 with scaling by 2^-s beyond, the rational
+// form solved by an LU with partial pivoting (PartialPivLU's unblocked_lu + its two triangular
+// solves), then s squarings.
+//
+// Layout: the n x n matrices (n <= 16) live in the wavefront's LDS, column-major with a padded
+// column stride; lane j owns column j of every matrix it writes (products, linear combinations,
+// the triangular solves of the right-hand side's column j), and reads the other operand with
+// wave-uniform addresses (LDS broadcast). The exponential of the dose interval is kept and reused
+// while the interval repeats (the same bits as recomputing it). HBM traffic per evaluation: the
+// parameter vector in, logp / status out; the patient's treatment and observation arrays are
+// shared by every wavefront (L2 resident).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "pk_math.h"
+#include "popk_kernel.h"
+
+namespace bcm3hip {
+namespace {
+
+constexpr int NM = BCM3HIP_EXPM_NMAX;
+constexpr int NP = NM + 1;  // padded column stride (doubles)
+using Mat = double[NM][NP];  // [column][row]
+
+struct ExpmShared {
+    Mat A, S, A2, A4, A6, U, V, W, E, Eo;
+    double y[NM];
+    double colsum[NM];
+    int perm[NM];
+    int fail;
+};
+
+__device__ __forceinline__ void wsync() { __syncthreads(); }
+
+// C = X Y (C distinct from X and Y): C(i,j) = X(i,0) Y(0,j) + ... in ascending k, the order of
+// Eigen's coefficient-based product for these sizes
+__device__ void matmul(Mat& C, const Mat& X, const Mat& Y, int n, int j)
+{
+    if (j < n) {
+        for (int i = 0; i < n; i++) {
+            double acc = X[0][i] * Y[j][0];
+            for (int k = 1; k < n; k++) acc = __builtin_fma(X[k][i], Y[j][k], acc);
+            C[j][i] = acc;
+        }
+    }
+    wsync();
+}
+
+// R = c2 X2 + c1 X1 + c0 X0 + ci I  (left to right, as Eigen evaluates the sum expression);
+// X0 may be null (term absent)
+__device__ void lincomb(Mat& R, double c2, const Mat& X2, double c1, const Mat& X1, double c0, const Mat* X0,
+                        double ci, int n, int j)
+{
+    if (j < n) {
+        for (int i = 0; i < n; i++) {
+            double r = c2 * X2[j][i] + c1 * X1[j][i];
+            if (X0) r = r + c0 * (*X0)[j][i];
+            r = r + ci * (i == j ? 1.0 : 0.0);
+            R[j][i] = r;
+        }
+    }
+    wsync();
+}
+
+// R += (c2 X2 + c1 X1 + c0 X0 + ci I)
+__device__ void lincomb_add(Mat& R, double c2, const Mat& X2, double c1, const Mat& X1, double c0, const Mat& X0,
+                            double ci, int n, int j)
+{
+    if (j < n) {
+        for (int i = 0; i < n; i++) {
+            double r = c2 * X2[j][i] + c1 * X1[j][i];
+            r = r + c0 * X0[j][i];
+            r = r + ci * (i == j ? 1.0 : 0.0);
+            R[j][i] = R[j][i] + r;
+        }
+    }
+    wsync();
+}
+
+// exp(M) into out (M = sh.S is overwritten by the scaling); matrix_exp_compute / computeUV<double>
+__device__ void expm(ExpmShared& sh, Mat& out, int n, int j)
+{
+    // l1norm = max over columns of the column sums of |M|
+    if (j < n) {
+        double s = 0.0;
+        for (int i = 0; i < n; i++) s += fabs(sh.S[j][i]);
+        sh.colsum[j] = s;
+    }
+    wsync();
+    double l1 = sh.colsum[0];
+    for (int k = 1; k < n; k++) l1 = (sh.colsum[k] > l1) ? sh.colsum[k] : l1;
+    int squarings = 0;
+    Mat& M = sh.S;
+    if (l1 < 1.495585217958292e-002) {
+        // pade3: b = {120, 60, 12, 1}
+        matmul(sh.A2, M, M, n, j);
+        lincomb(sh.W, 1.0, sh.A2, 0.0, sh.A2, 0.0, nullptr, 60.0, n, j);  // b3 A2 + b1 I
+        matmul(sh.U, M, sh.W, n, j);
+        lincomb(sh.V, 12.0, sh.A2, 0.0, sh.A2, 0.0, nullptr, 120.0, n, j);
+    } else if (l1 < 2.539398330063230e-001) {
+        // pade5: b = {30240, 15120, 3360, 420, 30, 1}
+        matmul(sh.A2, M, M, n, j);
+        matmul(sh.A4, sh.A2, sh.A2, n, j);
+        lincomb(sh.W, 1.0, sh.A4, 420.0, sh.A2, 0.0, nullptr, 15120.0, n, j);
+        matmul(sh.U, M, sh.W, n, j);
+        lincomb(sh.V, 30.0, sh.A4, 3360.0, sh.A2, 0.0, nullptr, 30240.0, n, j);
+    } else if (l1 < 9.504178996162932e-001) {
+        // pade7: b = {17297280, 8648640, 1995840, 277200, 25200, 1512, 56, 1}
+        matmul(sh.A2, M, M, n, j);
+        matmul(sh.A4, sh.A2, sh.A2, n, j);
+        matmul(sh.A6, sh.A4, sh.A2, n, j);
+        lincomb(sh.W, 1.0, sh.A6, 1512.0, sh.A4, 277200.0, &sh.A2, 8648640.0, n, j);
+        matmul(sh.U, M, sh.W, n, j);
+        lincomb(sh.V, 56.0, sh.A6, 25200.0, sh.A4, 1995840.0, &sh.A2, 17297280.0, n, j);
+    } else if (l1 < 2.097847961257068e+000) {
+        // pade9: b = {17643225600, 8821612800, 2075673600, 302702400, 30270240, 2162160, 110880,
+        //             3960, 90, 1}; tmp = b9 A8 + b7 A6 + b5 A4 + b3 A2 + b1 I (A8 in E as scratch)
+        matmul(sh.A2, M, M, n, j);
+        matmul(sh.A4, sh.A2, sh.A2, n, j);
+        matmul(sh.A6, sh.A4, sh.A2, n, j);
+        matmul(sh.Eo, sh.A6, sh.A2, n, j);  // A8 (Eo is free until the result is written)
+        if (j < n) {
+            for (int i = 0; i < n; i++) {
+                const double I = (i == j) ? 1.0 : 0.0;
+                double t = 1.0 * sh.Eo[j][i] + 3960.0 * sh.A6[j][i];
+                t = t + 2162160.0 * sh.A4[j][i];
+                t = t + 302702400.0 * sh.A2[j][i];
+                t = t + 8821612800.0 * I;
+                sh.W[j][i] = t;
+                double v = 90.0 * sh.Eo[j][i] + 110880.0 * sh.A6[j][i];
+                v = v + 30270240.0 * sh.A4[j][i];
+                v = v + 2075673600.0 * sh.A2[j][i];
+                v = v + 17643225600.0 * I;
+                sh.V[j][i] = v;
+            }
+        }
+        wsync();
+        matmul(sh.U, M, sh.W, n, j);
+    } else {
+        // pade13 on M / 2^s
+        int e;
+        frexp(l1 / 5.371920351148152, &e);
+        squarings = e < 0 ? 0 : e;
+        if (j < n)
+            for (int i = 0; i < n; i++) M[j][i] = ldexp(M[j][i], -squarings);
+        wsync();
+        matmul(sh.A2, M, M, n, j);
+        matmul(sh.A4, sh.A2, sh.A2, n, j);
+        matmul(sh.A6, sh.A4, sh.A2, n, j);
+        lincomb(sh.V, 1.0, sh.A6, 16380.0, sh.A4, 40840800.0, &sh.A2, 0.0, n, j);
+        matmul(sh.W, sh.A6, sh.V, n, j);
+        lincomb_add(sh.W, 33522128640.0, sh.A6, 10559470521600.0, sh.A4, 1187353796428800.0, sh.A2,
+                    32382376266240000.0, n, j);
+        matmul(sh.U, M, sh.W, n, j);
+        lincomb(sh.W, 182.0, sh.A6, 960960.0, sh.A4, 1323241920.0, &sh.A2, 0.0, n, j);
+        matmul(sh.V, sh.A6, sh.W, n, j);
+        lincomb_add(sh.V, 670442572800.0, sh.A6, 129060195264000.0, sh.A4, 7771770303897600.0, sh.A2,
+                    64764752532480000.0, n, j);
+    }
+    // numer = U + V (into out), denom = -U + V (into W)
+    if (j < n) {
+        for (int i = 0; i < n; i++) {
+            out[j][i] = sh.U[j][i] + sh.V[j][i];
+            sh.W[j][i] = -sh.U[j][i] + sh.V[j][i];
+        }
+    }
+    wsync();
+    // PartialPivLU (unblocked_lu) of W: pivot = first row of the largest |value| in column k
+    Mat& D = sh.W;
+    for (int k = 0; k < n; k++) {
+        wsync();
+        double big = fabs(D[k][k]);
+        int row = k;
+        for (int i = k + 1; i < n; i++) {
+            const double a = fabs(D[k][i]);
+            if (a > big) {
+                big = a;
+                row = i;
+            }
+        }
+        if (j == 0) sh.perm[k] = row;
+        if (big != 0.0) {
+            if (row != k && j < n) {
+                const double t = D[j][k];
+                D[j][k] = D[j][row];
+                D[j][row] = t;
+            }
+            wsync();
+            const double piv = D[k][k];
+            // column k below the pivot /= pivot (l_i), then the Schur update of the columns j > k:
+            // every lane forms the same quotients; column k is written after all reads of it
+            if (j > k && j < n) {
+                const double ukj = D[j][k];
+                for (int i = k + 1; i < n; i++) D[j][i] = D[j][i] - (D[k][i] / piv) * ukj;
+            }
+            wsync();
+            if (j == k)
+                for (int i = k + 1; i < n; i++) D[k][i] = D[k][i] / piv;
+        }
+        wsync();
+    }
+    // solve: permute the right-hand side rows, unit-lower forward substitution, then upper
+    // backward substitution with multiplication by 1/U_ii (TriangularSolverMatrix's column kernel)
+    if (j < n) {
+        for (int k = 0; k < n; k++) {
+            const int r = sh.perm[k];
+            if (r != k) {
+                const double t = out[j][k];
+                out[j][k] = out[j][r];
+                out[j][r] = t;
+            }
+        }
+        for (int k = 0; k < n; k++) {
+            const double b = out[j][k];
+            for (int i = k + 1; i < n; i++) out[j][i] = out[j][i] - b * D[k][i];
+        }
+        for (int k = n - 1; k >= 0; k--) {
+            const double b = out[j][k] * (1.0 / D[k][k]);
+            out[j][k] = b;
+            for (int i = 0; i < k; i++) out[j][i] = out[j][i] - b * D[k][i];
+        }
+    }
+    wsync();
+    // undo the scaling: result *= result
+    for (int s = 0; s < squarings; s++) {
+        matmul(sh.U, out, out, n, j);
+        if (j < n)
+            for (int i = 0; i < n; i++) out[j][i] = sh.U[j][i];
+        wsync();
+    }
+}
+
+// the rates of PharmacoLikelihoodSingle::EvaluateLogProbability (.cpp:153-197) into A
+// (PharmacokineticModel::ConstructMatrix, .cpp:189-247, in its order of += / -=)
+__device__ void construct_matrix(const ExpmPKDevModel& m, const double* v, Mat& A, double& conv, double& add_sd,
+                                 double& prop_sd)
+{
+    auto tv = [&](int ix) { return transform_var(m.transforms[ix], v[ix]); };
+    add_sd = m.additive_sd_ix >= 0 ? tv(m.additive_sd_ix) : 0.0;
+    prop_sd = m.proportional_sd_ix >= 0 ? tv(m.proportional_sd_ix) : 0.0;
+    const double absorption = tv(m.absorption_ix);
+    const double clearance = tv(m.clearance_ix);
+    const double vod = tv(m.vod_ix);
+    const double elimination = clearance / vod;
+    const double excretion = m.excretion_ix >= 0 ? tv(m.excretion_ix) : 0.0;
+    conv = (1e6 / m.MW) / vod;
+    int nc = 2, mi = -1, ft = 0;
+    if (m.peripheral) nc++;
+    if (m.metabolite) mi = nc++;
+    if (m.n_transit > 0) {
+        ft = nc;
+        nc += m.n_transit;
+    }
+    for (int c = 0; c < nc; c++)
+        for (int r = 0; r < nc; r++) A[c][r] = 0.0;
+    A[0][0] -= excretion;
+    A[0][0] -= absorption;
+    if (m.n_transit > 0) {
+        const int nt = m.n_transit;
+        const double tr = (nt + 1.0) / tv(m.mtt_ix);
+        A[0][ft] += absorption;
+        if (nt > 2) {
+            for (int i = 0; i < nt - 1; i++) {
+                A[ft + i][ft + i] -= tr;
+                A[ft + i][ft + i + 1] += tr;
+            }
+        }
+        A[ft + nt - 1][ft + nt - 1] = -tr;
+        A[ft + nt - 1][1] += tr;
+    } else {
+        A[0][1] += absorption;
+    }
+    if (m.peripheral) {
+        const double pf = tv(m.pf_ix), pb = tv(m.pb_ix);
+        A[1][1] -= pf;
+        A[1][2] += pf;
+        A[2][1] += pb;
+        A[2][2] -= pb;
+    }
+    if (m.biphasic) {
+        const double da = tv(m.direct_ix);
+        A[0][0] -= da;
+        A[0][1] += da;
+    }
+    if (m.metabolite) {
+        const double mc = tv(m.metab_conv_ix);
+        A[1][1] -= mc;
+        A[1][mi] += mc;
+        A[mi][mi] -= 1.0;  // SetMetaboliteElimination(1.0) (PharmacoLikelihoodSingle.cpp:140)
+    }
+    A[1][1] -= elimination;
+}
+
+__global__ void __launch_bounds__(64) expm_pk_kernel(ExpmPKDevModel m, int64_t nev, const double* __restrict__ values,
+                                                     double* __restrict__ logp, int32_t* __restrict__ status)
+{
+    __shared__ ExpmShared sh;
+    const int64_t e = blockIdx.x;
+    if (e >= nev) return;  // uniform per block
+    const int j = threadIdx.x;
+    const int n = m.n;
+    const double* v = values + e * m.d;
+    double conv, add_sd, prop_sd;
+    if (j == 0) {
+        double c, a, p;
+        construct_matrix(m, v, sh.A, c, a, p);
+        sh.colsum[0] = c;
+        sh.colsum[1] = a;
+        sh.colsum[2] = p;
+        sh.fail = 0;
+    }
+    if (j < n) sh.y[j] = 0.0;
+    wsync();
+    conv = sh.colsum[0];
+    add_sd = sh.colsum[1];
+    prop_sd = sh.colsum[2];
+    wsync();
+
+    // PharmacokineticModel::Solve (.cpp:127-174); the observation model of
+    // PharmacoLikelihoodSingle::EvaluateLogProbability (.cpp:199-215) folded in, in
+    // observation order (all observations are reached: the last interval ends at the last one)
+    const double simulate_until = m.obs_times[m.n_obs - 1];
+    double cached_dt = NAN;
+    double llh = 0.0;
+    bool llh_done = false;
+    int tti = 0, oti = 0;
+    double current_t = 0.0;
+    while (tti < m.n_treat && current_t < simulate_until) {
+        const double target_t = (tti < m.n_treat - 1) ? m.treat_times[tti + 1] : simulate_until;
+        if (j == 0) sh.y[0] += m.treat_doses[tti] * 1.0;  // bioavailability 1
+        wsync();
+        while (oti < m.n_obs && m.obs_times[oti] <= target_t) {
+            const double offset_t = m.obs_times[oti] - current_t;
+            if (j < n)
+                for (int i = 0; i < n; i++) sh.S[j][i] = sh.A[j][i] * offset_t;
+            wsync();
+            expm(sh, sh.Eo, n, j);
+            double c = sh.Eo[0][1] * sh.y[0];
+            for (int k = 1; k < n; k++) c = __builtin_fma(sh.Eo[k][1], sh.y[k], c);
+            if (!llh_done) {
+                const double x = conv * c;
+                if (isnan(x) || isinf(x)) {
+                    llh = -INFINITY;
+                    llh_done = true;
+                } else {
+                    const double yobs = m.obs_conc[oti];
+                    if (!isnan(yobs)) llh += log_pdf_tnu4(x, yobs, add_sd + prop_sd * fmax(x, 0.0));
+                }
+            }
+            oti++;
+        }
+        const double dt = target_t - current_t;
+        if (!(dt == cached_dt)) {
+            if (j < n)
+                for (int i = 0; i < n; i++) sh.S[j][i] = sh.A[j][i] * dt;
+            wsync();
+            expm(sh, sh.E, n, j);
+            cached_dt = dt;
+        }
+        double ynew = 0.0;
+        if (j < n) {
+            ynew = sh.E[0][j] * sh.y[0];
+            for (int k = 1; k < n; k++) ynew = __builtin_fma(sh.E[k][j], sh.y[k], ynew);
+        }
+        wsync();
+        if (j < n) {
+            sh.y[j] = ynew;
+            if (isnan(ynew)) sh.fail = 1;
+        }
+        wsync();
+        if (sh.fail) break;
+        current_t = target_t;
+        tti++;
+    }
+    if (j == 0) {
+        const bool fail = sh.fail != 0;
+        logp[e] = fail ? -INFINITY : llh;
+        if (status) status[e] = fail ? BCM3HIP_STATUS_SOLVER_FAIL : BCM3HIP_STATUS_OK;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_expm_pk(const ExpmPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
+                          hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop)
+{
+    if (n == 0) return hipSuccess;
+    if (ev_start) hipEventRecord(ev_start, stream);
+    hipLaunchKernelGGL(expm_pk_kernel, dim3((unsigned)n), dim3(64), 0, stream, m, n, values, logp, status);
+    const hipError_t e = hipGetLastError();
+    if (ev_stop) hipEventRecord(ev_stop, stream);
+    return e;
+}
+
+}  // namespace bcm3hip

@@ -527,6 +527,247 @@ bool LikelihoodPharmacokineticTrajectory::CheckEvaluable()
 }
 
 // ---------------------------------------------------------------------------------------------
+// PharmacoLikelihoodSingle::Initialize (PharmacoLikelihoodSingle.cpp:36-76) + Patient::Load
+// (PharmacoPatient.cpp:8-116). The reference opens "pkdata.nc"; this build reads the same
+// variables from the JSON sidecar named by pkdata_file (default "pkdata.json").
+bool PharmacoLikelihoodSingle::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& likelihood_node,
+                                          const OptionsMap& vm)
+{
+    varset = vs;
+    options = vm;
+    std::string trial, pkdata_file;
+    try {
+        const XmlNode* modelnode = likelihood_node.child("pk_model");
+        if (!modelnode) throw XmlError{"No such node (pk_model)"};
+        drug = modelnode->get("drug");
+        trial = modelnode->get("trial");
+        patient_id = modelnode->has_attr("patient") ? modelnode->get("patient") : std::string();
+        use_peripheral_compartment = modelnode->get_bool("peripheral_compartment", false);
+        const long nt = modelnode->get_long("num_transit_compartments", 0);
+        if (nt < 0) throw XmlError{"num_transit_compartments must be >= 0"};
+        num_transit_compartments = (size_t)nt;
+        biphasic_absorption = modelnode->get_bool("biphasic_absorption", false);
+        use_metabolite = modelnode->get_bool("metabolite", false);
+        pkdata_file = modelnode->has_attr("pkdata_file") ? modelnode->get("pkdata_file") : std::string("pkdata.json");
+    } catch (XmlError& e) {
+        LOGERROR("Error parsing likelihood file: %s", e.what.c_str());
+        return false;
+    }
+    const std::string use_patient = option_get(vm, "pharmacosingle.patient", "");
+    if (!use_patient.empty()) patient_id = use_patient;
+    if (patient_id.empty()) {
+        LOGERROR("Patient ID has not been specified in either the likelihood or as command-line option.");
+        return false;
+    }
+
+    std::string path = pkdata_file;
+    if (!file_exists(path)) {
+        std::string alt = option_get(vm, "likelihood_dir", ".") + "/" + pkdata_file;
+        if (file_exists(alt)) path = alt;
+    }
+    Json data;
+    try {
+        data = json_load(path);
+    } catch (JsonError& e) {
+        LOGERROR("Failed to open data file %s: %s", pkdata_file.c_str(), e.what.c_str());
+        return false;
+    }
+    const Json* g = data.find(trial);
+    if (!g) {
+        LOGERROR("Group \"%s\" not found in %s", trial.c_str(), path.c_str());
+        return false;
+    }
+    bool result = true;
+    auto var = [&](const std::string& name) -> const Json* {
+        const Json* v = g->find(name);
+        if (!v) {
+            LOGERROR("Variable \"%s\" not found in group \"%s\"", name.c_str(), trial.c_str());
+            result = false;
+        }
+        return v;
+    };
+    const Json* jt = var("time");
+    const Json* jp = var("patients");
+    const Json* jc = var(drug + "_plasma_concentration");
+    const Json* jd = var(drug + "_dose");
+    const Json* jdi = var(drug + "_dosing_interval");
+    const Json* jda = var(drug + "_dose_after_dose_change");
+    const Json* jdt = var(drug + "_dose_change_time");
+    const Json* jin = var(drug + "_intermittent");
+    const Json* jti = var("treatment_interruptions");
+    if (!result) return false;
+    size_t pix = jp->arr.size();
+    for (size_t j = 0; j < jp->arr.size(); j++) {
+        const Json& p = jp->arr[j];
+        const std::string id = p.type == Json::String ? p.str : std::to_string((long)p.num);
+        if (id == patient_id) {
+            pix = j;
+            break;
+        }
+    }
+    if (pix == jp->arr.size()) {
+        LOGERROR("Cannot find patient \"%s\" in data file", patient_id.c_str());
+        return false;
+    }
+    std::vector<Real> tp, conc;
+    Real dose, dosing_interval, dose_after_dose_change, dose_change_time;
+    unsigned int intermittent;
+    std::set<int> skipped_days;
+    try {
+        for (size_t i = 0; i < jt->arr.size(); i++) {
+            tp.push_back(jt->arr[i].as_double());
+            conc.push_back(jc->arr.at(pix).arr.at(i).as_double());
+        }
+        dose = jd->arr.at(pix).as_double();
+        dosing_interval = jdi->arr.at(pix).as_double();
+        dose_after_dose_change = jda->arr.at(pix).as_double();
+        dose_change_time = jdt->arr.at(pix).as_double();
+        intermittent = (unsigned int)jin->arr.at(pix).as_double();
+        for (int i = 0; i < 29; i++)
+            if (jti->arr.at(pix).arr.at(i).as_double() != 0.0) skipped_days.insert(i);
+    } catch (std::out_of_range&) {
+        LOGERROR("PK data arrays have inconsistent dimensions");
+        return false;
+    } catch (JsonError& e) {
+        LOGERROR("PK data: %s", e.what.c_str());
+        return false;
+    }
+    if (!(dosing_interval > 0.0)) {
+        LOGERROR("Dosing interval must be positive");  // the reference loops forever otherwise
+        return false;
+    }
+    // treatment schedule up to 696 h (PharmacoPatient.cpp:48-91)
+    treatment_timepoints.clear();
+    treatment_doses.clear();
+    const Real last_time = 696;
+    for (Real t = 0; t < last_time; t += dosing_interval) {
+        bool give_treatment = true;
+        const int day = static_cast<int>(floor(t / 24.0));
+        if (skipped_days.count(day)) give_treatment = false;
+        if (intermittent == 1) {
+            const Real time_in_week = t - 7.0 * 24.0 * floor(t / (7.0 * 24.0));
+            if (time_in_week >= 5.0 * 24.0) give_treatment = false;
+        } else if (intermittent == 2) {
+            const Real time_in_course = t - 28.0 * 24.0 * floor(t / (28.0 * 24.0));
+            if (time_in_course >= 21.0 * 24.0) give_treatment = false;
+        } else if (intermittent == 3) {
+            const Real time_in_week = t - 7.0 * 24.0 * floor(t / (7.0 * 24.0));
+            if (time_in_week >= 4.0 * 24.0) give_treatment = false;
+        }
+        if (give_treatment) treatment_timepoints.push_back(t);
+    }
+    for (Real t : treatment_timepoints)
+        treatment_doses.push_back((!std::isnan(dose_change_time) && t >= dose_change_time) ? dose_after_dose_change : dose);
+    // observations: sorted, NaN concentrations dropped (.cpp:93-113)
+    observation_timepoints.clear();
+    observed_concentrations.clear();
+    Real prev_time = -std::numeric_limits<Real>::infinity();
+    for (size_t i = 0; i < tp.size(); i++) {
+        if (tp[i] < prev_time) {
+            LOGERROR("Observation timepoints need to be sorted");
+            return false;
+        }
+        prev_time = tp[i];
+        if (!std::isnan(conc[i])) {
+            observation_timepoints.push_back(tp[i]);
+            observed_concentrations.push_back(conc[i]);
+        }
+    }
+    if (observation_timepoints.empty() || treatment_timepoints.empty()) {
+        // (the reference reads observation_timepoints.tail(1) and stale scratch here)
+        LOGERROR("Patient \"%s\" has no observations or no treatments", patient_id.c_str());
+        return false;
+    }
+    MW = molecular_weight(drug);
+    if (std::isnan(MW)) {
+        LOGERROR("Unknown drug \"%s\"", drug.c_str());
+        return false;
+    }
+    return true;
+}
+
+// PharmacoLikelihoodSingle::PostInitialize (.cpp:78-147)
+bool PharmacoLikelihoodSingle::PostInitialize()
+{
+    const size_t none = std::numeric_limits<size_t>::max();
+    auto ix = [&](const char* n, bool required) -> int32_t {
+        const size_t i = varset->GetVariableIndex(n, required);
+        return i == none ? -1 : (int32_t)i;
+    };
+    model = bcm3hip_expm_pk_model{};
+    model.additive_sd_ix = ix("additive_error_standard_deviation", false);
+    model.proportional_sd_ix = ix("proportional_error_standard_deviation", false);
+    if (model.additive_sd_ix < 0 && model.proportional_sd_ix < 0) {
+        LOGERROR("Neither \"additive_error_standard_deviation\" nor \"proportional_error_standard_deviation\" has been "
+                 "specified in the prior; at least one of these variables should be included.");
+        return false;
+    }
+    model.absorption_ix = ix("absorption", true);
+    model.clearance_ix = ix("clearance", true);
+    model.vod_ix = ix("volume_of_distribution", true);
+    if (model.absorption_ix < 0 || model.clearance_ix < 0 || model.vod_ix < 0) return false;
+    model.excretion_ix = ix("excretion", false);
+    model.pf_ix = model.pb_ix = model.mtt_ix = model.direct_ix = model.metab_conv_ix = -1;
+    if (use_peripheral_compartment) {
+        model.pf_ix = ix("peripheral_forward_rate", true);
+        model.pb_ix = ix("peripheral_backward_rate", true);
+        if (model.pf_ix < 0 || model.pb_ix < 0) {
+            LOGERROR("Peripheral compartmant was specified, but forward or backward rates have not both been specified in prior.");
+            return false;
+        }
+    }
+    if (num_transit_compartments > 0) {
+        model.mtt_ix = ix("mean_transit_time", true);
+        if (model.mtt_ix < 0) {
+            LOGERROR("Transit compartmants were specified, but mean transit time has not been specified in prior.");
+            return false;
+        }
+    }
+    if (biphasic_absorption) {
+        model.direct_ix = ix("direct_absorption", true);
+        if (model.direct_ix < 0) {
+            LOGERROR("Biphasic absorption was specified, but direct absorption rate has not been specified in prior.");
+            return false;
+        }
+    }
+    if (use_metabolite) {
+        model.metab_conv_ix = ix("metabolite_conversion_rate", true);
+        if (model.metab_conv_ix < 0) {
+            LOGERROR("Use of metabolite was specified, but metabolite conversion rate has not been specified in prior.");
+            return false;
+        }
+    }
+    transforms.resize(varset->GetNumVariables());
+    for (size_t i = 0; i < transforms.size(); i++) transforms[i] = (int32_t)varset->GetVariableTransform(i);
+    model.d = (int32_t)varset->GetNumVariables();
+    model.n_transit = (int32_t)num_transit_compartments;
+    model.peripheral = use_peripheral_compartment;
+    model.biphasic = biphasic_absorption;
+    model.metabolite = use_metabolite;
+    model.n_treat = (int32_t)treatment_timepoints.size();
+    model.n_obs = (int32_t)observation_timepoints.size();
+    model.MW = MW;
+    model.transforms = transforms.data();
+    model.treat_times = treatment_timepoints.data();
+    model.treat_doses = treatment_doses.data();
+    model.obs_times = observation_timepoints.data();
+    model.obs_conc = observed_concentrations.data();
+    const int ncomp = 2 + (use_peripheral_compartment ? 1 : 0) + (use_metabolite ? 1 : 0) + (int)num_transit_compartments;
+    if (ncomp > BCM3HIP_EXPM_NMAX) {
+        LOGERROR("%d compartments; this backend supports at most %d", ncomp, (int)BCM3HIP_EXPM_NMAX);
+        return false;
+    }
+    if (!OpenDevice(options)) return false;
+    if (option_get(options, "backend", "") == "none") return true;
+    const int r = bcm3hip_open_expm_pk(device, &model, &ctx);
+    if (r != 0) {
+        LOGERROR("Opening the pharmaco_single GPU context failed: %s", bcm3hip_error_string(r));
+        return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------------
 // TestLikelihoodBanana::Initialize (TestLikelihoodBanana.cpp:13-39)
 bool TestLikelihoodBanana::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& node, const OptionsMap& vm)
 {

@@ -3,6 +3,7 @@
 //   pop_pk_trajectory  LikelihoodPopPKTrajectory (src/likelihoods/LikelihoodPopPKTrajectory.h:10-115)
 //   pharmacokinetic_trajectory  LikelihoodPharmacokineticTrajectory
 //                      (src/likelihoods/LikelihoodPharmacokineticTrajectory.h; one patient, same solver)
+//   pharmaco_single    PharmacoLikelihoodSingle  (src/pharmaco/PharmacoLikelihoodSingle.h; matrix-exponential PK)
 //   banana             TestLikelihoodBanana      (src/likelihoods/TestLikelihoodBanana.cpp)
 //   circular           TestLikelihoodCircular    (src/likelihoods/TestLikelihoodCircular.cpp)
 // Each owns one libbcm3hip context (include/bcm3hip.h) on the configured device. There is no
@@ -99,6 +100,34 @@ private:
     std::vector<int32_t> intermittent, simulate_until, transforms;
     std::vector<uint8_t> skipped_days;
     bcm3hip_popk_model model{};
+};
+
+// One patient, linear compartment model solved by matrix exponentials
+// (PharmacoLikelihoodSingle.cpp:36-218, PharmacoPatient.cpp:8-116, PharmacokineticModel.cpp:111-247).
+// Initialize loads the patient (JSON sidecar of the reference's pkdata.nc); PostInitialize resolves
+// the variables by name and opens the device context, as the reference resolves them there.
+class PharmacoLikelihoodSingle : public LikelihoodGPUBase {
+public:
+    PharmacoLikelihoodSingle(size_t sampling_threads, size_t evaluation_threads) {}
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+    bool PostInitialize() override;
+    const std::string& GetPatientID() const { return patient_id; }
+    const bcm3hip_expm_pk_model& GetDeviceModel() const { return model; }
+    const std::vector<Real>& GetTreatmentTimepoints() const { return treatment_timepoints; }
+    const std::vector<Real>& GetTreatmentDoses() const { return treatment_doses; }
+    const std::vector<Real>& GetObservationTimepoints() const { return observation_timepoints; }
+    const std::vector<Real>& GetObservedConcentrations() const { return observed_concentrations; }
+
+private:
+    std::string drug, patient_id;
+    bool use_peripheral_compartment = false, biphasic_absorption = false, use_metabolite = false;
+    size_t num_transit_compartments = 0;
+    Real MW = NAN;
+    std::vector<Real> treatment_timepoints, treatment_doses, observation_timepoints, observed_concentrations;
+    std::vector<int32_t> transforms;
+    OptionsMap options;
+    bcm3hip_expm_pk_model model{};
 };
 
 class TestLikelihoodBanana : public LikelihoodGPUBase {

@@ -68,6 +68,16 @@ int bcm3_likelihood_popk_model(const bcm3_likelihood* h, void* model)
     return -2;
 }
 
+int bcm3_likelihood_expm_pk_model(const bcm3_likelihood* h, void* model)
+{
+    if (!h || !model) return -1;
+    if (auto* p = dynamic_cast<bcm3::PharmacoLikelihoodSingle*>(h->ll.get())) {
+        *(bcm3hip_expm_pk_model*)model = p->GetDeviceModel();
+        return 0;
+    }
+    return -2;
+}
+
 void bcm3_likelihood_destroy(bcm3_likelihood* h) { delete h; }
 
 int bcm3_likelihood_num_variables(const bcm3_likelihood* h) { return h ? (int)h->varset->GetNumVariables() : -1; }

@@ -39,4 +39,20 @@ struct AnalyticDevModel {
 hipError_t launch_analytic(const AnalyticDevModel& m, int64_t n, const double* values, double* logp,
                            int32_t* status, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
 
+// Same fields as bcm3hip_expm_pk_model, with device pointers.
+struct ExpmPKDevModel {
+    int32_t d, n, n_transit, peripheral, biphasic, metabolite;
+    int32_t additive_sd_ix, proportional_sd_ix, absorption_ix, clearance_ix, vod_ix, excretion_ix;
+    int32_t pf_ix, pb_ix, mtt_ix, direct_ix, metab_conv_ix, n_treat, n_obs;
+    double MW;
+    const int32_t* transforms;
+    const double* treat_times;
+    const double* treat_doses;
+    const double* obs_times;
+    const double* obs_conc;
+};
+
+hipError_t launch_expm_pk(const ExpmPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
+                          hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
+
 }  // namespace bcm3hip

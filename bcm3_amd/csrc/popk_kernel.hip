@@ -24,31 +24,13 @@
 #include "bdf_lane.h"
 #include "bdf_uni.h"
 #include "bdf_vec.h"
+#include "pk_math.h"
 #include "popk_kernel.h"
 
 namespace bcm3hip {
 
 // ---------------------------------------------------------------------------------------------
 // math on the path (ProbabilityDistributions.cpp, MathFunctions.h, VariableSet.cpp)
-
-BDF_INL double fastpow10(double x) { return exp(x * 2.3025850929940459); }
-
-BDF_INL double transform_var(int tf, double x)
-{
-    switch (tf) {
-    case 1: return exp(x);
-    case 2: return fastpow10(x);
-    case 3:
-        if (x > 0) {
-            double z = exp(-x);
-            return 1.0 / (1.0 + z);
-        } else {
-            double z = exp(x);
-            return z / (1.0 + z);
-        }
-    default: return x;
-    }
-}
 
 // standard normal quantile for p in (0, 0.5]: rational initial guess + Halley refinement
 __device__ double ndtri_lower(double p)
@@ -93,12 +75,6 @@ __device__ double quantile_normal(double p, double mu, double sigma)
     r *= sigma * 1.4142135623730951;
     r += mu;
     return r;
-}
-
-BDF_INL double log_pdf_tnu4(double x, double mu, double sigma)
-{
-    double xn = (x - mu) / sigma;
-    return -0.9808292530117262 - 2.5 * log1p(0.25 * xn * xn) - log(sigma);
 }
 
 // ---------------------------------------------------------------------------------------------

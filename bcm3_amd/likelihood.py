@@ -30,6 +30,7 @@ def lib() -> C.CDLL:
     L.bcm3_likelihood_create.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.POINTER(vp)]
     L.bcm3_likelihood_create_ex.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(vp)]
     L.bcm3_likelihood_popk_model.argtypes = [vp, C.POINTER(_hip.PopPKModel)]
+    L.bcm3_likelihood_expm_pk_model.argtypes = [vp, C.POINTER(_hip.ExpmPKModel)]
     L.bcm3_likelihood_destroy.argtypes = [vp]
     L.bcm3_likelihood_destroy.restype = None
     L.bcm3_likelihood_num_variables.argtypes = [vp]
@@ -83,6 +84,15 @@ class Likelihood:
         r = lib().bcm3_likelihood_popk_model(self.h, C.byref(m))
         if r != 0:
             _err("bcm3_likelihood_popk_model", r)
+        return m
+
+    def expm_pk_model(self) -> _hip.ExpmPKModel:
+        """bcm3_likelihood_expm_pk_model (pharmaco_single): treatment schedule, observations and
+        variable indices as the device sees them; the array pointers stay valid while self lives."""
+        m = _hip.ExpmPKModel()
+        r = lib().bcm3_likelihood_expm_pk_model(self.h, C.byref(m))
+        if r != 0:
+            _err("bcm3_likelihood_expm_pk_model", r)
         return m
 
     def set_learning_rate(self, lr: float):

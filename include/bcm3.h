@@ -35,6 +35,12 @@ int bcm3_likelihood_create_ex(const char* likelihood_xml, const char* prior_xml,
  * pop_pk_trajectory only). Pointers stay valid while the likelihood lives. `model` points to a
  * bcm3hip_popk_model (bcm3hip.h). */
 int bcm3_likelihood_popk_model(const bcm3_likelihood* ll, void* model);
+/* The flat matrix-exponential PK model a pharmaco_single likelihood hands to the device: the
+ * treatment schedule and filtered observations of PharmacoPatient::Load
+ * (src/pharmaco/PharmacoPatient.cpp:8-116) and the variable indices of
+ * PharmacoLikelihoodSingle::PostInitialize (.cpp:78-147), into a bcm3hip_expm_pk_model. Returns
+ * -2 for other likelihood types. */
+int bcm3_likelihood_expm_pk_model(const bcm3_likelihood* ll, void* model);
 void bcm3_likelihood_destroy(bcm3_likelihood* ll);
 int bcm3_likelihood_num_variables(const bcm3_likelihood* ll);
 /* name of variable i (prior.xml order, repeat-expanded); returns the name length or < 0 */

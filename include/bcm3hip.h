@@ -113,6 +113,39 @@ typedef struct {
     double p2;    /* circular: width */
 } bcm3hip_analytic_model;
 
+/* Linear-compartment PK model solved by matrix exponentials: the pharmaco_single likelihood
+ * (src/pharmaco/PharmacoLikelihoodSingle.cpp:149-218) over PharmacokineticModel::Solve /
+ * ConstructMatrix (src/pharmaco/PharmacokineticModel.cpp:111-247) with Eigen's
+ * MatrixBase::exp (Pade 3..13 + scaling and squaring, unsupported/Eigen/src/MatrixFunctions/
+ * MatrixExponential.h:65-366). Compartments: 2 (+1 peripheral) (+1 metabolite) (+n_transit),
+ * at most BCM3HIP_EXPM_NMAX. Treatment and observation arrays are what Patient::Load derives
+ * (src/pharmaco/PharmacoPatient.cpp:8-116): doses at treat_times, observations with NaN
+ * concentrations removed, sorted times. Variable indices are -1 when the variable is absent. */
+enum { BCM3HIP_EXPM_NMAX = 16 };
+typedef struct {
+    int32_t d;                  /* number of sampled variables */
+    int32_t n_transit;          /* num_transit_compartments, 0 = none */
+    int32_t peripheral;         /* 0/1 */
+    int32_t biphasic;           /* 0/1: direct_absorption */
+    int32_t metabolite;         /* 0/1 (metabolite elimination fixed at 1.0) */
+    int32_t additive_sd_ix;     /* additive_error_standard_deviation or -1 (sd 0) */
+    int32_t proportional_sd_ix; /* proportional_error_standard_deviation or -1 (sd 0) */
+    int32_t absorption_ix, clearance_ix, vod_ix; /* required */
+    int32_t excretion_ix;       /* -1: excretion 0 */
+    int32_t pf_ix, pb_ix;       /* peripheral_forward_rate / peripheral_backward_rate */
+    int32_t mtt_ix;             /* mean_transit_time */
+    int32_t direct_ix;          /* direct_absorption */
+    int32_t metab_conv_ix;      /* metabolite_conversion_rate */
+    int32_t n_treat;            /* >= 1 */
+    int32_t n_obs;              /* >= 1 */
+    double MW;                  /* molecular weight of the drug */
+    const int32_t* transforms;  /* [d] BCM3HIP_TF_* */
+    const double* treat_times;  /* [n_treat] ascending */
+    const double* treat_doses;  /* [n_treat] */
+    const double* obs_times;    /* [n_obs] ascending */
+    const double* obs_conc;     /* [n_obs] */
+} bcm3hip_expm_pk_model;
+
 typedef struct bcm3hip_ctx bcm3hip_ctx;
 
 /* Per-trajectory solver counters (parity/diagnostics), one record per (item, patient). */
@@ -135,6 +168,9 @@ const char* bcm3hip_error_string(int code);
 
 int bcm3hip_open_popk(int device, const bcm3hip_popk_model* model, bcm3hip_ctx** out);
 int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* model, bcm3hip_ctx** out);
+/* pharmaco_single (PharmacoLikelihoodSingle::EvaluateLogProbability); per-item status 1 when
+ * PharmacokineticModel::Solve fails (NaN state): logp = -inf */
+int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* model, bcm3hip_ctx** out);
 int bcm3hip_close(bcm3hip_ctx* ctx);
 int bcm3hip_set_option(bcm3hip_ctx* ctx, int option, int64_t value);
 int bcm3hip_num_variables(const bcm3hip_ctx* ctx);
