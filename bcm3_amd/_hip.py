@@ -47,7 +47,14 @@ class ExpmPKModel(C.Structure):
         "absorption_ix", "clearance_ix", "vod_ix", "excretion_ix", "pf_ix", "pb_ix", "mtt_ix", "direct_ix",
         "metab_conv_ix", "n_treat", "n_obs")] + \
         [("MW", C.c_double)] + \
-        [(k, C.c_void_p) for k in ("transforms", "treat_times", "treat_doses", "obs_times", "obs_conc")]
+        [(k, C.c_void_p) for k in ("transforms", "treat_times", "treat_doses", "obs_times", "obs_conc")] + \
+        [("param_map", C.c_int32), ("P", C.c_int32), ("sigma_ix", C.c_int32 * 5)] + \
+        [(k, C.c_void_p) for k in ("patient_ix", "treat_offset", "obs_offset")]
+
+
+# pharmaco_single's defaults for the population fields of bcm3hip_expm_pk_model
+EXPM_PK_SINGLE_DEFAULTS = {"param_map": 1, "P": 1, "sigma_ix": [-1] * 5, "patient_ix": None,
+                           "treat_offset": None, "obs_offset": None}
 
 
 class AnalyticModel(C.Structure):
@@ -179,10 +186,15 @@ class Context:
         m = ExpmPKModel()
         keep = []
         arrays = {"transforms": np.int32, "treat_times": np.float64, "treat_doses": np.float64,
-                  "obs_times": np.float64, "obs_conc": np.float64}
+                  "obs_times": np.float64, "obs_conc": np.float64, "patient_ix": np.int32,
+                  "treat_offset": np.int32, "obs_offset": np.int32}
         for name, _ in ExpmPKModel._fields_:
-            v = fields[name]
-            if name in arrays:
+            v = fields[name] if name in fields else EXPM_PK_SINGLE_DEFAULTS[name]
+            if name == "sigma_ix":
+                m.sigma_ix = (C.c_int32 * 5)(*v)
+            elif name in arrays and v is None:
+                setattr(m, name, None)
+            elif name in arrays:
                 a = np.ascontiguousarray(v, dtype=arrays[name])
                 keep.append(a)
                 setattr(m, name, a.ctypes.data)

@@ -231,6 +231,40 @@ int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* m, bcm3hip_ctx
     const int n = 2 + (m->peripheral ? 1 : 0) + (m->metabolite ? 1 : 0) + (m->n_transit > 0 ? m->n_transit : 0);
     if (m->n_transit < 0 || n > BCM3HIP_EXPM_NMAX || m->d <= 0) return BCM3HIP_ERR_MODEL;
     if (m->n_treat < 1 || m->n_obs < 1 || !(m->MW > 0.0)) return BCM3HIP_ERR_MODEL;
+    const bool single = m->param_map == BCM3HIP_PARAM_MAP_SINGLE;
+    if (!single && m->param_map != BCM3HIP_PARAM_MAP_POPULATION) return BCM3HIP_ERR_MODEL;
+    const int P = m->P;
+    if (P < 1 || (single && P != 1)) return BCM3HIP_ERR_MODEL;
+    if (P > 1 && (!m->treat_offset || !m->obs_offset)) return BCM3HIP_ERR_MODEL;
+    // per-patient ranges: at least one dose and one observation each, observations sorted
+    std::vector<int32_t> toff(P + 1), ooff(P + 1);
+    for (int j = 0; j <= P; j++) {
+        toff[j] = m->treat_offset ? m->treat_offset[j] : (j ? m->n_treat : 0);
+        ooff[j] = m->obs_offset ? m->obs_offset[j] : (j ? m->n_obs : 0);
+    }
+    if (toff[0] != 0 || ooff[0] != 0 || toff[P] != m->n_treat || ooff[P] != m->n_obs) return BCM3HIP_ERR_MODEL;
+    for (int j = 0; j < P; j++) {
+        if (toff[j + 1] - toff[j] < 1 || ooff[j + 1] - ooff[j] < 1) return BCM3HIP_ERR_MODEL;
+        for (int i = ooff[j] + 1; i < ooff[j + 1]; i++)
+            if (m->obs_times[i] < m->obs_times[i - 1]) return BCM3HIP_ERR_MODEL;  // PharmacoPatient.cpp:98-100
+    }
+    std::vector<int32_t> pix(6 * (size_t)P, -1);
+    if (!single) {
+        if (m->biphasic || m->metabolite) return BCM3HIP_ERR_MODEL;  // not options of the population model
+        for (int w = 0; w < 5; w++) {
+            if (m->sigma_ix[w] >= m->d) return BCM3HIP_ERR_MODEL;
+            if (m->sigma_ix[w] >= 0 && !m->patient_ix) return BCM3HIP_ERR_MODEL;
+        }
+        if (m->patient_ix) {
+            for (size_t k = 0; k < pix.size(); k++) {
+                pix[k] = m->patient_ix[k];
+                if (pix[k] >= m->d) return BCM3HIP_ERR_MODEL;
+            }
+            for (int w = 0; w < 5; w++)
+                for (int j = 0; j < P && m->sigma_ix[w] >= 0; j++)
+                    if (pix[w * P + j] < 0) return BCM3HIP_ERR_MODEL;
+        }
+    }
     auto bad = [&](int32_t ix, bool required) { return required ? (ix < 0 || ix >= m->d) : (ix >= m->d); };
     if (bad(m->absorption_ix, true) || bad(m->clearance_ix, true) || bad(m->vod_ix, true) ||
         bad(m->excretion_ix, false) || bad(m->additive_sd_ix, false) || bad(m->proportional_sd_ix, false) ||
@@ -238,8 +272,6 @@ int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* m, bcm3hip_ctx
         bad(m->direct_ix, m->biphasic != 0) || bad(m->metab_conv_ix, m->metabolite != 0))
         return BCM3HIP_ERR_MODEL;
     if (m->additive_sd_ix < 0 && m->proportional_sd_ix < 0) return BCM3HIP_ERR_MODEL;
-    for (int i = 1; i < m->n_obs; i++)
-        if (m->obs_times[i] < m->obs_times[i - 1]) return BCM3HIP_ERR_MODEL;  // PharmacoPatient.cpp:98-100
     bcm3hip_ctx* c = new (std::nothrow) bcm3hip_ctx();
     if (!c) return BCM3HIP_ERR_ALLOC;
     int r = ctx_common_init(c, device);
@@ -270,7 +302,13 @@ int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* m, bcm3hip_ctx
     x.n_treat = m->n_treat;
     x.n_obs = m->n_obs;
     x.MW = m->MW;
-    if ((r = upload(c, m->transforms, (size_t)m->d, &x.transforms)) ||
+    x.param_map = m->param_map;
+    x.P = P;
+    for (int w = 0; w < 5; w++) x.sigma_ix[w] = single ? -1 : m->sigma_ix[w];
+    if ((r = upload(c, pix.data(), pix.size(), &x.patient_ix)) ||
+        (r = upload(c, toff.data(), toff.size(), &x.treat_offset)) ||
+        (r = upload(c, ooff.data(), ooff.size(), &x.obs_offset)) ||
+        (r = upload(c, m->transforms, (size_t)m->d, &x.transforms)) ||
         (r = upload(c, m->treat_times, (size_t)m->n_treat, &x.treat_times)) ||
         (r = upload(c, m->treat_doses, (size_t)m->n_treat, &x.treat_doses)) ||
         (r = upload(c, m->obs_times, (size_t)m->n_obs, &x.obs_times)) ||
@@ -372,7 +410,10 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
                         c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
                         c->block_waves, c->uni_solver, s, e0, e1);
     } else if (c->kind == 3) {
-        e = launch_expm_pk(c->xm, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
+        if (c->xm.P > 1 && (grow(c->pllh, c->cap_traj, n * (size_t)c->xm.P) ||
+                            grow(c->tstatus, c->cap_tstatus, n * (size_t)c->xm.P)))
+            return BCM3HIP_ERR_ALLOC;
+        e = launch_expm_pk(c->xm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, s, e0, e1);
     } else {
         e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     }

@@ -1,6 +1,6 @@
 // expm_pk_kernel.hip -- batched pharmaco_single likelihood on MI355X (gfx950).
 //
-// One wavefront = one evaluation (one proposal of one chain). The linear compartment model
+// One wavefront = one evaluation (one proposal of one chain) of one patient. The linear compartment model
 // dy/dt = A y is advanced from dose to dose with matrix exponentials exactly as
 // PharmacokineticModel::Solve does (src/pharmaco/PharmacokineticModel.cpp:111-177), each
 // exp(A t) by Eigen's algorithm (unsupported/Eigen/src/MatrixFunctions/MatrixExponential.h):
@@ -238,19 +238,39 @@ __device__ void expm(ExpmShared& sh, Mat& out, int n, int j)
     }
 }
 
-// the rates of PharmacoLikelihoodSingle::EvaluateLogProbability (.cpp:153-197) into A
+// the rates of PharmacoLikelihoodSingle::EvaluateLogProbability (.cpp:153-197), or of patient j in
+// PharmacoLikelihoodPopulation::SetupSimulation (PharmacoLikelihoodPopulation.cpp:271-340), into A
 // (PharmacokineticModel::ConstructMatrix, .cpp:189-247, in its order of += / -=)
-__device__ void construct_matrix(const ExpmPKDevModel& m, const double* v, Mat& A, double& conv, double& add_sd,
-                                 double& prop_sd)
+__device__ void construct_matrix(const ExpmPKDevModel& m, const double* v, int j, Mat& A, double& conv,
+                                 double& add_sd, double& prop_sd, double& bioavailability)
 {
     auto tv = [&](int ix) { return transform_var(m.transforms[ix], v[ix]); };
     add_sd = m.additive_sd_ix >= 0 ? tv(m.additive_sd_ix) : 0.0;
     prop_sd = m.proportional_sd_ix >= 0 ? tv(m.proportional_sd_ix) : 0.0;
-    const double absorption = tv(m.absorption_ix);
-    const double clearance = tv(m.clearance_ix);
-    const double vod = tv(m.vod_ix);
+    double absorption, clearance, vod, excretion, transit_time = 0.0;
+    bioavailability = 1.0;
+    if (m.param_map == BCM3HIP_PARAM_MAP_SINGLE) {
+        absorption = tv(m.absorption_ix);
+        clearance = tv(m.clearance_ix);
+        vod = tv(m.vod_ix);
+        excretion = m.excretion_ix >= 0 ? tv(m.excretion_ix) : 0.0;
+        if (m.n_transit > 0) transit_time = tv(m.mtt_ix);
+    } else {
+        // mean only: fastpow10(mean); with a random effect: fastpow10(QuantileNormal(p_j, mean, sigma))
+        auto pop = [&](int which, int mean_ix) {
+            const int s = m.sigma_ix[which];
+            if (s < 0) return fastpow10(v[mean_ix]);
+            return fastpow10(quantile_normal(v[m.patient_ix[which * m.P + j]], v[mean_ix], v[s]));
+        };
+        absorption = pop(0, m.absorption_ix);
+        excretion = m.excretion_ix >= 0 ? pop(1, m.excretion_ix) : 0.0;
+        clearance = pop(2, m.clearance_ix);
+        vod = pop(3, m.vod_ix);
+        if (m.n_transit > 0) transit_time = (m.sigma_ix[4] < 0) ? tv(m.mtt_ix) : pop(4, m.mtt_ix);
+        const int bi = m.patient_ix[5 * m.P + j];
+        if (bi >= 0) bioavailability = v[bi];
+    }
     const double elimination = clearance / vod;
-    const double excretion = m.excretion_ix >= 0 ? tv(m.excretion_ix) : 0.0;
     conv = (1e6 / m.MW) / vod;
     int nc = 2, mi = -1, ft = 0;
     if (m.peripheral) nc++;
@@ -265,7 +285,7 @@ __device__ void construct_matrix(const ExpmPKDevModel& m, const double* v, Mat& 
     A[0][0] -= absorption;
     if (m.n_transit > 0) {
         const int nt = m.n_transit;
-        const double tr = (nt + 1.0) / tv(m.mtt_ix);
+        const double tr = (nt + 1.0) / transit_time;
         A[0][ft] += absorption;
         if (nt > 2) {
             for (int i = 0; i < nt - 1; i++) {
@@ -299,46 +319,58 @@ __device__ void construct_matrix(const ExpmPKDevModel& m, const double* v, Mat& 
     A[1][1] -= elimination;
 }
 
+// one block (one wavefront) per (evaluation e, patient j)
 __global__ void __launch_bounds__(64) expm_pk_kernel(ExpmPKDevModel m, int64_t nev, const double* __restrict__ values,
-                                                     double* __restrict__ logp, int32_t* __restrict__ status)
+                                                     double* __restrict__ logp, int32_t* __restrict__ status,
+                                                     double* __restrict__ patient_llh, int32_t* __restrict__ traj_status)
 {
     __shared__ ExpmShared sh;
-    const int64_t e = blockIdx.x;
+    const int64_t b = blockIdx.x;
+    const int64_t e = b / m.P;
+    const int pj = (int)(b - e * m.P);
     if (e >= nev) return;  // uniform per block
     const int j = threadIdx.x;
     const int n = m.n;
     const double* v = values + e * m.d;
-    double conv, add_sd, prop_sd;
+    const int t0 = m.treat_offset[pj], n_treat = m.treat_offset[pj + 1] - t0;
+    const int o0 = m.obs_offset[pj], n_obs = m.obs_offset[pj + 1] - o0;
+    const double* treat_times = m.treat_times + t0;
+    const double* treat_doses = m.treat_doses + t0;
+    const double* obs_times = m.obs_times + o0;
+    const double* obs_conc = m.obs_conc + o0;
     if (j == 0) {
-        double c, a, p;
-        construct_matrix(m, v, sh.A, c, a, p);
+        double c, a, p, ba;
+        construct_matrix(m, v, pj, sh.A, c, a, p, ba);
         sh.colsum[0] = c;
         sh.colsum[1] = a;
         sh.colsum[2] = p;
+        sh.colsum[3] = ba;
         sh.fail = 0;
     }
     if (j < n) sh.y[j] = 0.0;
     wsync();
-    conv = sh.colsum[0];
-    add_sd = sh.colsum[1];
-    prop_sd = sh.colsum[2];
+    const double conv = sh.colsum[0];
+    const double add_sd = sh.colsum[1];
+    const double prop_sd = sh.colsum[2];
+    const double bioavailability = sh.colsum[3];
     wsync();
 
     // PharmacokineticModel::Solve (.cpp:127-174); the observation model of
-    // PharmacoLikelihoodSingle::EvaluateLogProbability (.cpp:199-215) folded in, in
-    // observation order (all observations are reached: the last interval ends at the last one)
-    const double simulate_until = m.obs_times[m.n_obs - 1];
+    // PharmacoLikelihoodSingle::EvaluateLogProbability (.cpp:199-215) / PharmacoLikelihoodPopulation
+    // (.cpp:226-242) folded in, in observation order (all observations are reached: the last
+    // interval ends at the last one)
+    const double simulate_until = obs_times[n_obs - 1];
     double cached_dt = NAN;
     double llh = 0.0;
     bool llh_done = false;
     int tti = 0, oti = 0;
     double current_t = 0.0;
-    while (tti < m.n_treat && current_t < simulate_until) {
-        const double target_t = (tti < m.n_treat - 1) ? m.treat_times[tti + 1] : simulate_until;
-        if (j == 0) sh.y[0] += m.treat_doses[tti] * 1.0;  // bioavailability 1
+    while (tti < n_treat && current_t < simulate_until) {
+        const double target_t = (tti < n_treat - 1) ? treat_times[tti + 1] : simulate_until;
+        if (j == 0) sh.y[0] += treat_doses[tti] * bioavailability;
         wsync();
-        while (oti < m.n_obs && m.obs_times[oti] <= target_t) {
-            const double offset_t = m.obs_times[oti] - current_t;
+        while (oti < n_obs && obs_times[oti] <= target_t) {
+            const double offset_t = obs_times[oti] - current_t;
             if (j < n)
                 for (int i = 0; i < n; i++) sh.S[j][i] = sh.A[j][i] * offset_t;
             wsync();
@@ -351,7 +383,7 @@ __global__ void __launch_bounds__(64) expm_pk_kernel(ExpmPKDevModel m, int64_t n
                     llh = -INFINITY;
                     llh_done = true;
                 } else {
-                    const double yobs = m.obs_conc[oti];
+                    const double yobs = obs_conc[oti];
                     if (!isnan(yobs)) llh += log_pdf_tnu4(x, yobs, add_sd + prop_sd * fmax(x, 0.0));
                 }
             }
@@ -382,19 +414,48 @@ __global__ void __launch_bounds__(64) expm_pk_kernel(ExpmPKDevModel m, int64_t n
     }
     if (j == 0) {
         const bool fail = sh.fail != 0;
-        logp[e] = fail ? -INFINITY : llh;
-        if (status) status[e] = fail ? BCM3HIP_STATUS_SOLVER_FAIL : BCM3HIP_STATUS_OK;
+        const double r = fail ? -INFINITY : llh;
+        const int32_t st = fail ? BCM3HIP_STATUS_SOLVER_FAIL : BCM3HIP_STATUS_OK;
+        if (m.P == 1) {
+            logp[e] = r;
+            if (status) status[e] = st;
+        } else {
+            patient_llh[b] = r;
+            traj_status[b] = st;
+        }
     }
+}
+
+// logp = sum over patients in patient order (PharmacoLikelihoodPopulation.cpp:217-247)
+__global__ void expm_pk_reduce_kernel(int64_t nev, int P, const double* __restrict__ patient_llh,
+                                      const int32_t* __restrict__ traj_status, double* __restrict__ logp,
+                                      int32_t* __restrict__ status)
+{
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nev) return;
+    double s = 0.0;
+    int32_t st = BCM3HIP_STATUS_OK;
+    for (int j = 0; j < P; j++) {
+        s += patient_llh[e * P + j];
+        st = traj_status[e * P + j] != BCM3HIP_STATUS_OK ? BCM3HIP_STATUS_SOLVER_FAIL : st;
+    }
+    logp[e] = s;
+    if (status) status[e] = st;
 }
 
 }  // namespace
 
 hipError_t launch_expm_pk(const ExpmPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
-                          hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop)
+                          double* patient_llh, int32_t* traj_status, hipStream_t stream, hipEvent_t ev_start,
+                          hipEvent_t ev_stop)
 {
     if (n == 0) return hipSuccess;
     if (ev_start) hipEventRecord(ev_start, stream);
-    hipLaunchKernelGGL(expm_pk_kernel, dim3((unsigned)n), dim3(64), 0, stream, m, n, values, logp, status);
+    hipLaunchKernelGGL(expm_pk_kernel, dim3((unsigned)(n * m.P)), dim3(64), 0, stream, m, n, values, logp, status,
+                       patient_llh, traj_status);
+    if (m.P > 1)
+        hipLaunchKernelGGL(expm_pk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, m.P,
+                           patient_llh, traj_status, logp, status);
     const hipError_t e = hipGetLastError();
     if (ev_stop) hipEventRecord(ev_stop, stream);
     return e;

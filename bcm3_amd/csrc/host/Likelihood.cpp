@@ -55,7 +55,7 @@ std::string option_get(const OptionsMap& vm, const std::string& key, const std::
 
 std::vector<std::string> LikelihoodFactory::SupportedTypes()
 {
-    return {"pop_pk_trajectory", "pharmacokinetic_trajectory", "pharmaco_single", "banana", "circular"};
+    return {"pop_pk_trajectory", "pharmacokinetic_trajectory", "pharmaco_single", "pharmaco_population", "banana", "circular"};
 }
 
 std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::string& fn,
@@ -94,12 +94,14 @@ std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::strin
         ll = std::make_shared<LikelihoodPharmacokineticTrajectory>(sampling_threads, evaluation_threads);
     } else if (type == "pharmaco_single") {
         ll = std::make_shared<PharmacoLikelihoodSingle>(sampling_threads, evaluation_threads);
+    } else if (type == "pharmaco_population") {
+        ll = std::make_shared<PharmacoLikelihoodPopulation>(sampling_threads, evaluation_threads);
     } else if (type == "banana") {
         ll = std::make_shared<TestLikelihoodBanana>(sampling_threads, evaluation_threads);
     } else if (type == "circular") {
         ll = std::make_shared<TestLikelihoodCircular>(sampling_threads, evaluation_threads);
     } else {
-        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, pharmaco_single, banana, circular)",
+        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, pharmaco_single, pharmaco_population, banana, circular)",
                  type.c_str());
         return ll;
     }

@@ -527,56 +527,11 @@ bool LikelihoodPharmacokineticTrajectory::CheckEvaluable()
 }
 
 // ---------------------------------------------------------------------------------------------
-// PharmacoLikelihoodSingle::Initialize (PharmacoLikelihoodSingle.cpp:36-76) + Patient::Load
-// (PharmacoPatient.cpp:8-116). The reference opens "pkdata.nc"; this build reads the same
-// variables from the JSON sidecar named by pkdata_file (default "pkdata.json").
-bool PharmacoLikelihoodSingle::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& likelihood_node,
-                                          const OptionsMap& vm)
+// Patient::Load (PharmacoPatient.cpp:8-116) from group g of the JSON sidecar of pkdata.nc:
+// treatment schedule up to 696 h, observations sorted with NaN concentrations dropped
+static bool load_pharmaco_patient(const Json* g, const std::string& trial, const std::string& drug, size_t pix,
+                                  PharmacoPatient& out)
 {
-    varset = vs;
-    options = vm;
-    std::string trial, pkdata_file;
-    try {
-        const XmlNode* modelnode = likelihood_node.child("pk_model");
-        if (!modelnode) throw XmlError{"No such node (pk_model)"};
-        drug = modelnode->get("drug");
-        trial = modelnode->get("trial");
-        patient_id = modelnode->has_attr("patient") ? modelnode->get("patient") : std::string();
-        use_peripheral_compartment = modelnode->get_bool("peripheral_compartment", false);
-        const long nt = modelnode->get_long("num_transit_compartments", 0);
-        if (nt < 0) throw XmlError{"num_transit_compartments must be >= 0"};
-        num_transit_compartments = (size_t)nt;
-        biphasic_absorption = modelnode->get_bool("biphasic_absorption", false);
-        use_metabolite = modelnode->get_bool("metabolite", false);
-        pkdata_file = modelnode->has_attr("pkdata_file") ? modelnode->get("pkdata_file") : std::string("pkdata.json");
-    } catch (XmlError& e) {
-        LOGERROR("Error parsing likelihood file: %s", e.what.c_str());
-        return false;
-    }
-    const std::string use_patient = option_get(vm, "pharmacosingle.patient", "");
-    if (!use_patient.empty()) patient_id = use_patient;
-    if (patient_id.empty()) {
-        LOGERROR("Patient ID has not been specified in either the likelihood or as command-line option.");
-        return false;
-    }
-
-    std::string path = pkdata_file;
-    if (!file_exists(path)) {
-        std::string alt = option_get(vm, "likelihood_dir", ".") + "/" + pkdata_file;
-        if (file_exists(alt)) path = alt;
-    }
-    Json data;
-    try {
-        data = json_load(path);
-    } catch (JsonError& e) {
-        LOGERROR("Failed to open data file %s: %s", pkdata_file.c_str(), e.what.c_str());
-        return false;
-    }
-    const Json* g = data.find(trial);
-    if (!g) {
-        LOGERROR("Group \"%s\" not found in %s", trial.c_str(), path.c_str());
-        return false;
-    }
     bool result = true;
     auto var = [&](const std::string& name) -> const Json* {
         const Json* v = g->find(name);
@@ -587,7 +542,6 @@ bool PharmacoLikelihoodSingle::Initialize(std::shared_ptr<const VariableSet> vs,
         return v;
     };
     const Json* jt = var("time");
-    const Json* jp = var("patients");
     const Json* jc = var(drug + "_plasma_concentration");
     const Json* jd = var(drug + "_dose");
     const Json* jdi = var(drug + "_dosing_interval");
@@ -596,19 +550,6 @@ bool PharmacoLikelihoodSingle::Initialize(std::shared_ptr<const VariableSet> vs,
     const Json* jin = var(drug + "_intermittent");
     const Json* jti = var("treatment_interruptions");
     if (!result) return false;
-    size_t pix = jp->arr.size();
-    for (size_t j = 0; j < jp->arr.size(); j++) {
-        const Json& p = jp->arr[j];
-        const std::string id = p.type == Json::String ? p.str : std::to_string((long)p.num);
-        if (id == patient_id) {
-            pix = j;
-            break;
-        }
-    }
-    if (pix == jp->arr.size()) {
-        LOGERROR("Cannot find patient \"%s\" in data file", patient_id.c_str());
-        return false;
-    }
     std::vector<Real> tp, conc;
     Real dose, dosing_interval, dose_after_dose_change, dose_change_time;
     unsigned int intermittent;
@@ -636,9 +577,8 @@ bool PharmacoLikelihoodSingle::Initialize(std::shared_ptr<const VariableSet> vs,
         LOGERROR("Dosing interval must be positive");  // the reference loops forever otherwise
         return false;
     }
-    // treatment schedule up to 696 h (PharmacoPatient.cpp:48-91)
-    treatment_timepoints.clear();
-    treatment_doses.clear();
+    out.treatment_timepoints.clear();
+    out.treatment_doses.clear();
     const Real last_time = 696;
     for (Real t = 0; t < last_time; t += dosing_interval) {
         bool give_treatment = true;
@@ -654,13 +594,13 @@ bool PharmacoLikelihoodSingle::Initialize(std::shared_ptr<const VariableSet> vs,
             const Real time_in_week = t - 7.0 * 24.0 * floor(t / (7.0 * 24.0));
             if (time_in_week >= 4.0 * 24.0) give_treatment = false;
         }
-        if (give_treatment) treatment_timepoints.push_back(t);
+        if (give_treatment) out.treatment_timepoints.push_back(t);
     }
-    for (Real t : treatment_timepoints)
-        treatment_doses.push_back((!std::isnan(dose_change_time) && t >= dose_change_time) ? dose_after_dose_change : dose);
-    // observations: sorted, NaN concentrations dropped (.cpp:93-113)
-    observation_timepoints.clear();
-    observed_concentrations.clear();
+    for (Real t : out.treatment_timepoints)
+        out.treatment_doses.push_back((!std::isnan(dose_change_time) && t >= dose_change_time) ? dose_after_dose_change
+                                                                                              : dose);
+    out.observation_timepoints.clear();
+    out.observed_concentrations.clear();
     Real prev_time = -std::numeric_limits<Real>::infinity();
     for (size_t i = 0; i < tp.size(); i++) {
         if (tp[i] < prev_time) {
@@ -669,15 +609,91 @@ bool PharmacoLikelihoodSingle::Initialize(std::shared_ptr<const VariableSet> vs,
         }
         prev_time = tp[i];
         if (!std::isnan(conc[i])) {
-            observation_timepoints.push_back(tp[i]);
-            observed_concentrations.push_back(conc[i]);
+            out.observation_timepoints.push_back(tp[i]);
+            out.observed_concentrations.push_back(conc[i]);
         }
     }
-    if (observation_timepoints.empty() || treatment_timepoints.empty()) {
+    if (out.observation_timepoints.empty() || out.treatment_timepoints.empty()) {
         // (the reference reads observation_timepoints.tail(1) and stale scratch here)
-        LOGERROR("Patient \"%s\" has no observations or no treatments", patient_id.c_str());
+        LOGERROR("Patient \"%s\" has no observations or no treatments", out.patient_id.c_str());
         return false;
     }
+    return true;
+}
+
+static const Json* load_pharmaco_group(const OptionsMap& vm, const std::string& pkdata_file, const std::string& trial,
+                                       Json& data)
+{
+    std::string path = pkdata_file;
+    if (!file_exists(path)) {
+        std::string alt = option_get(vm, "likelihood_dir", ".") + "/" + pkdata_file;
+        if (file_exists(alt)) path = alt;
+    }
+    try {
+        data = json_load(path);
+    } catch (JsonError& e) {
+        LOGERROR("Failed to open data file %s: %s", pkdata_file.c_str(), e.what.c_str());
+        return nullptr;
+    }
+    const Json* g = data.find(trial);
+    if (!g) LOGERROR("Group \"%s\" not found in %s", trial.c_str(), path.c_str());
+    if (g && !g->find("patients")) {
+        LOGERROR("Variable \"patients\" not found in group \"%s\"", trial.c_str());
+        return nullptr;
+    }
+    return g;
+}
+
+static std::string patient_name(const Json& p) { return p.type == Json::String ? p.str : std::to_string((long)p.num); }
+
+// PharmacoLikelihoodSingle::Initialize (PharmacoLikelihoodSingle.cpp:36-76). The reference opens
+// "pkdata.nc"; this build reads the same variables from the JSON sidecar named by pkdata_file
+// (default "pkdata.json").
+bool PharmacoLikelihoodSingle::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& likelihood_node,
+                                          const OptionsMap& vm)
+{
+    varset = vs;
+    options = vm;
+    std::string trial, pkdata_file;
+    try {
+        const XmlNode* modelnode = likelihood_node.child("pk_model");
+        if (!modelnode) throw XmlError{"No such node (pk_model)"};
+        drug = modelnode->get("drug");
+        trial = modelnode->get("trial");
+        patient.patient_id = modelnode->has_attr("patient") ? modelnode->get("patient") : std::string();
+        use_peripheral_compartment = modelnode->get_bool("peripheral_compartment", false);
+        const long nt = modelnode->get_long("num_transit_compartments", 0);
+        if (nt < 0) throw XmlError{"num_transit_compartments must be >= 0"};
+        num_transit_compartments = (size_t)nt;
+        biphasic_absorption = modelnode->get_bool("biphasic_absorption", false);
+        use_metabolite = modelnode->get_bool("metabolite", false);
+        pkdata_file = modelnode->has_attr("pkdata_file") ? modelnode->get("pkdata_file") : std::string("pkdata.json");
+    } catch (XmlError& e) {
+        LOGERROR("Error parsing likelihood file: %s", e.what.c_str());
+        return false;
+    }
+    const std::string use_patient = option_get(vm, "pharmacosingle.patient", "");
+    if (!use_patient.empty()) patient.patient_id = use_patient;
+    if (patient.patient_id.empty()) {
+        LOGERROR("Patient ID has not been specified in either the likelihood or as command-line option.");
+        return false;
+    }
+    Json data;
+    const Json* g = load_pharmaco_group(vm, pkdata_file, trial, data);
+    if (!g) return false;
+    const Json* jp = g->find("patients");
+    size_t pix = jp->arr.size();
+    for (size_t j = 0; j < jp->arr.size(); j++) {
+        if (patient_name(jp->arr[j]) == patient.patient_id) {
+            pix = j;
+            break;
+        }
+    }
+    if (pix == jp->arr.size()) {
+        LOGERROR("Cannot find patient \"%s\" in data file", patient.patient_id.c_str());
+        return false;
+    }
+    if (!load_pharmaco_patient(g, trial, drug, pix, patient)) return false;
     MW = molecular_weight(drug);
     if (std::isnan(MW)) {
         LOGERROR("Unknown drug \"%s\"", drug.c_str());
@@ -744,14 +760,17 @@ bool PharmacoLikelihoodSingle::PostInitialize()
     model.peripheral = use_peripheral_compartment;
     model.biphasic = biphasic_absorption;
     model.metabolite = use_metabolite;
-    model.n_treat = (int32_t)treatment_timepoints.size();
-    model.n_obs = (int32_t)observation_timepoints.size();
+    model.n_treat = (int32_t)patient.treatment_timepoints.size();
+    model.n_obs = (int32_t)patient.observation_timepoints.size();
     model.MW = MW;
     model.transforms = transforms.data();
-    model.treat_times = treatment_timepoints.data();
-    model.treat_doses = treatment_doses.data();
-    model.obs_times = observation_timepoints.data();
-    model.obs_conc = observed_concentrations.data();
+    model.treat_times = patient.treatment_timepoints.data();
+    model.treat_doses = patient.treatment_doses.data();
+    model.obs_times = patient.observation_timepoints.data();
+    model.obs_conc = patient.observed_concentrations.data();
+    model.param_map = BCM3HIP_PARAM_MAP_SINGLE;
+    model.P = 1;
+    for (int w = 0; w < 5; w++) model.sigma_ix[w] = -1;
     const int ncomp = 2 + (use_peripheral_compartment ? 1 : 0) + (use_metabolite ? 1 : 0) + (int)num_transit_compartments;
     if (ncomp > BCM3HIP_EXPM_NMAX) {
         LOGERROR("%d compartments; this backend supports at most %d", ncomp, (int)BCM3HIP_EXPM_NMAX);
@@ -762,6 +781,163 @@ bool PharmacoLikelihoodSingle::PostInitialize()
     const int r = bcm3hip_open_expm_pk(device, &model, &ctx);
     if (r != 0) {
         LOGERROR("Opening the pharmaco_single GPU context failed: %s", bcm3hip_error_string(r));
+        return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// PharmacoLikelihoodPopulation::Initialize (PharmacoLikelihoodPopulation.cpp:43-98): every patient
+// of the trial, loaded as Patient::Load does, concatenated for the device (offsets per patient)
+bool PharmacoLikelihoodPopulation::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& likelihood_node,
+                                              const OptionsMap& vm)
+{
+    varset = vs;
+    options = vm;
+    std::string trial, pkdata_file;
+    try {
+        const XmlNode* modelnode = likelihood_node.child("pk_model");
+        if (!modelnode) throw XmlError{"No such node (pk_model)"};
+        drug = modelnode->get("drug");
+        trial = modelnode->get("trial");
+        use_peripheral_compartment = modelnode->get_bool("peripheral_compartment", false);
+        const long nt = modelnode->get_long("num_transit_compartments", 0);
+        if (nt < 0) throw XmlError{"num_transit_compartments must be >= 0"};
+        num_transit_compartments = (size_t)nt;
+        use_bioavailability = modelnode->get_bool("bioavailability", false);
+        // likelihood_cache_size: the reference's exact-match cache; nothing to size here
+        if (modelnode->get_long("likelihood_cache_size", 16) < 0) throw XmlError{"likelihood_cache_size must be >= 0"};
+        pkdata_file = modelnode->has_attr("pkdata_file") ? modelnode->get("pkdata_file") : std::string("pkdata.json");
+    } catch (XmlError& e) {
+        LOGERROR("Error parsing likelihood file: %s", e.what.c_str());
+        return false;
+    }
+    Json data;
+    const Json* g = load_pharmaco_group(vm, pkdata_file, trial, data);
+    if (!g) return false;
+    const Json* jp = g->find("patients");
+    patients.assign(jp->arr.size(), PharmacoPatient{});
+    if (patients.empty()) {
+        LOGERROR("No patients in group \"%s\"", trial.c_str());
+        return false;
+    }
+    treat_times.clear();
+    treat_doses.clear();
+    obs_times.clear();
+    obs_conc.clear();
+    treat_offset.assign(1, 0);
+    obs_offset.assign(1, 0);
+    for (size_t i = 0; i < patients.size(); i++) {
+        patients[i].patient_id = patient_name(jp->arr[i]);
+        if (!load_pharmaco_patient(g, trial, drug, i, patients[i])) return false;
+        const PharmacoPatient& p = patients[i];
+        treat_times.insert(treat_times.end(), p.treatment_timepoints.begin(), p.treatment_timepoints.end());
+        treat_doses.insert(treat_doses.end(), p.treatment_doses.begin(), p.treatment_doses.end());
+        obs_times.insert(obs_times.end(), p.observation_timepoints.begin(), p.observation_timepoints.end());
+        obs_conc.insert(obs_conc.end(), p.observed_concentrations.begin(), p.observed_concentrations.end());
+        treat_offset.push_back((int32_t)treat_times.size());
+        obs_offset.push_back((int32_t)obs_times.size());
+    }
+    MW = molecular_weight(drug);
+    if (std::isnan(MW)) {
+        LOGERROR("Unknown drug \"%s\"", drug.c_str());
+        return false;
+    }
+    return true;
+}
+
+// PharmacoLikelihoodPopulation::InitializePatientMarginals (.cpp:345-356): p<i>_<name>, i from 1
+bool PharmacoLikelihoodPopulation::InitializePatientMarginals(const std::string& name, int which)
+{
+    const size_t P = patients.size();
+    for (size_t i = 0; i < P; i++) {
+        const std::string varname = "p" + std::to_string(i + 1) + "_" + name;
+        const size_t ix = varset->GetVariableIndex(varname, false);
+        if (ix == std::numeric_limits<size_t>::max()) {
+            LOGERROR("Standard deviation found for \"%s\", but could not find prior variable for \"%s\"", name.c_str(),
+                     varname.c_str());
+            return false;
+        }
+        patient_ix[which * P + i] = (int32_t)ix;
+    }
+    return true;
+}
+
+// PharmacoLikelihoodPopulation::PostInitialize (.cpp:100-183)
+bool PharmacoLikelihoodPopulation::PostInitialize()
+{
+    const size_t none = std::numeric_limits<size_t>::max();
+    auto ix = [&](const std::string& n, bool required) -> int32_t {
+        const size_t i = varset->GetVariableIndex(n, required);
+        return i == none ? -1 : (int32_t)i;
+    };
+    model = bcm3hip_expm_pk_model{};
+    model.additive_sd_ix = ix("additive_error_standard_deviation", false);
+    model.proportional_sd_ix = ix("proportional_error_standard_deviation", false);
+    if (model.additive_sd_ix < 0 && model.proportional_sd_ix < 0) {
+        LOGERROR("Neither \"additive_error_standard_deviation\" nor \"proportional_error_standard_deviation\" has been "
+                 "specified in the prior; at least one of these variables should be included.");
+        return false;
+    }
+    model.absorption_ix = ix("mean_absorption", true);
+    model.clearance_ix = ix("mean_clearance", true);
+    model.vod_ix = ix("mean_volume_of_distribution", true);
+    if (model.absorption_ix < 0 || model.clearance_ix < 0 || model.vod_ix < 0) return false;
+    model.excretion_ix = ix("mean_excretion", false);
+    const size_t P = patients.size();
+    patient_ix.assign(6 * P, -1);
+    static const char* rates[5] = {"absorption", "excretion", "clearance", "volume_of_distribution", "transit_time"};
+    for (int w = 0; w < 5; w++) {
+        model.sigma_ix[w] = ix(std::string("sigma_") + rates[w], false);
+        if (model.sigma_ix[w] >= 0 && !InitializePatientMarginals(rates[w], w)) return false;
+    }
+    model.pf_ix = model.pb_ix = model.mtt_ix = model.direct_ix = model.metab_conv_ix = -1;
+    if (use_peripheral_compartment) {
+        model.pf_ix = ix("peripheral_forward_rate", true);
+        model.pb_ix = ix("peripheral_backward_rate", true);
+        if (model.pf_ix < 0 || model.pb_ix < 0) {
+            LOGERROR("Peripheral compartmant was specified, but forward or backward rates have not both been specified in prior.");
+            return false;
+        }
+    }
+    if (num_transit_compartments > 0) {
+        model.mtt_ix = ix("mean_transit_time", true);
+        if (model.mtt_ix < 0) {
+            LOGERROR("Transit compartmants were specified, but mean transit time has not been specified in prior.");
+            return false;
+        }
+    } else {
+        model.sigma_ix[4] = -1;  // the reference reads sigma_transit_time only with transit compartments
+    }
+    if (use_bioavailability && !InitializePatientMarginals("bioavailability", 5)) return false;
+    transforms.resize(varset->GetNumVariables());
+    for (size_t i = 0; i < transforms.size(); i++) transforms[i] = (int32_t)varset->GetVariableTransform(i);
+    model.d = (int32_t)varset->GetNumVariables();
+    model.n_transit = (int32_t)num_transit_compartments;
+    model.peripheral = use_peripheral_compartment;
+    model.n_treat = (int32_t)treat_times.size();
+    model.n_obs = (int32_t)obs_times.size();
+    model.MW = MW;
+    model.transforms = transforms.data();
+    model.treat_times = treat_times.data();
+    model.treat_doses = treat_doses.data();
+    model.obs_times = obs_times.data();
+    model.obs_conc = obs_conc.data();
+    model.param_map = BCM3HIP_PARAM_MAP_POPULATION;
+    model.P = (int32_t)P;
+    model.patient_ix = patient_ix.data();
+    model.treat_offset = treat_offset.data();
+    model.obs_offset = obs_offset.data();
+    const int ncomp = 2 + (use_peripheral_compartment ? 1 : 0) + (int)num_transit_compartments;
+    if (ncomp > BCM3HIP_EXPM_NMAX) {
+        LOGERROR("%d compartments; this backend supports at most %d", ncomp, (int)BCM3HIP_EXPM_NMAX);
+        return false;
+    }
+    if (!OpenDevice(options)) return false;
+    if (option_get(options, "backend", "") == "none") return true;
+    const int r = bcm3hip_open_expm_pk(device, &model, &ctx);
+    if (r != 0) {
+        LOGERROR("Opening the pharmaco_population GPU context failed: %s", bcm3hip_error_string(r));
         return false;
     }
     return true;

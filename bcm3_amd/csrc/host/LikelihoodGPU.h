@@ -102,6 +102,12 @@ private:
     bcm3hip_popk_model model{};
 };
 
+// Patient::Load's result (src/pharmaco/PharmacoPatient.h)
+struct PharmacoPatient {
+    std::string patient_id;
+    std::vector<Real> treatment_timepoints, treatment_doses, observation_timepoints, observed_concentrations;
+};
+
 // One patient, linear compartment model solved by matrix exponentials
 // (PharmacoLikelihoodSingle.cpp:36-218, PharmacoPatient.cpp:8-116, PharmacokineticModel.cpp:111-247).
 // Initialize loads the patient (JSON sidecar of the reference's pkdata.nc); PostInitialize resolves
@@ -112,20 +118,42 @@ public:
     bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
                     const OptionsMap& vm) override;
     bool PostInitialize() override;
-    const std::string& GetPatientID() const { return patient_id; }
+    const PharmacoPatient& GetPatient() const { return patient; }
     const bcm3hip_expm_pk_model& GetDeviceModel() const { return model; }
-    const std::vector<Real>& GetTreatmentTimepoints() const { return treatment_timepoints; }
-    const std::vector<Real>& GetTreatmentDoses() const { return treatment_doses; }
-    const std::vector<Real>& GetObservationTimepoints() const { return observation_timepoints; }
-    const std::vector<Real>& GetObservedConcentrations() const { return observed_concentrations; }
 
 private:
-    std::string drug, patient_id;
+    std::string drug;
+    PharmacoPatient patient;
     bool use_peripheral_compartment = false, biphasic_absorption = false, use_metabolite = false;
     size_t num_transit_compartments = 0;
     Real MW = NAN;
-    std::vector<Real> treatment_timepoints, treatment_doses, observation_timepoints, observed_concentrations;
     std::vector<int32_t> transforms;
+    OptionsMap options;
+    bcm3hip_expm_pk_model model{};
+};
+
+// Every patient of the trial, rates drawn per patient from the population distribution
+// (PharmacoLikelihoodPopulation.cpp:43-340), log-likelihoods summed in patient order. The
+// reference's exact-match result cache (likelihood_cache_size, .cpp:356-393) only returns values
+// the solve reproduces bit for bit; the batched device path evaluates every patient.
+class PharmacoLikelihoodPopulation : public LikelihoodGPUBase {
+public:
+    PharmacoLikelihoodPopulation(size_t sampling_threads, size_t evaluation_threads) {}
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+    bool PostInitialize() override;
+    size_t GetNumPatients() const { return patients.size(); }
+    const bcm3hip_expm_pk_model& GetDeviceModel() const { return model; }
+
+private:
+    bool InitializePatientMarginals(const std::string& name, int which);
+    std::string drug;
+    std::vector<PharmacoPatient> patients;
+    bool use_peripheral_compartment = false, use_bioavailability = false;
+    size_t num_transit_compartments = 0;
+    Real MW = NAN;
+    std::vector<int32_t> transforms, patient_ix, treat_offset, obs_offset;
+    std::vector<Real> treat_times, treat_doses, obs_times, obs_conc;
     OptionsMap options;
     bcm3hip_expm_pk_model model{};
 };

@@ -75,6 +75,10 @@ int bcm3_likelihood_expm_pk_model(const bcm3_likelihood* h, void* model)
         *(bcm3hip_expm_pk_model*)model = p->GetDeviceModel();
         return 0;
     }
+    if (auto* p = dynamic_cast<bcm3::PharmacoLikelihoodPopulation*>(h->ll.get())) {
+        *(bcm3hip_expm_pk_model*)model = p->GetDeviceModel();
+        return 0;
+    }
     return -2;
 }
 

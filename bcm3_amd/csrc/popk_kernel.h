@@ -50,9 +50,16 @@ struct ExpmPKDevModel {
     const double* treat_doses;
     const double* obs_times;
     const double* obs_conc;
+    int32_t param_map, P;
+    int32_t sigma_ix[5];
+    const int32_t* patient_ix;  // [6][P]
+    const int32_t* treat_offset;  // [P+1]
+    const int32_t* obs_offset;    // [P+1]
 };
 
+// patient_llh / traj_status: [n][P] scratch, used when P > 1
 hipError_t launch_expm_pk(const ExpmPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
-                          hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
+                          double* patient_llh, int32_t* traj_status, hipStream_t stream, hipEvent_t ev_start,
+                          hipEvent_t ev_stop);
 
 }  // namespace bcm3hip

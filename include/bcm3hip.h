@@ -144,6 +144,20 @@ typedef struct {
     const double* treat_doses;  /* [n_treat] */
     const double* obs_times;    /* [n_obs] ascending */
     const double* obs_conc;     /* [n_obs] */
+    /* pharmaco_population (src/pharmaco/PharmacoLikelihoodPopulation.cpp:202-340). With param_map
+     * POPULATION, absorption_ix / clearance_ix / vod_ix / excretion_ix / mtt_ix name the mean_*
+     * variables, each patient's rate is fastpow10(QuantileNormal(p<i>_<rate>, mean, sigma)) when
+     * sigma_ix[] of that rate is >= 0 (else fastpow10(mean); transit time: TransformVariable), and
+     * the P per-patient log-likelihoods are summed in patient order. For pharmaco_single: param_map
+     * SINGLE, P = 1, offsets may be NULL. */
+    int32_t param_map;          /* BCM3HIP_PARAM_MAP_SINGLE or BCM3HIP_PARAM_MAP_POPULATION */
+    int32_t P;                  /* patients (1 for single) */
+    int32_t sigma_ix[5];        /* sigma_absorption, _excretion, _clearance, _volume_of_distribution,
+                                   _transit_time; -1 = no random effect */
+    const int32_t* patient_ix;  /* [6][P]: p<i>_absorption, _excretion, _clearance,
+                                   _volume_of_distribution, _transit_time, _bioavailability; -1 = absent */
+    const int32_t* treat_offset; /* [P+1]: patient j's doses are treat_*[treat_offset[j], treat_offset[j+1]) */
+    const int32_t* obs_offset;   /* [P+1]: likewise for obs_* */
 } bcm3hip_expm_pk_model;
 
 typedef struct bcm3hip_ctx bcm3hip_ctx;

@@ -208,17 +208,53 @@ def _exp(x):
         return math.inf
 
 
-def construct_matrix(model, v):
-    """(A, conv, additive_sd, proportional_sd) for one parameter vector; model = dict of the
-    bcm3hip_expm_pk_model fields"""
+def quantile_normal(p, mu, sigma):
+    """bcm3::QuantileNormal (src/utils/ProbabilityDistributions.cpp:359-363): Boost
+    quantile(normal(mu, sigma), p) = mu - sigma sqrt(2) erfc_inv(2p); scipy's ndtri is the same
+    function (third-party implementations agree to a few ulp)"""
+    from scipy.special import ndtri
+    return mu + sigma * float(ndtri(p))
+
+
+def population_rates(model, v, j):
+    """PharmacoLikelihoodPopulation::SetupSimulation (PharmacoLikelihoodPopulation.cpp:271-340) for
+    patient j: (absorption, excretion, clearance, vod, transit_time, bioavailability)"""
+    P = model["P"]
+    sig = model["sigma_ix"]
+    pix = model["patient_ix"]
+
+    def pop(which, mean_ix):
+        if sig[which] < 0:
+            return _exp(v[mean_ix] * 2.3025850929940459)  # fastpow10 (MathFunctions.h:13)
+        return _exp(quantile_normal(v[pix[which * P + j]], v[mean_ix], v[sig[which]]) * 2.3025850929940459)
+
+    absorption = pop(0, model["absorption_ix"])
+    excretion = pop(1, model["excretion_ix"]) if model["excretion_ix"] >= 0 else 0.0
+    clearance = pop(2, model["clearance_ix"])
+    vod = pop(3, model["vod_ix"])
+    tt = 0.0
+    if model["n_transit"] > 0:
+        tt = transform(model["transforms"][model["mtt_ix"]], v[model["mtt_ix"]]) if sig[4] < 0 else pop(4, model["mtt_ix"])
+    bi = pix[5 * P + j]
+    return absorption, excretion, clearance, vod, tt, (v[bi] if bi >= 0 else 1.0)
+
+
+def construct_matrix(model, v, j=0):
+    """(A, conv, additive_sd, proportional_sd, bioavailability) for one parameter vector (and
+    patient j of a population model); model = dict of the bcm3hip_expm_pk_model fields"""
     tv = lambda ix: transform(model["transforms"][ix], v[ix])  # noqa: E731
     add_sd = tv(model["additive_sd_ix"]) if model["additive_sd_ix"] >= 0 else 0.0
     prop_sd = tv(model["proportional_sd_ix"]) if model["proportional_sd_ix"] >= 0 else 0.0
-    absorption = tv(model["absorption_ix"])
-    clearance = tv(model["clearance_ix"])
-    vod = tv(model["vod_ix"])
+    if model.get("param_map", 1) == 0:
+        absorption, excretion, clearance, vod, transit_time, bioavailability = population_rates(model, v, j)
+    else:
+        absorption = tv(model["absorption_ix"])
+        clearance = tv(model["clearance_ix"])
+        vod = tv(model["vod_ix"])
+        excretion = tv(model["excretion_ix"]) if model["excretion_ix"] >= 0 else 0.0
+        transit_time = tv(model["mtt_ix"]) if model["n_transit"] > 0 else 0.0
+        bioavailability = 1.0
     elimination = clearance / vod
-    excretion = tv(model["excretion_ix"]) if model["excretion_ix"] >= 0 else 0.0
     conv = (1e6 / model["MW"]) / vod
     nc, mi, ft = 2, -1, 0
     nt = model["n_transit"]
@@ -234,7 +270,7 @@ def construct_matrix(model, v):
     A[0, 0] -= excretion
     A[0, 0] -= absorption
     if nt > 0:
-        tr = (nt + 1.0) / tv(model["mtt_ix"])
+        tr = (nt + 1.0) / transit_time
         A[ft, 0] += absorption
         if nt > 2:
             for i in range(nt - 1):
@@ -260,10 +296,10 @@ def construct_matrix(model, v):
         A[mi, 1] += mc
         A[mi, mi] -= 1.0
     A[1, 1] -= elimination
-    return A, conv, add_sd, prop_sd
+    return A, conv, add_sd, prop_sd, bioavailability
 
 
-def solve(A, treat_times, treat_doses, obs_times, expm_fn=expm):
+def solve(A, treat_times, treat_doses, obs_times, expm_fn=expm, bioavailability=1.0):
     """PharmacokineticModel::Solve: (ok, central compartment at the observation times)"""
     n = A.shape[0]
     y = np.zeros(n)
@@ -273,7 +309,7 @@ def solve(A, treat_times, treat_doses, obs_times, expm_fn=expm):
     t = 0.0
     while tti < len(treat_times) and t < simulate_until:
         target = treat_times[tti + 1] if tti < len(treat_times) - 1 else simulate_until
-        y[0] += treat_doses[tti] * 1.0
+        y[0] += treat_doses[tti] * bioavailability
         while oti < len(obs_times) and obs_times[oti] <= target:
             E = expm_fn(A * (obs_times[oti] - t))
             out[oti] = (E @ y)[1]
@@ -293,26 +329,38 @@ def log_pdf_tnu4(x, mu, sigma):
 
 
 def evaluate(model, values, backend="restated"):
-    """logp[n], ok[n] for values[n][d] (PharmacoLikelihoodSingle::EvaluateLogProbability)"""
+    """logp[n], ok[n] for values[n][d]: PharmacoLikelihoodSingle::EvaluateLogProbability
+    (PharmacoLikelihoodSingle.cpp:149-218), or with param_map 0 the patient-ordered sum of
+    PharmacoLikelihoodPopulation::EvaluateLogProbability (PharmacoLikelihoodPopulation.cpp:202-248;
+    ok = every patient's solve succeeded)"""
     values = np.atleast_2d(np.asarray(values, dtype=np.float64))
     tt = np.asarray(model["treat_times"], dtype=np.float64)
     td = np.asarray(model["treat_doses"], dtype=np.float64)
     ot = np.asarray(model["obs_times"], dtype=np.float64)
     oc = np.asarray(model["obs_conc"], dtype=np.float64)
-    logp = np.empty(len(values))
-    ok = np.empty(len(values), dtype=bool)
+    P = model.get("P", 1)
+    toff = model.get("treat_offset") or [0, len(tt)]
+    ooff = model.get("obs_offset") or [0, len(ot)]
+    logp = np.zeros(len(values))
+    ok = np.ones(len(values), dtype=bool)
     with np.errstate(all="ignore"):  # non-finite rates propagate as in the reference
-        _evaluate_into(model, values, tt, td, ot, oc, backend, logp, ok)
+        for j in range(P):
+            lp = np.empty(len(values))
+            good = np.empty(len(values), dtype=bool)
+            _evaluate_into(model, values, j, tt[toff[j]:toff[j + 1]], td[toff[j]:toff[j + 1]],
+                           ot[ooff[j]:ooff[j + 1]], oc[ooff[j]:ooff[j + 1]], backend, lp, good)
+            logp += lp
+            ok &= good
     return logp, ok
 
 
-def _evaluate_into(model, values, tt, td, ot, oc, backend, logp, ok):
+def _evaluate_into(model, values, j, tt, td, ot, oc, backend, logp, ok):
     for e, v in enumerate(values):
-        A, conv, add_sd, prop_sd = construct_matrix(model, v)
+        A, conv, add_sd, prop_sd, bioavailability = construct_matrix(model, v, j)
         if backend == "ref":
-            good, central = solve_ref(A, tt, td, ot)
+            good, central = solve_ref(A, tt, td * bioavailability, ot)
         else:
-            good, central = solve(A, tt, td, ot)
+            good, central = solve(A, tt, td, ot, bioavailability=bioavailability)
         ok[e] = good
         if not good:
             logp[e] = -np.inf

@@ -132,7 +132,7 @@ def main():
     pk = {TRIAL: g}
     for j, pid in enumerate(PATIENTS):
         m = model_fields("peripheral", pid, pk)
-        A, conv, add_sd, prop_sd = X.construct_matrix(m, np.array(TRUE))
+        A, conv, add_sd, prop_sd, _ = X.construct_matrix(m, np.array(TRUE))
         ok, central = X.solve_ref(A, m["treat_times"], m["treat_doses"], np.array(TIME))
         assert ok
         x = conv * central
