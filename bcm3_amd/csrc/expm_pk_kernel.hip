@@ -9,9 +9,11 @@
 // solves), then s squarings.
 //
 // Layout: the n x n matrices (n <= 16) live in the wavefront's LDS, column-major with a padded
-// column stride; lane j owns column j of every matrix it writes (products, linear combinations,
-// the triangular solves of the right-hand side's column j), and reads the other operand with
-// wave-uniform addresses (LDS broadcast). The exponential of the dose interval is kept and reused
+// column stride. Products, linear combinations, scalings and the LU's Schur updates are
+// element-parallel (lane L computes entries L, L + 64, ...: all 64 lanes busy for n = 8, each
+// entry one dot product of length n); column sums, pivot swaps and the triangular solves of the
+// right-hand side stay column-per-lane (lane j owns column j). Every entry is formed by the same
+// operations in the same order either way. The exponential of the dose interval is kept and reused
 // while the interval repeats (the same bits as recomputing it). HBM traffic per evaluation: the
 // parameter vector in, logp / status out; the patient's treatment and observation arrays are
 // shared by every wavefront (L2 resident).
@@ -40,48 +42,55 @@ struct ExpmShared {
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }
 
+// element-parallel sweep: lane L visits the entries L, L + 64, ... of an n x n matrix in
+// column-major order, f(column, row); every entry is computed by exactly the arithmetic the
+// column-per-lane form used, so results do not depend on which lane computes them
+template <class F>
+__device__ __forceinline__ void for_elems(int n, int L, F f)
+{
+    const int nn = n * n;
+    for (int e = L; e < nn; e += 64) {
+        const int c = e / n;
+        f(c, e - c * n);
+    }
+}
+
 // C = X Y (C distinct from X and Y): C(i,j) = X(i,0) Y(0,j) + ... in ascending k, the order of
 // Eigen's coefficient-based product for these sizes
-__device__ void matmul(Mat& C, const Mat& X, const Mat& Y, int n, int j)
+__device__ void matmul(Mat& C, const Mat& X, const Mat& Y, int n, int L)
 {
-    if (j < n) {
-        for (int i = 0; i < n; i++) {
-            double acc = X[0][i] * Y[j][0];
-            for (int k = 1; k < n; k++) acc = __builtin_fma(X[k][i], Y[j][k], acc);
-            C[j][i] = acc;
-        }
-    }
+    for_elems(n, L, [&](int j, int i) {
+        double acc = X[0][i] * Y[j][0];
+        for (int k = 1; k < n; k++) acc = __builtin_fma(X[k][i], Y[j][k], acc);
+        C[j][i] = acc;
+    });
     wsync();
 }
 
 // R = c2 X2 + c1 X1 + c0 X0 + ci I  (left to right, as Eigen evaluates the sum expression);
 // X0 may be null (term absent)
 __device__ void lincomb(Mat& R, double c2, const Mat& X2, double c1, const Mat& X1, double c0, const Mat* X0,
-                        double ci, int n, int j)
+                        double ci, int n, int L)
 {
-    if (j < n) {
-        for (int i = 0; i < n; i++) {
-            double r = c2 * X2[j][i] + c1 * X1[j][i];
-            if (X0) r = r + c0 * (*X0)[j][i];
-            r = r + ci * (i == j ? 1.0 : 0.0);
-            R[j][i] = r;
-        }
-    }
+    for_elems(n, L, [&](int j, int i) {
+        double r = c2 * X2[j][i] + c1 * X1[j][i];
+        if (X0) r = r + c0 * (*X0)[j][i];
+        r = r + ci * (i == j ? 1.0 : 0.0);
+        R[j][i] = r;
+    });
     wsync();
 }
 
 // R += (c2 X2 + c1 X1 + c0 X0 + ci I)
 __device__ void lincomb_add(Mat& R, double c2, const Mat& X2, double c1, const Mat& X1, double c0, const Mat& X0,
-                            double ci, int n, int j)
+                            double ci, int n, int L)
 {
-    if (j < n) {
-        for (int i = 0; i < n; i++) {
-            double r = c2 * X2[j][i] + c1 * X1[j][i];
-            r = r + c0 * X0[j][i];
-            r = r + ci * (i == j ? 1.0 : 0.0);
-            R[j][i] = R[j][i] + r;
-        }
-    }
+    for_elems(n, L, [&](int j, int i) {
+        double r = c2 * X2[j][i] + c1 * X1[j][i];
+        r = r + c0 * X0[j][i];
+        r = r + ci * (i == j ? 1.0 : 0.0);
+        R[j][i] = R[j][i] + r;
+    });
     wsync();
 }
 
@@ -127,8 +136,8 @@ __device__ void expm(ExpmShared& sh, Mat& out, int n, int j)
         matmul(sh.A4, sh.A2, sh.A2, n, j);
         matmul(sh.A6, sh.A4, sh.A2, n, j);
         matmul(sh.Eo, sh.A6, sh.A2, n, j);  // A8 (Eo is free until the result is written)
-        if (j < n) {
-            for (int i = 0; i < n; i++) {
+        for_elems(n, j, [&](int j, int i) {
+            {
                 const double I = (i == j) ? 1.0 : 0.0;
                 double t = 1.0 * sh.Eo[j][i] + 3960.0 * sh.A6[j][i];
                 t = t + 2162160.0 * sh.A4[j][i];
@@ -141,7 +150,7 @@ __device__ void expm(ExpmShared& sh, Mat& out, int n, int j)
                 v = v + 17643225600.0 * I;
                 sh.V[j][i] = v;
             }
-        }
+        });
         wsync();
         matmul(sh.U, M, sh.W, n, j);
     } else {
@@ -149,8 +158,7 @@ __device__ void expm(ExpmShared& sh, Mat& out, int n, int j)
         int e;
         frexp(l1 / 5.371920351148152, &e);
         squarings = e < 0 ? 0 : e;
-        if (j < n)
-            for (int i = 0; i < n; i++) M[j][i] = ldexp(M[j][i], -squarings);
+        for_elems(n, j, [&](int j, int i) { M[j][i] = ldexp(M[j][i], -squarings); });
         wsync();
         matmul(sh.A2, M, M, n, j);
         matmul(sh.A4, sh.A2, sh.A2, n, j);
@@ -166,12 +174,10 @@ __device__ void expm(ExpmShared& sh, Mat& out, int n, int j)
                     64764752532480000.0, n, j);
     }
     // numer = U + V (into out), denom = -U + V (into W)
-    if (j < n) {
-        for (int i = 0; i < n; i++) {
-            out[j][i] = sh.U[j][i] + sh.V[j][i];
-            sh.W[j][i] = -sh.U[j][i] + sh.V[j][i];
-        }
-    }
+    for_elems(n, j, [&](int j, int i) {
+        out[j][i] = sh.U[j][i] + sh.V[j][i];
+        sh.W[j][i] = -sh.U[j][i] + sh.V[j][i];
+    });
     wsync();
     // PartialPivLU (unblocked_lu) of W: pivot = first row of the largest |value| in column k
     Mat& D = sh.W;
@@ -197,10 +203,12 @@ __device__ void expm(ExpmShared& sh, Mat& out, int n, int j)
             const double piv = D[k][k];
             // column k below the pivot /= pivot (l_i), then the Schur update of the columns j > k:
             // every lane forms the same quotients; column k is written after all reads of it
-            if (j > k && j < n) {
-                const double ukj = D[j][k];
-                for (int i = k + 1; i < n; i++) D[j][i] = D[j][i] - (D[k][i] / piv) * ukj;
-            }
+            // (element-parallel over the trailing (n-k-1)^2 block; row k and column k are only read)
+            const int m = n - k - 1;
+            for_elems(m, j, [&](int c, int r) {
+                const int jj = k + 1 + c, i = k + 1 + r;
+                D[jj][i] = D[jj][i] - (D[k][i] / piv) * D[jj][k];
+            });
             wsync();
             if (j == k)
                 for (int i = k + 1; i < n; i++) D[k][i] = D[k][i] / piv;
@@ -232,8 +240,7 @@ __device__ void expm(ExpmShared& sh, Mat& out, int n, int j)
     // undo the scaling: result *= result
     for (int s = 0; s < squarings; s++) {
         matmul(sh.U, out, out, n, j);
-        if (j < n)
-            for (int i = 0; i < n; i++) out[j][i] = sh.U[j][i];
+        for_elems(n, j, [&](int j, int i) { out[j][i] = sh.U[j][i]; });
         wsync();
     }
 }
@@ -371,8 +378,7 @@ __global__ void __launch_bounds__(64) expm_pk_kernel(ExpmPKDevModel m, int64_t n
         wsync();
         while (oti < n_obs && obs_times[oti] <= target_t) {
             const double offset_t = obs_times[oti] - current_t;
-            if (j < n)
-                for (int i = 0; i < n; i++) sh.S[j][i] = sh.A[j][i] * offset_t;
+            for_elems(n, j, [&](int j, int i) { sh.S[j][i] = sh.A[j][i] * offset_t; });
             wsync();
             expm(sh, sh.Eo, n, j);
             double c = sh.Eo[0][1] * sh.y[0];
@@ -391,8 +397,7 @@ __global__ void __launch_bounds__(64) expm_pk_kernel(ExpmPKDevModel m, int64_t n
         }
         const double dt = target_t - current_t;
         if (!(dt == cached_dt)) {
-            if (j < n)
-                for (int i = 0; i < n; i++) sh.S[j][i] = sh.A[j][i] * dt;
+            for_elems(n, j, [&](int j, int i) { sh.S[j][i] = sh.A[j][i] * dt; });
             wsync();
             expm(sh, sh.E, n, j);
             cached_dt = dt;

@@ -154,6 +154,27 @@ def extra_workloads(device, seed):
             rec["trajectories_per_s"] = 64 * n / (ms * 1e-3)
         out[tag] = rec
         ll.close()
+    out.update(expm_workloads(device, gen))
+    return out
+
+
+def expm_workloads(device, gen):
+    """Secondary lines for the matrix-exponential PK likelihoods (expm_pk_kernel.hip): pharmaco_single
+    (patient B2, all options: 8 compartments) and pharmaco_population (2 patients, peripheral + 3
+    transit compartments, every random effect, bioavailability), 256 chains each."""
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.sampler import DevicePrior, load_prior
+    out = {}
+    for tag, name, patients in (("pharmaco_single_256chains", "pharmaco_single", 1),
+                                ("pharmaco_population_256chains", "pharmaco_population", 2)):
+        lik = os.path.join(GOLDEN, f"{name}_likelihood.xml")
+        pri = os.path.join(GOLDEN, "pharmaco_prior.xml" if patients == 1 else "pharmaco_population_prior.xml")
+        ll = Likelihood(lik, pri, device=device.index or 0)
+        n = 256
+        x = DevicePrior(load_prior(pri), device).sample(n, gen).contiguous()
+        ms = _rate(ll, n, x, device)
+        out[tag] = {"chains": n, "patients": patients, "kernel_ms": ms, "evals_per_s": n / (ms * 1e-3)}
+        ll.close()
     return out
 
 

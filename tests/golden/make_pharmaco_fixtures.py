@@ -146,6 +146,8 @@ def main():
         json.dump(pk, f)
     with open(os.path.join(HERE, "pharmaco_prior.xml"), "w") as f:
         f.write(prior_xml())
+    with open(os.path.join(HERE, "pharmaco_single_likelihood.xml"), "w") as f:  # bench.py's workload
+        f.write(likelihood_xml("all", "B2"))
     out = {}
     for k, variant in enumerate(VARIANTS):
         for pid in PATIENTS:

@@ -125,6 +125,8 @@ def main():
         pk = json.load(f)
     with open(os.path.join(HERE, "pharmaco_population_prior.xml"), "w") as f:
         f.write(prior_xml())
+    with open(os.path.join(HERE, "pharmaco_population_likelihood.xml"), "w") as f:  # bench.py's workload
+        f.write(likelihood_xml("all"))
     out = {}
     for k, variant in enumerate(VARIANTS):
         m = model_fields(variant, pk)
