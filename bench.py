@@ -135,6 +135,48 @@ def _rate(ll, n, x, device, reps=3):
     return tt / nl
 
 
+def expm_cpu_baseline(budget_s: float, seed: int):
+    """The reference CPU path of the matrix-exponential PK likelihoods: PharmacokineticModel::Solve
+    on the reference's vendored Eigen (oracle/_ref/libexpmref.so, MatrixBase::exp), one thread,
+    timed over the solves of uniform prior draws (the matrix set-up and the observation model, a
+    few % of an evaluation, run untimed in Python)."""
+    import ctypes as C
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), GOLDEN]
+    import json
+    import numpy as np
+    import expm_pk as X
+    import make_pharmaco_fixtures as S
+    import make_pharmaco_population_fixtures as PF
+    lib = X.ref_lib()
+    with open(os.path.join(GOLDEN, "pharmaco_pkdata.json")) as f:
+        pk = json.load(f)
+    dp = C.POINTER(C.c_double)
+    out = {}
+    for tag, m, v in (("pharmaco_single_256chains", S.model_fields("all", "B2", pk), S.draws(4096, seed)),
+                      ("pharmaco_population_256chains", PF.model_fields("all", pk), PF.draws("all", 4096, seed))):
+        P = m.get("P", 1)
+        toff = m.get("treat_offset") or [0, m["n_treat"]]
+        ooff = m.get("obs_offset") or [0, m["n_obs"]]
+        arr = lambda k, j, off: np.ascontiguousarray(m[k][off[j]:off[j + 1]], dtype=np.float64)  # noqa: E731
+        pats = [(arr("treat_times", j, toff), arr("treat_doses", j, toff), arr("obs_times", j, ooff)) for j in range(P)]
+        t_solve, n = 0.0, 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget_s and n < len(v):
+            for j, (tt, td, ot) in enumerate(pats):
+                A, _, _, _, ba = X.construct_matrix(m, v[n], j)
+                a = np.asfortranarray(A)
+                tdb = td * ba
+                cen = np.empty(len(ot))
+                t1 = time.perf_counter()
+                lib.eigen_pk_solve(A.shape[0], a.ctypes.data_as(dp), len(tt), tt.ctypes.data_as(dp),
+                                   tdb.ctypes.data_as(dp), len(ot), ot.ctypes.data_as(dp), cen.ctypes.data_as(dp))
+                t_solve += time.perf_counter() - t1
+            n += 1
+        out[tag] = {"evals_per_s_1thread": n / t_solve, "cores": 1, "kind": "reference",
+                    "sample": f"{n} prior draws, {P} patient solve(s) each, {t_solve:.1f} s of Eigen solves"}
+    return out
+
+
 def extra_workloads(device, seed):
     """Secondary lines (not the headline): the P=64 population variant of C3 (256 chains x 64
     patient trajectories per launch) and config C2 (circular ridge, 256 chains)."""
@@ -265,6 +307,10 @@ def main():
     cpu = None
     if world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args.cpu_seconds, args.seed)
+        if args.extras:
+            for tag, rec in expm_cpu_baseline(2.0, args.seed).items():
+                if tag in extra:
+                    extra[tag]["cpu_baseline"] = rec
 
     acc_mut = float(loop.accepted_mutate) / max(1, loop.attempted_mutate)
     line = {

@@ -17,6 +17,7 @@ timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
 cat $O/bench.json
 BENCH="bench.py --steps 20 --warmup 3 --cpu-seconds 0 --throughput-batch 0 --extras 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- python3 $BENCH > $O/kt.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_extras -o kt -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --throughput-batch 0 --extras 1 > $O/kt_extras.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o pmc -- python3 $BENCH > $O/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o pmc -- python3 $BENCH > $O/pmc_write.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/pmc_sq -o pmc -- python3 $BENCH > $O/pmc_sq.log 2>&1
