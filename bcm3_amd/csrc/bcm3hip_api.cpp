@@ -44,6 +44,8 @@ struct bcm3hip_ctx {
     size_t cap_traj = 0, cap_tstatus = 0, cap_status = 0;
     double* traj = nullptr;
     size_t cap_trajout = 0;
+    double* exps = nullptr;  // expm pk: [n][n_jobs][n*n]
+    size_t cap_exps = 0;
     bcm3hip_traj_stats* stats = nullptr;
     size_t cap_stats = 0;
     int lanes_per_wave = 0;  // 0 = auto (auto_lanes_per_wave)
@@ -305,7 +307,42 @@ int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* m, bcm3hip_ctx
     x.param_map = m->param_map;
     x.P = P;
     for (int w = 0; w < 5; w++) x.sigma_ix[w] = single ? -1 : m->sigma_ix[w];
-    if ((r = upload(c, pix.data(), pix.size(), &x.patient_ix)) ||
+    // the step lengths PharmacokineticModel::Solve (.cpp:127-174) will exponentiate, per patient,
+    // by the loop's own arithmetic; equal values share one job
+    std::vector<double> job_dt;
+    std::vector<int32_t> job_patient, interval_job(m->n_treat, -1), obs_job(m->n_obs, -1);
+    for (int j = 0; j < P; j++) {
+        const size_t first = job_dt.size();
+        auto job = [&](double dt) -> int32_t {
+            for (size_t k = first; k < job_dt.size(); k++)
+                if (job_dt[k] == dt) return (int32_t)k;
+            job_dt.push_back(dt);
+            job_patient.push_back(j);
+            return (int32_t)(job_dt.size() - 1);
+        };
+        const double* tt = m->treat_times + toff[j];
+        const double* ot = m->obs_times + ooff[j];
+        const int nt = toff[j + 1] - toff[j], no = ooff[j + 1] - ooff[j];
+        const double until = ot[no - 1];
+        int tti = 0, oti = 0;
+        double cur = 0.0;
+        while (tti < nt && cur < until) {
+            const double target = (tti < nt - 1) ? tt[tti + 1] : until;
+            while (oti < no && ot[oti] <= target) {
+                obs_job[ooff[j] + oti] = job(ot[oti] - cur);
+                oti++;
+            }
+            interval_job[toff[j] + tti] = job(target - cur);
+            cur = target;
+            tti++;
+        }
+    }
+    x.n_jobs = (int32_t)job_dt.size();
+    if ((r = upload(c, job_dt.data(), job_dt.size(), &x.job_dt)) ||
+        (r = upload(c, job_patient.data(), job_patient.size(), &x.job_patient)) ||
+        (r = upload(c, interval_job.data(), interval_job.size(), &x.interval_job)) ||
+        (r = upload(c, obs_job.data(), obs_job.size(), &x.obs_job)) ||
+        (r = upload(c, pix.data(), pix.size(), &x.patient_ix)) ||
         (r = upload(c, toff.data(), toff.size(), &x.treat_offset)) ||
         (r = upload(c, ooff.data(), ooff.size(), &x.obs_offset)) ||
         (r = upload(c, m->transforms, (size_t)m->d, &x.transforms)) ||
@@ -329,6 +366,7 @@ int bcm3hip_close(bcm3hip_ctx* c)
     hipFree(c->logp);
     hipFree(c->status);
     hipFree(c->pllh);
+    hipFree(c->exps);
     hipFree(c->tstatus);
     hipFree(c->traj);
     hipFree(c->stats);
@@ -410,10 +448,9 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
                         c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
                         c->block_waves, c->uni_solver, s, e0, e1);
     } else if (c->kind == 3) {
-        if (c->xm.P > 1 && (grow(c->pllh, c->cap_traj, n * (size_t)c->xm.P) ||
-                            grow(c->tstatus, c->cap_tstatus, n * (size_t)c->xm.P)))
+        if (grow(c->exps, c->cap_exps, n * (size_t)c->xm.n_jobs * (size_t)(c->xm.n * c->xm.n)))
             return BCM3HIP_ERR_ALLOC;
-        e = launch_expm_pk(c->xm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, s, e0, e1);
+        e = launch_expm_pk(c->xm, (int64_t)n, dvalues, dlogp, dstatus, c->exps, s, e0, e1);
     } else {
         e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     }

@@ -1,6 +1,7 @@
 // expm_pk_kernel.hip -- batched pharmaco_single likelihood on MI355X (gfx950).
 //
-// One wavefront = one evaluation (one proposal of one chain) of one patient. The linear compartment model
+// Two phases: all matrix exponentials of a launch in parallel (one wavefront per evaluation x
+// distinct step length), then one wavefront per evaluation for the state chain. The linear compartment model
 // dy/dt = A y is advanced from dose to dose with matrix exponentials exactly as
 // PharmacokineticModel::Solve does (src/pharmaco/PharmacokineticModel.cpp:111-177), each
 // exp(A t) by Eigen's algorithm (unsupported/Eigen/src/MatrixFunctions/MatrixExponential.h):
@@ -326,141 +327,141 @@ __device__ void construct_matrix(const ExpmPKDevModel& m, const double* v, int j
     A[1][1] -= elimination;
 }
 
-// one block (one wavefront) per (evaluation e, patient j)
-__global__ void __launch_bounds__(64) expm_pk_kernel(ExpmPKDevModel m, int64_t nev, const double* __restrict__ values,
-                                                     double* __restrict__ logp, int32_t* __restrict__ status,
-                                                     double* __restrict__ patient_llh, int32_t* __restrict__ traj_status)
+// Phase 1: every matrix exponential of a launch at once. The exponentials of a solve depend on
+// the parameters and the schedule only, never on the state, so the host enumerates per patient
+// the distinct step lengths the Solve loop will use (job_dt: dose intervals and observation
+// offsets, computed with the loop's own subtractions) and one wavefront per (evaluation, job)
+// forms exp(A dt) -- n_eval x n_jobs independent waves instead of one sequential chain per
+// evaluation. Identical dt values share a job; exp is deterministic, so this is bit-identical to
+// recomputing them in the loop. Output: exps[e][job] column-major n x n.
+__global__ void __launch_bounds__(64) expm_pk_exp_kernel(ExpmPKDevModel m, int64_t nev,
+                                                         const double* __restrict__ values,
+                                                         double* __restrict__ exps)
 {
     __shared__ ExpmShared sh;
     const int64_t b = blockIdx.x;
-    const int64_t e = b / m.P;
-    const int pj = (int)(b - e * m.P);
+    const int64_t e = b / m.n_jobs;
+    const int job = (int)(b - e * m.n_jobs);
     if (e >= nev) return;  // uniform per block
-    const int j = threadIdx.x;
+    const int L = threadIdx.x;
     const int n = m.n;
-    const double* v = values + e * m.d;
-    const int t0 = m.treat_offset[pj], n_treat = m.treat_offset[pj + 1] - t0;
-    const int o0 = m.obs_offset[pj], n_obs = m.obs_offset[pj + 1] - o0;
-    const double* treat_times = m.treat_times + t0;
-    const double* treat_doses = m.treat_doses + t0;
-    const double* obs_times = m.obs_times + o0;
-    const double* obs_conc = m.obs_conc + o0;
-    if (j == 0) {
+    if (L == 0) {
         double c, a, p, ba;
-        construct_matrix(m, v, pj, sh.A, c, a, p, ba);
-        sh.colsum[0] = c;
-        sh.colsum[1] = a;
-        sh.colsum[2] = p;
-        sh.colsum[3] = ba;
-        sh.fail = 0;
+        construct_matrix(m, values + e * m.d, m.job_patient[job], sh.A, c, a, p, ba);
     }
-    if (j < n) sh.y[j] = 0.0;
     wsync();
-    const double conv = sh.colsum[0];
-    const double add_sd = sh.colsum[1];
-    const double prop_sd = sh.colsum[2];
-    const double bioavailability = sh.colsum[3];
+    const double dt = m.job_dt[job];
+    for_elems(n, L, [&](int j, int i) { sh.S[j][i] = sh.A[j][i] * dt; });
     wsync();
-
-    // PharmacokineticModel::Solve (.cpp:127-174); the observation model of
-    // PharmacoLikelihoodSingle::EvaluateLogProbability (.cpp:199-215) / PharmacoLikelihoodPopulation
-    // (.cpp:226-242) folded in, in observation order (all observations are reached: the last
-    // interval ends at the last one)
-    const double simulate_until = obs_times[n_obs - 1];
-    double cached_dt = NAN;
-    double llh = 0.0;
-    bool llh_done = false;
-    int tti = 0, oti = 0;
-    double current_t = 0.0;
-    while (tti < n_treat && current_t < simulate_until) {
-        const double target_t = (tti < n_treat - 1) ? treat_times[tti + 1] : simulate_until;
-        if (j == 0) sh.y[0] += treat_doses[tti] * bioavailability;
-        wsync();
-        while (oti < n_obs && obs_times[oti] <= target_t) {
-            const double offset_t = obs_times[oti] - current_t;
-            for_elems(n, j, [&](int j, int i) { sh.S[j][i] = sh.A[j][i] * offset_t; });
-            wsync();
-            expm(sh, sh.Eo, n, j);
-            double c = sh.Eo[0][1] * sh.y[0];
-            for (int k = 1; k < n; k++) c = __builtin_fma(sh.Eo[k][1], sh.y[k], c);
-            if (!llh_done) {
-                const double x = conv * c;
-                if (isnan(x) || isinf(x)) {
-                    llh = -INFINITY;
-                    llh_done = true;
-                } else {
-                    const double yobs = obs_conc[oti];
-                    if (!isnan(yobs)) llh += log_pdf_tnu4(x, yobs, add_sd + prop_sd * fmax(x, 0.0));
-                }
-            }
-            oti++;
-        }
-        const double dt = target_t - current_t;
-        if (!(dt == cached_dt)) {
-            for_elems(n, j, [&](int j, int i) { sh.S[j][i] = sh.A[j][i] * dt; });
-            wsync();
-            expm(sh, sh.E, n, j);
-            cached_dt = dt;
-        }
-        double ynew = 0.0;
-        if (j < n) {
-            ynew = sh.E[0][j] * sh.y[0];
-            for (int k = 1; k < n; k++) ynew = __builtin_fma(sh.E[k][j], sh.y[k], ynew);
-        }
-        wsync();
-        if (j < n) {
-            sh.y[j] = ynew;
-            if (isnan(ynew)) sh.fail = 1;
-        }
-        wsync();
-        if (sh.fail) break;
-        current_t = target_t;
-        tti++;
-    }
-    if (j == 0) {
-        const bool fail = sh.fail != 0;
-        const double r = fail ? -INFINITY : llh;
-        const int32_t st = fail ? BCM3HIP_STATUS_SOLVER_FAIL : BCM3HIP_STATUS_OK;
-        if (m.P == 1) {
-            logp[e] = r;
-            if (status) status[e] = st;
-        } else {
-            patient_llh[b] = r;
-            traj_status[b] = st;
-        }
-    }
+    expm(sh, sh.E, n, L);
+    double* out = exps + b * (int64_t)(n * n);
+    for_elems(n, L, [&](int j, int i) { out[j * n + i] = sh.E[j][i]; });
 }
 
-// logp = sum over patients in patient order (PharmacoLikelihoodPopulation.cpp:217-247)
-__global__ void expm_pk_reduce_kernel(int64_t nev, int P, const double* __restrict__ patient_llh,
-                                      const int32_t* __restrict__ traj_status, double* __restrict__ logp,
-                                      int32_t* __restrict__ status)
+// Phase 2: one wavefront per evaluation walks its patients in order: PharmacokineticModel::Solve
+// (.cpp:127-174) with the exponentials of phase 1 (lane j = state component j), the observation
+// model of PharmacoLikelihoodSingle::EvaluateLogProbability (.cpp:199-215) /
+// PharmacoLikelihoodPopulation (.cpp:217-247) folded in, log-likelihoods summed in patient order.
+__global__ void __launch_bounds__(64) expm_pk_chain_kernel(ExpmPKDevModel m, int64_t nev,
+                                                           const double* __restrict__ values,
+                                                           const double* __restrict__ exps,
+                                                           double* __restrict__ logp, int32_t* __restrict__ status)
 {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ Mat A;
+    __shared__ double y[NM];
+    __shared__ double scal[4];
+    __shared__ int fail;
+    const int64_t e = blockIdx.x;
     if (e >= nev) return;
-    double s = 0.0;
-    int32_t st = BCM3HIP_STATUS_OK;
-    for (int j = 0; j < P; j++) {
-        s += patient_llh[e * P + j];
-        st = traj_status[e * P + j] != BCM3HIP_STATUS_OK ? BCM3HIP_STATUS_SOLVER_FAIL : st;
+    const int j = threadIdx.x;
+    const int n = m.n;
+    const int nn = n * n;
+    const double* v = values + e * m.d;
+    const double* ex = exps + e * (int64_t)m.n_jobs * nn;
+    double total = 0.0;
+    bool any_fail = false;
+    for (int pj = 0; pj < m.P; pj++) {
+        if (j == 0) {
+            double c, a, p, ba;
+            construct_matrix(m, v, pj, A, c, a, p, ba);
+            scal[0] = c;
+            scal[1] = a;
+            scal[2] = p;
+            scal[3] = ba;
+            fail = 0;
+        }
+        if (j < n) y[j] = 0.0;
+        wsync();
+        const double conv = scal[0], add_sd = scal[1], prop_sd = scal[2], bioavailability = scal[3];
+        const int t0 = m.treat_offset[pj], n_treat = m.treat_offset[pj + 1] - t0;
+        const int o0 = m.obs_offset[pj], n_obs = m.obs_offset[pj + 1] - o0;
+        const double* treat_times = m.treat_times + t0;
+        const double* treat_doses = m.treat_doses + t0;
+        const double* obs_times = m.obs_times + o0;
+        const double* obs_conc = m.obs_conc + o0;
+        const double simulate_until = obs_times[n_obs - 1];
+        double llh = 0.0;
+        bool llh_done = false;
+        int tti = 0, oti = 0;
+        double current_t = 0.0;
+        while (tti < n_treat && current_t < simulate_until) {
+            const double target_t = (tti < n_treat - 1) ? treat_times[tti + 1] : simulate_until;
+            if (j == 0) y[0] += treat_doses[tti] * bioavailability;
+            wsync();
+            while (oti < n_obs && obs_times[oti] <= target_t) {
+                const double* Eo = ex + (int64_t)m.obs_job[o0 + oti] * nn;  // [col][row]
+                double c = Eo[1] * y[0];
+                for (int k = 1; k < n; k++) c = __builtin_fma(Eo[k * n + 1], y[k], c);
+                if (!llh_done) {
+                    const double x = conv * c;
+                    if (isnan(x) || isinf(x)) {
+                        llh = -INFINITY;
+                        llh_done = true;
+                    } else {
+                        const double yobs = obs_conc[oti];
+                        if (!isnan(yobs)) llh += log_pdf_tnu4(x, yobs, add_sd + prop_sd * fmax(x, 0.0));
+                    }
+                }
+                oti++;
+            }
+            const double* E = ex + (int64_t)m.interval_job[t0 + tti] * nn;
+            double ynew = 0.0;
+            if (j < n) {
+                ynew = E[j] * y[0];
+                for (int k = 1; k < n; k++) ynew = __builtin_fma(E[k * n + j], y[k], ynew);
+            }
+            wsync();
+            if (j < n) {
+                y[j] = ynew;
+                if (isnan(ynew)) fail = 1;
+            }
+            wsync();
+            if (fail) break;
+            current_t = target_t;
+            tti++;
+        }
+        const bool f = fail != 0;
+        total += f ? -INFINITY : llh;
+        any_fail = any_fail || f;
+        wsync();
     }
-    logp[e] = s;
-    if (status) status[e] = st;
+    if (j == 0) {
+        logp[e] = total;
+        if (status) status[e] = any_fail ? BCM3HIP_STATUS_SOLVER_FAIL : BCM3HIP_STATUS_OK;
+    }
 }
 
 }  // namespace
 
 hipError_t launch_expm_pk(const ExpmPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
-                          double* patient_llh, int32_t* traj_status, hipStream_t stream, hipEvent_t ev_start,
-                          hipEvent_t ev_stop)
+                          double* exps, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop)
 {
     if (n == 0) return hipSuccess;
     if (ev_start) hipEventRecord(ev_start, stream);
-    hipLaunchKernelGGL(expm_pk_kernel, dim3((unsigned)(n * m.P)), dim3(64), 0, stream, m, n, values, logp, status,
-                       patient_llh, traj_status);
-    if (m.P > 1)
-        hipLaunchKernelGGL(expm_pk_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, n, m.P,
-                           patient_llh, traj_status, logp, status);
+    if (m.n_jobs > 0)  // (none when every observation is at t = 0: the Solve loop never runs)
+        hipLaunchKernelGGL(expm_pk_exp_kernel, dim3((unsigned)(n * m.n_jobs)), dim3(64), 0, stream, m, n, values,
+                           exps);
+    hipLaunchKernelGGL(expm_pk_chain_kernel, dim3((unsigned)n), dim3(64), 0, stream, m, n, values, exps, logp, status);
     const hipError_t e = hipGetLastError();
     if (ev_stop) hipEventRecord(ev_stop, stream);
     return e;

@@ -55,11 +55,16 @@ struct ExpmPKDevModel {
     const int32_t* patient_ix;  // [6][P]
     const int32_t* treat_offset;  // [P+1]
     const int32_t* obs_offset;    // [P+1]
+    // the distinct step lengths of every patient's Solve loop (built by bcm3hip_open_expm_pk)
+    int32_t n_jobs;
+    const double* job_dt;          // [n_jobs]
+    const int32_t* job_patient;    // [n_jobs]
+    const int32_t* interval_job;   // [n_treat]: job of the step that ends dose interval tti
+    const int32_t* obs_job;        // [n_obs]: job of the offset from the interval start to observation oti
 };
 
-// patient_llh / traj_status: [n][P] scratch, used when P > 1
+// exps: [n][n_jobs][n*n] scratch
 hipError_t launch_expm_pk(const ExpmPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
-                          double* patient_llh, int32_t* traj_status, hipStream_t stream, hipEvent_t ev_start,
-                          hipEvent_t ev_stop);
+                          double* exps, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
 
 }  // namespace bcm3hip
