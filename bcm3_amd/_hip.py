@@ -110,14 +110,14 @@ def lib() -> C.CDLL:
     L.bcm3hip_num_variables.argtypes = [vp]
     u64 = C.c_uint64
     L.bcm3hip_ptmh_propose.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, i64, u64, u64, vp]
-    L.bcm3hip_ptmh_accept.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp, i64,
-                                      u64, u64, vp]
+    L.bcm3hip_ptmh_accept.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, C.c_double, vp, vp, vp, vp, vp, vp, vp,
+                                      i64, u64, u64, vp]
     L.bcm3hip_pt_exchange_local.argtypes = [C.c_int, C.c_int, i64, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp,
                                             u64, u64, vp]
     L.bcm3hip_ptmh_propose_adaptive.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                                 C.POINTER(Proposal), i64, u64, u64, vp]
     L.bcm3hip_ptmh_accept_adaptive.argtypes = [C.c_int, C.c_int, vp, vp, vp, vp, vp, C.c_double, vp, vp, vp, vp,
-                                               vp, vp, C.POINTER(Proposal), i64, u64, u64, vp]
+                                               vp, vp, vp, C.POINTER(Proposal), i64, u64, u64, vp]
     L.bcm3hip_pt_exchange_pair.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp,
                                            u64, u64, vp]
     L.bcm3hip_history_add.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp]
@@ -169,6 +169,14 @@ class Context:
                 setattr(m, name, a.ctypes.data)
             else:
                 setattr(m, name, v)
+        h = C.c_void_p()
+        check(lib().bcm3hip_open_popk(device, C.byref(m), C.byref(h)), "bcm3hip_open_popk")
+        return cls(h, int(m.d), int(m.P), int(m.N), int(m.T))
+
+    @classmethod
+    def from_popk_model(cls, m: "PopPKModel", device: int = 0) -> "Context":
+        """A second context on a model description some other owner keeps alive (e.g.
+        bcm3.Likelihood.popk_model(), whose arrays live as long as that likelihood)."""
         h = C.c_void_p()
         check(lib().bcm3hip_open_popk(device, C.byref(m), C.byref(h)), "bcm3hip_open_popk")
         return cls(h, int(m.d), int(m.P), int(m.N), int(m.T))
@@ -262,10 +270,11 @@ def ptmh_propose(C, d, kind, p0, p1, scale, temps, values, prop, lprior_prop, ch
 
 
 def ptmh_accept(C, d, temps, prop, lprior_prop, llh_prop, learning_rate, values, lprior, llh, lpp, accept_out,
-                accepted, chain0, seed, it, stream=None):
-    """bcm3hip_ptmh_accept on device pointers (ints; accept_out / accepted may be None)."""
+                accepted, chain0, seed, it, stream=None, nan_llh=None):
+    """bcm3hip_ptmh_accept on device pointers (ints; accept_out / accepted / nan_llh may be None)."""
     check(lib().bcm3hip_ptmh_accept(C, d, temps, prop, lprior_prop, llh_prop, learning_rate, values, lprior, llh, lpp,
-                                    accept_out, accepted, chain0, _u64(seed), _u64(it), stream), "ptmh_accept")
+                                    accept_out, accepted, nan_llh, chain0, _u64(seed), _u64(it), stream),
+          "ptmh_accept")
 
 
 def pt_exchange_local(C, d, g0, start, wrap_local, temps, values, llh, lprior, lpp, acc_mask, accepted, seed, rnd,
@@ -284,11 +293,11 @@ def ptmh_propose_adaptive(C, d, kind, p0, p1, p2, temps, values, prop, lprior_pr
 
 
 def ptmh_accept_adaptive(C, d, temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values, lprior, llh, lpp,
-                         accept_out, accepted, proposal: Proposal, chain0, seed, it, stream=None):
-    """bcm3hip_ptmh_accept_adaptive on device pointers (ints; accept_out / accepted may be None)."""
+                         accept_out, accepted, proposal: Proposal, chain0, seed, it, stream=None, nan_llh=None):
+    """bcm3hip_ptmh_accept_adaptive on device pointers (ints; accept_out / accepted / nan_llh may be None)."""
     check(lib().bcm3hip_ptmh_accept_adaptive(C, d, temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values,
-                                             lprior, llh, lpp, accept_out, accepted, C_byref(proposal), chain0,
-                                             _u64(seed), _u64(it), stream), "ptmh_accept_adaptive")
+                                             lprior, llh, lpp, accept_out, accepted, nan_llh, C_byref(proposal),
+                                             chain0, _u64(seed), _u64(it), stream), "ptmh_accept_adaptive")
 
 
 def pt_exchange_pair(C, d, i1, i2, g1, temps, values, llh, lprior, lpp, acc_out, accepted, seed, rnd, stream=None):

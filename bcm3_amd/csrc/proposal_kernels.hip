@@ -448,8 +448,9 @@ __global__ void ptmh_accept_adaptive_kernel(int C, int d, const double* __restri
                                             double learning_rate, double* __restrict__ values,
                                             double* __restrict__ lprior, double* __restrict__ llh,
                                             double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
-                                            unsigned long long* __restrict__ accepted, bcm3hip_proposal P,
-                                            int64_t chain0, uint64_t seed, uint64_t iter)
+                                            unsigned long long* __restrict__ accepted,
+                                            int32_t* __restrict__ nan_llh, bcm3hip_proposal P, int64_t chain0,
+                                            uint64_t seed, uint64_t iter)
 {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
@@ -458,7 +459,13 @@ __global__ void ptmh_accept_adaptive_kernel(int C, int d, const double* __restri
     const double nq = lprior_prop[c];
     bool acc;
     double npp;
-    if (T == 0.0) {
+    if (isnan(nl)) {
+        // Sampler::EvaluateLikelihood (Sampler.cpp:172-178): a NaN log-likelihood is fatal; the
+        // chain keeps its state (no EMA update) and the host raises at its next check of the flag
+        if (nan_llh) *nan_llh = 1;
+        acc = false;
+        npp = 0.0;
+    } else if (T == 0.0) {
         acc = true;
         npp = (nl == -INFINITY) ? nq : nq + T * nl;
     } else {
@@ -549,8 +556,8 @@ int bcm3hip_ptmh_propose_adaptive(int C, int d, const int32_t* prior_kind, const
 int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double* prop, const double* lprior_prop,
                                  const double* llh_prop, const double* log_mh, double learning_rate, double* values,
                                  double* lprior, double* llh, double* lpp, uint8_t* accept_out, uint64_t* accepted,
-                                 const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed, uint64_t iter,
-                                 void* stream)
+                                 int32_t* nan_llh, const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed,
+                                 uint64_t iter, void* stream)
 {
     if (C < 0 || d <= 0 || !proposal_ok(proposal, C, d) ||
         (C > 0 && (!temps || !prop || !lprior_prop || !llh_prop || !log_mh || !values || !lprior || !llh || !lpp)))
@@ -558,7 +565,7 @@ int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double
     if (C == 0) return 0;
     hipLaunchKernelGGL(ptmh_accept_adaptive_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d,
                        temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values, lprior, llh, lpp, accept_out,
-                       (unsigned long long*)accepted, *proposal, chain0, seed, iter);
+                       (unsigned long long*)accepted, nan_llh, *proposal, chain0, seed, iter);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -226,6 +226,9 @@ class PTMHDevice:
         self.lpp = torch.empty(C, dtype=torch.float64, device=dev)
         self.accepted_mutate = torch.zeros(1, dtype=torch.int64, device=dev)
         self.accepted_exchange = torch.zeros(1, dtype=torch.int64, device=dev)
+        # set by the accept kernels on a NaN log-likelihood (Sampler.cpp:172-178: fatal)
+        self.nan_llh = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.nan_check_every = 100
         self.attempted_mutate = 0
         self.attempted_exchange = 0
         # ptmhsampler.swapping_scheme / exchange_probability (SamplerPT.cpp:63-75, 163-164)
@@ -273,6 +276,9 @@ class PTMHDevice:
                                        self.prop.data_ptr(), self.lprior_prop.data_ptr(), self.g0, self.seed, it,
                                        self._stream())
             self._eval(self.prop, self.llh_prop)
+            if bool(torch.isnan(self.llh_prop * self.lr).any()):
+                # SamplerPTChain::Initialize -> EvaluatePriorLikelihood fails on NaN (Sampler.cpp:172-178)
+                raise RuntimeError("Likelihood evaluation returned NaN while finding starting positions")
             self.values.copy_(torch.where(bad.view(-1, 1), self.prop, self.values))
             self.lprior.copy_(torch.where(bad, self.lprior_prop, self.lprior))
             self.llh.copy_(torch.where(bad, self.llh_prop * self.lr, self.llh))
@@ -332,7 +338,8 @@ class PTMHDevice:
             h.ptmh_accept_adaptive(C, d, self.T.data_ptr(), self.prop.data_ptr(), self.lprior_prop.data_ptr(),
                                    self.llh_prop.data_ptr(), self.log_mh.data_ptr(), self.lr, self.values.data_ptr(),
                                    self.lprior.data_ptr(), self.llh.data_ptr(), self.lpp.data_ptr(), None,
-                                   self.accepted_mutate.data_ptr(), P, self.g0, self.seed, self.iter, st)
+                                   self.accepted_mutate.data_ptr(), P, self.g0, self.seed, self.iter, st,
+                                   nan_llh=self.nan_llh.data_ptr())
             self.history.add(self.T, self.values, None, st)  # SamplerPTChain.cpp:309
             self.attempted_mutate += C
             self.iter += 1
@@ -344,7 +351,7 @@ class PTMHDevice:
         h.ptmh_accept(C, d, self.T.data_ptr(), self.prop.data_ptr(), self.lprior_prop.data_ptr(),
                       self.llh_prop.data_ptr(), self.lr, self.values.data_ptr(), self.lprior.data_ptr(),
                       self.llh.data_ptr(), self.lpp.data_ptr(), None, self.accepted_mutate.data_ptr(), self.g0,
-                      self.seed, self.iter, st)
+                      self.seed, self.iter, st, nan_llh=self.nan_llh.data_ptr())
         self.attempted_mutate += C
         self.iter += 1
 
@@ -400,9 +407,21 @@ class PTMHDevice:
                     and self.adaptations_done < self.adapt_times):
                 self.adapt_proposal()
 
+    def check_nan(self) -> bool:
+        """Raise if any likelihood evaluation since the start returned NaN (the accept kernels set
+        the flag; Sampler::EvaluateLikelihood stops the sampler, Sampler.cpp:172-178). One host
+        synchronisation; run() calls it every nan_check_every iterations and at the end."""
+        if int(self.nan_llh.item()) != 0:
+            raise RuntimeError("Likelihood evaluation returned NaN (Sampler::EvaluateLikelihood, fatal)")
+        return False
+
     def adapt_proposal(self):
         """SamplerPTChain::AdaptProposal for every chain of the rank (T == 0 chains excepted)."""
+        self.check_nan()
         self.proposal.adapt(self.history.samples, self.history.counters)
+        # SamplerPTChain::AdaptProposal discards the history it adapted on (SampleHistory::Reset,
+        # SamplerPTChain.cpp:174-177 / SampleHistory.cpp:27-31)
+        self.history.counters.zero_()
         self.adaptations_done += 1
 
     def run(self, num_samples: int):
@@ -410,6 +429,9 @@ class PTMHDevice:
         total = num_samples * self.use_every_nth
         for si in range(total):
             self.iteration(last=(si + 1 == total))
+            if (si + 1) % self.nan_check_every == 0:
+                self.check_nan()
+        self.check_nan()
 
 def exchange_participants(C: int, g0: int, Ctot: int, world: int, start: int):
     """Chains of the rank owning global chains [g0, g0+C) that are in a pair in an exchange round

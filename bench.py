@@ -10,7 +10,13 @@ One step = one DeterministicEvenOdd PT-MH iteration of every chain on the rank
 run as ONE batched launch of the HIP BDF kernel (bcm3_likelihood_evaluate_batch_device).
 Everything stays in HBM; no host buffers inside the timed region.
 
-python bench.py --gpus N --steps K --warmup W        (N > 1: launched by torch.distributed.run)
+python bench.py --gpus N --steps K --warmup W
+    N > 1 without a torch.distributed environment: bench.py starts
+    `python -m torch.distributed.run --nproc-per-node N bench.py ...` as a child process (before
+    any GPU call) and exits with its code; under torch.distributed.run WORLD_SIZE must equal N.
+    Default: 256 chains per GPU ("scaling": "weak"; N=1 is C3, N=8 is C5's 2,048 chains).
+    --total-chains C fixes the ladder size over all GPUs instead ("scaling": "strong",
+    SURVEY.md §8(e): C=2048 at 1/2/4/8 GPUs).
 """
 from __future__ import annotations
 
@@ -36,7 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--chains", type=int, default=256, help="tempered chains per GPU")
+    ap.add_argument("--chains", type=int, default=256, help="tempered chains per GPU (weak scaling)")
+    ap.add_argument("--total-chains", type=int, default=0,
+                    help="tempered chains over all GPUs (strong scaling; must divide by the GPU count)")
     ap.add_argument("--lanes-per-wave", type=int, default=0, help="0 = auto")
     ap.add_argument("--proposal", default="gaussian_mixture",
                     help="ptmhsampler.proposal_type: gaussian_mixture (reference default) | global_covariance | "
@@ -54,6 +62,60 @@ def algorithmic_bytes_per_eval(m) -> int:
     vector in, the observations of every patient in, logp out. Output times / doses are shared
     by every lane of a launch and counted once per launch, not per eval."""
     return 8 * m.d + 8 * m.P * m.T + 8
+
+
+def flops_per_eval() -> float:
+    """F_alg: mean FP64 operations of one C3 evaluation, frozen by op-counting the CPU
+    restatement (tests/golden/c3_falg.json, tests/golden/make_falg.py)."""
+    with open(os.path.join(GOLDEN, "c3_falg.json")) as f:
+        return float(json.load(f)["flops_per_eval_mean"])
+
+
+CLOCK_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md)
+
+
+def issue_rate(ll, x_dev, device):
+    """Cycles per BDF step of the slowest trajectory of one launch (the launch lasts as long as its
+    slowest trajectory): the kernel's duration on these proposals times the clock, over that
+    trajectory's step count (solver statistics from a second, detail launch of the same inputs)."""
+    import numpy as np
+    from bcm3_amd import _hip
+    x = x_dev.detach().cpu().numpy()
+    ctx = _hip.Context.from_popk_model(ll.popk_model(), device.index or 0)
+    try:
+        ctx.eval(x)
+        times = []
+        for _ in range(3):
+            ctx.eval(x)
+            times.append(ctx.last_kernel_ms())
+        ms = min(times)
+        st = ctx.eval(x, detail=True)["stats"]
+    finally:
+        ctx.close()
+    nst = st["nst"].reshape(len(x), -1).sum(axis=1)
+    smax = int(nst.max())
+    return {"kernel_ms": ms, "steps_slowest": smax, "steps_mean": float(nst.mean()),
+            "cycles_per_step_slowest": ms * 1e-3 * CLOCK_GHZ * 1e9 / max(1, smax), "clock_ghz": CLOCK_GHZ,
+            "note": "launch time is set by the slowest trajectory; DESIGN.md §7 gives the per-step "
+                    "dependent critical path (~500 cycles) this is compared with"}
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 outside torch.distributed: run this script under torch.distributed.run as a
+    CHILD process (never an exec: nothing here has touched the GPU yet) and return its exit code."""
+    import socket
+    import subprocess
+    import torch
+    have = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if have < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, {have} visible", file=sys.stderr, flush=True)
+        return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd).returncode
 
 
 def traffic_from_profiles(tag: str, n: int):
@@ -120,6 +182,32 @@ def cpu_baseline(budget_s: float, seed: int):
                       f"{cores} threads, {el:.1f} s ({'oracle/_ref/libbcm3ref.so: reference CVODE 5.3.0 sources' if kind == 'reference' else 'oracle/liboracle.so restatement'})"}
 
 
+def p64_cpu_baseline(budget_s: float, seed: int):
+    """The reference CVODE (oracle/_ref) on the P=64 population variant, a thread per host core."""
+    sys.path[:0] = [os.path.join(ROOT, "oracle"), GOLDEN, os.path.join(ROOT, "tests")]
+    import numpy as np
+    import oracle as O
+    import helpers as H
+    kind = "reference"
+    try:
+        orc = O.Oracle("ref")
+    except FileNotFoundError:
+        orc, kind = O.Oracle("restated"), "port"
+    prob = H.c3_problem(64)
+    cores = host_cores()
+    rng = np.random.default_rng(seed)
+    lo = np.array([v.lower for v in prob.variables])
+    hi = np.array([v.upper for v in prob.variables])
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        x = lo + rng.random((cores, prob.d)) * (hi - lo)
+        orc.popk_eval(prob, x, nthreads=cores, want_traj=False, full_patients=False)
+        n += cores
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "log-likelihood evals/sec", "cores": cores, "kind": kind,
+            "sample": f"{n} uniform prior draws of the P=64 problem (64 trajectories each), {cores} threads, {el:.1f} s"}
+
+
 def _rate(ll, n, x, device, reps=3):
     import torch
     from bcm3_amd import _hip
@@ -137,9 +225,10 @@ def _rate(ll, n, x, device, reps=3):
 
 def expm_cpu_baseline(budget_s: float, seed: int):
     """The reference CPU path of the matrix-exponential PK likelihoods: PharmacokineticModel::Solve
-    on the reference's vendored Eigen (oracle/_ref/libexpmref.so, MatrixBase::exp), one thread,
-    timed over the solves of uniform prior draws (the matrix set-up and the observation model, a
-    few % of an evaluation, run untimed in Python)."""
+    on the reference's vendored Eigen (oracle/_ref/libexpmref.so, MatrixBase::exp) over uniform
+    prior draws (the matrix set-up and the observation model, a few % of an evaluation, run
+    untimed in Python): one thread, and the same solves on a thread per host core
+    (eigen_pk_solve_batch, TaskManager's one task per chain)."""
     import ctypes as C
     sys.path[:0] = [os.path.join(ROOT, "oracle"), GOLDEN]
     import json
@@ -172,8 +261,44 @@ def expm_cpu_baseline(budget_s: float, seed: int):
                                    tdb.ctypes.data_as(dp), len(ot), ot.ctypes.data_as(dp), cen.ctypes.data_as(dp))
                 t_solve += time.perf_counter() - t1
             n += 1
-        out[tag] = {"evals_per_s_1thread": n / t_solve, "cores": 1, "kind": "reference",
-                    "sample": f"{n} prior draws, {P} patient solve(s) each, {t_solve:.1f} s of Eigen solves"}
+        # the same draws' solves on every host core at once
+        cores = host_cores()
+        mats, jp, doses, doff, coff = [], [], [], [], []
+        nd = len(v)
+        tot_d = tot_c = 0
+        for e in range(nd):
+            for j, (tt, td, ot) in enumerate(pats):
+                A, _, _, _, ba = X.construct_matrix(m, v[e], j)
+                mats.append(np.asfortranarray(A).ravel(order="F"))
+                jp.append(j)
+                doses.append(td * ba)
+                doff.append(tot_d)
+                coff.append(tot_c)
+                tot_d += len(td)
+                tot_c += len(ot)
+        a_all = np.ascontiguousarray(np.concatenate(mats))
+        jp = np.array(jp, dtype=np.int32)
+        d_all = np.ascontiguousarray(np.concatenate(doses))
+        doff = np.array(doff, dtype=np.int64)
+        coff = np.array(coff, dtype=np.int64)
+        tofs = np.array(toff, dtype=np.int32)
+        oofs = np.array(ooff, dtype=np.int32)
+        tt_all = np.ascontiguousarray(m["treat_times"], dtype=np.float64)
+        ot_all = np.ascontiguousarray(m["obs_times"], dtype=np.float64)
+        cen = np.empty(tot_c)
+        nA = X.construct_matrix(m, v[0], 0)[0].shape[0]
+        reps, t1 = 0, time.perf_counter()
+        while reps < 1 or time.perf_counter() - t1 < 1.0:  # repeat the batch for >= 1 s
+            lib.eigen_pk_solve_batch(cores, len(jp), nA, a_all.ctypes.data, jp.ctypes.data, tofs.ctypes.data,
+                                     tt_all.ctypes.data, d_all.ctypes.data, doff.ctypes.data, oofs.ctypes.data,
+                                     ot_all.ctypes.data, coff.ctypes.data, cen.ctypes.data)
+            reps += 1
+        t_mt = (time.perf_counter() - t1) / reps
+        out[tag] = {"value": nd / t_mt, "unit": "log-likelihood evals/sec", "cores": cores, "kind": "reference",
+                    "evals_per_s_1thread": n / t_solve,
+                    "sample": f"{nd} prior draws x {P} patient solve(s) on {cores} threads, {t_mt:.3f} s per pass "
+                              f"({reps} passes); "
+                              f"1 thread: {n} draws, {t_solve:.1f} s of Eigen solves"}
     return out
 
 
@@ -222,9 +347,17 @@ def expm_workloads(device, gen):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.total_chains and args.total_chains % world:
+        print(f"bench.py: --total-chains {args.total_chains} does not divide over {world} GPUs", file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
@@ -242,7 +375,7 @@ def main():
     if args.lanes_per_wave:
         ll.set_option(_hip.OPT_LANES_PER_WAVE, args.lanes_per_wave)
     m = ll.popk_model()
-    C = args.chains
+    C = args.total_chains // world if args.total_chains else args.chains
     prior = DevicePrior(load_prior(PRIOR_XML), device)
     loop = PTMHDevice(ll, prior, temperature_ladder(C * world), rank=rank, world=world, seed=args.seed,
                       device=device, proposal=args.proposal)
@@ -265,16 +398,24 @@ def main():
     k_total, k_launches, k_max = ll.kernel_time_log()
     ll.set_option(_hip.OPT_TIMING_LOG, 0)
     k_avg = k_total / max(1, k_launches)
+    rank_k_ms = [k_avg]
     if world > 1:
         t = torch.tensor([dt, k_avg], dtype=torch.float64, device=device)
+        allk = [torch.zeros(1, dtype=torch.float64, device=device) for _ in range(world)]
+        dist.all_gather(allk, t[1:2].clone())
+        rank_k_ms = [float(a) for a in allk]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, k_avg = float(t[0]), float(t[1])
+    nan_flag = loop.check_nan() if hasattr(loop, "check_nan") else None
 
     evals = C * world * args.steps * loop.exploration_steps
     value = evals / dt
     b_eval = algorithmic_bytes_per_eval(m)
     achieved_gbs = b_eval * C / (k_avg * 1e-3) / 1e9
     tb = traffic_from_profiles("c3_256", C)
+    f_alg = flops_per_eval()
+    achieved_tf = f_alg * C / (k_avg * 1e-3) / 1e12  # the kernel's own rate, like achieved_gbs
+    issue = issue_rate(ll, loop.prop, device) if rank == 0 else None
 
     extra = {}
     if rank == 0 and args.throughput_batch > 0:
@@ -311,6 +452,8 @@ def main():
             for tag, rec in expm_cpu_baseline(2.0, args.seed).items():
                 if tag in extra:
                     extra[tag]["cpu_baseline"] = rec
+            if "popk_p64_256chains" in extra:
+                extra["popk_p64_256chains"]["cpu_baseline"] = p64_cpu_baseline(6.0, args.seed)
 
     acc_mut = float(loop.accepted_mutate) / max(1, loop.attempted_mutate)
     line = {
@@ -322,16 +465,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.total_chains else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (C3 PopPK data simulated from fixed true parameters; chains start at prior draws)",
         "config": {
             "workload": "PopPK ODE likelihood (pop_pk_trajectory, two-compartment lapatinib, 1 patient x 16 "
-                        "observations, 14 q24h doses, CVODE-BDF rtol 1e-6), 256 tempered chains per GPU; "
-                        "step = one PT-MH iteration (even/odd exchange + mutate with one batched eval)",
+                        f"observations, 14 q24h doses, CVODE-BDF rtol 1e-6), {C * world} tempered chains over "
+                        f"{world} GPU(s) ({C} per GPU); step = one PT-MH iteration (even/odd exchange + "
+                        "mutate with one batched eval)",
+            "config": ("C3" if C * world == 256 and world == 1 else
+                       "C5" if C * world == 2048 else "custom"),
             "chains_per_gpu": C,
             "global_chains": C * world,
+            "kernel_ms_per_rank": rank_k_ms,
             "lanes_per_wave": args.lanes_per_wave or "auto",
             "parallelism": f"chains sharded over {world} rank(s); PT swap = RCCL neighbour send/recv",
             "proposal": args.proposal,
@@ -346,8 +493,17 @@ def main():
             "kernel": "popk_traj_kernel<TWO>",
             "kernel_ms_avg": k_avg,
             "algorithmic_bytes_per_eval": b_eval,
-            "note": "the BDF lane kernel is FP64-VALU latency bound, not HBM bound (DESIGN.md §4)",
+            "achieved_fp64": achieved_tf,
+            "peak_fp64": FP64_VECTOR_PEAK_TFLOPS,
+            "unit_fp64": "TFLOP/s",
+            "frac_fp64": achieved_tf / FP64_VECTOR_PEAK_TFLOPS,
+            "flops_per_eval": f_alg,
+            "issue": issue,
+            "note": "the primary bound is FP64 VALU issue/latency (BASELINE.md §3, DESIGN.md §4): achieved_fp64 = "
+                    "F_alg (op-counted in the CPU restatement, tests/golden/c3_falg.json) x evals per launch / "
+                    "kernel time; the HBM fields follow the bench contract",
         },
+        "nan_llh_detected": nan_flag,
         "cpu_baseline": cpu,
         "kernel_share_of_step": k_avg / (dt / args.steps * 1e3),
         "mutate_acceptance": acc_mut,

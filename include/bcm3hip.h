@@ -233,11 +233,13 @@ int bcm3hip_ptmh_propose(int C, int d, const int32_t* prior_kind, const double* 
                          const double* scale, const double* temps, const double* values, double* prop,
                          double* lprior_prop, int64_t chain0, uint64_t seed, uint64_t iter, void* stream);
 /* TestSample + state update with llh_prop from the likelihood launch (times learning_rate);
- * accept_out[C] (may be NULL), *accepted += number accepted (may be NULL). */
+ * accept_out[C] (may be NULL), *accepted += number accepted (may be NULL). A NaN llh (after the
+ * learning rate) is fatal as in Sampler::EvaluateLikelihood (src/sampler/Sampler.cpp:172-178): the
+ * chain is left unchanged and *nan_llh (may be NULL) is set to 1 for the caller to stop on. */
 int bcm3hip_ptmh_accept(int C, int d, const double* temps, const double* prop, const double* lprior_prop,
                         const double* llh_prop, double learning_rate, double* values, double* lprior, double* llh,
-                        double* lpp, uint8_t* accept_out, uint64_t* accepted, int64_t chain0, uint64_t seed,
-                        uint64_t iter, void* stream);
+                        double* lpp, uint8_t* accept_out, uint64_t* accepted, int32_t* nan_llh, int64_t chain0,
+                        uint64_t seed, uint64_t iter, void* stream);
 /* Exchange round `round` (start = round % 2) for the pairs inside chains [g0, g0+C) of the ladder;
  * wrap_local: also the pair (C-1, 0) (single-rank ladder). acc_mask[C] marks accepted first chains. */
 int bcm3hip_pt_exchange_local(int C, int d, int64_t g0, int start, int wrap_local, const double* temps,
@@ -283,8 +285,8 @@ int bcm3hip_ptmh_propose_adaptive(int C, int d, const int32_t* prior_kind, const
 int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double* prop, const double* lprior_prop,
                                  const double* llh_prop, const double* log_mh, double learning_rate, double* values,
                                  double* lprior, double* llh, double* lpp, uint8_t* accept_out, uint64_t* accepted,
-                                 const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed, uint64_t iter,
-                                 void* stream);
+                                 int32_t* nan_llh, const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed,
+                                 uint64_t iter, void* stream);
 /* SampleHistory::AddSample for chains with T != 0 and (mask == NULL or mask[c] != 0):
  * history[C][H][d] float ring, counters[C][2] = {samples stored, calls since the last store}. */
 int bcm3hip_history_add(int C, int d, int H, int subsampling, const double* temps, const double* values,

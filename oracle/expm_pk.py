@@ -393,6 +393,8 @@ def ref_lib():
         L.eigen_expm.restype = i
         L.eigen_pk_solve.argtypes = [i, vp, i, vp, vp, i, vp, vp]
         L.eigen_pk_solve.restype = i
+        L.eigen_pk_solve_batch.argtypes = [i, i, i, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.eigen_pk_solve_batch.restype = i
         _ref = L
     return _ref
 

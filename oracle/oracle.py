@@ -28,6 +28,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_RESTATED = os.path.join(HERE, "liboracle.so")
 LIB_REF = os.path.join(HERE, "_ref", "libbcm3ref.so")
 LIB_REF_NOFMA = os.path.join(HERE, "_ref", "libbcm3ref_nofma.so")
+LIB_FLOPS = os.path.join(HERE, "libflops.so")  # op-counting build of the restatement (flopcount.hpp)
 
 ST_COUNT = 8
 ST_NAMES = ["nst", "nfe", "nni", "nsetups", "nje", "netf", "ncfn", "nreinit"]
@@ -266,7 +267,7 @@ class Oracle:
     """ctypes front-end for one oracle library (restated or reference-built)."""
 
     def __init__(self, which: str = "restated"):
-        path = {"restated": LIB_RESTATED, "ref": LIB_REF, "ref_nofma": LIB_REF_NOFMA}[which]
+        path = {"restated": LIB_RESTATED, "ref": LIB_REF, "ref_nofma": LIB_REF_NOFMA, "flops": LIB_FLOPS}[which]
         if not os.path.exists(path):
             raise FileNotFoundError(f"oracle library {path} not built (run make -C oracle)")
         self.which = which
@@ -283,6 +284,21 @@ class Oracle:
             getattr(L, fn).restype = C.c_double
         L.orc_transform.argtypes = [C.c_int32, C.c_double]
         L.orc_transform.restype = C.c_double
+        if which == "flops":
+            L.orc_flops_take.restype = C.c_longlong
+
+    def popk_flops(self, prob: PopPKProblem, values: np.ndarray) -> np.ndarray:
+        """FP64 operations of each evaluation (flops build only; SURVEY.md §8(d) counting rule:
+        +, -, *, /, fma, exp, log, pow, sqrt 1 each), one evaluation per call on this thread."""
+        if self.which != "flops":
+            raise ValueError("popk_flops needs Oracle('flops')")
+        values = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, prob.d)
+        out = np.empty(values.shape[0], dtype=np.int64)
+        self.lib.orc_flops_take()
+        for i in range(values.shape[0]):
+            self.popk_eval(prob, values[i:i + 1], nthreads=1, full_patients=False, want_traj=False)
+            out[i] = self.lib.orc_flops_take()
+        return out
 
     def popk_eval(self, prob: PopPKProblem, values: np.ndarray, nthreads: int = 1, full_patients: bool = True,
                   want_traj: bool = True):

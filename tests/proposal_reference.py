@@ -317,7 +317,9 @@ def accept(P, temps, prop, lprior_prop, llh_prop, log_mh, lr, values, lprior, ll
         T = temps[c]
         nl = llh_prop[c] * lr
         nq = lprior_prop[c]
-        if T == 0.0:
+        if math.isnan(nl):  # Sampler.cpp:172-178: fatal; the kernel flags it and keeps the chain
+            a, npp = False, 0.0
+        elif T == 0.0:
             a = True
             npp = nq if nl == -math.inf else nq + T * nl
         else:

@@ -71,7 +71,9 @@ def accept(temps, prop, lprior_prop, llh_prop, lr, values, lprior, llh, lpp, cha
         T = temps[c]
         nl = llh_prop[c] * lr
         nq = lprior_prop[c]
-        if T == 0.0:
+        if math.isnan(nl):  # Sampler.cpp:172-178: fatal; the kernel flags it and keeps the chain
+            a, npp = False, 0.0
+        elif T == 0.0:
             a = True
             npp = nq if nl == -math.inf else nq + T * nl
         else:

@@ -203,3 +203,82 @@ def test_device_sampler_stochastic_schemes(scheme):
     T = s.T
     want = torch.where(T == 0, s.lprior, s.lprior + T * s.llh)
     assert torch.allclose(s.lpp, want, rtol=0, atol=1e-9, equal_nan=True)
+
+
+@pytest.mark.parametrize("adaptive", [False, True])
+def test_accept_flags_nan_llh(adaptive):
+    """Sampler::EvaluateLikelihood (Sampler.cpp:172-178): a NaN log-likelihood is fatal. The accept
+    kernels leave that chain unchanged (T = 0 chains included) and raise the device flag."""
+    from bcm3_amd import _hip
+    from bcm3_amd.pt import temperature_ladder
+    rng = np.random.default_rng(11)
+    C, d = 64, 3
+    temps = np.array(temperature_ladder(C))
+    prop = rng.normal(size=(C, d))
+    lprior_prop = rng.normal(-3, 1, size=C)
+    llh_prop = rng.normal(-50, 3, size=C)
+    llh_prop[[0, 9, 40]] = math.nan  # chain 0 is the T = 0 chain
+    values = rng.normal(size=(C, d))
+    lprior = rng.normal(-3, 1, size=C)
+    llh = rng.normal(-50, 3, size=C)
+    lpp = np.where(temps == 0, lprior, lprior + temps * llh)
+    t = {k: torch.tensor(v, device="cuda") for k, v in dict(temps=temps, prop=prop, lprior_prop=lprior_prop,
+                                                             llh_prop=llh_prop, values=values, lprior=lprior,
+                                                             llh=llh, lpp=lpp).items()}
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    acc = torch.zeros(C, dtype=torch.uint8, device="cuda")
+    ptr = {k: v.data_ptr() for k, v in t.items()}
+    if adaptive:
+        from bcm3_amd.proposal import DeviceProposal
+        from bcm3_amd.sampler import DevicePrior, load_prior
+        prior = DevicePrior(load_prior(os.path.join(H.GOLDEN, "banana_prior.xml"))[:1] * d, "cuda")
+        P = DeviceProposal("gaussian_mixture", prior, t["temps"])
+        P.selected.fill_(0)  # the propose kernel's choice of component (accept updates its EMA)
+        log_mh = torch.zeros(C, dtype=torch.float64, device="cuda")
+        _hip.ptmh_accept_adaptive(C, d, ptr["temps"], ptr["prop"], ptr["lprior_prop"], ptr["llh_prop"],
+                                  log_mh.data_ptr(), 1.0, ptr["values"], ptr["lprior"], ptr["llh"], ptr["lpp"],
+                                  acc.data_ptr(), None, P.struct, 0, 5, 2, nan_llh=flag.data_ptr())
+    else:
+        _hip.ptmh_accept(C, d, ptr["temps"], ptr["prop"], ptr["lprior_prop"], ptr["llh_prop"], 1.0, ptr["values"],
+                         ptr["lprior"], ptr["llh"], ptr["lpp"], acc.data_ptr(), None, 0, 5, 2,
+                         nan_llh=flag.data_ptr())
+    torch.cuda.synchronize()
+    assert int(flag.item()) == 1
+    a = acc.cpu().numpy().astype(bool)
+    for c in (0, 9, 40):
+        assert not a[c]
+        assert np.array_equal(t["values"][c].cpu().numpy(), values[c])
+        assert t["llh"][c].item() == llh[c] and t["lpp"][c].item() == lpp[c]
+    assert a.sum() > 0
+
+
+def test_sampler_stops_on_nan_llh():
+    """A NaN from the likelihood stops PTMHDevice.run, as the reference sampler stops."""
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.pt import temperature_ladder
+    from bcm3_amd.sampler import DevicePrior, PTMHDevice, load_prior
+
+    class NaNAfter:
+        """The circular likelihood, with chain 5's result replaced by NaN from call `k` on."""
+
+        def __init__(self, ll, k):
+            self.ll, self.k, self.calls, self.loop = ll, k, 0, None
+
+        def evaluate_batch_device(self, n, x, out, status, stream):
+            self.ll.evaluate_batch_device(n, x, out, status, stream)
+            self.calls += 1
+            if self.loop is not None and self.calls >= self.k and out == self.loop.llh_prop.data_ptr():
+                self.loop.llh_prop[5] = math.nan
+
+    pri = os.path.join(H.GOLDEN, "circular_prior.xml")
+    ll = NaNAfter(Likelihood(os.path.join(H.GOLDEN, "circular_likelihood.xml"), pri, device=0), 10)
+    prior = DevicePrior(load_prior(pri), "cuda")
+    loop = PTMHDevice(ll, prior, temperature_ladder(16), seed=3, device="cuda")
+    ll.loop = loop
+    loop.nan_check_every = 5
+    with pytest.raises(RuntimeError, match="NaN"):
+        loop.run(50)
+    assert loop.samples_done <= 15
+    # without the NaN the same loop runs through
+    ok = PTMHDevice(ll.ll, prior, temperature_ladder(16), seed=3, device="cuda")
+    ok.run(50)
