@@ -121,6 +121,7 @@ def lib() -> C.CDLL:
     L.bcm3hip_pt_exchange_pair.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, i64, vp, vp, vp, vp, vp, vp, vp,
                                            u64, u64, vp]
     L.bcm3hip_history_add.argtypes = [C.c_int, C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp]
+    L.bcm3hip_gmm_eval.argtypes = [C.c_int, C.c_int, C.c_int, vp, vp, vp, vp, vp, vp, vp, vp]
     L.bcm3hip_kernel_time_log.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(i64), C.POINTER(C.c_double)]
     L.bcm3hip_eval_batch.argtypes = [vp, sz, sz, vp, vp, vp]
     L.bcm3hip_eval_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
@@ -313,3 +314,8 @@ def history_add(C, d, H, subsampling, temps, values, mask, history, counters, st
 
 
 C_byref = C.byref
+
+
+def gmm_eval(n, d, K, x, mean, chol, logc, weights, logpdf, resp, stream=None):
+    """bcm3hip_gmm_eval on device pointers (ints; logpdf / resp may be None)."""
+    check(lib().bcm3hip_gmm_eval(n, d, K, x, mean, chol, logc, weights, logpdf, resp, stream), "gmm_eval")

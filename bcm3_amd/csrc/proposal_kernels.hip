@@ -288,10 +288,11 @@ __device__ __forceinline__ double wave_seq_sum(int n, double x)
     return s;
 }
 
-// responsibilities of the point x (lane i = x_i); lane k of the result = r_k
-__device__ __forceinline__ double wave_responsibilities(int K, int d, double x, const double* mean,
-                                                        const double* chol, const double* logc, const double* w,
-                                                        int lane)
+// responsibilities of the point x (lane i = x_i); lane k of the result = r_k; lsum = the mixture's
+// log-density log sum_k w_k N(x; mean_k, L_k L_k^T) (logsum of GMM::CalculateResponsibilities)
+__device__ __forceinline__ double wave_responsibilities_lsum(int K, int d, double x, const double* mean,
+                                                             const double* chol, const double* logc,
+                                                             const double* w, int lane, double& lsum_out)
 {
     double r = 0.0;
     for (int k = 0; k < K; k++) {
@@ -311,7 +312,36 @@ __device__ __forceinline__ double wave_responsibilities(int K, int d, double x, 
     const double lsum = log(sum) + m;
     const double e = exp(r - lsum);
     const double tot = wave_seq_sum(K, e);
+    lsum_out = lsum;
     return e / tot;
+}
+
+__device__ __forceinline__ double wave_responsibilities(int K, int d, double x, const double* mean,
+                                                        const double* chol, const double* logc, const double* w,
+                                                        int lane)
+{
+    double lsum;
+    return wave_responsibilities_lsum(K, d, x, mean, chol, logc, w, lane, lsum);
+}
+
+// bcm3hip_gmm_eval: the propose kernel's mixture arithmetic (wave_responsibilities_lsum) at n
+// points, one wavefront per point -- the hook that pins the device proposal density to the
+// reference's GMM / dmvnormal golden values (tests/stats/GMM.cpp, tests/stats/mvn.cpp)
+__global__ void __launch_bounds__(64) gmm_eval_wave_kernel(int n, int d, int K, const double* __restrict__ X,
+                                                           const double* __restrict__ mean,
+                                                           const double* __restrict__ chol,
+                                                           const double* __restrict__ logc,
+                                                           const double* __restrict__ w, double* __restrict__ logpdf,
+                                                           double* __restrict__ resp)
+{
+    const int lane = threadIdx.x & 63;
+    const int p = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    if (p >= n) return;
+    const double x = (lane < d) ? X[(int64_t)p * d + lane] : 0.0;
+    double lsum;
+    const double r = wave_responsibilities_lsum(K, d, x, mean, chol, logc, w, lane, lsum);
+    if (resp && lane < K) resp[(int64_t)p * K + lane] = r;
+    if (logpdf && lane == 0) logpdf[p] = lsum;
 }
 
 __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
@@ -566,6 +596,17 @@ int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double
     hipLaunchKernelGGL(ptmh_accept_adaptive_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d,
                        temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values, lprior, llh, lpp, accept_out,
                        (unsigned long long*)accepted, nan_llh, *proposal, chain0, seed, iter);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_gmm_eval(int n, int d, int K, const double* x, const double* mean, const double* chol, const double* logc,
+                     const double* weights, double* logpdf, double* resp, void* stream)
+{
+    if (n < 0 || d <= 0 || d > 64 || K <= 0 || K > 64 || (n > 0 && (!x || !mean || !chol || !logc || !weights)))
+        return BCM3HIP_ERR_ARG;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(gmm_eval_wave_kernel, dim3(n), dim3(64), 0, (hipStream_t)stream, n, d, K, x, mean, chol, logc,
+                       weights, logpdf, resp);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -45,6 +45,10 @@ def lib() -> C.CDLL:
     L.bcm3_likelihood_kernel_time_log.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                                   C.POINTER(C.c_double)]
     L.bcm3_last_error.restype = C.c_char_p
+    i32, i64, u64 = C.c_int, C.c_int64, C.c_uint64
+    L.bcm3_adapt_proposals.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, vp, sz, vp, vp, u64, u64, i64, i32, vp,
+                                       vp, vp, vp, vp, vp]
+    L.bcm3_gmm_eval.argtypes = [i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp]
     _lib = L
     return L
 

@@ -8,20 +8,19 @@ for the device sampler:
   (src/sampler/ProposalGaussianMixture.cpp) with the base Proposal (src/sampler/Proposal.cpp):
   Cholesky factors, log normalisers, adaptive scales and acceptance-rate EMAs per chain;
 * Proposal::Initialize / InitializeImpl (Proposal.cpp:33-140, ProposalGlobalCovariance.cpp:64-104,
-  ProposalGaussianMixture.cpp:125-254) -- the infrequent adaptation step, run here with torch on
-  the device (batched covariance and Cholesky over all chains of the rank);
+  ProposalGaussianMixture.cpp:125-254) -- the infrequent adaptation step, on the host in C++
+  (libbcm3.so bcm3_adapt_proposals, csrc/host/GMM.cpp: history thinning, effective sample size,
+  GMM fits with 1, 2, 3, 4, 5, 8, 13 components by k-means++ + EM, AIC selection), one host thread
+  per core like the reference's per-chain adaptation tasks, then uploaded to HBM;
 * SampleHistory (src/sampler/SampleHistory.cpp) as a per-chain float ring buffer in HBM.
-
-Adaptation of gaussian_mixture fits a single Gaussian component to the history (mean and the
-(n-1)-normalised covariance). The reference fits mixtures with 1-13 components by EM and keeps the
-lowest AIC (ProposalGaussianMixture.cpp:157-189; src/stats/GMM.cpp); that fit is outside the
-hot-path scope. Mixtures fitted elsewhere are loaded with set_mixture().
 """
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _hip
@@ -108,9 +107,11 @@ class DeviceProposal:
         self.logc.copy_(torch.where(m, log_normaliser(self.chol), self.logc))
 
     def _reset_scales(self, chains, initial: bool):
+        """A freshly constructed proposal's scale state: every adaptation builds a new Proposal
+        object (SamplerPTChain::CreateProposalInstance, SamplerPTChain.cpp:428-462)."""
         m = chains.view(-1, 1)
         if self.kind == "gaussian_mixture":
-            # ProposalGaussianMixture::InitializeImpl (:250-251), at every (re)initialisation
+            # ProposalGaussianMixture::InitializeImpl (:250-251)
             s = torch.full_like(self.scale, 2.38 / math.sqrt(self.d))
             e = torch.full_like(self.ema, self.target)
         elif initial:
@@ -118,11 +119,10 @@ class DeviceProposal:
             s = torch.ones_like(self.scale)
             e = torch.full_like(self.ema, 0.23)
         else:
-            return  # ProposalGlobalCovariance keeps its adaptive scale across adaptations
+            return
         self.scale.copy_(torch.where(m, s, self.scale))
         self.ema.copy_(torch.where(m, e, self.ema))
-        # selected_component is set once, in the constructor (ProposalGaussianMixture.cpp:10-14); a
-        # refit keeps it unless it no longer names a component
+        # selected_component = -1 in the constructor (ProposalGaussianMixture.cpp:10-14)
         stale = (self.selected >= self.ncomp) if not initial else torch.ones_like(chains)
         self.selected.copy_(torch.where(chains & stale, torch.full_like(self.selected, -1), self.selected))
 
@@ -153,9 +153,53 @@ class DeviceProposal:
         self.selected[chain] = -1
 
     # ---- Proposal::Initialize from the sample history (AdaptProposal, SamplerPTChain.cpp:120-200)
-    def adapt(self, history: torch.Tensor, counters: torch.Tensor):
+    def adapt(self, history: torch.Tensor, counters: torch.Tensor, seed: int = 0, adaptation: int = 0,
+              chain0: int = 0, max_history_samples: int = 2000, adjusted_aic: bool = False,
+              nthreads: Optional[int] = None):
         """history [C][H][d] float32 ring, counters [C][2] (bcm3hip_history_add). Chains at T == 0
-        are not adapted (SamplerPTChain::AdaptProposal returns early)."""
+        are not adapted (SamplerPTChain::AdaptProposal returns early); every other chain gets a
+        freshly initialised proposal, as AdaptProposal creates a new Proposal object
+        (SamplerPTChain.cpp:143-152, 428-462): fitted state, default scales and EMAs, no selected
+        component. The fit runs in C++ on the host (bcm3_adapt_proposals)."""
+        from .likelihood import lib as host_lib
+        C, H, d = history.shape
+        K = self.kmax
+        hist = np.ascontiguousarray(history.detach().to("cpu").numpy(), dtype=np.float32)
+        counts = np.ascontiguousarray(counters[:, 0].detach().to("cpu").numpy(), dtype=np.int64)
+        active = np.ascontiguousarray((self.temps != 0.0).to("cpu").numpy(), dtype=np.uint8)
+        pm = np.ascontiguousarray(self.prior_mean.to("cpu").numpy(), dtype=np.float64)
+        pv = np.ascontiguousarray(self.prior_var.to("cpu").numpy(), dtype=np.float64)
+        ncomp = np.zeros(C, dtype=np.int32)
+        fitted = np.zeros(C, dtype=np.int32)
+        w = np.zeros((C, K))
+        mu = np.zeros((C, K, d))
+        L = np.zeros((C, K, d, d))
+        lc = np.zeros((C, K))
+        if nthreads is None:
+            nthreads = max(1, min(16, len(os.sched_getaffinity(0))))
+        kind = 1 if self.kind == "gaussian_mixture" else 0
+        rc = host_lib().bcm3_adapt_proposals(kind, int(adjusted_aic), C, H, d, K, hist.ctypes.data, counts.ctypes.data,
+                                             active.ctypes.data, int(max_history_samples), pm.ctypes.data,
+                                             pv.ctypes.data, int(seed) & ((1 << 64) - 1), int(adaptation),
+                                             int(chain0), int(nthreads), ncomp.ctypes.data, w.ctypes.data,
+                                             mu.ctypes.data, L.ctypes.data, lc.ctypes.data, fitted.ctypes.data)
+        if rc != 0:
+            msg = host_lib().bcm3_last_error()
+            raise RuntimeError(f"proposal adaptation failed: {msg.decode() if msg else rc}")
+        dev = self.chol.device
+        act = torch.from_numpy(active.astype(bool)).to(dev)
+        m = act.view(-1, 1)
+        self.ncomp.copy_(torch.where(act, torch.from_numpy(ncomp).to(dev), self.ncomp))
+        self.weights.copy_(torch.where(m, torch.from_numpy(w).to(dev), self.weights))
+        self.mean.copy_(torch.where(m.view(-1, 1, 1), torch.from_numpy(mu).to(dev), self.mean))
+        self.chol.copy_(torch.where(m.view(-1, 1, 1, 1), torch.from_numpy(L).to(dev), self.chol))
+        self.logc.copy_(torch.where(m, torch.from_numpy(lc).to(dev), self.logc))
+        self._reset_scales(act, initial=True)
+        self.last_fitted = fitted
+
+    def adapt_torch_single(self, history: torch.Tensor, counters: torch.Tensor):
+        """Round-1 device-side adaptation (one Gaussian from the history's mean and covariance);
+        kept for comparison only -- adapt() is the reference's algorithm."""
         C, H, d = history.shape
         n = torch.clamp(counters[:, 0], max=H)
         active = self.temps != 0.0

@@ -136,14 +136,23 @@ class PTExchange:
         start = self.round % 2
         C, r = self.C, self.rank
         g0 = r * C
-        dev = self.device
-        acc_mask = torch.zeros(C, dtype=torch.bool, device=dev)
+        acc_mask = torch.zeros(C, dtype=torch.bool, device=self.device)
+        # (Ctot-1, 0) both local
+        wrap_local = self.world == 1 and (self.Ctot - 1 - start) % 2 == 0 and self.Ctot > 1
+        self.local_pairs(values, llh, lprior, lpp, start, wrap_local, acc_mask)
+        if self.world > 1 and (g0 + C - 1 - start) % 2 == 0:
+            self._cross(values, llh, lprior, lpp, acc_mask)
+        self.round += 1
+        return acc_mask
+
+    def local_pairs(self, values, llh, lprior, lpp, start: int, wrap_local: bool, acc_mask=None):
+        """The pairs of this round inside the rank's slice, with tensor ops (the device sampler
+        runs the same decisions in pt_exchange_kernel)."""
+        C, g0, dev = self.C, self.rank * self.C, self.device
+        if acc_mask is None:
+            acc_mask = torch.zeros(C, dtype=torch.bool, device=dev)
         # local pairs: global first index i with i >= g0, i+1 < g0 + C
         loc_first = [i for i in range(C - 1) if (g0 + i - start) % 2 == 0]
-        if self.world == 1 and (self.Ctot - 1 - start) % 2 == 0 and self.Ctot > 1:
-            wrap_local = True  # (Ctot-1, 0) both local
-        else:
-            wrap_local = False
         if loc_first:
             i1 = torch.tensor(loc_first, dtype=torch.int64, device=dev)
             i2 = i1 + 1
@@ -162,9 +171,6 @@ class PTExchange:
             acc_mask[i1] = a
             self.attempted += 1
             self.accepted = self.accepted + a.sum()
-        if self.world > 1 and (g0 + C - 1 - start) % 2 == 0:
-            self._cross(values, llh, lprior, lpp, acc_mask)
-        self.round += 1
         return acc_mask
 
     def step_single(self, values: torch.Tensor, llh: torch.Tensor, lprior: torch.Tensor, lpp: torch.Tensor, ci: int):

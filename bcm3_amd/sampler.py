@@ -191,10 +191,11 @@ class PTMHDevice:
 
     def __init__(self, likelihood, prior: DevicePrior, temperatures, rank=0, world=1, seed=0, device="cuda",
                  learning_rate: float = 1.0, exploration_steps: int = 1, group=None,
-                 proposal: str = "gaussian_mixture", t_dof: float = 0.0, kmax: int = 1,
+                 proposal: str = "gaussian_mixture", t_dof: float = 0.0, kmax: Optional[int] = None,
                  adapt_proposal_samples: int = 2000, adapt_proposal_times: int = 2, max_history_size: int = 2000,
                  use_every_nth: int = 1, swapping_scheme: str = "deterministic_even_odd",
-                 exchange_probability: float = 0.5, initial_position_tries: int = 100):
+                 exchange_probability: float = 0.5, initial_position_tries: int = 100,
+                 adapt_proposal_max_history_samples: int = 2000):
         from . import _hip
         self._hip = _hip
         _hip.lib()  # fails loudly without the HIP library
@@ -237,8 +238,16 @@ class PTMHDevice:
         self.scheme = swapping_scheme
         self.exchange_probability = float(exchange_probability)
         # proposals (ptmhsampler.proposal_type) and the sample history that adapts them
+        # gaussian_mixture_adjustedAIC: the same proposal, selection by adjusted AIC
+        # (SamplerPTChain.cpp:433-436)
+        self.adjusted_aic = proposal == "gaussian_mixture_adjustedAIC"
+        if self.adjusted_aic:
+            proposal = "gaussian_mixture"
         self.proposal_type = proposal
         self.adaptive = proposal != "random_walk"
+        self.max_history_samples = int(adapt_proposal_max_history_samples)
+        if kmax is None:
+            kmax = 13 if proposal == "gaussian_mixture" else 1  # GMM candidates 1..13 components
         self.use_every_nth = int(use_every_nth)
         self.adapt_samples, self.adapt_times = int(adapt_proposal_samples), int(adapt_proposal_times)
         self.adaptations_done = 0
@@ -297,23 +306,19 @@ class PTMHDevice:
 
     def exchange(self):
         """DoExchangeMove round (SamplerPT.cpp:277-298): local pairs on the GPU, boundary pairs
-        over RCCL point-to-point."""
+        over RCCL point-to-point (sharded_exchange_round)."""
         if self.Ctot < 2:
             return
         start = self.round % 2
-        wrap_local = self.world == 1 and (self.Ctot - 1 - start) % 2 == 0
-        self._hip.pt_exchange_local(self.C, self.d, self.g0, start, wrap_local, self.T.data_ptr(),
-                                    self.values.data_ptr(), self.llh.data_ptr(), self.lprior.data_ptr(),
-                                    self.lpp.data_ptr(), None, self.accepted_exchange.data_ptr(), self.seed,
-                                    self.round, self._stream())
-        n_local = sum(1 for i in range(self.C - 1) if (self.g0 + i - start) % 2 == 0) + int(wrap_local)
-        self.attempted_exchange += n_local
-        if self.world > 1 and (self.g0 + self.C - 1 - start) % 2 == 0:
-            acc = torch.zeros(self.C, dtype=torch.bool, device=self.dev)
-            self.ex.round = self.round
-            self.ex._cross(self.values, self.llh, self.lprior, self.lpp, acc)
-            self.accepted_exchange += acc[self.C - 1:].to(torch.int64)
-            self.attempted_exchange += 1
+
+        def local_pairs(start_, wrap_local):
+            self._hip.pt_exchange_local(self.C, self.d, self.g0, start_, wrap_local, self.T.data_ptr(),
+                                        self.values.data_ptr(), self.llh.data_ptr(), self.lprior.data_ptr(),
+                                        self.lpp.data_ptr(), None, self.accepted_exchange.data_ptr(), self.seed,
+                                        self.round, self._stream())
+
+        self.attempted_exchange += sharded_exchange_round(self.ex, local_pairs, self.values, self.llh, self.lprior,
+                                                          self.lpp, self.round, self.accepted_exchange)
         if self.adaptive:
             # ExchangeMove adds the (possibly swapped) state of both chains of a pair to their
             # histories (SamplerPTChain.cpp:374-379)
@@ -418,7 +423,9 @@ class PTMHDevice:
     def adapt_proposal(self):
         """SamplerPTChain::AdaptProposal for every chain of the rank (T == 0 chains excepted)."""
         self.check_nan()
-        self.proposal.adapt(self.history.samples, self.history.counters)
+        self.proposal.adapt(self.history.samples, self.history.counters, seed=self.seed,
+                            adaptation=self.adaptations_done, chain0=self.g0,
+                            max_history_samples=self.max_history_samples, adjusted_aic=self.adjusted_aic)
         # SamplerPTChain::AdaptProposal discards the history it adapted on (SampleHistory::Reset,
         # SamplerPTChain.cpp:174-177 / SampleHistory.cpp:27-31)
         self.history.counters.zero_()
@@ -432,6 +439,30 @@ class PTMHDevice:
             if (si + 1) % self.nan_check_every == 0:
                 self.check_nan()
         self.check_nan()
+
+def sharded_exchange_round(ex: PTExchange, local_pairs, values, llh, lprior, lpp, rnd: int,
+                           accepted: torch.Tensor) -> int:
+    """One even/odd exchange round of a rank's ladder slice (SamplerPT::DoExchangeMove,
+    SamplerPT.cpp:277-298): local_pairs(start, wrap_local) swaps the pairs inside the slice (the
+    HIP kernel in PTMHDevice), then -- on ranks whose last chain starts a pair this round, which
+    with an even slice size is every rank or none -- the two slice-boundary pairs go over
+    point-to-point send/recv with the neighbours (PTExchange._cross; RCCL over xGMI, gloo in the
+    CPU tests). Returns the number of pairs this rank attempted (pairs counted on the rank of
+    their first chain); accepted += the accepted ones of the cross pair."""
+    C, Ctot, world = ex.C, ex.Ctot, ex.world
+    g0 = ex.rank * C
+    start = rnd % 2
+    wrap_local = world == 1 and (Ctot - 1 - start) % 2 == 0
+    local_pairs(start, wrap_local)
+    attempted = sum(1 for i in range(C - 1) if (g0 + i - start) % 2 == 0) + int(wrap_local)
+    if world > 1 and (g0 + C - 1 - start) % 2 == 0:
+        acc = torch.zeros(C, dtype=torch.bool, device=values.device)
+        ex.round = rnd
+        ex._cross(values, llh, lprior, lpp, acc)
+        accepted += acc[C - 1:].to(torch.int64)
+        attempted += 1
+    return attempted
+
 
 def exchange_participants(C: int, g0: int, Ctot: int, world: int, start: int):
     """Chains of the rank owning global chains [g0, g0+C) that are in a pair in an exchange round

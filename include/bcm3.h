@@ -67,6 +67,33 @@ int bcm3_likelihood_set_option(bcm3_likelihood* ll, int option, int64_t value);
 
 const char* bcm3_last_error(void);
 
+/* ---- proposal adaptation (host C++, GMM.cpp) ----
+ * SamplerPTChain::AdaptProposal (src/sampler/SamplerPTChain.cpp:120-178) for the C chains of a rank:
+ * Proposal::Initialize's history thinning to max_history_samples (Proposal.cpp:92-121), then
+ *   BCM3_PROPOSAL_GAUSSIAN_MIXTURE: ProposalGaussianMixture::InitializeImpl
+ *     (ProposalGaussianMixture.cpp:125-254): ESS from autocorrelations, GMM::Fit for 1, 2, 3, 4, 5,
+ *     8, 13 components (k-means++ + EM, src/stats/GMM.cpp:48-158), lowest AIC (adjusted_aic != 0:
+ *     the gaussian_mixture_adjustedAIC selection), else the prior's moments;
+ *   BCM3_PROPOSAL_GLOBAL_COVARIANCE: ProposalGlobalCovariance::InitializeImpl (:64-104).
+ * history[C][H][d] float rings with counts[C] samples stored (bcm3hip_history_add); active[C]
+ * (may be NULL) selects the chains to adapt (T != 0). Outputs per chain, sized for kmax
+ * components (kmax >= 13 for every candidate of the mixture fit): ncomp[C], weights[C][kmax],
+ * means[C][kmax][d], chol[C][kmax][d][d] (lower Cholesky factors, row-major; identity for unused
+ * slots), logc[C][kmax], fitted[C] (may be NULL; 0 = prior fallback). Random numbers: counter
+ * based, keyed by (seed, adaptation, chain0 + c). nthreads host threads. */
+enum { BCM3_PROPOSAL_GLOBAL_COVARIANCE = 0, BCM3_PROPOSAL_GAUSSIAN_MIXTURE = 1 };
+int bcm3_adapt_proposals(int kind, int adjusted_aic, int C, int H, int d, int kmax, const float* history,
+                         const int64_t* counts, const uint8_t* active, size_t max_history_samples,
+                         const double* prior_mean, const double* prior_var, uint64_t seed, uint64_t adaptation,
+                         int64_t chain0, int nthreads, int32_t* ncomp, double* weights, double* means, double* chol,
+                         double* logc, int32_t* fitted);
+/* GMM::Set + LogPdf + CalculateResponsibilities (src/stats/GMM.cpp:14-45, 160-186) of K components
+ * (covariances[K][d][d]) at n points x[n][d]: logpdf[n], resp[n][K], and the Cholesky factors /
+ * log normalisers the device proposal state holds (chol_out[K][d][d], logc_out[K]); any output
+ * may be NULL. */
+int bcm3_gmm_eval(int K, int d, const double* weights, const double* means, const double* covariances, int n,
+                  const double* x, double* logpdf, double* resp, double* chol_out, double* logc_out);
+
 #ifdef __cplusplus
 }
 #endif

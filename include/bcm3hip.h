@@ -287,6 +287,12 @@ int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double
                                  double* lprior, double* llh, double* lpp, uint8_t* accept_out, uint64_t* accepted,
                                  int32_t* nan_llh, const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed,
                                  uint64_t iter, void* stream);
+/* The propose kernel's mixture arithmetic (GMM::CalculateResponsibilities, src/stats/GMM.cpp:172-186,
+ * with the component densities of GMM::LogPdfMVN :392-398) at n points x[n][d] (device buffers,
+ * d <= 64, K <= 64): logpdf[n] = log sum_k w_k N(x; mean_k, L_k L_k^T), resp[n][K]; either may be
+ * NULL. mean[K][d], chol[K][d][d] (lower, row-major), logc[K], weights[K] as in bcm3hip_proposal. */
+int bcm3hip_gmm_eval(int n, int d, int K, const double* x, const double* mean, const double* chol, const double* logc,
+                     const double* weights, double* logpdf, double* resp, void* stream);
 /* SampleHistory::AddSample for chains with T != 0 and (mask == NULL or mask[c] != 0):
  * history[C][H][d] float ring, counters[C][2] = {samples stored, calls since the last store}. */
 int bcm3hip_history_add(int C, int d, int H, int subsampling, const double* temps, const double* values,

@@ -82,40 +82,46 @@ def test_initial_state_from_prior():
 
 
 def test_adapt_from_history():
+    """DeviceProposal.adapt runs the reference's InitializeImpl on the host (bcm3_adapt_proposals,
+    checked in detail by tests/test_gmm.py): stored samples of the ring only, T == 0 untouched,
+    fallback to the prior's moments below two samples, fresh scales / EMAs per adaptation."""
+    import gmm_oracle as G
     from bcm3_amd.proposal import DeviceProposal
     prior = _prior()
     d, C, Hs = prior.d, 4, 50
     temps = torch.tensor([0.0, 0.3, 0.7, 1.0], dtype=torch.float64)
-    P = DeviceProposal("gaussian_mixture", prior, temps)
+    P = DeviceProposal("gaussian_mixture", prior, temps, kmax=13)
     P.scale.fill_(0.5)
     rng = np.random.default_rng(1)
     hist = torch.tensor(rng.normal(size=(C, Hs, d)) * 0.1 + 1.0, dtype=torch.float32)
     counters = torch.tensor([[0, 0], [Hs + 17, 0], [30, 1], [1, 0]], dtype=torch.int64)
     chol0 = P.chol.clone()
-    P.adapt(hist, counters)
+    P.adapt(hist, counters, seed=3, adaptation=0, chain0=0)
     # T == 0 chain untouched
     assert torch.equal(P.chol[0], chol0[0]) and P.scale[0, 0] == 0.5
-    # chains 1, 2: covariance of their stored samples (full ring / first 30), (n-1)-normalised
+    pm, pv = P.prior_mean.numpy(), P.prior_var.numpy()
     for c, n in ((1, Hs), (2, 30)):
-        x = hist[c, :n].double().numpy()
-        cov = np.cov(x, rowvar=False, ddof=1)
+        r = G.CtrRng(3, G.chain_key(c, 0))
+        g, have = G.fit_gaussian_mixture(hist[c, :n].double().numpy(), r, pm, pv)
+        assert int(P.ncomp[c]) == len(g.means)
         L = P.chol[c, 0].numpy()
-        np.testing.assert_allclose(L @ L.T, cov, rtol=1e-10, atol=1e-14)
-        np.testing.assert_allclose(P.mean[c, 0].numpy(), x.mean(axis=0), rtol=1e-12)
+        np.testing.assert_allclose(L @ L.T, g.covs[0], rtol=1e-9, atol=1e-14)
+        np.testing.assert_allclose(P.mean[c, 0].numpy(), g.means[0], rtol=1e-12)
         assert P.scale[c, 0] == 2.38 / math.sqrt(d) and P.ema[c, 0] == P.target
     # chain 3 (one sample) restarts from the prior's moments
-    assert torch.equal(P.chol[3], chol0[3])
-    # global covariance keeps its adaptive scale and floors the diagonal at 1e-6 prior variance
-    G = DeviceProposal("global_covariance", prior, temps)
-    G.scale.fill_(0.7)
+    assert torch.equal(P.chol[3, 0], chol0[3, 0])
+    # global covariance: a fresh Proposal (adaptive scale 1, EMA 0.23) and the diagonal floored at
+    # 1e-6 of the prior variance (ProposalGlobalCovariance.cpp:83-87)
+    Gp = DeviceProposal("global_covariance", prior, temps)
+    Gp.scale.fill_(0.7)
     flat = torch.ones((C, Hs, d), dtype=torch.float32)
     flat[:, ::2, 0] = 2.0
-    G.adapt(flat, torch.tensor([[0, 0], [Hs, 0], [Hs, 0], [Hs, 0]], dtype=torch.int64))
-    L = G.chol[1, 0].numpy()
+    Gp.adapt(flat, torch.tensor([[0, 0], [Hs, 0], [Hs, 0], [Hs, 0]], dtype=torch.int64))
+    L = Gp.chol[1, 0].numpy()
     cov = L @ L.T
     var = ((prior.b - prior.a) ** 2 / 12.0).numpy()
     np.testing.assert_allclose(np.diag(cov)[1:], 1e-6 * var[1:], rtol=1e-12)
-    assert G.scale[1, 0] == 0.7
+    assert Gp.scale[1, 0] == 1.0 and Gp.ema[1, 0] == 0.23 and Gp.scale[0, 0] == 0.7
 
 
 def test_set_mixture_validates():

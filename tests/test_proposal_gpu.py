@@ -253,3 +253,48 @@ def test_prior_all_marginal_types(tmp_path):
             assert abs(np.median(x[:, i]) - 0.8) < 0.08
             continue
         assert abs(x[:, i].mean() - mean[i]) < 5 * sd[i] / math.sqrt(C), (i, x[:, i].mean(), mean[i])
+
+
+def test_device_mixture_density_pinned_to_reference_golden_values():
+    """The propose kernel's mixture arithmetic (wave_responsibilities_lsum, through
+    bcm3hip_gmm_eval) against the reference's own golden values: GMM LogPdf / responsibilities
+    (tests/stats/GMM.cpp:4-31) and dmvnormal (tests/stats/mvn.cpp:17-44), 1e-12 relative. The
+    Cholesky factors and log normalisers come from the host GMM::Set (bcm3_gmm_eval)."""
+    import test_gmm as TG
+    from bcm3_amd import _hip
+    cases = [(TG.GMM_W, TG.GMM_MU, TG.GMM_COV, TG.GMM_X, TG.GMM_LOGPDF, TG.GMM_RESP)]
+    cases += [([1.0], [mu], [sig], x, lp, [1.0]) for mu, sig, x, _, lp in TG.MVN_CASES]
+    for w, mu, cov, x, want_lp, want_r in cases:
+        _, _, L, lc = TG.gmm_eval(w, mu, cov, x)
+        K, d = len(w), len(x)
+        t = {k: torch.tensor(np.asarray(v, dtype=np.float64).ravel(), device="cuda")
+             for k, v in dict(x=x, mean=mu, chol=L, logc=lc, w=w).items()}
+        lp = torch.empty(1, dtype=torch.float64, device="cuda")
+        r = torch.empty(K, dtype=torch.float64, device="cuda")
+        _hip.gmm_eval(1, d, K, t["x"].data_ptr(), t["mean"].data_ptr(), t["chol"].data_ptr(), t["logc"].data_ptr(),
+                      t["w"].data_ptr(), lp.data_ptr(), r.data_ptr())
+        torch.cuda.synchronize()
+        assert abs(lp.item() / want_lp - 1) < 1e-12, (lp.item(), want_lp)
+        np.testing.assert_allclose(r.cpu().numpy(), want_r, rtol=1e-12)
+
+
+def test_circular_ridge_adapts_to_a_mixture():
+    """Config C2 (circular ridge, bimodal): after an adaptation from the device history the
+    gaussian_mixture proposals of the tempered chains hold more than one component
+    (ProposalGaussianMixture::InitializeImpl selecting K > 1 by AIC)."""
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.pt import temperature_ladder
+    from bcm3_amd.sampler import DevicePrior, PTMHDevice, load_prior
+    pri = os.path.join(H.GOLDEN, "circular_prior.xml")
+    ll = Likelihood(os.path.join(H.GOLDEN, "circular_likelihood.xml"), pri, device=0)
+    prior = DevicePrior(load_prior(pri), "cuda")
+    loop = PTMHDevice(ll, prior, temperature_ladder(32), seed=6, device="cuda", adapt_proposal_samples=400,
+                      adapt_proposal_times=1)
+    loop.run(401)
+    torch.cuda.synchronize()
+    assert loop.adaptations_done == 1
+    nc = loop.proposal.ncomp.cpu().numpy()
+    assert nc.max() > 1, nc
+    assert (loop.proposal.selected.cpu().numpy() >= -1).all()
+    acc = int(loop.accepted_mutate.item()) / loop.attempted_mutate
+    assert 0.05 < acc < 0.9

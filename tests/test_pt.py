@@ -216,3 +216,84 @@ def test_single_pair_sharded_gloo_matches_sequential(world, Ctot):
     for r in range(world):
         _compare(chains, log, results[r], r, C)
     assert any(a for pairs in log for ci, _, a in pairs if (ci + 1) % C == 0)  # a cross-rank swap happened
+
+
+# ---- the device sampler's exchange driver (sampler.sharded_exchange_round + exchange_participants),
+# with the pairs inside a slice on PTExchange.local_pairs in place of the HIP kernel
+
+def _run_driver(temps, values, llh, lprior, seed, rounds, rank, world):
+    from bcm3_amd.sampler import exchange_participants, sharded_exchange_round
+    ex = pt.PTExchange(temps, rank=rank, world=world, seed=seed)
+    C, Ctot = ex.C, ex.Ctot
+    g0 = rank * C
+    sl = slice(g0, g0 + C)
+    v = torch.tensor(values[sl]).clone()
+    l = torch.tensor(llh[sl]).clone()
+    q = torch.tensor(lprior[sl]).clone()
+    lpp = ex.lpowerposterior(l, q)
+    accepted = torch.zeros(1, dtype=torch.int64)
+    attempted = 0
+    hist = []
+    for r in range(rounds):
+        def local(start, wrap_local, r=r):
+            ex.round = r
+            a = ex.local_pairs(v, l, q, lpp, start, wrap_local)
+            accepted.add_(a.sum())
+        attempted += sharded_exchange_round(ex, local, v, l, q, lpp, r, accepted)
+        masks = exchange_participants(C, g0, Ctot, world, r % 2)
+        cnt = np.zeros(C, dtype=int)
+        for m in masks:
+            cnt += 1 if m is None else np.array(m, dtype=int)
+        hist.append(cnt)
+    return (v.numpy(), l.numpy(), q.numpy(), lpp.numpy()), attempted, int(accepted.item()), np.array(hist)
+
+
+def _worker_driver(rank, world, port, Ctot, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        temps = pt.temperature_ladder(Ctot)
+        values, llh, lprior = _initial_state(Ctot, 3, 99)
+        q.put((rank, _run_driver(temps, values, llh, lprior, 5, ROUNDS, rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,Ctot", [(1, 8), (2, 8), (4, 16)])
+def test_device_exchange_driver_matches_sequential(world, Ctot):
+    """PTMHDevice.exchange's driver: states bit-identical to the sequential DoExchangeMove replay,
+    attempted / accepted counts per rank (each pair on the rank of its first chain), and the
+    history masks add each chain exactly as often as the reference's ExchangeMove adds it
+    (SamplerPTChain.cpp:374-379: both chains of every pair)."""
+    temps = pt.temperature_ladder(Ctot)
+    values, llh, lprior = _initial_state(Ctot, 3, 99)
+    chains, log = _run_oracle(temps, values, llh, lprior, 5, ROUNDS)
+    if world == 1:
+        results = {0: _run_driver(temps, values, llh, lprior, 5, ROUNDS, 0, 1)}
+    else:
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker_driver, args=(r, world, port, Ctot, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        results = dict(q.get(timeout=120) for _ in range(world))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    C = Ctot // world
+    for r in range(world):
+        state, attempted, accepted, hist = results[r]
+        _compare(chains, [[]] * ROUNDS, (*state, None), r, C)
+        mine = [(ci, a) for pairs in log for ci, _, a in pairs if r * C <= ci < (r + 1) * C]
+        assert attempted == len(mine)
+        assert accepted == sum(a for _, a in mine)
+        for rnd, pairs in enumerate(log):
+            want = np.zeros(C, dtype=int)
+            for ci, ix2, _ in pairs:
+                for g in (ci, ix2):
+                    if r * C <= g < (r + 1) * C:
+                        want[g - r * C] += 1
+            assert np.array_equal(hist[rnd], want), (r, rnd)
