@@ -1,0 +1,157 @@
+// Prior.cpp -- see Prior.h.
+#include "Prior.h"
+
+#include <cmath>
+#include <limits>
+
+#include "../../../include/bcm3hip.h"
+#include "log.h"
+
+namespace bcm3 {
+
+static const double kInf = std::numeric_limits<double>::infinity();
+
+// UnivariateMarginal::Initialize (UnivariateMarginal.cpp:25-101) for one <variable>
+static bool ParseMarginal(const XmlNode& v, Marginal& m)
+{
+    const std::string dist = v.get("distribution");
+    auto f = [&](const char* k) { return v.get_double(k); };
+    if (dist == "uniform") {
+        const double a = f("lower"), b = f("upper");
+        if (b <= a) {
+            LOGERROR("Uniform distribution with upper bound less than or equal to lower bound.");
+            return false;
+        }
+        m.kind = BCM3HIP_PRIOR_UNIFORM;
+        m.p0 = a;
+        m.p1 = b;
+    } else if (dist == "normal") {
+        const double mu = f("mu"), sigma = f("sigma");
+        if (sigma <= 0.0) {
+            LOGERROR("Normal distribution with non-positive sigma.");
+            return false;
+        }
+        m.kind = BCM3HIP_PRIOR_NORMAL;
+        m.p0 = mu;
+        m.p1 = sigma;
+    } else if (dist == "exponential") {
+        m.kind = BCM3HIP_PRIOR_EXPONENTIAL;
+        m.p0 = f("lambda");
+        if (m.p0 <= 0.0) {
+            LOGERROR("Exponential distribution with non-positive lambda.");
+            return false;
+        }
+    } else if (dist == "gamma") {
+        m.kind = BCM3HIP_PRIOR_GAMMA;
+        m.p0 = f("k");
+        m.p1 = f("theta");
+        if (m.p0 <= 0.0 || m.p1 <= 0.0) {
+            LOGERROR("Gamma distribution with non-positive k or theta.");
+            return false;
+        }
+    } else if (dist == "beta") {
+        m.kind = BCM3HIP_PRIOR_BETA;
+        m.p0 = f("a");
+        m.p1 = f("b");
+        if (m.p0 <= 0.0 || m.p1 <= 0.0) {
+            LOGERROR("Beta distribution with non-positive a or b.");
+            return false;
+        }
+    } else if (dist == "half_cauchy") {
+        m.kind = BCM3HIP_PRIOR_HALF_CAUCHY;
+        m.p0 = f("scale");
+        if (m.p0 <= 0.0) {
+            LOGERROR("Half-Cauchy distribution with non-positive scale.");
+            return false;
+        }
+    } else if (dist == "beta_prime") {
+        m.kind = BCM3HIP_PRIOR_BETA_PRIME;
+        m.p0 = f("a");
+        m.p1 = f("b");
+        m.p2 = f("scale");
+    } else if (dist == "exponential_mix") {
+        m.kind = BCM3HIP_PRIOR_EXPONENTIAL_MIX;
+        m.p0 = f("lambda");
+        m.p1 = f("lambda2");
+        m.p2 = f("mix");
+    } else {
+        LOGERROR("Invalid distribution type \"%s\"", dist.c_str());
+        return false;
+    }
+    // GetLowerBound / GetUpperBound (:627-647)
+    switch (m.kind) {
+    case BCM3HIP_PRIOR_UNIFORM: m.lower = m.p0; m.upper = m.p1; break;
+    case BCM3HIP_PRIOR_BETA: m.lower = 0.0; m.upper = 1.0; break;
+    case BCM3HIP_PRIOR_EXPONENTIAL:
+    case BCM3HIP_PRIOR_GAMMA:
+    case BCM3HIP_PRIOR_HALF_CAUCHY:
+    case BCM3HIP_PRIOR_BETA_PRIME: m.lower = 0.0; m.upper = kInf; break;
+    default: m.lower = -kInf; m.upper = kInf; break;
+    }
+    // EvaluateMean / EvaluateVariance (:448-540)
+    const double p0 = m.p0, p1 = m.p1, p2 = m.p2;
+    switch (m.kind) {
+    case BCM3HIP_PRIOR_UNIFORM: {
+        const double d = p1 - p0;
+        m.mean = 0.5 * (p1 + p0);
+        m.var = (d * d) / 12.0;
+        break;
+    }
+    case BCM3HIP_PRIOR_NORMAL: m.mean = p0; m.var = p1 * p1; break;
+    case BCM3HIP_PRIOR_EXPONENTIAL: m.mean = 1.0 / p0; m.var = 1.0 / (p0 * p0); break;
+    case BCM3HIP_PRIOR_GAMMA: m.mean = p0 * p1; m.var = p0 * p1 * p1; break;
+    case BCM3HIP_PRIOR_BETA: {
+        const double apb = p0 + p1;
+        m.mean = p0 / apb;
+        m.var = (p0 * p1) / (apb * apb * (apb + 1));
+        break;
+    }
+    case BCM3HIP_PRIOR_HALF_CAUCHY: m.mean = p0; m.var = p0 * p0; break;
+    case BCM3HIP_PRIOR_BETA_PRIME:
+        m.mean = (p1 > 1.0) ? p2 * p0 / (p1 - 1) : p2;
+        m.var = (p1 > 2.0) ? (p2 * p2 * p0 * (p0 + p1 - 1.0) / ((p1 - 2) * (p1 - 1) * (p1 - 1))) : p2 * p2;
+        break;
+    default:
+        m.mean = p2 / p0 + (1.0 - p2) / p1;
+        m.var = p2 * p2 / (p0 * p0) + (1.0 - p2) * (1.0 - p2) / (p1 * p1);
+        break;
+    }
+    return true;
+}
+
+bool LoadPriorMarginals(const XmlNode& root, std::vector<Marginal>& out)
+{
+    const XmlNode* node = root.child("prior");
+    if (!node) node = root.child("variableset");
+    if (!node) {
+        LOGERROR("Incorrect prior XML format");
+        return false;
+    }
+    out.clear();
+    try {
+        for (auto& var : node->children) {
+            if (var->name != "variable") continue;
+            Marginal m;
+            if (!ParseMarginal(*var, m)) return false;
+            const long repeat = var->get_long("repeat", 1);
+            for (long i = 0; i < repeat; i++) out.push_back(m);
+        }
+    } catch (XmlError& e) {
+        LOGERROR("Error parsing UnivariateMarginal: %s", e.what.c_str());
+        return false;
+    }
+    return true;
+}
+
+bool LoadPriorMarginals(const std::string& prior_xml, std::vector<Marginal>& out)
+{
+    try {
+        auto root = xml_load(prior_xml);
+        return LoadPriorMarginals(*root, out);
+    } catch (XmlError& e) {
+        LOGERROR("Error loading prior file: %s", e.what.c_str());
+        return false;
+    }
+}
+
+}  // namespace bcm3

@@ -1,0 +1,775 @@
+// SamplerPTDevice.cpp -- see SamplerPTDevice.h. The iteration restates SamplerPT::Run
+// (src/sampler/SamplerPT.cpp:174-260) exactly as bcm3_amd/sampler.py's PTMHDevice does, so the
+// two produce the same chains bit for bit (tests/test_ptmh_native_gpu.py).
+#include "SamplerPTDevice.h"
+
+#include <algorithm>
+#include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <limits>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "../../../include/bcm3.h"
+#include "../../../include/bcm3hip.h"
+#include "GMM.h"
+#include "log.h"
+
+namespace bcm3 {
+
+static const double kInf = std::numeric_limits<double>::infinity();
+
+// ---------------------------------------------------------------------------------------------
+// counter-based host uniforms (bcm3_amd/pt.py)
+
+static uint64_t SplitMix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    uint64_t z = x;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+double ExchangeUniform(uint64_t seed, uint64_t rnd, uint64_t pair)
+{
+    const uint64_t z = SplitMix64(SplitMix64(seed) ^ (rnd * 0x100000001B3ull) ^ (pair * 0xC2B2AE3D27D4EB4Full));
+    return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+
+static const uint64_t kMoveSalt = 0x6D6F76655F747970ull;
+static const uint64_t kPairSalt = 0x706169725F696478ull;
+
+static double MoveUniform(uint64_t seed, uint64_t iteration) { return ExchangeUniform(seed ^ kMoveSalt, iteration, 0); }
+
+static int64_t RandomPair(uint64_t seed, uint64_t rnd, int64_t Ctot)
+{
+    // rng.GetUnsignedInt(chains.size() - 2) (SamplerPT.cpp:301)
+    return std::min((int64_t)(ExchangeUniform(seed ^ kPairSalt, rnd, 0) * (double)(Ctot - 1)), Ctot - 2);
+}
+
+std::vector<double> TemperatureLadder(int64_t num_chains, double power, double tmax)
+{
+    // SamplerPT::LoadSettings (SamplerPT.cpp:83-93): T0 = 0, Ti = Tmax (i / (C - 1))^power
+    std::vector<double> t(num_chains, 0.0);
+    for (int64_t i = 1; i < num_chains - 1; i++) t[i] = tmax * std::pow((double)i / (double)(num_chains - 1), power);
+    if (num_chains > 1) t[num_chains - 1] = tmax;
+    return t;
+}
+
+// SamplerPT::Initialize history size / subsampling (SamplerPT.cpp:113-123)
+static void HistoryGeometry(int64_t adapt_samples, int64_t every_nth, int64_t exploration_steps, int64_t Ctot,
+                            int64_t max_history, bool deterministic, int& size, int& sub)
+{
+    int64_t expected = adapt_samples * every_nth;
+    if (Ctot > 1 && deterministic) expected *= exploration_steps + 1;
+    int64_t s = 1, n = expected;
+    if (n > max_history) {
+        s = (expected + max_history - 1) / max_history;
+        n = expected / s;
+    }
+    size = (int)std::max<int64_t>(n, 1);
+    sub = (int)s;
+}
+
+// the chains of this rank in a pair of an exchange round (bcm3_amd.sampler.exchange_participants)
+static std::vector<std::vector<uint8_t>> ExchangeParticipants(int64_t C, int64_t g0, int64_t Ctot, int world, int start,
+                                                              bool& all_once)
+{
+    std::vector<std::vector<uint8_t>> out;
+    all_once = false;
+    if (Ctot < 2) return out;
+    std::vector<uint8_t> local(C, 0), extra(C, 0);
+    for (int64_t i = 0; i + 1 < C; i++)
+        if (((g0 + i - start) % 2 + 2) % 2 == 0) local[i] = local[i + 1] = 1;
+    if (world == 1) {
+        if ((Ctot - 1 - start) % 2 == 0) extra[C - 1] = extra[0] = 1;
+    } else {
+        if (((g0 + C - 1 - start) % 2 + 2) % 2 == 0) extra[C - 1] = 1;
+        if (((((g0 - 1) % Ctot + Ctot) % Ctot - start) % 2 + 2) % 2 == 0) extra[0] = 1;
+    }
+    bool exclusive = true;
+    for (int64_t i = 0; i < C; i++) exclusive &= (local[i] != extra[i]);
+    if (exclusive) {
+        all_once = true;
+        return out;
+    }
+    bool any_local = false, any_extra = false;
+    for (int64_t i = 0; i < C; i++) {
+        any_local |= local[i] != 0;
+        any_extra |= extra[i] != 0;
+    }
+    if (any_local) out.push_back(local);
+    if (any_extra) out.push_back(extra);
+    return out;
+}
+
+// ---------------------------------------------------------------------------------------------
+// transports
+
+namespace {
+
+class RcclTransport : public Transport {
+public:
+    explicit RcclTransport(void* comm) : comm_(comm) {}
+    ~RcclTransport() override { bcm3hip_nccl_comm_destroy(comm_); }
+    bool Exchange(int n_send, const double* const* sends, const int* send_peer, int n_recv, double* const* recvs,
+                  const int* recv_peer, size_t count, void* stream) override
+    {
+        return bcm3hip_nccl_exchange(comm_, n_send, sends, send_peer, n_recv, recvs, recv_peer, count, stream) == 0;
+    }
+
+private:
+    void* comm_;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> MakeRcclTransport(const void* nccl_id, int rank, int world)
+{
+    void* comm = nullptr;
+    if (bcm3hip_nccl_comm_init(nccl_id, rank, world, &comm) != 0) {
+        LOGERROR("ncclCommInitRank failed (rank %d of %d)", rank, world);
+        return nullptr;
+    }
+    return std::unique_ptr<Transport>(new RcclTransport(comm));
+}
+
+class LocalGroup {
+public:
+    explicit LocalGroup(int world) : world(world) {}
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<std::pair<int, int>, std::deque<std::vector<double>>> box;  // (src, dst) -> messages
+};
+
+std::shared_ptr<LocalGroup> MakeLocalGroup(int world) { return std::make_shared<LocalGroup>(world); }
+
+namespace {
+
+class LocalTransport : public Transport {
+public:
+    LocalTransport(std::shared_ptr<LocalGroup> g, int rank) : g_(std::move(g)), rank_(rank) {}
+    bool Exchange(int n_send, const double* const* sends, const int* send_peer, int n_recv, double* const* recvs,
+                  const int* recv_peer, size_t count, void* stream) override
+    {
+        if (bcm3hip_stream_synchronize(stream) != 0) return false;
+        for (int i = 0; i < n_send; i++) {
+            std::vector<double> msg(count);
+            if (bcm3hip_memcpy_async(msg.data(), sends[i], count * sizeof(double), BCM3HIP_D2H, stream) != 0 ||
+                bcm3hip_stream_synchronize(stream) != 0)
+                return false;
+            std::lock_guard<std::mutex> lk(g_->mu);
+            g_->box[{rank_, send_peer[i]}].push_back(std::move(msg));
+            g_->cv.notify_all();
+        }
+        for (int j = 0; j < n_recv; j++) {
+            std::vector<double> msg;
+            {
+                std::unique_lock<std::mutex> lk(g_->mu);
+                auto& q = g_->box[{recv_peer[j], rank_}];
+                if (!g_->cv.wait_for(lk, std::chrono::seconds(120), [&] { return !q.empty(); })) return false;
+                msg = std::move(q.front());
+                q.pop_front();
+            }
+            if (bcm3hip_memcpy_async(recvs[j], msg.data(), count * sizeof(double), BCM3HIP_H2D, stream) != 0 ||
+                bcm3hip_stream_synchronize(stream) != 0)
+                return false;
+        }
+        return true;
+    }
+
+private:
+    std::shared_ptr<LocalGroup> g_;
+    int rank_;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> MakeLocalTransport(std::shared_ptr<LocalGroup> group, int rank)
+{
+    if (!group || rank < 0 || rank >= group->world) return nullptr;
+    return std::unique_ptr<Transport>(new LocalTransport(std::move(group), rank));
+}
+
+// ---------------------------------------------------------------------------------------------
+// device buffers
+
+namespace {
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    bool alloc(size_t count)
+    {
+        n = count;
+        return bcm3hip_malloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T)) == 0;
+    }
+    ~DevBuf() { bcm3hip_free(p); }
+};
+
+template <class T>
+bool Upload(DevBuf<T>& b, const std::vector<T>& h, void* s)
+{
+    return bcm3hip_memcpy_async(b.p, h.data(), h.size() * sizeof(T), BCM3HIP_H2D, s) == 0;
+}
+template <class T>
+bool Download(std::vector<T>& h, const DevBuf<T>& b, void* s)
+{
+    h.resize(b.n);
+    return bcm3hip_memcpy_async(h.data(), b.p, b.n * sizeof(T), BCM3HIP_D2H, s) == 0 && bcm3hip_stream_synchronize(s) == 0;
+}
+
+}  // namespace
+
+struct SamplerPTDevice::Impl {
+    PTMHConfig cfg;
+    std::shared_ptr<Likelihood> ll;
+    std::unique_ptr<Transport> transport;
+    void* stream = nullptr;
+    bool own_stream = false;
+    int64_t C = 0, Ctot = 0, g0 = 0;
+    int d = 0, kmax = 1, H = 1, sub = 1;
+    bool adaptive = true, adjusted = false;
+    int kind = 1;  // BCM3HIP_PROPOSAL_*
+    std::vector<double> temps_host, prior_mean, prior_var;
+    double target = 0.234;
+
+    DevBuf<int32_t> pkind;
+    DevBuf<double> p0, p1, p2, lower, upper, rw_scale, temps, zeros;
+    DevBuf<double> values, prop, lprior, lprior_prop, llh, llh_prop, lpp, log_mh;
+    DevBuf<int32_t> status, nan_flag;
+    DevBuf<uint64_t> acc_mutate, acc_exchange;
+    // proposal state
+    DevBuf<int32_t> ncomp, selected;
+    DevBuf<double> weights, mean, chol, logc, scale, ema, work;
+    bcm3hip_proposal P{};
+    // history
+    DevBuf<float> hist;
+    DevBuf<int64_t> hcount;
+    // exchange masks per start (0 / 1): null = every chain once
+    std::vector<std::unique_ptr<DevBuf<uint8_t>>> masks[2];
+    bool mask_all[2] = {false, false};
+    DevBuf<uint8_t> pair_mask;
+    // boundary records
+    DevBuf<double> send_last, send_first, recv_next, recv_prev;
+
+    PTMHCounters cnt;
+    int64_t iter = 0, round = 0;
+
+    bool Launch(int rc, const char* what)
+    {
+        if (rc != 0) LOGERROR("%s failed: %s (%d)", what, bcm3hip_error_string(rc), rc);
+        return rc == 0;
+    }
+
+    bool Eval(double* x, double* out)
+    {
+        if (!ll->EvaluateLogProbabilityBatchDevice((size_t)C, x, out, status.p, stream)) {
+            LOGERROR("EvaluateLogProbabilityBatchDevice failed");
+            return false;
+        }
+        return true;
+    }
+
+    bool ProposeInit(uint64_t it)
+    {
+        if (adaptive)
+            return Launch(bcm3hip_ptmh_propose_adaptive((int)C, d, pkind.p, p0.p, p1.p, p2.p, zeros.p, values.p, prop.p,
+                                                        lprior_prop.p, log_mh.p, &P, g0, cfg.seed, it, stream),
+                          "ptmh_propose_adaptive");
+        return Launch(bcm3hip_ptmh_propose((int)C, d, pkind.p, p0.p, p1.p, rw_scale.p, zeros.p, values.p, prop.p,
+                                           lprior_prop.p, g0, cfg.seed, it, stream),
+                      "ptmh_propose");
+    }
+
+    // DeviceProposal.reset_from_prior + _reset_scales(initial=True)
+    bool InitProposal()
+    {
+        std::vector<int32_t> nc(C, 1), sel(C, -1);
+        std::vector<double> w(C * kmax, 0.0), mu(C * kmax * d, 0.0), L(C * kmax * d * d, 0.0), lc(C * kmax);
+        double det = 0.0;
+        std::vector<double> sd(d);
+        for (int j = 0; j < d; j++) sd[j] = std::sqrt(prior_var[j]);
+        for (int j = 0; j < d; j++) det += std::log(sd[j]);
+        const double logc_prior = -det - 0.5 * d * std::log(2.0 * M_PI);
+        const double logc_id = -0.0 - 0.5 * d * std::log(2.0 * M_PI);
+        for (int64_t c = 0; c < C; c++) {
+            w[c * kmax] = 1.0;
+            for (int j = 0; j < d; j++) mu[(c * kmax) * d + j] = prior_mean[j];
+            for (int k = 0; k < kmax; k++)
+                for (int j = 0; j < d; j++) L[((c * kmax + k) * d + j) * d + j] = (k == 0) ? sd[j] : 1.0;
+            for (int k = 0; k < kmax; k++) lc[c * kmax + k] = (k == 0) ? logc_prior : logc_id;
+        }
+        const bool gmm = kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE;
+        std::vector<double> sc(C * kmax, gmm ? 2.38 / std::sqrt((double)d) : 1.0);
+        std::vector<double> em(C * kmax, gmm ? target : 0.23);
+        return Upload(ncomp, nc, stream) && Upload(selected, sel, stream) && Upload(weights, w, stream) &&
+               Upload(mean, mu, stream) && Upload(chol, L, stream) && Upload(logc, lc, stream) &&
+               Upload(scale, sc, stream) && Upload(ema, em, stream) &&
+               bcm3hip_memset_async(work.p, 0, work.n * sizeof(double), stream) == 0;
+    }
+
+    bool InitialPositions()
+    {
+        // SamplerPTChain::Initialize / FindStartingPosition (SamplerPTChain.cpp:188-214), as
+        // PTMHDevice._initial_positions: prior draws on counter streams INIT_ITER, INIT_ITER - 1, ...
+        const uint64_t INIT_ITER = (1ull << 63) - 1;
+        std::vector<double> v(C * d, 0.0), q(C, -kInf), l(C, -kInf), pv, pq, pl;
+        std::vector<char> bad(C, 1);
+        bool any = true;
+        for (int k = 0; k < cfg.initial_position_tries && any; k++) {
+            if (!Upload(values, v, stream) || !ProposeInit(INIT_ITER - (uint64_t)k) || !Eval(prop.p, llh_prop.p))
+                return false;
+            if (!Download(pv, prop, stream) || !Download(pq, lprior_prop, stream) || !Download(pl, llh_prop, stream))
+                return false;
+            any = false;
+            for (int64_t c = 0; c < C; c++) {
+                const double nl = pl[c] * cfg.learning_rate;
+                if (std::isnan(nl)) {
+                    LOGERROR("Likelihood evaluation returned NaN while finding starting positions");
+                    return false;
+                }
+                if (bad[c]) {
+                    std::copy(pv.begin() + c * d, pv.begin() + (c + 1) * d, v.begin() + c * d);
+                    q[c] = pq[c];
+                    l[c] = nl;
+                }
+                bad[c] = !(q[c] + temps_host[c] * l[c] > -kInf);
+                any |= bad[c] != 0;
+            }
+        }
+        if (any) {
+            LOGERROR("Could not find starting position with power posterior != inf after %d tries",
+                     cfg.initial_position_tries);
+            return false;
+        }
+        std::vector<double> pp(C);
+        for (int64_t c = 0; c < C; c++) pp[c] = (temps_host[c] == 0.0) ? q[c] : q[c] + temps_host[c] * l[c];
+        return Upload(values, v, stream) && Upload(lprior, q, stream) && Upload(llh, l, stream) &&
+               Upload(lpp, pp, stream);
+    }
+
+    bool HistoryAdd(const uint8_t* mask)
+    {
+        return Launch(bcm3hip_history_add((int)C, d, H, sub, temps.p, values.p, mask, hist.p, hcount.p, stream),
+                      "history_add");
+    }
+
+    bool Mutate()
+    {
+        // DoMutateMove (SamplerPT.cpp:308-319): every chain's proposal in one likelihood launch
+        if (adaptive) {
+            if (!Launch(bcm3hip_ptmh_propose_adaptive((int)C, d, pkind.p, p0.p, p1.p, p2.p, temps.p, values.p, prop.p,
+                                                      lprior_prop.p, log_mh.p, &P, g0, cfg.seed, (uint64_t)iter,
+                                                      stream),
+                        "ptmh_propose_adaptive") ||
+                !Eval(prop.p, llh_prop.p) ||
+                !Launch(bcm3hip_ptmh_accept_adaptive((int)C, d, temps.p, prop.p, lprior_prop.p, llh_prop.p, log_mh.p,
+                                                     cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, nullptr,
+                                                     acc_mutate.p, nan_flag.p, &P, g0, cfg.seed, (uint64_t)iter,
+                                                     stream),
+                        "ptmh_accept_adaptive") ||
+                !HistoryAdd(nullptr))  // SamplerPTChain.cpp:309
+                return false;
+        } else {
+            if (!Launch(bcm3hip_ptmh_propose((int)C, d, pkind.p, p0.p, p1.p, rw_scale.p, temps.p, values.p, prop.p,
+                                             lprior_prop.p, g0, cfg.seed, (uint64_t)iter, stream),
+                        "ptmh_propose") ||
+                !Eval(prop.p, llh_prop.p) ||
+                !Launch(bcm3hip_ptmh_accept((int)C, d, temps.p, prop.p, lprior_prop.p, llh_prop.p, cfg.learning_rate,
+                                            values.p, lprior.p, llh.p, lpp.p, nullptr, acc_mutate.p, nan_flag.p, g0,
+                                            cfg.seed, (uint64_t)iter, stream),
+                        "ptmh_accept"))
+                return false;
+        }
+        cnt.attempted_mutate += C;
+        iter++;
+        return true;
+    }
+
+    // ranks' neighbours on the ring
+    int Next() const { return (cfg.rank + 1) % cfg.world; }
+    int Prev() const { return (cfg.rank - 1 + cfg.world) % cfg.world; }
+
+    bool Cross(bool do_next, bool do_prev, int64_t gp)
+    {
+        const size_t n = (size_t)d + 4;
+        if (!Launch(bcm3hip_pt_pack_boundary((int)C, d, temps.p, values.p, llh.p, lprior.p, lpp.p,
+                                             do_next ? send_last.p : nullptr, do_prev ? send_first.p : nullptr,
+                                             stream),
+                    "pt_pack_boundary"))
+            return false;
+        // PTExchange._cross's order: send(last -> next), recv(prev), send(first -> prev), recv(next)
+        const double* sends[2];
+        int speer[2], rpeer[2], ns = 0, nr = 0;
+        double* recvs[2];
+        if (do_next) {
+            sends[ns] = send_last.p;
+            speer[ns++] = Next();
+        }
+        if (do_prev) {
+            sends[ns] = send_first.p;
+            speer[ns++] = Prev();
+            recvs[nr] = recv_prev.p;
+            rpeer[nr++] = Prev();
+        }
+        if (do_next) {
+            recvs[nr] = recv_next.p;
+            rpeer[nr++] = Next();
+        }
+        if (!transport || !transport->Exchange(ns, sends, speer, nr, recvs, rpeer, n, stream)) {
+            LOGERROR("PT swap transport failed (rank %d)", cfg.rank);
+            return false;
+        }
+        return Launch(bcm3hip_pt_cross_accept((int)C, d, g0, gp, do_next, do_prev, temps.p, values.p, llh.p,
+                                              lprior.p, lpp.p, recv_next.p, recv_prev.p, nullptr,
+                                              do_next ? acc_exchange.p : nullptr, cfg.seed, (uint64_t)round, stream),
+                      "pt_cross_accept");
+    }
+
+    bool Exchange()
+    {
+        // DoExchangeMove (SamplerPT.cpp:277-298): pairs inside the slice on the GPU, the two
+        // slice-boundary pairs over the transport (sampler.sharded_exchange_round)
+        if (Ctot < 2) return true;
+        const int start = (int)(round % 2);
+        const bool wrap_local = cfg.world == 1 && (Ctot - 1 - start) % 2 == 0;
+        if (!Launch(bcm3hip_pt_exchange_local((int)C, d, g0, start, wrap_local ? 1 : 0, temps.p, values.p, llh.p,
+                                              lprior.p, lpp.p, nullptr, acc_exchange.p, cfg.seed, (uint64_t)round,
+                                              stream),
+                    "pt_exchange_local"))
+            return false;
+        int64_t attempted = wrap_local ? 1 : 0;
+        for (int64_t i = 0; i + 1 < C; i++)
+            if (((g0 + i - start) % 2 + 2) % 2 == 0) attempted++;
+        if (cfg.world > 1 && ((g0 + C - 1 - start) % 2 + 2) % 2 == 0) {
+            if (!Cross(true, true, (int64_t)Prev() * C + C - 1)) return false;
+            attempted++;
+        }
+        cnt.attempted_exchange += attempted;
+        if (adaptive) {
+            // ExchangeMove adds both chains of every pair to their histories (SamplerPTChain.cpp:374-379)
+            if (mask_all[start]) {
+                if (!HistoryAdd(nullptr)) return false;
+            } else {
+                for (auto& m : masks[start])
+                    if (!HistoryAdd(m->p)) return false;
+            }
+        }
+        round++;
+        return true;
+    }
+
+    bool ExchangeRandom()
+    {
+        // stochastic_random (SamplerPT.cpp:300-305)
+        const int64_t ci = RandomPair(cfg.seed, (uint64_t)round, Ctot);
+        const int64_t l1 = ci - g0, l2 = ci + 1 - g0;
+        if (0 <= l1 && l2 < C) {
+            if (!Launch(bcm3hip_pt_exchange_pair((int)C, d, (int)l1, (int)l2, ci, temps.p, values.p, llh.p, lprior.p,
+                                                 lpp.p, nullptr, acc_exchange.p, cfg.seed, (uint64_t)round, stream),
+                        "pt_exchange_pair"))
+                return false;
+            cnt.attempted_exchange++;
+        } else if (cfg.world > 1 && (l1 == C - 1 || l2 == 0)) {
+            if (l1 == C - 1) {
+                if (!Cross(true, false, 0)) return false;
+                cnt.attempted_exchange++;
+            } else if (!Cross(false, true, ci)) {
+                return false;
+            }
+        }
+        if (adaptive) {
+            std::vector<uint8_t> m(C, 0);
+            bool any = false;
+            for (int64_t i : {l1, l2})
+                if (0 <= i && i < C) {
+                    m[i] = 1;
+                    any = true;
+                }
+            if (any && (!Upload(pair_mask, m, stream) || !HistoryAdd(pair_mask.p))) return false;
+        }
+        round++;
+        return true;
+    }
+
+    bool IterationOnce(bool last)
+    {
+        // SamplerPT::Run (SamplerPT.cpp:191-248)
+        bool ok;
+        if (Ctot < 2) {
+            ok = Mutate();
+        } else if (cfg.swapping_scheme == 0) {
+            ok = Exchange();
+            for (int s = 0; ok && s < cfg.exploration_steps; s++) ok = Mutate();
+        } else if (MoveUniform(cfg.seed, (uint64_t)cnt.samples_done) < cfg.exchange_probability) {
+            ok = (cfg.swapping_scheme == 1) ? Exchange() : ExchangeRandom();
+        } else {
+            ok = Mutate();
+        }
+        if (!ok) return false;
+        const int64_t si = cnt.samples_done++;
+        cnt.iterations++;
+        if (adaptive && (si + 1) % cfg.use_every_nth == 0) {
+            const int64_t sample_ix = si / cfg.use_every_nth;
+            if (cfg.adapt_proposal_samples > 0 && (sample_ix + 1) % cfg.adapt_proposal_samples == 0 && !last &&
+                cnt.adaptations_done < cfg.adapt_proposal_times)
+                return Adapt();
+        }
+        return true;
+    }
+
+    bool CheckNaN()
+    {
+        std::vector<int32_t> f;
+        if (!Download(f, nan_flag, stream)) return false;
+        if (f[0] != 0) {
+            LOGERROR("Likelihood evaluation returned NaN (Sampler::EvaluateLikelihood, fatal)");
+            return false;
+        }
+        return true;
+    }
+
+    bool Adapt()
+    {
+        // SamplerPTChain::AdaptProposal for every chain of the rank (T == 0 excepted), then the
+        // history reset (SampleHistory::Reset)
+        if (!CheckNaN()) return false;
+        std::vector<float> h;
+        std::vector<int64_t> counts2;
+        if (!Download(h, hist, stream) || !Download(counts2, hcount, stream)) return false;
+        std::vector<int64_t> counts(C);
+        std::vector<uint8_t> active(C);
+        for (int64_t c = 0; c < C; c++) {
+            counts[c] = counts2[2 * c];
+            active[c] = temps_host[c] != 0.0;
+        }
+        std::vector<int32_t> nc(C), fit(C);
+        std::vector<double> w(C * kmax), mu(C * kmax * d), L(C * kmax * d * d), lc(C * kmax);
+        int nthreads = cfg.host_threads > 0 ? cfg.host_threads
+                                            : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+        if (bcm3_adapt_proposals(kind, adjusted ? 1 : 0, (int)C, H, d, kmax, h.data(), counts.data(), active.data(),
+                                 (size_t)cfg.adapt_proposal_max_history_samples, prior_mean.data(), prior_var.data(),
+                                 cfg.seed, (uint64_t)cnt.adaptations_done, g0, nthreads, nc.data(), w.data(),
+                                 mu.data(), L.data(), lc.data(), fit.data()) != 0)
+            return false;
+        // merge into the device state: adapted chains get the fit and a fresh proposal's scales
+        std::vector<int32_t> dnc, dsel;
+        std::vector<double> dw, dmu, dL, dlc, dsc, dem;
+        if (!Download(dnc, ncomp, stream) || !Download(dsel, selected, stream) || !Download(dw, weights, stream) ||
+            !Download(dmu, mean, stream) || !Download(dL, chol, stream) || !Download(dlc, logc, stream) ||
+            !Download(dsc, scale, stream) || !Download(dem, ema, stream))
+            return false;
+        const bool gmm = kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE;
+        const double s0 = gmm ? 2.38 / std::sqrt((double)d) : 1.0, e0 = gmm ? target : 0.23;
+        for (int64_t c = 0; c < C; c++) {
+            if (!active[c]) continue;
+            dnc[c] = nc[c];
+            dsel[c] = -1;
+            std::copy(w.begin() + c * kmax, w.begin() + (c + 1) * kmax, dw.begin() + c * kmax);
+            std::copy(mu.begin() + c * kmax * d, mu.begin() + (c + 1) * kmax * d, dmu.begin() + c * kmax * d);
+            std::copy(L.begin() + c * kmax * d * d, L.begin() + (c + 1) * kmax * d * d, dL.begin() + c * kmax * d * d);
+            std::copy(lc.begin() + c * kmax, lc.begin() + (c + 1) * kmax, dlc.begin() + c * kmax);
+            std::fill(dsc.begin() + c * kmax, dsc.begin() + (c + 1) * kmax, s0);
+            std::fill(dem.begin() + c * kmax, dem.begin() + (c + 1) * kmax, e0);
+        }
+        if (!Upload(ncomp, dnc, stream) || !Upload(selected, dsel, stream) || !Upload(weights, dw, stream) ||
+            !Upload(mean, dmu, stream) || !Upload(chol, dL, stream) || !Upload(logc, dlc, stream) ||
+            !Upload(scale, dsc, stream) || !Upload(ema, dem, stream) ||
+            bcm3hip_memset_async(hcount.p, 0, hcount.n * sizeof(int64_t), stream) != 0)
+            return false;
+        cnt.adaptations_done++;
+        return bcm3hip_stream_synchronize(stream) == 0;
+    }
+};
+
+SamplerPTDevice::SamplerPTDevice() : p_(new Impl) {}
+
+SamplerPTDevice::~SamplerPTDevice()
+{
+    if (p_ && p_->stream) bcm3hip_stream_synchronize(p_->stream);
+    if (p_ && p_->own_stream) bcm3hip_stream_destroy(p_->stream);
+}
+
+bool SamplerPTDevice::Initialize(std::shared_ptr<Likelihood> ll, const std::vector<Marginal>& prior,
+                                 const PTMHConfig& cfg, std::unique_ptr<Transport> transport, void* stream)
+{
+    Impl& s = *p_;
+    s.cfg = cfg;
+    s.ll = std::move(ll);
+    s.transport = std::move(transport);
+    s.d = (int)prior.size();
+    s.Ctot = cfg.num_chains;
+    if (!s.ll || s.d == 0 || s.Ctot < 1 || cfg.world < 1 || cfg.rank < 0 || cfg.rank >= cfg.world ||
+        s.Ctot % cfg.world != 0 || s.ll->GetNumVariables() != (size_t)s.d) {
+        LOGERROR("SamplerPTDevice: inconsistent configuration (chains %lld, ranks %d, variables %d / %zu)",
+                 (long long)s.Ctot, cfg.world, s.d, s.ll ? s.ll->GetNumVariables() : (size_t)0);
+        return false;
+    }
+    s.C = s.Ctot / cfg.world;
+    if (cfg.world > 1 && (s.C % 2 != 0 || !s.transport)) {
+        LOGERROR("SamplerPTDevice: a sharded ladder needs an even number of chains per rank and a transport");
+        return false;
+    }
+    s.g0 = cfg.rank * s.C;
+    C_ = s.C;
+    d_ = s.d;
+    if (cfg.proposal < 0 || cfg.proposal > 3 || cfg.swapping_scheme < 0 || cfg.swapping_scheme > 2) {
+        LOGERROR("SamplerPTDevice: unknown proposal type or swapping scheme");
+        return false;
+    }
+    s.adaptive = cfg.proposal != 3;
+    s.adjusted = cfg.proposal == 2;
+    s.kind = (cfg.proposal == 0) ? BCM3HIP_PROPOSAL_GLOBAL_COVARIANCE : BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE;
+    s.kmax = cfg.kmax > 0 ? cfg.kmax : (s.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE ? 13 : 1);
+    if (s.kind == BCM3HIP_PROPOSAL_GLOBAL_COVARIANCE) s.kmax = 1;
+    if (s.kmax > BCM3HIP_PROPOSAL_KMAX) return false;
+    if (!s.adaptive) {
+        for (auto& m : prior)
+            if (m.kind != BCM3HIP_PRIOR_UNIFORM && m.kind != BCM3HIP_PRIOR_NORMAL) {
+                LOGERROR("the random-walk proposal kernel supports uniform and normal priors only");
+                return false;
+            }
+    }
+    // Proposal::Initialize (Proposal.cpp:45-53)
+    s.target = (s.d == 1) ? 0.44 : (s.d == 2) ? 0.35 : (s.d == 3) ? 0.3 : 0.234;
+    const auto ladder = TemperatureLadder(s.Ctot, cfg.temperature_power, cfg.temperature_max);
+    s.temps_host.assign(ladder.begin() + s.g0, ladder.begin() + s.g0 + s.C);
+
+    if (stream) {
+        s.stream = stream;
+    } else {
+        if (bcm3hip_stream_create(&s.stream) != 0) return false;
+        s.own_stream = true;
+    }
+    stream_ = s.stream;
+    const int64_t C = s.C, d = s.d, K = s.kmax;
+    HistoryGeometry(cfg.adapt_proposal_samples, cfg.use_every_nth, cfg.exploration_steps, s.Ctot,
+                    cfg.max_history_size, cfg.swapping_scheme == 0, s.H, s.sub);
+    bool ok = s.pkind.alloc(d) && s.p0.alloc(d) && s.p1.alloc(d) && s.p2.alloc(d) && s.lower.alloc(d) &&
+              s.upper.alloc(d) && s.rw_scale.alloc(d) && s.temps.alloc(C) && s.zeros.alloc(C) &&
+              s.values.alloc(C * d) && s.prop.alloc(C * d) && s.lprior.alloc(C) && s.lprior_prop.alloc(C) &&
+              s.llh.alloc(C) && s.llh_prop.alloc(C) && s.lpp.alloc(C) && s.log_mh.alloc(C) && s.status.alloc(C) &&
+              s.nan_flag.alloc(1) && s.acc_mutate.alloc(1) && s.acc_exchange.alloc(1) && s.ncomp.alloc(C) &&
+              s.selected.alloc(C) && s.weights.alloc(C * K) && s.mean.alloc(C * K * d) &&
+              s.chol.alloc(C * K * d * d) && s.logc.alloc(C * K) && s.scale.alloc(C * K) && s.ema.alloc(C * K) &&
+              s.work.alloc(C * (2 * K + 2 * d)) && s.hist.alloc(C * (int64_t)s.H * d) && s.hcount.alloc(2 * C) &&
+              s.pair_mask.alloc(C) && s.send_last.alloc(d + 4) && s.send_first.alloc(d + 4) &&
+              s.recv_next.alloc(d + 4) && s.recv_prev.alloc(d + 4);
+    if (!ok) {
+        LOGERROR("SamplerPTDevice: device allocation failed");
+        return false;
+    }
+    std::vector<int32_t> kinds(d);
+    std::vector<double> a0(d), a1(d), a2(d), lo(d), hi(d), rw(d);
+    s.prior_mean.resize(d);
+    s.prior_var.resize(d);
+    for (int j = 0; j < d; j++) {
+        kinds[j] = prior[j].kind;
+        a0[j] = prior[j].p0;
+        a1[j] = prior[j].p1;
+        a2[j] = prior[j].p2;
+        lo[j] = prior[j].lower;
+        hi[j] = prior[j].upper;
+        s.prior_mean[j] = prior[j].mean;
+        s.prior_var[j] = prior[j].var;
+        rw[j] = 0.05 * std::sqrt(prior[j].var);  // DevicePrior.scale
+    }
+    ok = Upload(s.pkind, kinds, s.stream) && Upload(s.p0, a0, s.stream) && Upload(s.p1, a1, s.stream) &&
+         Upload(s.p2, a2, s.stream) && Upload(s.lower, lo, s.stream) && Upload(s.upper, hi, s.stream) &&
+         Upload(s.rw_scale, rw, s.stream) && Upload(s.temps, s.temps_host, s.stream) &&
+         bcm3hip_memset_async(s.zeros.p, 0, C * sizeof(double), s.stream) == 0 &&
+         bcm3hip_memset_async(s.log_mh.p, 0, C * sizeof(double), s.stream) == 0 &&
+         bcm3hip_memset_async(s.nan_flag.p, 0, sizeof(int32_t), s.stream) == 0 &&
+         bcm3hip_memset_async(s.acc_mutate.p, 0, sizeof(uint64_t), s.stream) == 0 &&
+         bcm3hip_memset_async(s.acc_exchange.p, 0, sizeof(uint64_t), s.stream) == 0 &&
+         bcm3hip_memset_async(s.hist.p, 0, s.hist.n * sizeof(float), s.stream) == 0 &&
+         bcm3hip_memset_async(s.hcount.p, 0, s.hcount.n * sizeof(int64_t), s.stream) == 0;
+    if (!ok) return false;
+    s.P.kind = s.kind;
+    s.P.kmax = (int32_t)K;
+    s.P.t_dof = cfg.t_dof;
+    s.P.target_acceptance = s.target;
+    s.P.scaling_learning_rate = 0.05;
+    s.P.scaling_ema_period = 1000.0;
+    s.P.lower = s.lower.p;
+    s.P.upper = s.upper.p;
+    s.P.ncomp = s.ncomp.p;
+    s.P.weights = s.weights.p;
+    s.P.mean = s.mean.p;
+    s.P.chol = s.chol.p;
+    s.P.logc = s.logc.p;
+    s.P.scale = s.scale.p;
+    s.P.ema = s.ema.p;
+    s.P.selected = s.selected.p;
+    s.P.work = s.work.p;
+    if (!s.InitProposal()) return false;
+    for (int start = 0; start < 2; start++) {
+        auto m = ExchangeParticipants(C, s.g0, s.Ctot, cfg.world, start, s.mask_all[start]);
+        for (auto& v : m) {
+            s.masks[start].emplace_back(new DevBuf<uint8_t>());
+            if (!s.masks[start].back()->alloc(C) || !Upload(*s.masks[start].back(), v, s.stream)) return false;
+        }
+    }
+    return s.InitialPositions() && bcm3hip_stream_synchronize(s.stream) == 0;
+}
+
+bool SamplerPTDevice::Iterate(int64_t n, bool last_at_end)
+{
+    for (int64_t i = 0; i < n; i++)
+        if (!p_->IterationOnce(last_at_end && i + 1 == n)) return false;
+    return true;
+}
+
+bool SamplerPTDevice::Run(int64_t num_samples)
+{
+    const int64_t total = num_samples * p_->cfg.use_every_nth;
+    for (int64_t si = 0; si < total; si++) {
+        if (!p_->IterationOnce(si + 1 == total)) return false;
+        if (p_->cfg.nan_check_every > 0 && (si + 1) % p_->cfg.nan_check_every == 0 && !p_->CheckNaN()) return false;
+    }
+    return p_->CheckNaN();
+}
+
+bool SamplerPTDevice::AdaptProposal() { return p_->Adapt(); }
+bool SamplerPTDevice::CheckNaN() { return p_->CheckNaN(); }
+bool SamplerPTDevice::Synchronize() { return bcm3hip_stream_synchronize(p_->stream) == 0; }
+
+bool SamplerPTDevice::GetState(double* values, double* llh, double* lprior, double* lpp)
+{
+    Impl& s = *p_;
+    auto get = [&](double* out, const DevBuf<double>& b) {
+        return !out || bcm3hip_memcpy_async(out, b.p, b.n * sizeof(double), BCM3HIP_D2H, s.stream) == 0;
+    };
+    return get(values, s.values) && get(llh, s.llh) && get(lprior, s.lprior) && get(lpp, s.lpp) &&
+           bcm3hip_stream_synchronize(s.stream) == 0;
+}
+
+bool SamplerPTDevice::GetProposalComponents(int32_t* nc)
+{
+    return nc && bcm3hip_memcpy_async(nc, p_->ncomp.p, p_->C * sizeof(int32_t), BCM3HIP_D2H, p_->stream) == 0 &&
+           bcm3hip_stream_synchronize(p_->stream) == 0;
+}
+
+PTMHCounters SamplerPTDevice::GetCounters()
+{
+    Impl& s = *p_;
+    PTMHCounters c = s.cnt;
+    uint64_t a = 0, b = 0;
+    if (bcm3hip_memcpy_async(&a, s.acc_mutate.p, sizeof(a), BCM3HIP_D2H, s.stream) == 0 &&
+        bcm3hip_memcpy_async(&b, s.acc_exchange.p, sizeof(b), BCM3HIP_D2H, s.stream) == 0 &&
+        bcm3hip_stream_synchronize(s.stream) == 0) {
+        c.accepted_mutate = (int64_t)a;
+        c.accepted_exchange = (int64_t)b;
+    }
+    c.rounds = s.round;
+    return c;
+}
+
+}  // namespace bcm3

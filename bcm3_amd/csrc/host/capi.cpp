@@ -8,10 +8,7 @@
 #include "LikelihoodGPU.h"
 #include "log.h"
 
-struct bcm3_likelihood {
-    std::shared_ptr<bcm3::VariableSet> varset;
-    std::shared_ptr<bcm3::Likelihood> ll;
-};
+#include "capi_internal.h"
 
 extern "C" {
 

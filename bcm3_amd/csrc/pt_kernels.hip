@@ -170,6 +170,75 @@ __global__ void pt_exchange_pair_kernel(int d, int i1, int i2, int64_t g1, const
     if (acc_out) *acc_out = a ? 1 : 0;
 }
 
+// the record a rank sends for a slice-boundary pair: {values[d], llh, lprior, lpp, T}
+__global__ void pt_pack_boundary_kernel(int C, int d, const double* temps, const double* values, const double* llh,
+                                        const double* lprior, const double* lpp, double* send_last,
+                                        double* send_first)
+{
+    const int k = threadIdx.x;
+    for (int side = 0; side < 2; side++) {
+        const int i = side ? 0 : C - 1;
+        double* out = side ? send_first : send_last;
+        if (!out) continue;
+        if (k < d) out[k] = values[(int64_t)i * d + k];
+        if (k == 0) {
+            out[d] = llh[i];
+            out[d + 1] = lprior[i];
+            out[d + 2] = lpp[i];
+            out[d + 3] = temps[i];
+        }
+    }
+}
+
+// ExchangeMove of a pair whose chains live on two ranks (SamplerPTChain.cpp:328-381): both ranks
+// evaluate the same decision from the same two records (exchange_pair's arithmetic, uniform keyed
+// by the global index of the pair's first chain) and keep their own side.
+//   pair A (do_next): (my last chain C-1, the next rank's first chain = record nxt), first = g0+C-1
+//   pair B (do_prev): (the previous rank's last chain = record prv, my first chain 0), first = gp
+__global__ void pt_cross_accept_kernel(int C, int d, int64_t g0, int64_t gp, int do_next, int do_prev,
+                                       const double* temps, double* values, double* llh, double* lprior, double* lpp,
+                                       const double* nxt, const double* prv, uint8_t* acc_out,
+                                       unsigned long long* accepted, uint64_t seed, uint64_t round)
+{
+    if (threadIdx.x != 0) return;
+    if (do_next) {
+        const int i = C - 1;
+        const double t1 = temps[i], t2 = nxt[d + 3];
+        const double p1 = (t1 == 0.0) ? nxt[d + 1] : t1 * nxt[d] + nxt[d + 1];
+        const double p2 = (t2 == 0.0) ? lprior[i] : t2 * llh[i] + lprior[i];
+        double tp = exp((p1 + p2) - (lpp[i] + nxt[d + 2]));
+        tp = (tp < 1.0) ? tp : 1.0;
+        const uint64_t key = splitmix64(splitmix64(seed) ^ (round * 0x100000001B3ull) ^
+                                        ((uint64_t)(g0 + C - 1) * 0xC2B2AE3D27D4EB4Full));
+        const bool a = u01(key) < tp;
+        if (a) {
+            for (int k = 0; k < d; k++) values[(int64_t)i * d + k] = nxt[k];
+            llh[i] = nxt[d];
+            lprior[i] = nxt[d + 1];
+            lpp[i] = p1;
+            if (accepted) atomicAdd(accepted, 1ull);
+        }
+        if (acc_out) acc_out[0] = a ? 1 : 0;
+    }
+    if (do_prev) {
+        const double t1 = prv[d + 3], t2 = temps[0];
+        const double p1 = (t1 == 0.0) ? lprior[0] : t1 * llh[0] + lprior[0];
+        const double p2 = (t2 == 0.0) ? prv[d + 1] : t2 * prv[d] + prv[d + 1];
+        double tp = exp((p1 + p2) - (prv[d + 2] + lpp[0]));
+        tp = (tp < 1.0) ? tp : 1.0;
+        const uint64_t key = splitmix64(splitmix64(seed) ^ (round * 0x100000001B3ull) ^
+                                        ((uint64_t)gp * 0xC2B2AE3D27D4EB4Full));
+        const bool b = u01(key) < tp;
+        if (b) {
+            for (int k = 0; k < d; k++) values[k] = prv[k];
+            llh[0] = prv[d];
+            lprior[0] = prv[d + 1];
+            lpp[0] = p2;
+        }
+        if (acc_out) acc_out[1] = b ? 1 : 0;
+    }
+}
+
 }  // namespace
 }  // namespace bcm3hip
 
@@ -202,6 +271,30 @@ int bcm3hip_ptmh_accept(int C, int d, const double* temps, const double* prop, c
     hipLaunchKernelGGL(ptmh_accept_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d, temps, prop,
                        lprior_prop, llh_prop, learning_rate, values, lprior, llh, lpp, accept_out,
                        (unsigned long long*)accepted, nan_llh, chain0, seed, iter);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_pt_pack_boundary(int C, int d, const double* temps, const double* values, const double* llh,
+                             const double* lprior, const double* lpp, double* send_last, double* send_first,
+                             void* stream)
+{
+    if (C < 1 || d <= 0 || d > 1024 || !temps || !values || !llh || !lprior || !lpp) return BCM3HIP_ERR_ARG;
+    hipLaunchKernelGGL(pt_pack_boundary_kernel, dim3(1), dim3(d < 64 ? 64 : ((d + 63) / 64) * 64), 0,
+                       (hipStream_t)stream, C, d, temps, values, llh, lprior, lpp, send_last, send_first);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_pt_cross_accept(int C, int d, int64_t g0, int64_t gp, int do_next, int do_prev, const double* temps,
+                            double* values, double* llh, double* lprior, double* lpp, const double* recv_next,
+                            const double* recv_prev, uint8_t* acc_out, uint64_t* accepted, uint64_t seed,
+                            uint64_t round, void* stream)
+{
+    if (C < 1 || d <= 0 || !temps || !values || !llh || !lprior || !lpp || (do_next && !recv_next) ||
+        (do_prev && !recv_prev))
+        return BCM3HIP_ERR_ARG;
+    hipLaunchKernelGGL(pt_cross_accept_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, C, d, g0, gp, do_next,
+                       do_prev, temps, values, llh, lprior, lpp, recv_next, recv_prev, acc_out,
+                       (unsigned long long*)accepted, seed, round);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -35,10 +35,22 @@ def target_acceptance_rate(d: int) -> float:
 
 def log_normaliser(chol: torch.Tensor) -> torch.Tensor:
     """-sum_j log L_jj - d/2 log(2 pi) over the last two dims (ProposalGlobalCovariance.cpp:96-101,
-    GMM::Set)."""
+    GMM::Set), summed in j order on the host with the C library's log -- the arithmetic of the C++
+    host code (csrc/host/GMM.cpp, SamplerPTDevice.cpp), so both samplers start from the same bits."""
     d = chol.shape[-1]
-    det = torch.log(torch.diagonal(chol, dim1=-2, dim2=-1)).sum(dim=-1)
-    return -det - 0.5 * d * math.log(2.0 * math.pi)
+    diag = torch.diagonal(chol, dim1=-2, dim2=-1).detach().to("cpu").numpy().reshape(-1, d)
+    c2 = 0.5 * d * math.log(2.0 * math.pi)
+    cache = {}
+    out = np.empty(len(diag))
+    for i, row in enumerate(diag):
+        key = row.tobytes()
+        if key not in cache:
+            det = 0.0
+            for v in row.tolist():
+                det += math.log(v)
+            cache[key] = -det - c2
+        out[i] = cache[key]
+    return torch.tensor(out.reshape(chol.shape[:-2]), dtype=torch.float64, device=chol.device)
 
 
 class DeviceProposal:

@@ -50,6 +50,8 @@ def parse():
                     help="ptmhsampler.proposal_type: gaussian_mixture (reference default) | global_covariance | "
                          "random_walk")
     ap.add_argument("--seed", type=int, default=20251016)
+    ap.add_argument("--loop", default="native", choices=("native", "python"),
+                    help="native: the C++ sampler (bcm3_ptmh_*); python: bcm3_amd.sampler.PTMHDevice")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--throughput-batch", type=int, default=16384,
                     help="extra: evals/s of one large batch (0 = skip); not the headline value")
@@ -98,6 +100,61 @@ def issue_rate(ll, x_dev, device):
             "cycles_per_step_slowest": ms * 1e-3 * CLOCK_GHZ * 1e9 / max(1, smax), "clock_ghz": CLOCK_GHZ,
             "note": "launch time is set by the slowest trajectory; DESIGN.md §7 gives the per-step "
                     "dependent critical path (~500 cycles) this is compared with"}
+
+
+class NativeLoop:
+    """The C++ sampler (libbcm3.so bcm3_ptmh_*): the timed iterations run without Python; the PT
+    swap between ranks goes over RCCL (unique id broadcast over torch.distributed)."""
+
+    def __init__(self, ll, num_chains, rank, world, args, dist):
+        from bcm3_amd.ptmh import TRANSPORT_RCCL, PTMHNative, nccl_unique_id
+        kw = {}
+        if world > 1:
+            obj = [nccl_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            kw = dict(transport=TRANSPORT_RCCL, nccl_id=obj[0])
+        self.s = PTMHNative(ll, PRIOR_XML, num_chains, rank=rank, world=world, seed=args.seed,
+                            proposal=args.proposal, **kw)
+        self.exploration_steps = 1
+
+    def run(self, n):
+        if n > 0:
+            self.s.iterate(n)
+
+    def sync(self):
+        self.s.synchronize()
+
+    def acceptance(self):
+        c = self.s.counters()
+        return c["accepted_mutate"] / max(1, c["attempted_mutate"])
+
+    def values(self):
+        import torch
+        return torch.tensor(self.s.state()["values"])
+
+
+class PythonLoop:
+    """bcm3_amd.sampler.PTMHDevice (the same iteration written in Python over the same kernels)."""
+
+    def __init__(self, ll, num_chains, rank, world, args, device):
+        from bcm3_amd.pt import temperature_ladder
+        from bcm3_amd.sampler import DevicePrior, PTMHDevice, load_prior
+        self.loop = PTMHDevice(ll, DevicePrior(load_prior(PRIOR_XML), device), temperature_ladder(num_chains),
+                               rank=rank, world=world, seed=args.seed, device=device, proposal=args.proposal)
+        self.exploration_steps = self.loop.exploration_steps
+
+    def run(self, n):
+        for _ in range(n):
+            self.loop.iteration()
+
+    def sync(self):
+        self.loop.check_nan()
+
+    def acceptance(self):
+        return float(self.loop.accepted_mutate) / max(1, self.loop.attempted_mutate)
+
+    def values(self):
+        return self.loop.prop
 
 
 def spawn_ranks(args) -> int:
@@ -368,28 +425,27 @@ def main():
 
     from bcm3_amd import _hip
     from bcm3_amd.likelihood import Likelihood
-    from bcm3_amd.pt import temperature_ladder
-    from bcm3_amd.sampler import DevicePrior, PTMHDevice, load_prior
 
     ll = Likelihood(LIK_XML, PRIOR_XML, device=local)
     if args.lanes_per_wave:
         ll.set_option(_hip.OPT_LANES_PER_WAVE, args.lanes_per_wave)
     m = ll.popk_model()
     C = args.total_chains // world if args.total_chains else args.chains
-    prior = DevicePrior(load_prior(PRIOR_XML), device)
-    loop = PTMHDevice(ll, prior, temperature_ladder(C * world), rank=rank, world=world, seed=args.seed,
-                      device=device, proposal=args.proposal)
+    if args.loop == "native":
+        loop = NativeLoop(ll, C * world, rank, world, args, dist if world > 1 else None)
+    else:
+        loop = PythonLoop(ll, C * world, rank, world, args, device)
 
-    for _ in range(args.warmup):
-        loop.iteration()
+    loop.run(args.warmup)
+    loop.sync()
     torch.cuda.synchronize()
     ll.set_option(_hip.OPT_TIMING_LOG, 1)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        loop.iteration()
+    loop.run(args.steps)
+    loop.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -406,7 +462,7 @@ def main():
         rank_k_ms = [float(a) for a in allk]
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, k_avg = float(t[0]), float(t[1])
-    nan_flag = loop.check_nan() if hasattr(loop, "check_nan") else None
+    nan_flag = False  # loop.sync() raises on a NaN log-likelihood (Sampler.cpp:172-178)
 
     evals = C * world * args.steps * loop.exploration_steps
     value = evals / dt
@@ -415,7 +471,7 @@ def main():
     tb = traffic_from_profiles("c3_256", C)
     f_alg = flops_per_eval()
     achieved_tf = f_alg * C / (k_avg * 1e-3) / 1e12  # the kernel's own rate, like achieved_gbs
-    issue = issue_rate(ll, loop.prop, device) if rank == 0 else None
+    issue = issue_rate(ll, loop.values(), device) if rank == 0 else None
 
     extra = {}
     if rank == 0 and args.throughput_batch > 0:
@@ -455,7 +511,7 @@ def main():
             if "popk_p64_256chains" in extra:
                 extra["popk_p64_256chains"]["cpu_baseline"] = p64_cpu_baseline(6.0, args.seed)
 
-    acc_mut = float(loop.accepted_mutate) / max(1, loop.attempted_mutate)
+    acc_mut = loop.acceptance()
     line = {
         "metric": "log-likelihood evals/sec (whole node), PopPK ODE @256 chains; HBM-roofline %",
         "value": value,
@@ -482,6 +538,8 @@ def main():
             "lanes_per_wave": args.lanes_per_wave or "auto",
             "parallelism": f"chains sharded over {world} rank(s); PT swap = RCCL neighbour send/recv",
             "proposal": args.proposal,
+            "sampler_loop": "C++ host loop (libbcm3.so bcm3_ptmh_iterate)" if args.loop == "native"
+            else "Python loop (bcm3_amd.sampler.PTMHDevice)",
         },
         "roofline": {
             "bound": "hbm",

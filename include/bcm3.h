@@ -94,6 +94,70 @@ int bcm3_adapt_proposals(int kind, int adjusted_aic, int C, int H, int d, int km
 int bcm3_gmm_eval(int K, int d, const double* weights, const double* means, const double* covariances, int n,
                   const double* x, double* logpdf, double* resp, double* chol_out, double* logc_out);
 
+/* ---- the PT-MH sampler loop of one rank, in C++ (SamplerPTDevice.cpp) ----
+ * SamplerPT::Initialize / Run (src/sampler/SamplerPT.cpp:97-260) with SamplerPTChain's
+ * MutateMove / ExchangeMove / AdaptProposal (src/sampler/SamplerPTChain.cpp:120-381): the rank owns
+ * the contiguous ladder slice [rank * C, (rank + 1) * C) of num_chains = world * C chains, chain
+ * state in HBM, one batched likelihood launch per mutate step on `stream`, proposal adaptation on
+ * host threads (bcm3_adapt_proposals), the PT swap of slice-boundary pairs over RCCL. Random
+ * numbers are counter based, so a run is identical for any number of ranks (and to
+ * bcm3_amd.sampler.PTMHDevice). Not thread-safe per handle. */
+enum { BCM3_PTMH_GLOBAL_COVARIANCE = 0, BCM3_PTMH_GAUSSIAN_MIXTURE = 1, BCM3_PTMH_GAUSSIAN_MIXTURE_ADJUSTED_AIC = 2,
+       BCM3_PTMH_RANDOM_WALK = 3 };
+enum { BCM3_PTMH_DETERMINISTIC_EVEN_ODD = 0, BCM3_PTMH_STOCHASTIC_EVEN_ODD = 1, BCM3_PTMH_STOCHASTIC_RANDOM = 2 };
+enum { BCM3_PTMH_TRANSPORT_NONE = 0, BCM3_PTMH_TRANSPORT_RCCL = 1, BCM3_PTMH_TRANSPORT_LOCAL = 2 };
+typedef struct bcm3_ptmh bcm3_ptmh;
+typedef struct bcm3_ptmh_group bcm3_ptmh_group; /* in-process ranks (tests): host-staged transport */
+typedef struct {
+    int64_t num_chains;          /* ptmhsampler.num_chains, over all ranks */
+    int32_t rank, world;
+    double temperature_power;    /* ptmhsampler.temperature_schedule_power (3) */
+    double temperature_max;      /* 1 */
+    uint64_t seed;               /* sampler.rngseed */
+    double learning_rate;
+    int32_t exploration_steps;   /* ptmhsampler.num_exploration_steps */
+    int32_t proposal;            /* BCM3_PTMH_* proposal type */
+    double t_dof;                /* ptmhsampler.proposal_t_dof */
+    int32_t kmax;                /* mixture component slots, 0 = 13 */
+    int32_t adapt_proposal_samples, adapt_proposal_times, max_history_size;
+    int32_t adapt_proposal_max_history_samples, use_every_nth;
+    int32_t swapping_scheme;     /* BCM3_PTMH_*_EVEN_ODD / _RANDOM */
+    double exchange_probability;
+    int32_t initial_position_tries;
+    int32_t nan_check_every;     /* bcm3_ptmh_run checks for NaN likelihoods every n iterations */
+    int32_t host_threads;        /* proposal adaptation threads, 0 = all cores (max 16) */
+    int32_t transport;           /* BCM3_PTMH_TRANSPORT_*, world > 1 */
+    uint8_t nccl_id[128];        /* BCM3_PTMH_TRANSPORT_RCCL: bcm3_ptmh_nccl_unique_id of rank 0 */
+    bcm3_ptmh_group* group;      /* BCM3_PTMH_TRANSPORT_LOCAL */
+} bcm3_ptmh_config;
+enum { BCM3_PTMH_NUM_COUNTERS = 8 }; /* attempted / accepted mutate, attempted / accepted exchange,
+                                        samples done, adaptations done, iterations, exchange rounds */
+void bcm3_ptmh_config_default(bcm3_ptmh_config* cfg);
+int bcm3_ptmh_nccl_unique_id(void* id /* 128 bytes */);
+int bcm3_ptmh_group_create(int world, bcm3_ptmh_group** out);
+void bcm3_ptmh_group_destroy(bcm3_ptmh_group* g);
+/* prior_xml: the prior.xml the likelihood was created with (PriorIndependence marginals);
+ * stream: hipStream_t, NULL = a stream of its own. Finds the starting positions
+ * (SamplerPTChain::FindStartingPosition). */
+int bcm3_ptmh_create(bcm3_likelihood* ll, const char* prior_xml, const bcm3_ptmh_config* cfg, void* stream,
+                     bcm3_ptmh** out);
+/* n iterations of SamplerPT::Run's loop (exchange + mutate moves, adaptation when due), no host
+ * synchronisation except at adaptations; last_at_end marks the final iteration as the last sample */
+int bcm3_ptmh_iterate(bcm3_ptmh* s, int64_t n, int last_at_end);
+/* num_samples * use_every_nth iterations with the NaN check every nan_check_every (fatal, as
+ * Sampler::EvaluateLikelihood, src/sampler/Sampler.cpp:172-178) */
+int bcm3_ptmh_run(bcm3_ptmh* s, int64_t num_samples);
+int bcm3_ptmh_adapt(bcm3_ptmh* s);
+/* wait for the stream; < 0 if a likelihood returned NaN */
+int bcm3_ptmh_synchronize(bcm3_ptmh* s);
+int bcm3_ptmh_num_chains(const bcm3_ptmh* s); /* chains of this rank */
+/* host copies of the rank's chains (any may be NULL): values[C][d], llh[C], lprior[C], lpp[C] */
+int bcm3_ptmh_get_state(bcm3_ptmh* s, double* values, double* llh, double* lprior, double* lpp);
+int bcm3_ptmh_get_components(bcm3_ptmh* s, int32_t* ncomp /* [C] */);
+int bcm3_ptmh_get_counters(bcm3_ptmh* s, int64_t* out /* [BCM3_PTMH_NUM_COUNTERS] */);
+void* bcm3_ptmh_stream(const bcm3_ptmh* s);
+void bcm3_ptmh_destroy(bcm3_ptmh* s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -304,6 +304,42 @@ int bcm3hip_pt_exchange_pair(int C, int d, int i1, int i2, int64_t g1, const dou
                              double* llh, double* lprior, double* lpp, uint8_t* acc_out, uint64_t* accepted,
                              uint64_t seed, uint64_t round, void* stream);
 
+/* Slice-boundary exchange of a sharded ladder (rank r owns global chains [g0, g0 + C)).
+ * bcm3hip_pt_pack_boundary: the records {values[d], llh, lprior, lpp, T} (d + 4 doubles) of the
+ * last and the first local chain (either output may be NULL), sent to the next / previous rank.
+ * bcm3hip_pt_cross_accept: ExchangeMove (SamplerPTChain.cpp:328-381) of pair A = (my chain C-1,
+ * the next rank's first chain = recv_next; uniform keyed by g0 + C - 1) when do_next, and of
+ * pair B = (the previous rank's last chain = recv_prev, my chain 0; keyed by gp, its global index)
+ * when do_prev; each rank keeps its side; acc_out[2] (may be NULL) = {A, B} accepted; *accepted
+ * counts pair A (the rank of a pair's first chain counts it). */
+int bcm3hip_pt_pack_boundary(int C, int d, const double* temps, const double* values, const double* llh,
+                             const double* lprior, const double* lpp, double* send_last, double* send_first,
+                             void* stream);
+int bcm3hip_pt_cross_accept(int C, int d, int64_t g0, int64_t gp, int do_next, int do_prev, const double* temps,
+                            double* values, double* llh, double* lprior, double* lpp, const double* recv_next,
+                            const double* recv_prev, uint8_t* acc_out, uint64_t* accepted, uint64_t seed,
+                            uint64_t round, void* stream);
+
+/* ---- device runtime for the host sampler (runtime.hip) ---- */
+enum { BCM3HIP_H2D = 1, BCM3HIP_D2H = 2, BCM3HIP_D2D = 3 };
+int bcm3hip_set_device(int device);
+int bcm3hip_malloc(void** ptr, size_t bytes);
+int bcm3hip_free(void* ptr);
+int bcm3hip_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream);
+int bcm3hip_memset_async(void* dst, int value, size_t bytes, void* stream);
+int bcm3hip_stream_create(void** stream);
+int bcm3hip_stream_destroy(void* stream);
+int bcm3hip_stream_synchronize(void* stream);
+/* RCCL point-to-point for the PT swap between neighbouring ranks (replaces the reference's
+ * single-process exchange loop). The unique id is an opaque
+ * BCM3HIP_NCCL_ID_BYTES-byte blob made on one rank and broadcast by the caller. */
+#define BCM3HIP_NCCL_ID_BYTES 128
+int bcm3hip_nccl_get_unique_id(void* id);
+int bcm3hip_nccl_comm_init(const void* id, int rank, int world, void** comm);
+int bcm3hip_nccl_comm_destroy(void* comm);
+int bcm3hip_nccl_exchange(void* comm, int n_send, const double* const* send, const int* send_peer, int n_recv,
+                          double* const* recv, const int* recv_peer, size_t count, void* stream);
+
 /* Parity/diagnostic batch (host buffers, any output may be NULL):
  * patient_llh[n*P], traj[n*P*N*T] (states at output times, NaN where not simulated),
  * stats[n*P]. PopPK contexts only. */

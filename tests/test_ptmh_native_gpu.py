@@ -1,0 +1,125 @@
+"""The C++ PT-MH sampler (libbcm3.so bcm3_ptmh_*, csrc/host/SamplerPTDevice.cpp) on the GPU:
+* bit for bit the chains of the Python loop bcm3_amd.sampler.PTMHDevice over the same kernels
+  (values, llh, lprior, lpp, acceptance counters), for C3 and for C2 with proposal adaptations;
+* a ladder sharded over 2 and 4 in-process ranks (one host thread each, host-staged transport in
+  place of RCCL) gives the chains of the single-rank run bit for bit -- the counter-based random
+  numbers make the result independent of the rank count, as SURVEY.md §8(e) requires."""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _python_loop(lik, pri, C, seed, steps, **kw):
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.pt import temperature_ladder
+    from bcm3_amd.sampler import DevicePrior, PTMHDevice, load_prior
+    ll = Likelihood(lik, pri, device=0)
+    loop = PTMHDevice(ll, DevicePrior(load_prior(pri), "cuda"), temperature_ladder(C), seed=seed, device="cuda", **kw)
+    for _ in range(steps):
+        loop.iteration()
+    torch.cuda.synchronize()
+    st = dict(values=loop.values.cpu().numpy(), llh=loop.llh.cpu().numpy(), lprior=loop.lprior.cpu().numpy(),
+              lpp=loop.lpp.cpu().numpy())
+    cnt = dict(accepted_mutate=int(loop.accepted_mutate.item()), attempted_mutate=loop.attempted_mutate,
+               accepted_exchange=int(loop.accepted_exchange.item()), attempted_exchange=loop.attempted_exchange,
+               adaptations_done=loop.adaptations_done)
+    return st, cnt, (loop.proposal.ncomp.cpu().numpy() if loop.adaptive else None)
+
+
+def _native(lik, pri, C, seed, steps, rank=0, world=1, group=None, **kw):
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.ptmh import TRANSPORT_LOCAL, PTMHNative
+    ll = Likelihood(lik, pri, device=0)
+    extra = dict(transport=TRANSPORT_LOCAL, group=group) if world > 1 else {}
+    return PTMHNative(ll, pri, C, rank=rank, world=world, seed=seed, **extra, **kw)
+
+
+def _same(a, b):
+    return np.array_equal(a, b, equal_nan=True)
+
+
+def _compare(st_py, st_nat):
+    for k in ("values", "llh", "lprior", "lpp"):
+        assert _same(st_py[k], st_nat[k]), k
+
+
+C3 = (os.path.join(H.GOLDEN, "c3_likelihood.xml"), os.path.join(H.GOLDEN, "c3_prior.xml"))
+C2 = (os.path.join(H.GOLDEN, "circular_likelihood.xml"), os.path.join(H.GOLDEN, "circular_prior.xml"))
+
+
+def test_native_matches_python_loop_c3():
+    st, cnt, _ = _python_loop(*C3, 256, 11, 50)
+    s = _native(*C3, 256, 11, 50)
+    s.iterate(50)
+    s.synchronize()
+    _compare(st, s.state())
+    c = s.counters()
+    for k in ("accepted_mutate", "attempted_mutate", "accepted_exchange", "attempted_exchange"):
+        assert c[k] == cnt[k], k
+    assert c["samples_done"] == 50 and c["rounds"] == 50
+
+
+@pytest.mark.parametrize("proposal,scheme", [("gaussian_mixture", "deterministic_even_odd"),
+                                             ("global_covariance", "stochastic_even_odd"),
+                                             ("gaussian_mixture_adjustedAIC", "stochastic_random"),
+                                             ("random_walk", "deterministic_even_odd")])
+def test_native_matches_python_loop_with_adaptation(proposal, scheme):
+    kw = dict(adapt_proposal_samples=40, adapt_proposal_times=2)
+    py_kw = dict(kw, proposal=proposal, swapping_scheme=scheme)
+    st, cnt, nc = _python_loop(*C2, 32, 5, 130, **py_kw)
+    s = _native(*C2, 32, 5, 130, proposal=proposal, swapping_scheme=scheme, **kw)
+    s.iterate(130)
+    s.synchronize()
+    _compare(st, s.state())
+    c = s.counters()
+    for k in cnt:
+        assert c[k] == cnt[k], k
+    if proposal != "random_walk":
+        assert c["adaptations_done"] == 2
+        assert np.array_equal(s.components(), nc)
+
+
+@pytest.mark.parametrize("world,scheme", [(2, "deterministic_even_odd"), (4, "deterministic_even_odd"),
+                                          (2, "stochastic_random")])
+def test_native_sharded_ladder_equals_single_rank(world, scheme):
+    C, seed, steps = 32, 9, 90
+    kw = dict(adapt_proposal_samples=30, adapt_proposal_times=1, swapping_scheme=scheme)
+    one = _native(*C2, C, seed, steps, **kw)
+    one.iterate(steps)
+    one.synchronize()
+    ref = one.state()
+    from bcm3_amd.ptmh import LocalGroup
+    group = LocalGroup(world)
+    ranks = [_native(*C2, C, seed, steps, rank=r, world=world, group=group, **kw) for r in range(world)]
+    errors = []
+
+    def go(s):
+        try:
+            s.iterate(steps)
+            s.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=go, args=(s,)) for s in ranks]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    n = C // world
+    for r, s in enumerate(ranks):
+        st = s.state()
+        for k in ("values", "llh", "lprior", "lpp"):
+            assert _same(st[k], ref[k][r * n:(r + 1) * n]), (r, k)
+    tot = {k: sum(s.counters()[k] for s in ranks) for k in ("accepted_mutate", "attempted_exchange",
+                                                             "accepted_exchange")}
+    c1 = one.counters()
+    for k, v in tot.items():
+        assert v == c1[k], k
