@@ -12,6 +12,8 @@
 #include <new>
 #include <vector>
 
+#include <algorithm>
+
 #include "../../include/bcm3hip.h"
 #include "popk_kernel.h"
 
@@ -48,6 +50,12 @@ struct bcm3hip_ctx {
     size_t cap_exps = 0;
     bcm3hip_traj_stats* stats = nullptr;
     size_t cap_stats = 0;
+    // the grow-only scratch above is shared by every launch of the context: a launch on another
+    // stream than the previous one waits for that one (scratch_ev), so concurrent callers on
+    // different streams cannot overwrite each other's exponentials / per-patient results
+    hipEvent_t scratch_ev = nullptr;
+    hipStream_t scratch_stream = nullptr;
+    bool scratch_used = false;
     int lanes_per_wave = 0;  // 0 = auto (auto_lanes_per_wave)
     int uni_solver = 0;      // BCM3HIP_OPT_UNI_SOLVER
     int block_waves = 1;
@@ -99,6 +107,7 @@ static int ctx_common_init(bcm3hip_ctx* c, int device)
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
+    HIPCHK(hipEventCreateWithFlags(&c->scratch_ev, hipEventDisableTiming));
     return 0;
 }
 
@@ -372,6 +381,7 @@ int bcm3hip_close(bcm3hip_ctx* c)
     hipFree(c->stats);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->scratch_ev) hipEventDestroy(c->scratch_ev);
     for (hipEvent_t e : c->log_ev) hipEventDestroy(e);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
@@ -424,10 +434,15 @@ static int auto_lanes_per_wave(size_t ntraj)
     return lpw;
 }
 
+// scratch of the matrix-exponential path per launch: exps[n][n_jobs][n^2]; larger batches run in
+// chunks of evaluations so that it stays under this many bytes
+static const size_t kExpmScratchBytes = (size_t)1 << 30;
+
 static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp, int32_t* dstatus,
                   double* dtraj, bcm3hip_traj_stats* dstats, hipStream_t s)
 {
     hipError_t e;
+    if (c->scratch_used && c->scratch_stream != s) HIPCHK(hipStreamWaitEvent(s, c->scratch_ev, 0));
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (c->log_timing) {
         if (c->log_ev.size() < 2 * (c->log_used + 1)) {
@@ -448,9 +463,16 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
                         c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
                         c->block_waves, c->uni_solver, s, e0, e1);
     } else if (c->kind == 3) {
-        if (grow(c->exps, c->cap_exps, n * (size_t)c->xm.n_jobs * (size_t)(c->xm.n * c->xm.n)))
-            return BCM3HIP_ERR_ALLOC;
-        e = launch_expm_pk(c->xm, (int64_t)n, dvalues, dlogp, dstatus, c->exps, s, e0, e1);
+        const size_t per_eval = (size_t)c->xm.n_jobs * (size_t)(c->xm.n * c->xm.n);
+        const size_t chunk = per_eval == 0 ? n : std::max<size_t>(1, kExpmScratchBytes / (per_eval * sizeof(double)));
+        const size_t nc = std::min(n, chunk);
+        if (grow(c->exps, c->cap_exps, std::max<size_t>(nc * per_eval, 1))) return BCM3HIP_ERR_ALLOC;
+        e = hipSuccess;
+        for (size_t i0 = 0; i0 < n && e == hipSuccess; i0 += nc) {
+            const size_t m = std::min(nc, n - i0);
+            e = launch_expm_pk(c->xm, (int64_t)m, dvalues + i0 * (size_t)c->d, dlogp + i0, dstatus ? dstatus + i0 : nullptr,
+                               c->exps, s, i0 == 0 ? e0 : nullptr, i0 + m >= n ? e1 : nullptr);
+        }
     } else {
         e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     }
@@ -458,6 +480,9 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
         fprintf(stderr, "bcm3hip: kernel launch failed: %s\n", hipGetErrorString(e));
         return BCM3HIP_ERR_HIP;
     }
+    HIPCHK(hipEventRecord(c->scratch_ev, s));
+    c->scratch_stream = s;
+    c->scratch_used = true;
     c->last0 = e0;
     c->last1 = e1;
     c->timed = true;

@@ -3,6 +3,7 @@
 
 #include <cmath>
 
+#include "LikelihoodDLL.h"
 #include "LikelihoodGPU.h"
 #include "log.h"
 
@@ -55,7 +56,8 @@ std::string option_get(const OptionsMap& vm, const std::string& key, const std::
 
 std::vector<std::string> LikelihoodFactory::SupportedTypes()
 {
-    return {"pop_pk_trajectory", "pharmacokinetic_trajectory", "pharmaco_single", "pharmaco_population", "banana", "circular"};
+    return {"pop_pk_trajectory", "pharmacokinetic_trajectory", "pharmaco_single", "pharmaco_population", "banana", "circular",
+            "dll"};
 }
 
 std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::string& fn,
@@ -100,8 +102,10 @@ std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::strin
         ll = std::make_shared<TestLikelihoodBanana>(sampling_threads, evaluation_threads);
     } else if (type == "circular") {
         ll = std::make_shared<TestLikelihoodCircular>(sampling_threads, evaluation_threads);
+    } else if (type == "dll") {
+        ll = std::make_shared<LikelihoodDLL>(sampling_threads, evaluation_threads);
     } else {
-        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, pharmaco_single, pharmaco_population, banana, circular)",
+        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, pharmaco_single, pharmaco_population, banana, circular, dll)",
                  type.c_str());
         return ll;
     }

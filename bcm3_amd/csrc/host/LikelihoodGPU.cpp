@@ -38,8 +38,38 @@ bool LikelihoodGPUBase::OpenDevice(const OptionsMap& vm)
 
 bool LikelihoodGPUBase::EvaluateLogProbability(size_t threadix, const VectorReal& values, Real& logp)
 {
-    int32_t st = 0;
-    return EvaluateLogProbabilityBatch(1, values.data(), &logp, &st);
+    // request combining: the caller that finds no launch in flight takes every queued request
+    // (its own included) into one batched launch; the others wait for their results
+    if (values.size() != GetNumVariables()) return false;
+    Request me{values.data(), 0.0, false, false};
+    std::unique_lock<std::mutex> lk(comb_mutex);
+    comb_queue.push_back(&me);
+    while (!me.done) {
+        if (comb_busy) {
+            comb_cv.wait(lk);
+            continue;
+        }
+        comb_busy = true;
+        std::vector<Request*> batch;
+        batch.swap(comb_queue);
+        lk.unlock();
+        const size_t d = GetNumVariables(), n = batch.size();
+        std::vector<Real> v(n * d), out(n);
+        std::vector<int32_t> st(n);
+        for (size_t i = 0; i < n; i++) std::copy(batch[i]->values, batch[i]->values + d, v.begin() + i * d);
+        const bool ok = EvaluateLogProbabilityBatch(n, v.data(), out.data(), st.data());
+        lk.lock();
+        for (size_t i = 0; i < n; i++) {
+            batch[i]->logp = out[i];
+            batch[i]->ok = ok;
+            batch[i]->done = true;
+        }
+        comb_busy = false;
+        comb_cv.notify_all();
+    }
+    lk.unlock();
+    logp = me.logp;
+    return me.ok;
 }
 
 bool LikelihoodGPUBase::EvaluateLogProbabilityBatch(size_t n, const Real* values, Real* logp, int32_t* status)

@@ -10,8 +10,10 @@
 // CPU fallback: without a GPU, Initialize fails.
 #pragma once
 #include <cmath>
+#include <condition_variable>
 #include <mutex>
 #include <set>
+#include <vector>
 
 #include "../../../include/bcm3hip.h"
 #include "Likelihood.h"
@@ -21,8 +23,11 @@ namespace bcm3 {
 class LikelihoodGPUBase : public Likelihood {
 public:
     ~LikelihoodGPUBase() override;
-    // Reentrant: concurrent single evaluations are serialised on the context; the sampler's
-    // batched path issues one launch per mutate step.
+    // Reentrant: concurrent single evaluations from the reference's sampling threads (TaskManager,
+    // one task per chain) are combined into batched launches -- the threads that arrive while a
+    // launch runs go into the next one -- so the drop-in single-vector route (EvaluateLogProbability,
+    // and the LikelihoodDLL C plugin on top of it) approaches the batched rate when there are
+    // many sampling threads. Each result depends only on its own vector.
     bool IsReentrant() override { return true; }
     bool EvaluateLogProbability(size_t threadix, const VectorReal& values, Real& logp) override;
     bool EvaluateLogProbabilityBatch(size_t n, const Real* values, Real* logp, int32_t* status) override;
@@ -38,6 +43,17 @@ protected:
     int device = 0;
     bcm3hip_ctx* ctx = nullptr;
     std::mutex mutex;
+
+private:
+    struct Request {
+        const Real* values;
+        Real logp;
+        bool done, ok;
+    };
+    std::mutex comb_mutex;
+    std::condition_variable comb_cv;
+    std::vector<Request*> comb_queue;
+    bool comb_busy = false;
 };
 
 class LikelihoodPopPKTrajectory : public LikelihoodGPUBase {

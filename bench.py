@@ -431,9 +431,25 @@ def main():
         ll.set_option(_hip.OPT_LANES_PER_WAVE, args.lanes_per_wave)
     m = ll.popk_model()
     C = args.total_chains // world if args.total_chains else args.chains
+    loop_kind = args.loop
     if args.loop == "native":
-        loop = NativeLoop(ll, C * world, rank, world, args, dist if world > 1 else None)
-    else:
+        try:
+            loop = NativeLoop(ll, C * world, rank, world, args, dist if world > 1 else None)
+        except RuntimeError as e:
+            if world == 1:
+                raise
+            # the C++ loop's own RCCL communicator could not be set up on this node: the same
+            # iteration in Python, its PT swap over torch.distributed (also RCCL); both logged
+            print(f"bench.py rank {rank}: C++ sampler unavailable ({e}); using the Python loop", file=sys.stderr,
+                  flush=True)
+            loop_kind = "python"
+        ok = torch.tensor([1 if loop_kind == "native" else 0], device=device)
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 0 and loop_kind == "native":
+            loop.s.close()
+            loop_kind = "python"
+    if loop_kind == "python":
         loop = PythonLoop(ll, C * world, rank, world, args, device)
 
     loop.run(args.warmup)
@@ -538,7 +554,7 @@ def main():
             "lanes_per_wave": args.lanes_per_wave or "auto",
             "parallelism": f"chains sharded over {world} rank(s); PT swap = RCCL neighbour send/recv",
             "proposal": args.proposal,
-            "sampler_loop": "C++ host loop (libbcm3.so bcm3_ptmh_iterate)" if args.loop == "native"
+            "sampler_loop": "C++ host loop (libbcm3.so bcm3_ptmh_iterate)" if loop_kind == "native"
             else "Python loop (bcm3_amd.sampler.PTMHDevice)",
         },
         "roofline": {
