@@ -495,7 +495,8 @@ def main():
         n = args.throughput_batch
         gen = torch.Generator(device=device)
         gen.manual_seed(args.seed + 1)
-        x = prior.sample(n, gen).contiguous()
+        from bcm3_amd.sampler import DevicePrior, load_prior
+        x = DevicePrior(load_prior(PRIOR_XML), device).sample(n, gen).contiguous()
         out = torch.empty(n, dtype=torch.float64, device=device)
         stream = torch.cuda.current_stream(device).cuda_stream
         ll.evaluate_batch_device(n, x.data_ptr(), out.data_ptr(), None, stream)
