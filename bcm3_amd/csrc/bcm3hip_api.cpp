@@ -19,9 +19,19 @@
 
 using namespace bcm3hip;
 
+namespace bcm3hip {
+struct CellPopDev;
+int cellpop_create(int device, const bcm3hip_cellpop_model* m, CellPopDev** out);
+void cellpop_destroy(CellPopDev* c);
+int cellpop_launch(CellPopDev* c, size_t n, const double* values, double* logp, int32_t* status, hipStream_t s,
+                   hipEvent_t e0, hipEvent_t e1);
+int cellpop_cells(CellPopDev* c, size_t item, int32_t* count, bcm3hip_cell_record* rec, double* values, double* end_y);
+}  // namespace bcm3hip
+
 struct bcm3hip_ctx {
     int device = 0;
-    int kind = 0;  // 1 popk, 2 analytic, 3 expm pk
+    int kind = 0;  // 1 popk, 2 analytic, 3 expm pk, 4 cell population
+    bcm3hip::CellPopDev* cp = nullptr;
     int d = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -235,6 +245,34 @@ int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* m, bcm3hip_c
     return 0;
 }
 
+int bcm3hip_open_cellpop(int device, const bcm3hip_cellpop_model* m, bcm3hip_ctx** out)
+{
+    if (!m || !out) return BCM3HIP_ERR_ARG;
+    *out = nullptr;
+    bcm3hip_ctx* c = new (std::nothrow) bcm3hip_ctx();
+    if (!c) return BCM3HIP_ERR_ALLOC;
+    int r = ctx_common_init(c, device);
+    if (r == 0) r = bcm3hip::cellpop_create(device, m, &c->cp);
+    if (r) {
+        bcm3hip_close(c);
+        return r;
+    }
+    c->kind = 4;
+    c->d = m->d;
+    *out = c;
+    return 0;
+}
+
+int bcm3hip_cellpop_cells(bcm3hip_ctx* c, size_t item, int32_t* count, bcm3hip_cell_record* records, double* values,
+                          double* end_y)
+{
+    if (!c || c->kind != 4 || !count) return BCM3HIP_ERR_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipDeviceSynchronize());
+    return bcm3hip::cellpop_cells(c->cp, item, count, records, values, end_y);
+}
+
 int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* m, bcm3hip_ctx** out)
 {
     if (!m || !out) return BCM3HIP_ERR_ARG;
@@ -370,6 +408,7 @@ int bcm3hip_close(bcm3hip_ctx* c)
 {
     if (!c) return 0;
     if (c->stream) hipSetDevice(c->device);
+    if (c->cp) bcm3hip::cellpop_destroy(c->cp);
     for (void* p : c->model_allocs) hipFree(p);
     hipFree(c->values);
     hipFree(c->logp);
@@ -473,6 +512,10 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
             e = launch_expm_pk(c->xm, (int64_t)m, dvalues + i0 * (size_t)c->d, dlogp + i0, dstatus ? dstatus + i0 : nullptr,
                                c->exps, s, i0 == 0 ? e0 : nullptr, i0 + m >= n ? e1 : nullptr);
         }
+    } else if (c->kind == 4) {
+        const int r = bcm3hip::cellpop_launch(c->cp, n, dvalues, dlogp, dstatus, s, e0, e1);
+        if (r) return r;
+        e = hipSuccess;
     } else {
         e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     }

@@ -1,0 +1,34 @@
+// cellpop_args.h -- argument block of cp_solve_kernel (cellpop_solver.h), shared by the run-time
+// compiled kernel and the host launcher (cellpop_rt.cpp), so both see one layout.
+#pragma once
+#include <stdint.h>
+
+namespace cpk {
+
+struct CpSolveArgs {
+    const int32_t* work;          // [n_work] cell slots of this launch
+    int32_t n_work;
+    int32_t M;                    // output entries (sorted simulation time points) = CP_M
+    const double* output_times;   // [M] experiment times
+    const int32_t* output_species;  // [M] ODE species index or -1
+    const double* params;         // [slot][NP] cell-specific transformed variables
+    const double* y0;             // [slot][NS]
+    const double* creation;       // [slot]
+    const double* constant_species;  // [NC]
+    double end_time;              // Experiment target time
+    double rtol, atol, hmin;
+    int32_t max_steps;
+    int32_t divide_cells;
+    double past_cs;               // simulate_past_chromatid_separation_time
+    int32_t ev[7];                // event species (simulated-species index applied to the ODE state), -1 = none
+    // outputs
+    double* out_values;           // [slot][M]
+    double* end_y;                // [slot][NS]
+    double* sim_end;              // [slot] cell time
+    double* achieved;             // [slot] experiment time
+    int32_t* flags;               // [slot] bit0 ok, bit1 divided, bit2 died, bit3 entered mitosis
+    double* event_times;          // [slot][5]
+    int32_t* nsteps;              // [slot]
+};
+
+}  // namespace cpk

@@ -1,0 +1,856 @@
+// cellpop_solver.h -- the cell-population ODE solve kernel, compiled at run time (hipRTC) per
+// model together with the model's generated right-hand side (cellpop_rt.cpp prepends the
+// definitions CP_NS / CP_NC / CP_NP and `generated_derivative`, the text of the reference's
+// SBMLModel::GenerateCode, src/sbml/SBMLModel.cpp:291-367, as a device template).
+//
+// One workgroup = one wavefront = one cell. The reference integrates each cell with CVODE 5.3.0
+// BDF (ODESolverCVODE::Solve, src/odecommon/ODESolverCVODE.cpp:322-463; Cell::Simulate,
+// src/cellpop/Cell.cpp:193-273): Newton with a difference-quotient Jacobian
+// (ODESolverCVODE::DifferenceQuotientJacobian, :496-537) and a dense partial-pivoting LU
+// (PartialPivLUExtended::compute_optimized, src/utils/EigenPartialPivLUSomewhatSparse.h) --
+// N = tens of species, so unlike the PopPK kernels nothing is closed-form:
+//   * lane i holds component i of every solver vector (Nordsieck zn[0..5], ewt, acor): every
+//     component-wise operation of the BDF step is one instruction, as in bdf_vec.h;
+//   * the saved Jacobian and the LU factors live in LDS (column-major N x N per wave); the
+//     factorisation runs lanes = rows, the row swaps lanes = columns; solves are
+//     column-oriented substitutions with one broadcast per column;
+//   * the generated right-hand side runs wave-uniform (every lane evaluates the model's rate
+//     laws on the broadcast state) and lane i keeps component i; the N perturbed evaluations of
+//     the difference-quotient Jacobian run in ONE pass, lane j evaluating f(y + inc_j e_j), so a
+//     Jacobian costs one RHS evaluation instead of N;
+//   * weighted norms sum the rounded squares in component order (nvector_serial's N_VWrmsNorm).
+// The step control is the reference's cvode.c (the runtime-order form of bdf_lane.h, with the
+// hmin rules cellpop sets: CVodeSetMinStep, cvode.c:1123-1124, 2893-2903, 2977-3007); the cell
+// driver restates Cell::integration_step_cb (Cell.cpp:463-538) in the non-stored mode.
+#pragma once
+#include "bdf_lane.h"
+#include "cellpop_args.h"
+
+namespace cpk {
+using namespace bcm3hip;
+
+constexpr int WAVE = 64;
+
+
+
+BDF_INL int lane() { return (int)threadIdx.x; }
+
+BDF_INL double bcast(double v, int k)
+{
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_readlane((int)b, k);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), k);
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+BDF_INL void wave_sync() { __syncthreads(); }
+
+struct LdsSpecies {
+    const double* y;
+    BDF_INL double operator[](int k) const { return y[k]; }
+};
+// lane j: the state with component j perturbed (DifferenceQuotientJacobian's y_copy)
+struct PertSpecies {
+    const double* y;
+    double yp;
+    int me;
+    BDF_INL double operator[](int k) const { return (me == k) ? yp : y[k]; }
+};
+
+template <int NS, int NP, int NC, int M>
+struct Shared {
+    double outl[M];      // the cell's values at the output entries
+    double sy[WAVE];     // state broadcast
+    double sf[WAVE];     // f(y) broadcast (Jacobian)
+    double red[WAVE];    // reductions
+    double J[NS * NS];   // saved Jacobian, column-major
+    double A[NS * NS];   // I - gamma J -> LU factors, column-major
+    int perm[NS];        // (P b)[i] = b[perm[i]]
+    double prm[NP > 0 ? NP : 1];
+    double cs[NC > 0 ? NC : 1];
+};
+
+template <int NS>
+struct GenState {
+    double rtol, atol, hmin;
+    double zn[QMAX + 1];  // lane i: component i
+    double ewt, acor;
+    double tau[QMAX + 2], tq[6], l[QMAX + 1];
+    double tn, h, hprime, eta, hscale, hu, tretlast;
+    double gamma, gammap, gamrat, crate, delp, acnrm, etamax, saved_tq5;
+    int q, qprime, qwait, L;
+    int nst, nstlp, nstlj;
+    int nls_jcur;
+};
+
+// sum over the components in component order of a lane value (uniform result)
+template <int NS, class SH>
+BDF_INL double lane_sum(SH& sh, double p)
+{
+    wave_sync();
+    sh.red[lane()] = p;
+    wave_sync();
+    double s = sh.red[0];
+#pragma unroll
+    for (int i = 1; i < NS; i++) s += sh.red[i];
+    return s;
+}
+
+// N_VWrmsNorm
+template <int NS, class SH>
+BDF_INL double wrms(SH& sh, double x, double w)
+{
+    const double p = x * w;
+    return fsqrt(fdiv_c(lane_sum<NS>(sh, p * p), (double)NS, 1.0 / NS));
+}
+
+// ---- the model ---------------------------------------------------------------------------------
+template <int NS, int NP, int NC, class SH>
+BDF_INL double rhs_v(SH& sh, double y)
+{
+    wave_sync();
+    if (lane() < NS) sh.sy[lane()] = y;
+    wave_sync();
+    double o[NS];
+    generated_derivative(o, LdsSpecies{sh.sy}, sh.cs, sh.prm, (const double*)nullptr);
+    double r = o[NS - 1];
+#pragma unroll
+    for (int k = NS - 2; k >= 0; k--) r = (lane() == k) ? o[k] : r;
+    return r;
+}
+
+// DifferenceQuotientJacobian (ODESolverCVODE.cpp:496-537) into sh.J: lane j evaluates the
+// perturbed state of column j
+template <int NS, int NP, int NC, class SH, class S>
+BDF_INL void dq_jacobian(SH& sh, const S& s, double y, double fy)
+{
+    const double p = fy * s.ewt;
+    const double fnorm = sqrt(lane_sum<NS>(sh, p * p) / NS);
+    const double srur = 1.4901161193847656e-08;  // SUNRsqrt(DBL_EPSILON)
+    const double minInc = (fnorm != 0.0) ? (1000.0 * fabs(s.h) * UROUND * NS * fnorm) : 1.0;
+    const double inc = fmax(srur * fabs(y), minInc / s.ewt);
+    wave_sync();
+    if (lane() < NS) {
+        sh.sy[lane()] = y;
+        sh.sf[lane()] = fy;
+    }
+    wave_sync();
+    double o[NS];
+    generated_derivative(o, PertSpecies{sh.sy, y + inc, lane()}, sh.cs, sh.prm, (const double*)nullptr);
+    const double inc_inv = 1.0 / inc;
+    if (lane() < NS) {
+#pragma unroll
+        for (int i = 0; i < NS; i++) sh.J[lane() * NS + i] = inc_inv * (o[i] - sh.sf[i]);
+    }
+    wave_sync();
+}
+
+// A = I - gamma J (SUNMatCopy + SUNMatScaleAddI), then PartialPivLUExtended::compute_optimized
+template <int NS, class SH>
+BDF_INL void lin_setup(SH& sh, double gamma)
+{
+    const int ln = lane();
+    wave_sync();
+    if (ln < NS) {
+        for (int j = 0; j < NS; j++) {
+            double a = (-gamma) * sh.J[j * NS + ln];
+            if (j == ln) a += 1.0;
+            sh.A[j * NS + ln] = a;
+        }
+        sh.perm[ln] = ln;
+    }
+    wave_sync();
+    for (int k = 0; k < NS; k++) {
+        // pivot: first row of the largest |A(i, k)|, i >= k (maxCoeff)
+        double v = (ln >= k && ln < NS) ? fabs(sh.A[k * NS + ln]) : -1.0;
+        int ix = ln;
+#pragma unroll
+        for (int off = 1; off < WAVE; off <<= 1) {
+            const double ov = __shfl_xor(v, off);
+            const int oi = __shfl_xor(ix, off);
+            const bool take = (ov > v) || ((ov == v) && (oi < ix));
+            v = take ? ov : v;
+            ix = take ? oi : ix;
+        }
+        const int p = __builtin_amdgcn_readfirstlane(ix);
+        const double biggest = wave_uniform(v);
+        if (biggest != 0.0) {
+            if (p != k) {
+                // swap rows k and p: lanes = columns
+                if (ln < NS) {
+                    const double a = sh.A[ln * NS + k];
+                    const double b = sh.A[ln * NS + p];
+                    sh.A[ln * NS + k] = b;
+                    sh.A[ln * NS + p] = a;
+                }
+                if (ln == 0) {
+                    const int t = sh.perm[k];
+                    sh.perm[k] = sh.perm[p];
+                    sh.perm[p] = t;
+                }
+                wave_sync();
+            }
+            const double inv = 1.0 / sh.A[k * NS + k];
+            if (ln > k && ln < NS) sh.A[k * NS + ln] *= inv;
+            wave_sync();
+        }
+        // Schur update of the columns with a non-zero pivot-row entry
+        const double lik = (ln > k && ln < NS) ? sh.A[k * NS + ln] : 0.0;
+        for (int j = k + 1; j < NS; j++) {
+            const double akj = sh.A[j * NS + k];
+            if (akj != 0.0) {
+                if (ln > k && ln < NS) sh.A[j * NS + ln] -= akj * lik;
+            }
+        }
+        wave_sync();
+    }
+}
+
+// x = A^-1 b: P b, unit-lower forward and upper backward substitution (PartialPivLU::solve)
+template <int NS, class SH>
+BDF_INL double lin_solve(SH& sh, double b)
+{
+    const int ln = lane();
+    wave_sync();
+    if (ln < NS) sh.red[ln] = b;
+    wave_sync();
+    double x = (ln < NS) ? sh.red[sh.perm[ln]] : 0.0;
+    for (int j = 0; j < NS - 1; j++) {
+        const double xj = bcast(x, j);
+        if (ln > j && ln < NS) x = x - sh.A[j * NS + ln] * xj;
+    }
+    for (int j = NS - 1; j >= 0; j--) {
+        if (ln == j) x = x / sh.A[j * NS + j];
+        const double xj = bcast(x, j);
+        if (ln < j) x = x - sh.A[j * NS + ln] * xj;
+    }
+    return x;
+}
+
+// ---- BDF (runtime order; bdf_lane.h with the state across lanes) --------------------------------
+template <class S>
+BDF_INL void ewt_set(S& s)
+{
+    s.ewt = frcp(__builtin_fma(s.rtol, fabs(s.zn[0]), s.atol));
+}
+
+template <class S>
+BDF_INL void rescale(S& s)
+{
+    double c = s.eta;
+    cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q) s.zn[CI(j)] *= c;
+        c = s.eta * c;
+    });
+    s.h = s.hscale * s.eta;
+    s.hscale = s.h;
+}
+
+template <class S>
+BDF_INL void predict(S& s)
+{
+    s.tn += s.h;
+    cfor<1, QMAX + 1>([&](auto k) __attribute__((always_inline)) {
+        cfor_down<QMAX, CI(k)>([&](auto j) __attribute__((always_inline)) {
+            if (CI(j) <= s.q) s.zn[CI(j) - 1] += s.zn[CI(j)];
+        });
+    });
+}
+
+template <class S>
+BDF_INL void restore(S& s, double saved_t)
+{
+    s.tn = saved_t;
+    cfor<1, QMAX + 1>([&](auto k) __attribute__((always_inline)) {
+        cfor_down<QMAX, CI(k)>([&](auto j) __attribute__((always_inline)) {
+            if (CI(j) <= s.q) s.zn[CI(j) - 1] -= s.zn[CI(j)];
+        });
+    });
+}
+
+template <class S>
+BDF_INL double znq_of(const S& s, int q)
+{
+    double v = 0.0;
+    cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { v = (q == CI(j)) ? s.zn[CI(j)] : v; });
+    return v;
+}
+
+template <class S>
+BDF_INL void increase_bdf(S& s)
+{
+    double alpha0, alpha1, prod, xi, xiold, hsum, A1;
+    double l[QMAX + 1];
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = 0.0; });
+    l[2] = alpha1 = prod = xiold = 1.0;
+    alpha0 = -1.0;
+    hsum = s.hscale;
+    cfor<1, QMAX - 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) < s.q) {
+            hsum += s.tau[CI(j) + 1];
+            xi = fdiv(hsum, s.hscale);
+            prod *= xi;
+            alpha0 -= 1.0 / (CI(j) + 1);
+            alpha1 += frcp(xi);
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xiold, l[CI(i) - 1]); });
+            xiold = xi;
+        }
+    });
+    A1 = fdiv(-alpha0 - alpha1, prod);
+    const double znL = A1 * s.zn[QMAX];
+    cfor<2, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) == s.q + 1)
+            s.zn[CI(j)] = znL;
+        else if (CI(j) <= s.q)
+            s.zn[CI(j)] = __builtin_fma(l[CI(j)], znL, s.zn[CI(j)]);
+    });
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
+}
+
+template <class S>
+BDF_INL void decrease_bdf(S& s)
+{
+    double l[QMAX + 1];
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = 0.0; });
+    l[2] = 1.0;
+    double hsum = 0.0;
+    cfor<1, QMAX - 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q - 2) {
+            hsum += s.tau[CI(j)];
+            const double xi = fdiv(hsum, s.hscale);
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xi, l[CI(i) - 1]); });
+        }
+    });
+    const double znq = znq_of(s, s.q);
+    cfor<2, QMAX>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) < s.q) s.zn[CI(j)] = __builtin_fma(-l[CI(j)], znq, s.zn[CI(j)]);
+    });
+    cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
+}
+
+template <class S>
+BDF_INL void adjust_order(S& s, int deltaq)
+{
+    if ((s.q == 2) && (deltaq != 1)) return;
+    if (deltaq == 1)
+        increase_bdf(s);
+    else if (deltaq == -1)
+        decrease_bdf(s);
+}
+
+template <class S>
+BDF_INL int get_dky(const S& s, double t, double& dky)
+{
+    double tfuzz = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.hu));
+    if (s.hu < 0.0) tfuzz = -tfuzz;
+    const double tp = s.tn - s.hu - tfuzz;
+    const double tn1 = s.tn + tfuzz;
+    if ((t - tp) * (t - tn1) > 0.0) return CV_BAD_T;
+    const double sv = fdiv(t - s.tn, s.h);
+    double c[QMAX + 1];
+    c[0] = 1.0;
+    cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { c[CI(j)] = c[CI(j) - 1] * sv; });
+    dky = 0.0;
+    cfor_down<QMAX, 0>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q) dky = __builtin_fma(c[CI(j)], s.zn[CI(j)], dky);
+    });
+    return CV_SUCCESS;
+}
+
+template <class S>
+BDF_INL double set_bdf(S& s)
+{
+    const int q = s.q;
+    double alpha0, alpha0_hat, xi_inv, xistar_inv, hsum;
+    s.l[0] = s.l[1] = xi_inv = xistar_inv = 1.0;
+    cfor<2, QMAX + 1>([&](auto i) __attribute__((always_inline)) {
+        if (CI(i) <= q) s.l[CI(i)] = 0.0;
+    });
+    alpha0 = alpha0_hat = -1.0;
+    hsum = s.h;
+    if (q > 1) {
+        cfor<2, QMAX>([&](auto j) __attribute__((always_inline)) {
+            if (CI(j) < q) {
+                hsum += s.tau[CI(j) - 1];
+                xi_inv = fdiv(s.h, hsum);
+                alpha0 -= 1.0 / CI(j);
+                cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xi_inv, s.l[CI(i)]); });
+            }
+        });
+        alpha0 -= recip_int(q);
+        xistar_inv = -s.l[1] - alpha0;
+        hsum += sel(s.tau, q - 1);
+        xi_inv = fdiv(s.h, hsum);
+        alpha0_hat = -s.l[1] - xi_inv;
+        cfor_down<QMAX, 1>([&](auto i) __attribute__((always_inline)) {
+            if (CI(i) <= q) s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xistar_inv, s.l[CI(i)]);
+        });
+    }
+    const double A1 = 1.0 - alpha0_hat + alpha0;
+    const double A2 = __builtin_fma((double)q, A1, 1.0);
+    const double lq = sel(s.l, q);
+    s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
+    s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
+    if (s.qwait == 1) {
+        if (q > 1) {
+            const double C = fdiv(xistar_inv, lq);
+            const double A3 = alpha0 + recip_int(q);
+            const double A4 = alpha0_hat + xi_inv;
+            const double Cpinv = fdiv_c(1.0 - A4 + A3, A3, tq_ra3(q));
+            s.tq[1] = fabs(C * Cpinv);
+        } else {
+            s.tq[1] = 1.0;
+        }
+        hsum += sel(s.tau, q);
+        xi_inv = fdiv(s.h, hsum);
+        const double A5 = alpha0 - recip_int(q + 1);
+        const double A6 = alpha0_hat - xi_inv;
+        const double Cppinv = fdiv(1.0 - A6 + A5, A2);
+        s.tq[3] = fabs(fdiv(Cppinv, xi_inv * (double)(q + 2) * A5));
+    }
+    const double rl1 = frcp(s.l[1]);
+    s.gamma = s.h * rl1;
+    if (s.nst == 0) s.gammap = s.gamma;
+    s.gamrat = (s.nst > 0) ? fdiv(s.gamma, s.gammap) : 1.0;
+    return rl1;
+}
+
+// Newton iteration of cvNls (sunnonlinsol_newton.c:183-322, cvode_nls.c, cvode_ls.c:1415-1663)
+template <int NS, int NP, int NC, class SH, class S>
+BDF_INL bool newton(SH& sh, S& s, double rl1, int convfail, bool callSetup)
+{
+    bool jbad = false;
+    double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
+    int curiter = 0;
+    for (;;) {
+        const double y = s.zn[0] + s.acor;
+        const double f = rhs_v<NS, NP, NC>(sh, y);
+        double delta = __builtin_fma(rl1, s.zn[1], s.acor);
+        delta = __builtin_fma(-s.gamma, f, delta);
+        if (callSetup) {
+            if (jbad) convfail = CONV_BAD_J;
+            const double dgamma = fabs(fdiv(s.gamma, s.gammap) - 1.0);
+            const bool jnew = (s.nst == 0) || (s.nst > s.nstlj + CVLS_MSBJ) ||
+                              ((convfail == CONV_BAD_J) && (dgamma < CVLS_DGMAX)) || (convfail == CONV_OTHER);
+            if (jnew) {
+                s.nstlj = s.nst;
+                dq_jacobian<NS, NP, NC>(sh, s, y, f);
+            }
+            lin_setup<NS>(sh, s.gamma);
+            s.nls_jcur = jnew;
+            s.gamrat = 1.0;
+            cscale = 1.0;
+            s.gammap = s.gamma;
+            s.crate = 1.0;
+            s.nstlp = s.nst;
+            callSetup = false;
+            curiter = 0;
+        }
+        double x = lin_solve<NS>(sh, -delta);
+        if (s.gamrat != 1.0) x *= cscale;
+        s.acor += x;
+        const double del = wrms<NS>(sh, x, s.ewt);
+        if (curiter > 0) s.crate = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
+        if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
+            s.acnrm = (curiter == 0) ? del : wrms<NS>(sh, s.acor, s.ewt);
+            s.nls_jcur = 0;
+            return true;
+        }
+        bool fail = (curiter >= 1) && (del > RDIV * s.delp);
+        if (!fail) {
+            s.delp = del;
+            curiter++;
+            fail = (curiter >= NLS_MAXCOR);
+            if (!fail) continue;
+        }
+        if (!s.nls_jcur) {
+            callSetup = true;
+            jbad = true;
+            s.acor = 0.0;
+            continue;
+        }
+        return false;
+    }
+}
+
+// cvHin (cvode.c:1884-1990)
+template <int NS, int NP, int NC, class SH, class S>
+BDF_INL int hin(SH& sh, S& s, double tout)
+{
+    const double tdiff = tout - s.tn;
+    if (tdiff == 0.0) return CV_TOO_CLOSE;
+    const int sign = (tdiff > 0.0) ? 1 : -1;
+    const double tdist = fabs(tdiff);
+    const double tround = UROUND * SUNMAX(fabs(s.tn), fabs(tout));
+    if (tdist < 2.0 * tround) return CV_TOO_CLOSE;
+    const double hlb = HLB_FACTOR * tround;
+    double t1 = frcp(s.ewt);
+    t1 = __builtin_fma(HUB_FACTOR, fabs(s.zn[0]), t1);
+    const double r = fdiv(fabs(s.zn[1]), t1);
+    wave_sync();
+    sh.red[lane()] = r;
+    wave_sync();
+    double hub_inv = sh.red[0];
+    for (int i = 1; i < NS; i++) {
+        const double ri = sh.red[i];
+        hub_inv = (ri > hub_inv) ? ri : hub_inv;
+    }
+    double hub = HUB_FACTOR * tdist;
+    if (hub * hub_inv > 1.0) hub = frcp(hub_inv);
+    double hg = fsqrt(hlb * hub);
+    if (hub < hlb) {
+        s.h = (sign == -1) ? -hg : hg;
+        return CV_SUCCESS;
+    }
+    double hnew = hg;
+    for (int count1 = 1; count1 <= MAX_ITERS; count1++) {
+        const double hgs = hg * sign;
+        const double yy = __builtin_fma(hgs, s.zn[1], s.zn[0]);
+        double tv = rhs_v<NS, NP, NC>(sh, yy);
+        const double a = frcp(hgs);
+        tv = a * (tv - s.zn[1]);
+        const double yddnrm = wrms<NS>(sh, tv, s.ewt);
+        hnew = (yddnrm * hub * hub > 2.0) ? fsqrt(fdiv(2.0, yddnrm)) : fsqrt(hg * hub);
+        if (count1 == MAX_ITERS) break;
+        const double hrat = fdiv(hnew, hg);
+        if ((hrat > 0.5) && (hrat < 2.0)) break;
+        if ((count1 > 1) && (hrat > 2.0)) {
+            hnew = hg;
+            break;
+        }
+        hg = hnew;
+    }
+    double h0 = H_BIAS * hnew;
+    if (h0 < hlb) h0 = hlb;
+    if (h0 > hub) h0 = hub;
+    if (sign == -1) h0 = -h0;
+    s.h = h0;
+    return CV_SUCCESS;
+}
+
+constexpr double ONEPSM = 1.000001;
+
+// CVode(..., CV_ONE_STEP) without tstop (cells have no discontinuities without treatment
+// trajectories); returns tret and the state in s.zn[0]
+template <int NS, int NP, int NC, class SH, class S>
+BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
+{
+    if (s.nst == 0) {
+        s.tretlast = tret = s.tn;
+        ewt_set(s);
+        s.nstlj = 0;
+        s.nls_jcur = 0;
+        s.zn[1] = rhs_v<NS, NP, NC>(sh, s.zn[0]);
+        const int hflag = hin<NS, NP, NC>(sh, s, tout);
+        if (hflag != CV_SUCCESS) return hflag;
+        // hmax_inv = 0 (no clamp); |h| < hmin -> hmin (cvode.c:1121-1124)
+        if (fabs(s.h) < s.hmin) s.h *= s.hmin / fabs(s.h);
+        s.hscale = s.h;
+        s.hprime = s.h;
+        s.zn[1] *= s.h;
+    } else {
+        const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+        if (fabs(s.tn - s.tretlast) > troundoff) {
+            s.tretlast = tret = s.tn;
+            return CV_SUCCESS;
+        }
+        ewt_set(s);
+    }
+    {
+        const double p = s.zn[0] * s.ewt;
+        const double ss = lane_sum<NS>(sh, p * p);
+        if (ss > (double)NS * (1.0 / (UROUND * UROUND))) {
+            s.tretlast = tret = s.tn;
+            return CV_TOO_MUCH_ACC;
+        }
+    }
+    const double saved_t = s.tn;
+    int ncf = 0, nef = 0, nflag = FIRST_CALL;
+    bool do_rescale = false;
+    if ((s.nst > 0) && (s.hprime != s.h)) {
+        if (s.qprime != s.q) {
+            adjust_order(s, s.qprime - s.q);
+            s.q = s.qprime;
+            s.L = s.q + 1;
+            s.qwait = s.L;
+        }
+        do_rescale = true;
+    }
+    double dsm = 0.0;
+    for (;;) {
+        if (do_rescale) rescale(s);
+        do_rescale = true;
+        predict(s);
+        const double rl1 = set_bdf(s);
+        const int convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
+        const bool callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (s.nst == 0) ||
+                               (s.nst >= s.nstlp + MSBP) || (fabs(s.gamrat - 1.0) > DGMAX);
+        s.acor = 0.0;
+        const bool conv = newton<NS, NP, NC>(sh, s, rl1, convfail, callSetup);
+        if (conv) {
+            dsm = s.acnrm * s.tq[2];
+            if (dsm <= 1.0) break;
+        }
+        restore(s, saved_t);
+        if (!conv) {
+            // cvHandleNFlag (cvode.c:2886-2910)
+            ncf++;
+            s.etamax = 1.0;
+            if ((fabs(s.h) <= s.hmin * ONEPSM) || (ncf == MXNCF)) return CV_CONV_FAILURE;
+            s.eta = SUNMAX(ETACF, (s.hmin / fabs(s.h)));
+            nflag = PREV_CONV_FAIL;
+            continue;
+        }
+        // cvDoErrorTest (cvode.c:2958-3030)
+        nef++;
+        nflag = PREV_ERR_FAIL;
+        if ((fabs(s.h) <= s.hmin * ONEPSM) || (nef == MXNEF)) return CV_ERR_FAILURE;
+        s.etamax = 1.0;
+        if (nef <= MXNEF1) {
+            double eta = eta_from(BIAS2 * dsm, s.L);
+            eta = SUNMAX(ETAMIN, SUNMAX(eta, (s.hmin / fabs(s.h))));
+            if (nef >= SMALL_NEF) eta = SUNMIN(eta, ETAMXF);
+            s.eta = eta;
+            continue;
+        }
+        if (s.q > 1) {
+            s.eta = SUNMAX(ETAMIN, (s.hmin / fabs(s.h)));
+            adjust_order(s, -1);
+            s.L = s.q;
+            s.q--;
+            s.qwait = s.L;
+            continue;
+        }
+        s.eta = SUNMAX(ETAMIN, (s.hmin / fabs(s.h)));
+        s.h *= s.eta;
+        s.hscale = s.h;
+        s.qwait = LONG_WAIT;
+        const double tv = rhs_v<NS, NP, NC>(sh, s.zn[0]);
+        s.zn[1] = s.h * tv;
+        do_rescale = false;
+    }
+    // cvCompleteStep
+    s.nst++;
+    s.hu = s.h;
+    cfor_down<QMAX, 2>([&](auto i) __attribute__((always_inline)) {
+        if (CI(i) <= s.q) s.tau[CI(i)] = s.tau[CI(i) - 1];
+    });
+    if ((s.q == 1) && (s.nst > 1)) s.tau[2] = s.tau[1];
+    s.tau[1] = s.h;
+    cfor<0, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q) s.zn[CI(j)] = __builtin_fma(s.l[CI(j)], s.acor, s.zn[CI(j)]);
+    });
+    s.qwait--;
+    if ((s.qwait == 1) && (s.q != QMAX)) {
+        s.zn[QMAX] = s.acor;
+        s.saved_tq5 = s.tq[5];
+    }
+    // cvPrepareNextStep
+    if (s.etamax == 1.0) {
+        s.qwait = SUNMAX(s.qwait, 2);
+        s.qprime = s.q;
+        s.hprime = s.h;
+        s.eta = 1.0;
+    } else {
+        const double etaq = eta_from(BIAS2 * dsm, s.L);
+        double eta = etaq;
+        s.qprime = s.q;
+        if (s.qwait == 0) {
+            s.qwait = 2;
+            double etaqm1 = 0.0, etaqp1 = 0.0;
+            if (s.q > 1) etaqm1 = eta_from(BIAS1 * wrms<NS>(sh, znq_of(s, s.q), s.ewt) * s.tq[1], s.q);
+            if ((s.q != QMAX) && (s.saved_tq5 != 0.0)) {
+                const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), s.L);
+                const double tv = __builtin_fma(-cquot, s.zn[QMAX], s.acor);
+                etaqp1 = eta_from(BIAS3 * wrms<NS>(sh, tv, s.ewt) * s.tq[3], s.L + 1);
+            }
+            const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
+            if (etam < THRESH) {
+                eta = 1.0;
+            } else if (etam == etaq) {
+                eta = etaq;
+            } else if (etam == etaqm1) {
+                eta = etaqm1;
+                s.qprime = s.q - 1;
+            } else {
+                eta = etaqp1;
+                s.qprime = s.q + 1;
+                s.zn[QMAX] = s.acor;
+            }
+        }
+        if (eta < THRESH) {
+            s.eta = 1.0;
+            s.hprime = s.h;
+        } else {
+            s.eta = SUNMIN(eta, s.etamax);
+            s.hprime = s.h * s.eta;
+        }
+    }
+    s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
+    s.acor *= s.tq[2];
+    s.tretlast = tret = s.tn;
+    return CV_SUCCESS;
+}
+
+// get_threshold_crossing_time in the non-stored mode (see oracle/cellpop_ref.cpp): the
+// interpolant of the unused buffer is 0, so the bisection only walks to one end
+BDF_INL double crossing_time(double t, double prev, double threshold, bool above)
+{
+    double dt = (t - prev) * 0.5;
+    double time = prev + dt;
+    for (int it = 0; it < 10; it++) {
+        const double x = 0.0;
+        dt *= 0.5;
+        const bool down = above ? (x > threshold) : (x < threshold);
+        time = down ? time - dt : time + dt;
+    }
+    return time;
+}
+
+}  // namespace cpk
+
+// One cell per workgroup (64 lanes): Cell::Simulate -> ODESolver::SolveReturnSolution ->
+// ODESolverCVODE::Solve with the integration-step callback, then the values the experiment's
+// data likelihoods read (GetInterpolatedSpeciesValue) at every output entry.
+extern "C" __global__ __launch_bounds__(64) void cp_solve_kernel(cpk::CpSolveArgs a)
+{
+    using namespace cpk;
+    constexpr int NS = CP_NS, NP = CP_NP, NC = CP_NC;
+    constexpr int MM = CP_M;
+    __shared__ Shared<NS, NP, NC, MM> sh;
+    const int wi = (int)blockIdx.x;
+    if (wi >= a.n_work) return;
+    const int slot = a.work[wi];
+    const int ln = lane();
+    if (ln < NP) sh.prm[ln] = a.params[(size_t)slot * NP + ln];
+    if (ln < NC) sh.cs[ln] = a.constant_species[ln];
+    const double creation = a.creation[slot];
+    const double y0 = (ln < NS) ? a.y0[(size_t)slot * NS + ln] : 0.0;
+    const int M = MM;
+    double* outv = sh.outl;
+    for (int k = ln; k < M; k += WAVE) outv[k] = __builtin_nan("");
+    wave_sync();
+
+    // Cell::Simulate (Cell.cpp:193-210)
+    double previous_step_time = 0.0;
+    double sim_end = a.end_time - creation;
+    if (M > 0) sim_end = fmax(sim_end, a.output_times[M - 1] - creation);
+    double ev[5];
+    for (int k = 0; k < 5; k++) ev[k] = __builtin_nan("");
+    bool divided = false, died = false, ok = true;
+    int nst = 0;
+    // SolveReturnSolution: output times before the cell's t = 0 + DBL_EPSILON get y0
+    int ti = 0;
+    while (ti < M && a.output_times[ti] - creation < 2.220446049250313e-16) {
+        const int sp = a.output_species[ti];
+        if (sp >= 0 && ln == sp) outv[ti] = y0;
+        ti++;
+    }
+    double yend = y0;
+    if (ti < M) {
+        GenState<NS> s;
+        s.rtol = a.rtol;
+        s.atol = a.atol;
+        s.hmin = a.hmin;
+        cfor<0, QMAX + 1>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j)] = 0.0; });
+        cfor<0, QMAX + 2>([&](auto j) __attribute__((always_inline)) { s.tau[CI(j)] = 0.0; });
+        cfor<0, 6>([&](auto j) __attribute__((always_inline)) { s.tq[CI(j)] = 0.0; });
+        cfor<0, QMAX + 1>([&](auto j) __attribute__((always_inline)) { s.l[CI(j)] = 0.0; });
+        s.h = s.hprime = s.eta = s.hscale = s.tretlast = 0.0;
+        s.gamma = s.gammap = s.gamrat = s.crate = s.delp = s.acnrm = s.saved_tq5 = 0.0;
+        s.crate = 1.0;
+        s.qprime = 1;
+        s.nstlj = 0;
+        s.nls_jcur = 0;
+        s.ewt = 0.0;
+        s.acor = 0.0;
+        // CVodeReInit(0, y0)
+        s.tn = 0.0;
+        s.q = 1;
+        s.L = 2;
+        s.qwait = 2;
+        s.etamax = ETAMX1;
+        s.hu = 0.0;
+        s.zn[0] = y0;
+        s.nst = 0;
+        s.nstlp = 0;
+        double end_time = a.output_times[M - 1] - creation;
+        double t = 0.0;
+        int tpi = ti;
+        for (;;) {
+            double tret;
+            const int r = cvode_one_step<NS, NP, NC>(sh, s, end_time, tret);
+            if (r < 0) {
+                ok = false;
+                break;
+            }
+            t = tret;
+            nst++;
+            while (tpi < M && tret >= a.output_times[tpi] - creation) {
+                double dky;
+                if (get_dky(s, a.output_times[tpi] - creation, dky) != CV_SUCCESS) {
+                    ok = false;
+                    break;
+                }
+                const int sp = a.output_species[tpi];
+                if (sp >= 0 && ln == sp) outv[tpi] = dky;
+                tpi++;
+            }
+            if (!ok) break;
+            // Cell::integration_step_cb (Cell.cpp:463-538)
+            const double y = s.zn[0];
+            bool cont = true;
+            if (a.ev[0] >= 0 && ev[0] != ev[0] && bcast(y, a.ev[0]) > 1e-4) ev[0] = crossing_time(t, previous_step_time, 1e-4, true);
+            if (a.ev[1] >= 0 && ev[1] != ev[1] && bcast(y, a.ev[1]) > 1.95) ev[1] = crossing_time(t, previous_step_time, 1.95, true);
+            if (a.ev[2] >= 0 && ev[2] != ev[2] && bcast(y, a.ev[2]) > 0.5) ev[2] = crossing_time(t, previous_step_time, 0.5, true);
+            if (a.ev[3] >= 0 && ev[3] != ev[3] && bcast(y, a.ev[3]) < 0.5) ev[3] = crossing_time(t, previous_step_time, 0.5, false);
+            if (a.ev[4] >= 0 && ev[4] != ev[4] && bcast(y, a.ev[4]) > 1e-3) {
+                ev[4] = crossing_time(t, previous_step_time, 1e-3, true);
+                sim_end = fmax(sim_end, ev[4] + a.past_cs);
+                end_time = sim_end;
+            }
+            if (a.divide_cells && a.ev[5] >= 0 && bcast(y, a.ev[5]) > 1.0) {
+                sim_end = t;
+                yend = y;
+                divided = true;
+                cont = false;
+            }
+            if (a.ev[6] >= 0 && bcast(y, a.ev[6]) > 1.0) {
+                sim_end = t;
+                yend = y;
+                died = true;
+                cont = false;
+            }
+            previous_step_time = t;
+            if (!cont) break;
+            if (t >= end_time) break;
+            if (nst == a.max_steps) {
+                ok = false;
+                break;
+            }
+        }
+        if (ok && !divided && !died) {
+            // simulation_end_y = the solution at the last output time
+            double dky = 0.0;
+            get_dky(s, a.output_times[M - 1] - creation, dky);
+            yend = dky;
+        }
+    }
+    // GetInterpolatedSpeciesValue: NaN outside [0, simulation_end_time] of the cell
+    wave_sync();
+    for (int k = ln; k < M; k += WAVE) {
+        const double ct = a.output_times[k] - creation;
+        a.out_values[(size_t)slot * M + k] = (ct < 0.0 || ct > sim_end) ? __builtin_nan("") : outv[k];
+    }
+    if (ln < NS) a.end_y[(size_t)slot * NS + ln] = yend;
+    if (ln == 0) {
+        const double achieved_cell_time = (divided || died) ? sim_end : (a.output_times[M - 1] - creation);
+        a.sim_end[slot] = sim_end;
+        a.achieved[slot] = achieved_cell_time + creation;
+        // bit4: SimulateCell adds two daughters (divide_cells && divide && achieved_time < target)
+        const bool spawn = ok && divided && (achieved_cell_time + creation < a.end_time);
+        a.flags[slot] = (ok ? 1 : 0) | (divided ? 2 : 0) | (died ? 4 : 0) | ((ev[3] == ev[3]) ? 8 : 0) | (spawn ? 16 : 0);
+        for (int k = 0; k < 5; k++) a.event_times[(size_t)slot * 5 + k] = ev[k];
+        a.nsteps[slot] = nst;
+    }
+}

@@ -1,0 +1,44 @@
+// cellpop_static.h -- the model-independent cell-population kernels (cellpop_kernels.hip) and
+// their host launcher (cellpop_rt.cpp): one definition of the shared structures.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/bcm3hip.h"
+
+namespace bcm3hip {
+
+struct CpStatic {
+    int32_t NS, NC, d, M, n0, max_cells;
+    const int32_t* transforms;
+    const double* y_init;
+    int32_t n_reset;
+    const int32_t* reset_index;
+    const double* reset_value;
+    bcm3hip_value_ref entry_time;
+    int32_t sobol_dims;
+    const double* sobol;
+    const bcm3hip_value_ref* scales;
+    int32_t n_actions;
+    const bcm3hip_variability_action* actions;
+    const double* output_times;
+    int32_t n_data;
+    const bcm3hip_cellpop_data* data;  // device copy; observed / entry point to device arrays
+};
+
+// one work item = one new cell: slot, eval, parent slot (-1 = initial cell), sobol index, flags
+struct CpInitItem {
+    int32_t slot, eval, parent, sobol_ix, is_initial;
+};
+
+hipError_t launch_cp_init(const CpStatic& m, int32_t n_items, const CpInitItem* items, const double* values,
+                          double* params, double* y0, double* creation, const double* end_y, const double* achieved,
+                          hipStream_t s);
+hipError_t launch_cp_popavg(const CpStatic& m, int32_t n, const double* values, const int32_t* ncells,
+                            const int32_t* failed, const double* out_values, const double* creation,
+                            const double* sim_end, double* avg, double* logp, int32_t* status, hipStream_t s);
+// out[w] = flags[work[w]]
+hipError_t launch_cp_gather(const int32_t* work, int32_t n, const int32_t* flags, int32_t* out, hipStream_t s);
+
+}  // namespace bcm3hip

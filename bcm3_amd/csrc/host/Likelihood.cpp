@@ -1,5 +1,6 @@
 // Likelihood.cpp -- bcm3::Likelihood defaults (src/sampler/Likelihood.cpp:1-44) and the factory.
 #include "Likelihood.h"
+#include "LikelihoodCellPopulation.h"
 
 #include <cmath>
 
@@ -57,7 +58,7 @@ std::string option_get(const OptionsMap& vm, const std::string& key, const std::
 std::vector<std::string> LikelihoodFactory::SupportedTypes()
 {
     return {"pop_pk_trajectory", "pharmacokinetic_trajectory", "pharmaco_single", "pharmaco_population", "banana", "circular",
-            "dll"};
+            "cell_population", "dll"};
 }
 
 std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::string& fn,
@@ -102,10 +103,12 @@ std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::strin
         ll = std::make_shared<TestLikelihoodBanana>(sampling_threads, evaluation_threads);
     } else if (type == "circular") {
         ll = std::make_shared<TestLikelihoodCircular>(sampling_threads, evaluation_threads);
+    } else if (type == "cell_population") {
+        ll = std::make_shared<LikelihoodCellPopulation>(sampling_threads, evaluation_threads);
     } else if (type == "dll") {
         ll = std::make_shared<LikelihoodDLL>(sampling_threads, evaluation_threads);
     } else {
-        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, pharmaco_single, pharmaco_population, banana, circular, dll)",
+        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, pharmaco_single, pharmaco_population, banana, circular, cell_population, dll)",
                  type.c_str());
         return ll;
     }

@@ -1,0 +1,442 @@
+// LikelihoodCellPopulation.cpp -- see LikelihoodCellPopulation.h. File:line citations are to the
+// reference's src/cellpop unless stated otherwise.
+#include "LikelihoodCellPopulation.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <fstream>
+#include <limits>
+
+#include "json.h"
+#include "log.h"
+
+namespace bcm3 {
+
+namespace {
+constexpr double NaN = std::numeric_limits<double>::quiet_NaN();
+
+bool file_exists(const std::string& p)
+{
+    std::ifstream f(p);
+    return (bool)f;
+}
+
+std::string resolve(const std::string& fn, const OptionsMap& vm)
+{
+    if (file_exists(fn)) return fn;
+    const std::string alt = option_get(vm, "likelihood_dir", ".") + "/" + fn;
+    return file_exists(alt) ? alt : fn;
+}
+
+bool parse_double(const std::string& s, double& v)
+{
+    char* end = nullptr;
+    v = strtod(s.c_str(), &end);
+    if (end == s.c_str()) return false;
+    while (*end && std::isspace((unsigned char)*end)) end++;
+    return *end == '\0';
+}
+
+// Joe & Kuo (2008) new-joe-kuo-6.21201, dimensions 2..13: (s, a, m_1..m_s)
+struct JK {
+    int s, a;
+    unsigned m[5];
+};
+const JK kJoeKuo[] = {{1, 0, {1}},          {2, 1, {1, 3}},          {3, 1, {1, 3, 1}},        {3, 2, {1, 1, 1}},
+                      {4, 1, {1, 1, 3, 3}}, {4, 4, {1, 3, 5, 13}},   {5, 2, {1, 1, 5, 5, 17}}, {5, 4, {1, 1, 5, 5, 5}},
+                      {5, 7, {1, 1, 7, 11, 19}}, {5, 11, {1, 1, 5, 1, 1}}, {5, 13, {1, 1, 1, 3, 11}}, {5, 14, {1, 3, 5, 5, 31}}};
+}  // namespace
+
+std::vector<double> SobolPoints(size_t points, size_t dims)
+{
+    std::vector<double> out(points * dims);
+    if (dims == 0) return out;
+    const int bits = 64;
+    std::vector<std::vector<uint64_t>> v(dims, std::vector<uint64_t>(bits));
+    for (size_t d = 0; d < dims; d++) {
+        if (d == 0) {
+            for (int k = 0; k < bits; k++) v[d][k] = (uint64_t)1 << (bits - 1 - k);
+            continue;
+        }
+        const JK& jk = kJoeKuo[d - 1];
+        std::vector<uint64_t> m(jk.m, jk.m + jk.s);
+        for (int k = jk.s; k < bits; k++) {
+            uint64_t x = m[k - jk.s] ^ (m[k - jk.s] << jk.s);
+            for (int j = 1; j < jk.s; j++)
+                if ((jk.a >> (jk.s - 1 - j)) & 1) x ^= m[k - j] << j;
+            m.push_back(x);
+        }
+        for (int k = 0; k < bits; k++) v[d][k] = m[k] << (bits - 1 - k);
+    }
+    std::vector<uint64_t> state(dims, 0);
+    for (size_t i = 0; i < points; i++) {
+        int c = 0;
+        for (size_t x = i; x & 1; x >>= 1) c++;
+        for (size_t d = 0; d < dims; d++) {
+            state[d] ^= v[d][c];
+            out[i * dims + d] = (double)state[d] * 5.42101086242752217e-20;  // 2^-64
+        }
+    }
+    return out;
+}
+
+LikelihoodCellPopulation::LikelihoodCellPopulation(size_t sampling_threads, size_t evaluation_threads) {}
+
+bool LikelihoodCellPopulation::ParseRef(const std::string& s, bcm3hip_value_ref& r) const
+{
+    // ValueReference::Load (ValueReference.cpp:16-41): sampled variable, else a number
+    const size_t ix = varset->GetVariableIndex(s, false);
+    if (ix != SIZE_MAX) {
+        r = bcm3hip_value_ref{BCM3HIP_REF_VARIABLE, (int32_t)ix, 0.0};
+        return true;
+    }
+    double v;
+    if (!parse_double(s, v)) {
+        LOGERROR("Could not find variable for parameter \"%s\", and also could not cast it to a constant real value", s.c_str());
+        return false;
+    }
+    r = bcm3hip_value_ref{BCM3HIP_REF_FIXED, -1, v};
+    return true;
+}
+
+// CellPopulationLikelihood::Initialize (CellPopulationLikelihood.cpp:19-44)
+bool LikelihoodCellPopulation::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& likelihood_node,
+                                          const OptionsMap& vm)
+{
+    varset = vs;
+    host_only = option_get(vm, "backend", "") == "none";
+    std::vector<const XmlNode*> exps = likelihood_node.children_named("experiment");
+    if (exps.size() != 1) {
+        LOGERROR("cell_population: exactly one <experiment> is supported (got %zu)", exps.size());
+        return false;
+    }
+    try {
+        if (!LoadExperiment(*exps[0], vm)) return false;
+    } catch (XmlError& e) {
+        LOGERROR("Error parsing likelihood file: %s", e.what.c_str());
+        return false;
+    }
+    return OpenDevice(vm);
+}
+
+// Experiment::Load + Initialize (Experiment.cpp:404-633)
+bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMap& vm)
+{
+    name = ex.get("name");
+    const std::string model_file = resolve(ex.get("model_file"), vm);
+    const std::string data_file = ex.has_attr("data_file") ? ex.get("data_file") : std::string();
+    const std::string solver_type = ex.has_attr("solver_type") ? ex.get("solver_type") : std::string("CVODE");
+    if (solver_type != "CVODE") {
+        LOGERROR("cell_population: solver_type \"%s\" is not supported (CVODE only)", solver_type.c_str());
+        return false;
+    }
+    const double feps4 = 4 * (double)std::numeric_limits<float>::epsilon();
+    hmin = ex.get_double("solver_min_timestep", 1e-8);
+    const double hmax = ex.get_double("solver_max_timestep", std::numeric_limits<double>::infinity());
+    if (!std::isinf(hmax)) {
+        LOGERROR("cell_population: a finite solver_max_timestep is not supported");
+        return false;
+    }
+    max_steps = (int32_t)ex.get_long("solver_max_steps", 10000);
+    atol = ex.get_double("solver_absolute_tolerance", feps4);
+    rtol = ex.get_double("solver_relative_tolerance", feps4);
+
+    std::string err;
+    if (!sbml.LoadSBML(model_file, err)) {
+        LOGERROR("%s", err.c_str());
+        return false;
+    }
+    num_cells = (int32_t)ex.get_long("num_cells", 1);
+    max_cells = (int32_t)ex.get_long("max_cells", 20);
+    divide_cells = ex.get_bool("divide_cells", true);
+    trailing = ex.get_double("trailing_simulation_time", 0.0);
+    past_cs = ex.get_double("simulate_past_chromatid_separation_time", 0.0);
+
+    for (const auto& c : ex.children) {
+        if (c->name == "set_parameter") {
+            const std::string p = c->get("parameter_name");
+            if (!sbml.HasParameter(p)) {
+                LOGERROR("Fixed parameter value requested for \"%s\", but there is no parameter with that ID in the SBML model", p.c_str());
+                return false;
+            }
+            forced[p] = c->get_double("value");
+        } else if (c->name == "set_species" || c->name == "experiment_specific_parameter" ||
+                   c->name == "treatment_trajectory") {
+            LOGERROR("cell_population: <%s> is not supported", c->name.c_str());
+            return false;
+        }
+    }
+    // cell variabilities (VariabilityDescription::Load, VariabilityDescriptionVariable::Load)
+    for (const XmlNode* cv : ex.children_named("cell_variability")) {
+        if (cv->get("distribution") != "diagonal_gaussian") {
+            LOGERROR("cell_population: only diagonal_gaussian cell variability is supported");
+            return false;
+        }
+        std::vector<VarVariable> vv;
+        for (const XmlNode* v : cv->children_named("variable")) {
+            VarVariable x;
+            x.species = v->has_attr("initial_condition_species") ? v->get("initial_condition_species") : "";
+            x.parameter = v->has_attr("model_parameter") ? v->get("model_parameter") : "";
+            x.entry_time = v->has_attr("entry_time") && !v->get("entry_time").empty();
+            const int count = (!x.species.empty()) + (!x.parameter.empty()) + (x.entry_time ? 1 : 0);
+            if (count != 1) {
+                LOGERROR("Cell variability description needs exactly one of initial_condition_species, model_parameter, entry_time");
+                return false;
+            }
+            x.only_initial = v->get_bool("only_initial_cells", x.entry_time);
+            const std::string a = v->get("apply");
+            static const std::map<std::string, int32_t> apply = {
+                {"additive", BCM3HIP_APPLY_ADDITIVE}, {"additive_log", BCM3HIP_APPLY_ADDITIVE_LOG},
+                {"additive_log2", BCM3HIP_APPLY_ADDITIVE_LOG2}, {"multiplicative", BCM3HIP_APPLY_MULTIPLICATIVE},
+                {"multiplicative_log", BCM3HIP_APPLY_MULTIPLICATIVE_LOG},
+                {"multiplicative_log2", BCM3HIP_APPLY_MULTIPLICATIVE_LOG2}, {"replace", BCM3HIP_APPLY_REPLACE}};
+            auto it = apply.find(a);
+            if (it == apply.end()) {
+                LOGERROR("Unknown variability application type \"%s\"", a.c_str());
+                return false;
+            }
+            x.apply = it->second;
+            x.negate = v->get_bool("negate", false);
+            if (!ParseRef(v->get("scale"), x.scale)) return false;
+            vv.push_back(x);
+        }
+        variabilities.push_back(vv);
+    }
+    if (!ParseRef(ex.get("entry_time"), entry_time)) return false;
+
+    // data (DataLikelihoodBase::Load, DataLikelihoodTimeCourseBase::Load,
+    // DataLikelihoodTimeCoursePopulationAverage::Load); the sidecar holds the netCDF group
+    // {"<experiment>": {"<var>": {"dims": [...], "data": [...]}}}
+    if (data_file.empty()) {
+        LOGERROR("cell_population: a data_file is required");
+        return false;
+    }
+    Json doc;
+    try {
+        doc = json_load(resolve(data_file, vm));
+    } catch (JsonError& e) {
+        LOGERROR("Failed to open data file %s: %s", data_file.c_str(), e.what.c_str());
+        return false;
+    }
+    const Json* group = doc.find(name);
+    if (!group) {
+        LOGERROR("Group \"%s\" not found in %s", name.c_str(), data_file.c_str());
+        return false;
+    }
+    for (const XmlNode* dn : ex.children_named("data")) {
+        const std::string type = dn->has_attr("type") ? dn->get("type") : std::string("time_course");
+        if (type != "time_course_population_average") {
+            LOGERROR("cell_population: data type \"%s\" is not supported (time_course_population_average only)", type.c_str());
+            return false;
+        }
+        DataLikelihood d;
+        d.data_name = dn->get("data_name");
+        d.weight = dn->get_double("weight", 1.0);
+        const std::string em = dn->has_attr("error_model") ? dn->get("error_model") : std::string("normal");
+        if (em == "normal" || em == "additive_normal")
+            d.error_model = 0;
+        else if (em == "student_t4" || em == "t4")
+            d.error_model = 1;
+        else {
+            LOGERROR("cell_population: error model \"%s\" is not supported", em.c_str());
+            return false;
+        }
+        if (dn->get_bool("relative_to_time_average", false) || dn->get_bool("use_log_ratio", false) ||
+            dn->get_bool("optimize_offset_scale", false) || dn->get_bool("include_only_cells_that_went_through_mitosis", false) ||
+            dn->has_attr("saturation_scale")) {
+            LOGERROR("cell_population: unsupported option on data \"%s\"", d.data_name.c_str());
+            return false;
+        }
+        if (!ParseRef(dn->get("stdev"), d.stdev)) return false;
+        d.offset = bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0};
+        d.scale = bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 1.0};
+        if (dn->has_attr("offset") && !ParseRef(dn->get("offset"), d.offset)) return false;
+        if (dn->has_attr("scale") && !ParseRef(dn->get("scale"), d.scale)) return false;
+        const Json* var = group->find(d.data_name);
+        const Json* dims = var ? var->find("dims") : nullptr;
+        const Json* values = var ? var->find("data") : nullptr;
+        if (!dims || !values || dims->arr.empty()) {
+            LOGERROR("Data \"%s\" not found in group \"%s\"", d.data_name.c_str(), name.c_str());
+            return false;
+        }
+        const Json* tvar = group->find(dims->arr[0].str);
+        const Json* tdata = tvar ? tvar->find("data") : nullptr;
+        if (!tdata) {
+            LOGERROR("Time dimension \"%s\" not found", dims->arr[0].str.c_str());
+            return false;
+        }
+        for (const auto& t : tdata->arr) d.times.push_back(t.as_double());
+        const size_t T = d.times.size();
+        d.R = dims->arr.size() == 1 ? 1 : (int32_t)values->arr[0].arr.size();
+        d.observed.assign((size_t)d.R * T, NaN);
+        for (size_t i = 0; i < T && i < values->arr.size(); i++)
+            for (int j = 0; j < d.R; j++)
+                d.observed[(size_t)j * T + i] = dims->arr.size() == 1 ? values->arr[i].as_double() : values->arr[i].arr[j].as_double();
+        // species reference (RequestSimulationInfo): ODE species, else constant species
+        d.species_name = dn->get("species_name");
+        size_t six = sbml.GetODEIntegratedSpeciesByName(d.species_name);
+        if (six == SIZE_MAX) {
+            LOGERROR("cell_population: \"%s\" is not an ODE-integrated species (sums, ratios and constant species are not supported)",
+                     d.species_name.c_str());
+            return false;
+        }
+        d.species_ix = (int32_t)six;
+        data.push_back(d);
+    }
+    return true;
+}
+
+// Experiment::PostInitialize (Experiment.cpp:145-237) + the flat device model
+bool LikelihoodCellPopulation::PostInitialize()
+{
+    std::string err;
+    if (!sbml.GenerateDerivative(varset->GetVariableNames(), forced, derivative_body, err)) {
+        LOGERROR("%s", err.c_str());
+        return false;
+    }
+    const size_t NS = sbml.GetNumODEIntegratedSpecies(), NC = sbml.GetNumConstantSpecies();
+    if (NS < 1 || NS > 64) {
+        LOGERROR("cell_population: %zu ODE species (1..64 supported)", NS);
+        return false;
+    }
+    // simulation time points: (data likelihood, time, time index, species), sorted stably by time
+    struct TP {
+        int dl;
+        double t;
+        int ti;
+        int species;
+    };
+    std::vector<TP> tps;
+    for (size_t k = 0; k < data.size(); k++)
+        for (size_t i = 0; i < data[k].times.size(); i++) tps.push_back(TP{(int)k, data[k].times[i], (int)i, data[k].species_ix});
+    std::stable_sort(tps.begin(), tps.end(), [](const TP& a, const TP& b) { return a.t < b.t; });
+    if (tps.empty()) {
+        LOGERROR("cell_population: no data time points");
+        return false;
+    }
+    output_times.clear();
+    output_species.clear();
+    for (auto& d : data) d.entry.assign(d.times.size(), -1);
+    for (size_t k = 0; k < tps.size(); k++) {
+        output_times.push_back(tps[k].t);
+        output_species.push_back(tps[k].species);
+        data[tps[k].dl].entry[tps[k].ti] = (int32_t)k;
+    }
+    transforms.clear();
+    for (size_t i = 0; i < varset->GetNumVariables(); i++) transforms.push_back((int32_t)varset->GetVariableTransform(i));
+    y_init.clear();
+    for (size_t i = 0; i < NS; i++) y_init.push_back(sbml.GetODEIntegratedSpecies(i).initial);
+    constant_init.clear();
+    for (size_t i = 0; i < NC; i++) constant_init.push_back(sbml.GetConstantSpecies(i).initial);
+    // daughters (Cell::SetInitialConditionsFromOtherCell, Cell.cpp:127-133): these species must exist
+    reset_index.clear();
+    reset_value.clear();
+    if (divide_cells) {
+        const std::pair<const char*, double> resets[] = {{"cytokinesis", 0.0}, {"nuclear_envelope", 1.0}, {"G1S_break", 1.0},
+                                                         {"G2_break", 1.0}, {"spindle_components", 0.0},
+                                                         {"assembled_spindle", 0.0}, {"chromatid_separation", 0.0}};
+        for (auto& r : resets) {
+            const size_t ix = sbml.GetODEIntegratedSpeciesByName(r.first);
+            if (ix == SIZE_MAX) {
+                LOGERROR("cell_population: dividing cells need an ODE species \"%s\" (Cell.cpp:127-133)", r.first);
+                return false;
+            }
+            reset_index.push_back((int32_t)ix);
+            reset_value.push_back(r.second);
+        }
+    }
+    // event species: SIMULATED-species indices applied to the ODE state, as Cell's constructor
+    // looks them up (Cell.cpp:44-50) and integration_step_cb reads them (:467-533)
+    const char* ev_names[7] = {"replicating_DNA", "replicated_DNA", "PCNA_gfp", "nuclear_envelope",
+                               "chromatid_separation", "cytokinesis", "apoptosis"};
+    int32_t events[7];
+    for (int k = 0; k < 7; k++) {
+        const size_t ix = sbml.GetSimulatedSpeciesByName(ev_names[k]);
+        events[k] = ix == SIZE_MAX ? -1 : (int32_t)ix;
+    }
+    // variabilities: Sobol table, per-dimension scales, application list in Cell::Initialize order
+    scales.clear();
+    actions.clear();
+    int dim0 = 0;
+    for (const auto& vv : variabilities) {
+        for (size_t k = 0; k < vv.size(); k++) {
+            if (vv[k].entry_time) {
+                LOGERROR("cell_population: entry_time variability is not supported");
+                return false;
+            }
+            scales.push_back(vv[k].scale);
+        }
+        for (size_t i = 0; i < varset->GetNumVariables(); i++)
+            for (size_t k = 0; k < vv.size(); k++)
+                if (!vv[k].parameter.empty() && vv[k].parameter == varset->GetVariableName(i))
+                    actions.push_back(bcm3hip_variability_action{dim0 + (int32_t)k, 0, (int32_t)i, vv[k].apply, vv[k].negate,
+                                                                 vv[k].only_initial});
+        for (size_t i = 0; i < NS; i++)
+            for (size_t k = 0; k < vv.size(); k++)
+                if (!vv[k].species.empty() && vv[k].species == sbml.GetODEIntegratedSpecies(i).name)
+                    actions.push_back(bcm3hip_variability_action{dim0 + (int32_t)k, 1, (int32_t)i, vv[k].apply, vv[k].negate,
+                                                                 vv[k].only_initial});
+        for (size_t k = 0; k < vv.size(); k++) {
+            if (!vv[k].parameter.empty() && varset->GetVariableIndex(vv[k].parameter, false) == SIZE_MAX) {
+                LOGERROR("Variability has been specified for parameter \"%s\", but the parameter is not sampled",
+                         vv[k].parameter.c_str());
+                return false;
+            }
+            if (!vv[k].species.empty() && sbml.GetODEIntegratedSpeciesByName(vv[k].species) == SIZE_MAX) {
+                LOGERROR("Could not find species \"%s\"", vv[k].species.c_str());
+                return false;
+            }
+        }
+        dim0 += (int)vv.size();
+    }
+    const int sobol_points = scales.empty() ? 0 : num_cells * 100;
+    sobol = SobolPoints(sobol_points, scales.size());
+
+    data_flat.clear();
+    for (const auto& d : data)
+        data_flat.push_back(bcm3hip_cellpop_data{(int32_t)d.times.size(), d.R, d.observed.data(), d.entry.data(), d.stdev,
+                                                 d.offset, d.scale, d.weight, d.error_model});
+    model = bcm3hip_cellpop_model{};
+    model.derivative_body = derivative_body.c_str();
+    model.NS = (int32_t)NS;
+    model.NC = (int32_t)NC;
+    model.d = (int32_t)varset->GetNumVariables();
+    model.M = (int32_t)output_times.size();
+    model.transforms = transforms.data();
+    model.y_init = y_init.data();
+    model.constant_species = constant_init.data();
+    model.output_times = output_times.data();
+    model.output_species = output_species.data();
+    model.rtol = rtol;
+    model.atol = atol;
+    model.hmin = hmin;
+    model.max_steps = max_steps;
+    model.divide_cells = divide_cells ? 1 : 0;
+    model.end_time = output_times.back() + trailing;
+    model.past_cs = past_cs;
+    for (int k = 0; k < 7; k++) model.events[k] = events[k];
+    model.n_reset = (int32_t)reset_index.size();
+    model.reset_index = reset_index.data();
+    model.reset_value = reset_value.data();
+    model.num_cells = num_cells;
+    model.max_cells = max_cells;
+    model.entry_time = entry_time;
+    model.sobol_dims = (int32_t)scales.size();
+    model.sobol_points = sobol_points;
+    model.sobol = sobol.data();
+    model.scales = scales.data();
+    model.n_actions = (int32_t)actions.size();
+    model.actions = actions.data();
+    model.n_data = (int32_t)data_flat.size();
+    model.data = data_flat.data();
+    if (host_only) return true;
+    const int r = bcm3hip_open_cellpop(device, &model, &ctx);
+    if (r) {
+        LOGERROR("bcm3hip_open_cellpop failed: %s", bcm3hip_error_string(r));
+        return false;
+    }
+    return true;
+}
+
+}  // namespace bcm3

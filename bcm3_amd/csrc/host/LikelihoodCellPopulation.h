@@ -1,0 +1,80 @@
+// LikelihoodCellPopulation.h -- likelihood type "cell_population" (CellPopulationLikelihood,
+// src/cellpop/CellPopulationLikelihood.h) on the MI355X: the experiment description of
+// Experiment::Load / PostInitialize (src/cellpop/Experiment.cpp:145-237, 404-633) is built here on
+// the host; the cells are simulated by libbcm3hip's cell-population context (bcm3hip_open_cellpop:
+// the per-model ODE kernel compiled with hipRTC, generation-by-generation division).
+//
+// Supported (the reference's options this path uses): one <experiment> with model_file, data_file
+// (a JSON sidecar with the netCDF group's variables), num_cells, max_cells, divide_cells,
+// entry_time, trailing_simulation_time, simulate_past_chromatid_separation_time, solver_* settings
+// (solver_type CVODE); <set_parameter>; <cell_variability distribution="diagonal_gaussian">;
+// <data type="time_course_population_average"> with the normal / additive_normal / student_t4
+// error models, stdev / offset / scale / weight. Not built: treatment trajectories (time-varying
+// constant species), synchronised data (time_course, time_points, duration likelihoods), the DP5
+// solver, full_gaussian variability, several experiments in one likelihood, non-sampled parameters.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "LikelihoodGPU.h"
+#include "SBMLModel.h"
+
+namespace bcm3 {
+
+class LikelihoodCellPopulation : public LikelihoodGPUBase {
+public:
+    LikelihoodCellPopulation(size_t sampling_threads, size_t evaluation_threads);
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+    bool PostInitialize() override;
+
+    const std::string& GetGeneratedCode() const { return derivative_body; }
+    const bcm3hip_cellpop_model& GetDeviceModel() const { return model; }
+
+private:
+    struct DataLikelihood {
+        std::string data_name, species_name;
+        int32_t species_ix = -1;
+        std::vector<double> times;
+        std::vector<double> observed;  // [R][T]
+        int32_t R = 0;
+        bcm3hip_value_ref stdev{}, offset{}, scale{};
+        double weight = 1.0;
+        int32_t error_model = 0;
+        std::vector<int32_t> entry;
+    };
+    bool LoadExperiment(const XmlNode& ex, const OptionsMap& vm);
+    bool ParseRef(const std::string& s, bcm3hip_value_ref& r) const;
+
+    SBMLModel sbml;
+    std::string name, derivative_body;
+    std::map<std::string, double> forced;
+    double rtol = 0, atol = 0, hmin = 0;
+    int32_t max_steps = 10000, num_cells = 1, max_cells = 20;
+    bool divide_cells = true;
+    double trailing = 0, past_cs = 0;
+    bcm3hip_value_ref entry_time{};
+    struct VarVariable {
+        std::string species, parameter;
+        bool entry_time = false, negate = false, only_initial = false;
+        int32_t apply = 0;
+        bcm3hip_value_ref scale{};
+    };
+    std::vector<std::vector<VarVariable>> variabilities;
+    std::vector<DataLikelihood> data;
+
+    // flat device model and its arrays
+    std::vector<int32_t> transforms, output_species, reset_index;
+    std::vector<double> y_init, constant_init, output_times, reset_value, sobol;
+    std::vector<bcm3hip_value_ref> scales;
+    std::vector<bcm3hip_variability_action> actions;
+    std::vector<bcm3hip_cellpop_data> data_flat;
+    bcm3hip_cellpop_model model{};
+    bool host_only = false;
+};
+
+// boost::random::sobol (Joe & Kuo 2008 direction numbers, first point skipped) through
+// uniform_01<double>: points x dims, row-major (VariabilityPseudoRandomIterator::Initialize)
+std::vector<double> SobolPoints(size_t points, size_t dims);
+
+}  // namespace bcm3

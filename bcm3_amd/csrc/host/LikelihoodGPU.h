@@ -36,6 +36,7 @@ public:
     float LastKernelMilliseconds() override;
     bool KernelTimeLog(double& total_ms, int64_t& launches, double& max_ms) override;
     bool SetBackendOption(int option, int64_t value) override;
+    bcm3hip_ctx* Context() const { return ctx; }
 
 protected:
     bool OpenDevice(const OptionsMap& vm);

@@ -1,4 +1,5 @@
 // capi.cpp -- include/bcm3.h on top of the C++ host layer.
+#include <algorithm>
 #include <cstring>
 #include <memory>
 
@@ -9,6 +10,7 @@
 #include "log.h"
 
 #include "capi_internal.h"
+#include "LikelihoodCellPopulation.h"
 
 extern "C" {
 
@@ -49,6 +51,36 @@ int bcm3_likelihood_create_ex(const char* likelihood_xml, const char* prior_xml,
         p = e + 1;
     }
     return create(likelihood_xml, prior_xml, vm, out);
+}
+
+int bcm3_likelihood_generated_code(const bcm3_likelihood* h, char* buf, size_t buflen)
+{
+    if (!h || !h->ll) return -1;
+    auto* p = dynamic_cast<bcm3::LikelihoodCellPopulation*>(h->ll.get());
+    if (!p) return -2;
+    const std::string& code = p->GetGeneratedCode();
+    if (buf && buflen) {
+        const size_t n = std::min(buflen - 1, code.size());
+        memcpy(buf, code.data(), n);
+        buf[n] = '\0';
+    }
+    return (int)code.size();
+}
+
+int bcm3_sobol_points(size_t points, size_t dims, double* out)
+{
+    const std::vector<double> v = bcm3::SobolPoints(points, dims);
+    std::copy(v.begin(), v.end(), out);
+    return 0;
+}
+
+int bcm3_likelihood_cellpop_cells(bcm3_likelihood* h, size_t item, int32_t* count, void* records, double* values,
+                                  double* end_y)
+{
+    if (!h || !h->ll) return -1;
+    auto* p = dynamic_cast<bcm3::LikelihoodCellPopulation*>(h->ll.get());
+    if (!p || !p->Context()) return -2;
+    return bcm3hip_cellpop_cells(p->Context(), item, count, (bcm3hip_cell_record*)records, values, end_y);
 }
 
 int bcm3_likelihood_popk_model(const bcm3_likelihood* h, void* model)

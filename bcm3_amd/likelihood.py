@@ -45,6 +45,8 @@ def lib() -> C.CDLL:
     L.bcm3_likelihood_kernel_time_log.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_int64),
                                                   C.POINTER(C.c_double)]
     L.bcm3_last_error.restype = C.c_char_p
+    L.bcm3_likelihood_generated_code.argtypes = [vp, C.c_char_p, sz]
+    L.bcm3_likelihood_cellpop_cells.argtypes = [vp, sz, C.POINTER(C.c_int32), vp, vp, vp]
     i32, i64, u64 = C.c_int, C.c_int64, C.c_uint64
     L.bcm3_adapt_proposals.argtypes = [i32, i32, i32, i32, i32, i32, vp, vp, vp, sz, vp, vp, u64, u64, i64, i32, vp,
                                        vp, vp, vp, vp, vp]
@@ -98,6 +100,33 @@ class Likelihood:
         if r != 0:
             _err("bcm3_likelihood_expm_pk_model", r)
         return m
+
+    def generated_code(self) -> str:
+        """cell_population: the generated_derivative body this likelihood compiled (SBMLModel::GenerateCode)."""
+        n = lib().bcm3_likelihood_generated_code(self.h, None, 0)
+        if n < 0:
+            _err("bcm3_likelihood_generated_code", n)
+        buf = C.create_string_buffer(n + 1)
+        lib().bcm3_likelihood_generated_code(self.h, buf, n + 1)
+        return buf.value.decode()
+
+    def cellpop_cells(self, item: int, M: int, NS: int):
+        """cell_population: per-cell records, data values [cells][M] and end states [cells][NS] of
+        item `item` of the last batch (bcm3hip_cellpop_cells)."""
+        rec_t = np.dtype([("creation", "f8"), ("sim_end", "f8"), ("achieved", "f8"), ("flags", "i4"), ("nsteps", "i4")])
+        count = C.c_int32()
+        r = lib().bcm3_likelihood_cellpop_cells(self.h, item, C.byref(count), None, None, None)
+        if r != 0:
+            _err("bcm3_likelihood_cellpop_cells", r)
+        n = count.value
+        rec = np.zeros(n, dtype=rec_t)
+        vals = np.empty((n, M))
+        endy = np.empty((n, NS))
+        r = lib().bcm3_likelihood_cellpop_cells(self.h, item, C.byref(count), rec.ctypes.data, vals.ctypes.data,
+                                                endy.ctypes.data)
+        if r != 0:
+            _err("bcm3_likelihood_cellpop_cells", r)
+        return rec, vals, endy
 
     def set_learning_rate(self, lr: float):
         if lib().bcm3_likelihood_set_learning_rate(self.h, lr) != 0:

@@ -41,6 +41,15 @@ int bcm3_likelihood_popk_model(const bcm3_likelihood* ll, void* model);
  * PharmacoLikelihoodSingle::PostInitialize (.cpp:78-147), into a bcm3hip_expm_pk_model. Returns
  * -2 for other likelihood types. */
 int bcm3_likelihood_expm_pk_model(const bcm3_likelihood* ll, void* model);
+/* cell_population: the generated_derivative body (SBMLModel::GenerateCode, src/sbml/SBMLModel.cpp:
+ * 291-367) this likelihood compiled; returns its length (buf may be NULL), < 0 for other types */
+int bcm3_likelihood_generated_code(const bcm3_likelihood* ll, char* buf, size_t buflen);
+/* VariabilityPseudoRandomIterator's sequence (boost::random::sobol through uniform_01, restated):
+ * points x dims, row-major */
+int bcm3_sobol_points(size_t points, size_t dims, double* out);
+/* cell_population: the cells of item `item` of the last batch (bcm3hip_cellpop_cells) */
+int bcm3_likelihood_cellpop_cells(bcm3_likelihood* ll, size_t item, int32_t* count, void* records /*bcm3hip_cell_record*/,
+                                  double* values, double* end_y);
 void bcm3_likelihood_destroy(bcm3_likelihood* ll);
 int bcm3_likelihood_num_variables(const bcm3_likelihood* ll);
 /* name of variable i (prior.xml order, repeat-expanded); returns the name length or < 0 */

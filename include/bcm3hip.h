@@ -160,6 +160,87 @@ typedef struct {
     const int32_t* obs_offset;   /* [P+1]: likewise for obs_* */
 } bcm3hip_expm_pk_model;
 
+/* ---- cell-population likelihood (type "cell_population", src/cellpop) ----------------------
+ * One Experiment of CellPopulationLikelihood (src/cellpop/CellPopulationLikelihood.cpp:82-101,
+ * Experiment.cpp:239-372, 635-782): heterogeneous cells of an SBML model integrated with CVODE
+ * BDF, dividing cells spawning two daughters, a population-average time-course data likelihood.
+ * The host layer (libbcm3.so, LikelihoodCellPopulation) derives everything below from
+ * likelihood.xml + prior.xml + the SBML file + the data file. */
+typedef struct {
+    int32_t kind; /* BCM3HIP_REF_VARIABLE: transformed variable `index`; BCM3HIP_REF_FIXED: `value`;
+                     BCM3HIP_REF_NONE: absent (offset 0, scale 1) */
+    int32_t index;
+    double value;
+} bcm3hip_value_ref;
+enum { BCM3HIP_REF_NONE = 0, BCM3HIP_REF_VARIABLE = 1, BCM3HIP_REF_FIXED = 2 };
+
+/* VariabilityDescriptionVariable::Apply types (VariabilityDescriptionVariable.cpp) */
+enum {
+    BCM3HIP_APPLY_ADDITIVE = 0, BCM3HIP_APPLY_ADDITIVE_LOG = 1, BCM3HIP_APPLY_ADDITIVE_LOG2 = 2,
+    BCM3HIP_APPLY_MULTIPLICATIVE = 3, BCM3HIP_APPLY_MULTIPLICATIVE_LOG = 4, BCM3HIP_APPLY_MULTIPLICATIVE_LOG2 = 5,
+    BCM3HIP_APPLY_REPLACE = 6
+};
+/* One application of a variability dimension in Cell::Initialize order (Cell.cpp:162-176):
+ * description by description, the sampled variables in order, then the ODE species in order. */
+typedef struct {
+    int32_t dim;          /* Sobol / pseudorandom-vector dimension */
+    int32_t target_kind;  /* 0 = sampled variable (cell parameter), 1 = ODE species initial condition */
+    int32_t target_index;
+    int32_t apply;        /* BCM3HIP_APPLY_* */
+    int32_t negate;
+    int32_t only_initial_cells;
+} bcm3hip_variability_action;
+
+/* DataLikelihoodTimeCoursePopulationAverage (one species) */
+typedef struct {
+    int32_t T;                /* time points */
+    int32_t R;                /* replicates */
+    const double* observed;   /* [R*T], NaN = missing */
+    const int32_t* entry;     /* [T] output entry (sorted simulation time point) of each time point */
+    bcm3hip_value_ref stdev, offset, scale;
+    double weight;
+    int32_t error_model;      /* 0 normal, 1 student t4 */
+} bcm3hip_cellpop_data;
+
+typedef struct {
+    const char* derivative_body; /* SBMLModel::GenerateCode's generated_derivative body */
+    int32_t NS;                  /* ODE-integrated species (<= 64) */
+    int32_t NC;                  /* constant species */
+    int32_t d;                   /* sampled variables */
+    int32_t M;                   /* output entries: the experiment's simulation time points, sorted */
+    const int32_t* transforms;   /* [d] BCM3HIP_TF_* */
+    const double* y_init;        /* [NS] SBML initial amounts */
+    const double* constant_species; /* [NC] */
+    const double* output_times;  /* [M] */
+    const int32_t* output_species; /* [M] ODE species read at each entry (-1 = none) */
+    double rtol, atol, hmin;     /* solver_relative/absolute_tolerance, solver_min_timestep */
+    int32_t max_steps;           /* solver_max_steps */
+    int32_t divide_cells;
+    double end_time;             /* last time point + trailing_simulation_time */
+    double past_cs;              /* simulate_past_chromatid_separation_time */
+    int32_t events[7];           /* replicating_DNA, replicated_DNA, PCNA_gfp, nuclear_envelope,
+                                    chromatid_separation, cytokinesis, apoptosis (-1 = absent) */
+    int32_t n_reset;             /* daughter initial conditions (SetInitialConditionsFromOtherCell) */
+    const int32_t* reset_index;
+    const double* reset_value;
+    int32_t num_cells, max_cells;
+    bcm3hip_value_ref entry_time;
+    int32_t sobol_dims, sobol_points;
+    const double* sobol;         /* [sobol_points*sobol_dims] uniforms */
+    const bcm3hip_value_ref* scales; /* [sobol_dims] log-scale of each dimension (diagonal_gaussian) */
+    int32_t n_actions;
+    const bcm3hip_variability_action* actions;
+    int32_t n_data;
+    const bcm3hip_cellpop_data* data;
+} bcm3hip_cellpop_model;
+
+/* Per-cell results of the last evaluation (bcm3hip_cellpop_cells), one record per cell slot. */
+typedef struct {
+    double creation, sim_end, achieved;
+    int32_t flags;   /* bit0 ok, bit1 divided, bit2 died, bit3 entered mitosis, bit4 spawned daughters */
+    int32_t nsteps;
+} bcm3hip_cell_record;
+
 typedef struct bcm3hip_ctx bcm3hip_ctx;
 
 /* Per-trajectory solver counters (parity/diagnostics), one record per (item, patient). */
@@ -185,6 +266,17 @@ int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* model, bcm3h
 /* pharmaco_single (PharmacoLikelihoodSingle::EvaluateLogProbability); per-item status 1 when
  * PharmacokineticModel::Solve fails (NaN state): logp = -inf */
 int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* model, bcm3hip_ctx** out);
+/* cell_population (CellPopulationLikelihood::EvaluateLogProbability with one experiment): the
+ * cell ODE kernel is compiled at open time with hipRTC for this model's generated right-hand
+ * side (the reference compiles its generated code with cmake + make and dlopen()s it,
+ * src/cellpop/SolverCodeGenerator.cpp:32-431); code objects are cached on disk
+ * ($BCM3_CODEGEN_DIR, default <library dir>/codegen). Per-item status 1 when the experiment fails
+ * (solver failure, too many cells): logp = -inf. */
+int bcm3hip_open_cellpop(int device, const bcm3hip_cellpop_model* model, bcm3hip_ctx** out);
+/* cells of item `item` of the last cellpop evaluation: *count cells, records / values[count*M]
+ * (the data likelihood's values per output entry) / end_y[count*NS] may be NULL */
+int bcm3hip_cellpop_cells(bcm3hip_ctx* ctx, size_t item, int32_t* count, bcm3hip_cell_record* records,
+                          double* values, double* end_y);
 int bcm3hip_close(bcm3hip_ctx* ctx);
 int bcm3hip_set_option(bcm3hip_ctx* ctx, int option, int64_t value);
 int bcm3hip_num_variables(const bcm3hip_ctx* ctx);

@@ -1,0 +1,458 @@
+"""TEST INFRASTRUCTURE (oracle). Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use
+this module; the product path never imports it.
+
+CPU oracle of the reference's cell-population likelihood (likelihood type "cell_population"):
+  CellPopulationLikelihood::Initialize / EvaluateLogProbability  src/cellpop/CellPopulationLikelihood.cpp:19-101
+  Experiment::Load / PostInitialize / Initialize                  src/cellpop/Experiment.cpp:145-237, 404-633
+  Experiment::EvaluateLogProbability / Simulate / SimulateCell    src/cellpop/Experiment.cpp:239-372, 635-782
+  CellPopulation::AddNewCell / CountCellsAtTime                   src/cellpop/CellPopulation.cpp:36-121
+  Cell::SetInitialConditionsFromOtherCell / Initialize            src/cellpop/Cell.cpp:79-191
+  VariabilityDescription(+Variable)::GetPseudorandomVector / Apply* (diagonal_gaussian)
+                                                                  src/cellpop/VariabilityDescription*.cpp
+  VariabilityPseudoRandomIterator (Sobol)                          src/cellpop/VariabilityPseudoRandomIterator.cpp
+  DataLikelihoodTimeCoursePopulationAverage                       src/cellpop/DataLikelihoodTimeCoursePopulationAverage.cpp
+  DataLikelihoodTimeCourseBase / DataLikelihoodBase (Normal / t4 error models)
+Each cell is integrated by oracle/_ref/libcellpopref.so (the reference's vendored CVODE + its
+PartialPivLU, see oracle/cellpop_ref.cpp) on the generated derivative (oracle/sbml_codegen.py)
+compiled for the host. The experiment logic runs here in Python in the reference's sequential
+order (the single-thread FIFO of ParallelSimulation: cells in index order, children appended).
+
+Restated without a pin (the reference gets them from Boost, absent here):
+  * the Sobol sequence: boost::random::sobol (Joe & Kuo 2008 direction numbers, the first point
+    skipped) through boost::random::uniform_01 (= x / 2^64) -- restated in sobol_points();
+  * QuantileNormal = boost::math::quantile(normal) -- scipy.special.ndtri.
+"""
+import ctypes as C
+import hashlib
+import json
+import math
+import os
+import subprocess
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+import sbml_codegen as SG
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+NAN = float("nan")
+FLT_EPS = float(np.finfo(np.float32).eps)
+
+
+class CellIn(C.Structure):
+    _fields_ = [("N", C.c_int), ("rhs", C.c_void_p), ("constant_species", C.c_void_p), ("parameters", C.c_void_p),
+                ("non_sampled_parameters", C.c_void_p), ("y0", C.c_void_p), ("creation_time", C.c_double),
+                ("end_time", C.c_double), ("M", C.c_int), ("output_times", C.c_void_p), ("output_species", C.c_void_p),
+                ("rtol", C.c_double), ("atol", C.c_double), ("hmin", C.c_double), ("hmax", C.c_double),
+                ("max_steps", C.c_int), ("divide_cells", C.c_int), ("simulate_past_chromatid_separation_time", C.c_double),
+                ("ev_replicating", C.c_int), ("ev_replicated", C.c_int), ("ev_pcna", C.c_int),
+                ("ev_nuclear_envelope", C.c_int), ("ev_chromatid_separation", C.c_int), ("ev_cytokinesis", C.c_int),
+                ("ev_apoptosis", C.c_int)]
+
+
+class CellOut(C.Structure):
+    _fields_ = [("ok", C.c_int), ("divided", C.c_int), ("died", C.c_int), ("sim_end", C.c_double),
+                ("achieved_time", C.c_double), ("event_times", C.c_double * 5), ("nsteps", C.c_long)]
+
+
+_libs = {}
+
+
+def ref_lib(variant=""):
+    """variant "" = the reference's flags; "nofma" = FMA contraction off (the build-to-build spread)"""
+    if variant not in _libs:
+        L = C.CDLL(os.path.join(HERE, "_ref", f"libcellpopref{'_' + variant if variant else ''}.so"))
+        L.cp_simulate_cell.argtypes = [C.POINTER(CellIn), C.POINTER(CellOut), C.c_void_p, C.c_void_p]
+        L.cp_simulate_cell.restype = C.c_int
+        _libs[variant] = L
+    return _libs[variant]
+
+
+def compile_derivative(body: str, variant: str = "") -> C.CDLL:
+    """The generated derivative for the host, with the reference's flags for generated code
+    (SolverCodeGenerator.cpp:326: -O3 -march=native; x86-64-v3 here so it runs on any host)."""
+    src = SG.host_translation_unit(body)
+    h = hashlib.sha1((src + variant).encode()).hexdigest()[:16]
+    d = os.path.join(HERE, "_ref", "codegen")
+    os.makedirs(d, exist_ok=True)
+    so = os.path.join(d, f"deriv_{h}.so")
+    if not os.path.exists(so):
+        cpp = os.path.join(d, f"deriv_{h}.cpp")
+        with open(cpp, "w") as f:
+            f.write(src)
+        tmp = so + f".{os.getpid()}.tmp"
+        flags = ["-ffp-contract=off"] if variant == "nofma" else []
+        subprocess.run(["g++", "-O3", "-march=x86-64-v3", *flags, "-fPIC", "-shared", "-o", tmp, cpp], check=True)
+        os.replace(tmp, so)
+    return C.CDLL(so)
+
+
+# ---- Sobol (boost::random::sobol, restated) --------------------------------------------------
+# Joe & Kuo (2008) new-joe-kuo-6.21201: dimension d >= 2 -> (s, a, m_1..m_s); dimension 1 is the
+# van der Corput sequence.
+_JOE_KUO = [(1, 0, [1]), (2, 1, [1, 3]), (3, 1, [1, 3, 1]), (3, 2, [1, 1, 1]), (4, 1, [1, 1, 3, 3]),
+            (4, 4, [1, 3, 5, 13]), (5, 2, [1, 1, 5, 5, 17]), (5, 4, [1, 1, 5, 5, 5]), (5, 7, [1, 1, 7, 11, 19]),
+            (5, 11, [1, 1, 5, 1, 1]), (5, 13, [1, 1, 1, 3, 11]), (5, 14, [1, 3, 5, 5, 31])]
+
+
+def _directions(dim, bits=64):
+    if dim == 0:
+        return [1 << (bits - 1 - k) for k in range(bits)]
+    s, a, m = _JOE_KUO[dim - 1]
+    m = list(m)
+    for k in range(s, bits):
+        v = m[k - s] ^ (m[k - s] << s)
+        for j in range(1, s):
+            if (a >> (s - 1 - j)) & 1:
+                v ^= m[k - j] << j
+        m.append(v)
+    return [(m[k] << (bits - 1 - k)) & ((1 << bits) - 1) for k in range(bits)]
+
+
+def sobol_points(n, dims):
+    """n points of boost::random::sobol(dims) through uniform_01<double>: Gray-code order, the
+    state XOR-ed with the direction of the lowest zero bit of the point counter before each point
+    (so the first point is 0.5 in every dimension), value = state * 2^-64."""
+    out = np.empty((n, dims))
+    if dims == 0:
+        return out
+    v = [_directions(d) for d in range(dims)]
+    state = [0] * dims
+    for i in range(n):
+        c = 0
+        x = i
+        while x & 1:
+            x >>= 1
+            c += 1
+        for d in range(dims):
+            state[d] ^= v[d][c]
+            out[i, d] = float(state[d]) * 2.0 ** -64
+    return out
+
+
+def quantile_normal(p):
+    from scipy.special import ndtri
+    return float(ndtri(p))
+
+
+# ---- problem set-up ---------------------------------------------------------------------------
+def fastpow10(x):
+    return math.exp(x * 2.3025850929940459)
+
+
+def transform(tf, x):
+    if tf == "log10":
+        return fastpow10(x)
+    return x
+
+
+def _bool(s, default):
+    if s is None:
+        return default
+    return s.strip().lower() in ("1", "true")
+
+
+def load_problem(likelihood_xml, prior_xml, num_cells=None, max_cells=None, variant=""):
+    root = ET.parse(prior_xml).getroot()
+    variables, transforms = [], []
+    for v in root.iter("variable"):
+        for _ in range(int(v.get("repeat", "1"))):
+            variables.append(v.get("name"))
+            transforms.append("log10" if _bool(v.get("logspace"), False) else "none")
+    base = os.path.dirname(os.path.abspath(likelihood_xml))
+    lik = ET.parse(likelihood_xml).getroot()
+    assert lik.get("type") == "cell_population"
+    exps = []
+    for ex in lik.iter("experiment"):
+        exps.append(_load_experiment(ex, base, variables, num_cells, max_cells, variant))
+    return dict(variables=variables, transforms=transforms, experiments=exps, variant=variant)
+
+
+def _ref_value(s, variables):
+    """ValueReference / DataLikelihoodBase::ParseString: sampled variable index, else a number."""
+    if s in variables:
+        return ("var", variables.index(s))
+    return ("fixed", float(s))
+
+
+def _load_experiment(ex, base, variables, num_cells, max_cells, variant=""):
+    model = SG.SBMLModel(os.path.join(base, ex.get("model_file")))
+    e = dict(name=ex.get("name"), model=model)
+    e["rtol"] = float(ex.get("solver_relative_tolerance", 4 * FLT_EPS))
+    e["atol"] = float(ex.get("solver_absolute_tolerance", 4 * FLT_EPS))
+    e["hmin"] = float(ex.get("solver_min_timestep", 1e-8))
+    e["hmax"] = float(ex.get("solver_max_timestep", "inf"))
+    e["max_steps"] = int(ex.get("solver_max_steps", 10000))
+    e["num_cells"] = int(num_cells if num_cells is not None else ex.get("num_cells", 1))
+    e["max_cells"] = int(max_cells if max_cells is not None else ex.get("max_cells", 20))
+    e["divide_cells"] = _bool(ex.get("divide_cells"), True)
+    e["trailing"] = float(ex.get("trailing_simulation_time", 0.0))
+    e["past_cs"] = float(ex.get("simulate_past_chromatid_separation_time", 0.0))
+    forced = {}
+    for sp in ex.iter("set_parameter"):
+        forced[sp.get("parameter_name")] = float(sp.get("value"))
+    e["forced"] = forced
+    # variabilities (VariabilityDescription::Load; diagonal_gaussian)
+    vds = []
+    for cv in ex.iter("cell_variability"):
+        assert cv.get("distribution") == "diagonal_gaussian"
+        vv = []
+        for v in cv.iter("variable"):
+            entry_time = v.get("entry_time", "") != ""
+            vv.append(dict(species=v.get("initial_condition_species", ""), parameter=v.get("model_parameter", ""),
+                           entry_time=entry_time, apply=v.get("apply"), scale=_ref_value(v.get("scale"), variables),
+                           negate=_bool(v.get("negate"), False),
+                           only_initial=_bool(v.get("only_initial_cells"), entry_time)))
+        vds.append(vv)
+    e["variabilities"] = vds
+    # data file (JSON sidecar with the netCDF group's variables)
+    with open(os.path.join(base, ex.get("data_file"))) as f:
+        data = json.load(f)[e["name"]]
+    dls = []
+    timepoints = []  # Experiment::simulation_timepoints: (dl index, time, time_ix, species_ix)
+    for dl in ex.iter("data"):
+        assert dl.get("type", "time_course") == "time_course_population_average"
+        var = data[dl.get("data_name")]
+        tdim = var["dims"][0]
+        times = [float(t) for t in data[tdim]["data"]]
+        obs = np.array(var["data"], dtype=float)
+        if obs.ndim == 1:
+            obs = obs[:, None]
+        obs = obs.T  # replicates x timepoints
+        sname = dl.get("species_name").strip()
+        six = model.ode_index(sname)
+        if six is None:
+            six = len(model.ode) + model.constant_index(sname)
+        em = dl.get("error_model", "normal")
+        d = dict(times=times, observed=obs, species=six, weight=float(dl.get("weight", 1.0)),
+                 stdev=_ref_value(dl.get("stdev"), variables),
+                 offset=_ref_value(dl.get("offset"), variables) if dl.get("offset") else None,
+                 scale=_ref_value(dl.get("scale"), variables) if dl.get("scale") else None,
+                 error_model={"normal": "normal", "additive_normal": "normal", "student_t4": "t4", "t4": "t4"}[em],
+                 relative_to_time_average=_bool(dl.get("relative_to_time_average"), False))
+        for ti, t in enumerate(times):
+            timepoints.append((len(dls), t, ti, six))
+        dls.append(d)
+    # bubble sort by time (stable), Experiment.cpp:593-600
+    timepoints.sort(key=lambda x: x[1])
+    e["data"] = dls
+    e["timepoints"] = timepoints
+    e["output_times"] = sorted(t[1] for t in timepoints)
+    e["entry_time"] = _ref_value(ex.get("entry_time"), variables)
+    # derivative code (SBMLModel::GenerateCode) for the host copy
+    e["derivative_body"] = model.generate_derivative(variables, forced)
+    e["deriv_lib"] = compile_derivative(e["derivative_body"], variant)
+    # event species: SIMULATED-species indices (Cell.cpp:44-50)
+    def sim_ix(name):
+        for i, s in enumerate(model.simulated):
+            if model.species[s]["name"] == name:
+                return i
+        return -1
+    e["events"] = [sim_ix(n) for n in ("replicating_DNA", "replicated_DNA", "PCNA_gfp", "nuclear_envelope",
+                                       "chromatid_separation", "cytokinesis", "apoptosis")]
+    e["reset"] = [(model.ode_index(n), v) for n, v in (("cytokinesis", 0.0), ("nuclear_envelope", 1.0), ("G1S_break", 1.0),
+                                                       ("G2_break", 1.0), ("spindle_components", 0.0),
+                                                       ("assembled_spindle", 0.0), ("chromatid_separation", 0.0))]
+    dims = sum(len(v) for v in vds)
+    e["sobol"] = sobol_points(e["num_cells"] * 100, dims) if dims else None
+    e["y_init"] = np.array([model.species[s]["initial"] for s in model.ode])
+    e["constant_init"] = np.array([model.species[s]["initial"] for s in model.constant])
+    return e
+
+
+def _apply(kind, x, value):
+    # VariabilityDescriptionVariable::Apply
+    if kind == "additive":
+        return x + value
+    if kind == "additive_log":
+        return x + math.exp(value)
+    if kind == "additive_log2":
+        return x + math.pow(2.0, value)
+    if kind == "multiplicative":
+        return x * value
+    if kind == "multiplicative_log":
+        return x * math.exp(value)
+    if kind == "multiplicative_log2":
+        return x * math.pow(2.0, value)
+    if kind == "replace":
+        return value
+    raise ValueError(kind)
+
+
+def _refval(ref, tv):
+    return tv[ref[1]] if ref[0] == "var" else ref[1]
+
+
+def _cell_init(e, prob, tv, y, sobol_ix, is_initial):
+    """Cell::Initialize: variability on parameters and initial conditions."""
+    params = np.array(tv, dtype=float)
+    y = np.array(y, dtype=float)
+    k = 0
+    for vv in e["variabilities"]:
+        # VariabilityDescription::GetPseudorandomVector (diagonal)
+        pr = []
+        for v in vv:
+            scale = _refval(v["scale"], tv)
+            pr.append(quantile_normal(e["sobol"][sobol_ix, k]) * math.exp(scale))
+            k += 1
+        for i, name in enumerate(prob["variables"]):
+            for v, r in zip(vv, pr):
+                if v["parameter"] and v["parameter"] == name and (not v["only_initial"] or is_initial):
+                    params[i] = _apply(v["apply"], params[i], -r if v["negate"] else r)
+        for i, s in enumerate(e["model"].ode):
+            name = e["model"].species[s]["name"]
+            for v, r in zip(vv, pr):
+                if v["species"] and v["species"] == name and (not v["only_initial"] or is_initial):
+                    y[i] = _apply(v["apply"], y[i], -r if v["negate"] else r)
+    return params, y
+
+
+def simulate_experiment(e, prob, values):
+    """Experiment::EvaluateLogProbability for one parameter vector: per-cell records, population
+    averages, logp."""
+    tv = [transform(tf, x) for tf, x in zip(prob["transforms"], values)]
+    model = e["model"]
+    N = len(model.ode)
+    out_times = np.array(e["output_times"], dtype=float)
+    M = len(out_times)
+    # per sorted output index: the species the data likelihoods read there
+    out_species = np.full(M, -1, dtype=np.int32)
+    for k, tp in enumerate(e["timepoints"]):
+        out_species[k] = tp[3]
+    end_time = (e["timepoints"][-1][1] if e["timepoints"] else 0.0) + e["trailing"]
+    entry_time = _refval(e["entry_time"], tv)
+    lib = ref_lib(prob.get("variant", ""))
+    rhs = C.cast(e["deriv_lib"].generated_derivative, C.c_void_p).value
+    const = np.ascontiguousarray(e["constant_init"], dtype=float)
+    cells = []  # dicts
+    fail = False
+
+    def add_cell(creation, parent, child_ix, is_initial):
+        if len(cells) == e["max_cells"]:
+            return None
+        ix = len(cells)
+        if parent is None:
+            y = e["y_init"].copy()
+            sidx = ix
+        else:
+            y = parent["end_y"].copy()
+            for r, v in e["reset"]:
+                y[r] = v
+            sidx = e["num_cells"] + parent["sobol_ix"] * 2 + child_ix
+            if e["sobol"] is not None and sidx >= e["sobol"].shape[0]:
+                return None
+        params, y = (_cell_init(e, prob, tv, y, sidx, is_initial) if e["sobol"] is not None
+                     else (np.array(tv, dtype=float), y))
+        c = dict(index=ix, creation=creation, sobol_ix=sidx, params=params, y0=y, parent=parent["index"] if parent else -1)
+        cells.append(c)
+        return c
+
+    n0 = e["num_cells"]
+    if n0 > 1:
+        for i in range(n0):
+            add_cell(entry_time, None, -1, True)
+    else:
+        add_cell(entry_time, None, -1, False)
+    if entry_time < -7.0 * 24.0 * 60.0 * 60.0:
+        return dict(ok=False, logp=-math.inf, cells=cells)
+    i = 0
+    while i < len(cells):  # FIFO: ParallelSimulation with one thread
+        c = cells[i]
+        cin = CellIn()
+        cin.N = N
+        cin.rhs = rhs
+        cin.constant_species = const.ctypes.data
+        prm = np.ascontiguousarray(c["params"])
+        y0 = np.ascontiguousarray(c["y0"])
+        cin.parameters = prm.ctypes.data
+        cin.non_sampled_parameters = None
+        cin.y0 = y0.ctypes.data
+        cin.creation_time = c["creation"]
+        cin.end_time = end_time
+        cin.M = M
+        cin.output_times = out_times.ctypes.data
+        cin.output_species = out_species.ctypes.data
+        cin.rtol, cin.atol, cin.hmin, cin.hmax = e["rtol"], e["atol"], e["hmin"], e["hmax"]
+        cin.max_steps = e["max_steps"]
+        cin.divide_cells = 1 if e["divide_cells"] else 0
+        cin.simulate_past_chromatid_separation_time = e["past_cs"]
+        (cin.ev_replicating, cin.ev_replicated, cin.ev_pcna, cin.ev_nuclear_envelope, cin.ev_chromatid_separation,
+         cin.ev_cytokinesis, cin.ev_apoptosis) = e["events"]
+        cout = CellOut()
+        vals = np.empty(M)
+        end_y = np.empty(N)
+        lib.cp_simulate_cell(C.byref(cin), C.byref(cout), vals.ctypes.data, end_y.ctypes.data)
+        c.update(ok=bool(cout.ok), divided=bool(cout.divided), died=bool(cout.died), sim_end=cout.sim_end,
+                 achieved=cout.achieved_time, events=list(cout.event_times), values=vals, end_y=end_y,
+                 nsteps=cout.nsteps)
+        if not cout.ok:
+            fail = True
+            break
+        if e["divide_cells"] and c["divided"] and c["achieved"] < end_time:
+            c1 = add_cell(c["achieved"], c, 0, False)
+            c2 = add_cell(c["achieved"], c, 1, False)
+            if c1 is None or c2 is None:
+                fail = True
+                break
+        i += 1
+    if fail:
+        return dict(ok=False, logp=-math.inf, cells=cells)
+    # population averages (Experiment.cpp:298-311 + NotifySimulatedValue)
+    avgs = [np.zeros((len(d["times"]), 1)) for d in e["data"]]
+    for k, (dli, t, ti, six) in enumerate(e["timepoints"]):
+        alive = [c for c in cells if 0.0 <= t - c["creation"] <= c["sim_end"]]
+        pop = len(alive)
+        for c in cells:
+            x = c["values"][k]
+            if x == x:
+                avgs[dli][ti, 0] += x / pop
+    logp = 0.0
+    for dli, d in enumerate(e["data"]):
+        logp += _popavg_logp(d, avgs[dli], tv)
+    return dict(ok=True, logp=logp, cells=cells, population_average=[a[:, 0] for a in avgs])
+
+
+def _popavg_logp(d, avg, tv):
+    """DataLikelihoodTimeCoursePopulationAverage::Evaluate (one species)."""
+    stdev = _refval(d["stdev"], tv)
+    offset = _refval(d["offset"], tv) if d["offset"] else 0.0
+    scale = _refval(d["scale"], tv) if d["scale"] else 1.0
+    a = avg.copy()
+    assert not d["relative_to_time_average"]
+    a *= scale
+    a += offset
+    minus_log_sigma = -math.log(stdev)
+    inv2 = 1.0 / (2.0 * stdev * stdev)
+    logp = 0.0
+    obs = d["observed"]
+    times = d["times"]
+    for i in range(len(times)):
+        x = a[i].sum()
+        if math.isnan(x):
+            raise NotImplementedError("missing-simulation penalty")
+        for j in range(obs.shape[0]):
+            o = obs[j, i]
+            if not math.isnan(o):
+                if d["error_model"] == "normal":
+                    dd = x - o  # EvaluateValue(observed_data, x): d = observed - simulated with the arguments swapped
+                    logp += minus_log_sigma - 0.91893853320467274178032973640562 - dd * dd * inv2
+                else:
+                    z = (o - x) / stdev
+                    logp += -0.9808292530117262 - 2.5 * math.log1p(0.25 * z * z) - math.log(stdev)
+    return logp * d["weight"]
+
+
+def simulate(prob, values):
+    values = np.atleast_2d(np.asarray(values, dtype=float))
+    res = []
+    for v in values:
+        logp = 0.0
+        avgs, ncells = [], []
+        for e in prob["experiments"]:
+            r = simulate_experiment(e, prob, v)
+            logp += r["logp"]
+            avgs.append(r.get("population_average", [None])[0])
+            ncells.append(len(r["cells"]))
+        res.append(dict(logp=logp, avg=avgs[0], ncells=ncells[0], detail=r))
+    return dict(logp=np.array([r["logp"] for r in res]), population_average=[r["avg"] for r in res],
+                num_cells=[r["ncells"] for r in res], detail=[r["detail"] for r in res])

@@ -1,0 +1,377 @@
+/*
+ * cellpop_ref.cpp -- TEST INFRASTRUCTURE (oracle). Never linked into the product.
+ *
+ * One cell of the reference's cell-population likelihood on the reference's own integrator and
+ * linear algebra, built by oracle/Makefile into oracle/_ref/libcellpopref.so from the sources
+ * where they lie under /root/reference:
+ *   - vendored SUNDIALS CVODE 5.3.0 (dependencies/cvode-5.3.0; BDF, Newton, dense matrix);
+ *   - the reference's PartialPivLUExtended::compute_optimized (src/utils/
+ *     EigenPartialPivLUSomewhatSparse.h) + Eigen 3.4-rc1's PartialPivLU::solve
+ *     (dependencies/eigen-3.4-rc1) as the SUNLinearSolver, as src/odecommon/
+ *     sunlinsol_dense_eigen.cpp:95-108, 146-156 uses them for N >= 4.
+ * Restated here (their files need Boost): the difference-quotient Jacobian
+ * (ODESolverCVODE::DifferenceQuotientJacobian, src/odecommon/ODESolverCVODE.cpp:496-537; cells
+ * register no analytic Jacobian, Cell.cpp:57-76), the ONE_STEP driver of ODESolverCVODE::Solve
+ * (:322-463) with SolveReturnSolution (ODESolver.cpp:93-134), Cell::Simulate (Cell.cpp:193-273)
+ * and Cell::integration_step_cb (:463-538) with get_threshold_crossing_time (ODESolverCVODE.cpp:
+ * 264-320) in the non-stored mode a cell population without synchronisation runs in.
+ * N_Vector: the vendored nvector_serial stands in for nvector_serial_eigen.cpp (same formulas).
+ * The cell right-hand side is the generated derivative (oracle/sbml_codegen.py) compiled for the
+ * host and passed in as a function pointer.
+ */
+#include <cvode/cvode.h>
+#include <nvector/nvector_serial.h>
+#include <sundials/sundials_linearsolver.h>
+#include <sundials/sundials_math.h>
+#include <sunmatrix/sunmatrix_dense.h>
+#include <sunnonlinsol/sunnonlinsol_newton.h>
+
+#include <Eigen/Dense>
+
+#include "EigenPartialPivLUSomewhatSparse.h"
+
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+#include "cvode_impl.h"
+
+typedef void (*derivative_fn)(double* out, const double* species, const double* constant_species,
+                              const double* parameters, const double* non_sampled_parameters);
+
+extern "C" {
+// one cell: inputs
+typedef struct {
+    int N;
+    derivative_fn rhs;
+    const double* constant_species;
+    const double* parameters;
+    const double* non_sampled_parameters;
+    const double* y0;             // [N]
+    double creation_time;
+    double end_time;              // Experiment target time (experiment time)
+    int M;                        // output times (sorted experiment times)
+    const double* output_times;   // [M]
+    const int* output_species;    // [M] species index whose value is reported (-1 = none)
+    double rtol, atol, hmin, hmax;
+    int max_steps;
+    int divide_cells;
+    double simulate_past_chromatid_separation_time;
+    // event species: SIMULATED-species indices used on the ODE state (Cell.cpp:44-50); -1 = absent
+    int ev_replicating, ev_replicated, ev_pcna, ev_nuclear_envelope, ev_chromatid_separation, ev_cytokinesis,
+        ev_apoptosis;
+} cp_cell_in;
+
+typedef struct {
+    int ok;              // Cell::Simulate result
+    int divided, died;
+    double sim_end;      // simulation_end_time (cell time)
+    double achieved_time;
+    double event_times[5];  // replication start, replication finish, PCNA increase, NEBD, anaphase onset
+    long nsteps;
+} cp_cell_out;
+}
+
+namespace {
+
+struct LU {
+    int N;
+    PartialPivLUExtended<Eigen::MatrixXd> lu;
+    Eigen::MatrixXd A;
+};
+
+SUNLinearSolver_Type ls_gettype(SUNLinearSolver) { return SUNLINEARSOLVER_DIRECT; }
+SUNLinearSolver_ID ls_getid(SUNLinearSolver) { return SUNLINEARSOLVER_CUSTOM; }
+int ls_initialize(SUNLinearSolver) { return SUNLS_SUCCESS; }
+int ls_setup(SUNLinearSolver S, SUNMatrix A)
+{
+    LU* c = (LU*)S->content;
+    c->A = Eigen::Map<Eigen::MatrixXd>(SM_DATA_D(A), c->N, c->N);
+    c->lu.compute_optimized(c->A);
+    return SUNLS_SUCCESS;
+}
+int ls_solve(SUNLinearSolver S, SUNMatrix, N_Vector x, N_Vector b, realtype)
+{
+    LU* c = (LU*)S->content;
+    Eigen::Map<Eigen::VectorXd> xv(NV_DATA_S(x), c->N);
+    Eigen::VectorXd bv = Eigen::Map<Eigen::VectorXd>(NV_DATA_S(b), c->N);
+    xv.noalias() = c->lu.solve(bv);
+    return SUNLS_SUCCESS;
+}
+sunindextype ls_lastflag(SUNLinearSolver) { return 0; }
+int ls_free(SUNLinearSolver S)
+{
+    if (!S) return SUNLS_SUCCESS;
+    delete (LU*)S->content;
+    if (S->ops) free(S->ops);
+    free(S);
+    return SUNLS_SUCCESS;
+}
+
+SUNLinearSolver make_ls(int N)
+{
+    SUNLinearSolver S = SUNLinSolNewEmpty();
+    S->ops->gettype = ls_gettype;
+    S->ops->getid = ls_getid;
+    S->ops->initialize = ls_initialize;
+    S->ops->setup = ls_setup;
+    S->ops->solve = ls_solve;
+    S->ops->lastflag = ls_lastflag;
+    S->ops->free = ls_free;
+    LU* c = new LU;
+    c->N = N;
+    S->content = c;
+    return S;
+}
+
+struct Cell {
+    const cp_cell_in* in;
+    int N;
+    void* mem;
+    std::vector<double> y_copy, work;
+    // Cell / ODESolver state
+    double t;
+    double previous_integration_step_time;
+    double simulation_end_time;
+    bool divided, died;
+    double ev[5];
+};
+
+void silent_err(int, const char*, const char*, char*, void*) {}
+
+int rhs_fn(realtype t, N_Vector y, N_Vector ydot, void* user)
+{
+    Cell* c = (Cell*)user;
+    c->in->rhs(NV_DATA_S(ydot), NV_DATA_S(y), c->in->constant_species, c->in->parameters, c->in->non_sampled_parameters);
+    return 0;
+}
+
+// ODESolverCVODE::DifferenceQuotientJacobian (ODESolverCVODE.cpp:496-537)
+int jac_fn(realtype t, N_Vector y, N_Vector fy, SUNMatrix J, void* user, N_Vector, N_Vector, N_Vector)
+{
+    Cell* c = (Cell*)user;
+    CVodeMem cv_mem = (CVodeMem)c->mem;
+    const int N = c->N;
+    const double MIN_INC_MULT = 1000.0;
+    double* yd = NV_DATA_S(y);
+    double* fd = NV_DATA_S(fy);
+    double* ewt = NV_DATA_S(cv_mem->cv_ewt);
+    for (int i = 0; i < N; i++) c->y_copy[i] = yd[i];
+    const double srur = SUNRsqrt(cv_mem->cv_uround);
+    Eigen::Map<Eigen::VectorXd> ydot(fd, N), ewtv(ewt, N);
+    const double fnorm = sqrt((ydot.array() * ewtv.array()).square().sum() / N);
+    double minInc;
+    if (fnorm != 0.0)
+        minInc = (MIN_INC_MULT * fabs(cv_mem->cv_h) * cv_mem->cv_uround * N * fnorm);
+    else
+        minInc = 1.0;
+    for (int j = 0; j < N; j++) {
+        const double inc = std::max(srur * fabs(yd[j]), minInc / ewt[j]);
+        c->y_copy[j] += inc;
+        c->in->rhs(c->work.data(), c->y_copy.data(), c->in->constant_species, c->in->parameters,
+                   c->in->non_sampled_parameters);
+        c->y_copy[j] = yd[j];
+        const double inc_inv = 1.0 / inc;
+        double* col = SM_COLUMN_D(J, j);
+        for (int i = 0; i < N; i++) col[i] = inc_inv * (c->work[i] - fd[i]);
+    }
+    return 0;
+}
+
+// get_threshold_crossing_time without stored integration points: the reference reads the
+// default-constructed timepoint record (cv_q = 0, NaN times) and a zero-filled Nordsieck buffer,
+// so the interpolant is 0 and the bisection only walks towards one end (ODESolverCVODE.cpp:264-320)
+double threshold_crossing_time(const Cell* c, double threshold, bool above, double prev_time)
+{
+    double dt = (c->t - prev_time) * 0.5;
+    double time = prev_time + dt;
+    for (int iter = 0; iter < 10; iter++) {
+        const double x = 0.0;
+        dt *= 0.5;
+        if (above) {
+            if (x > threshold) time -= dt; else time += dt;
+        } else {
+            if (x < threshold) time -= dt; else time += dt;
+        }
+    }
+    return time;
+}
+
+// Cell::integration_step_cb (Cell.cpp:463-538), non-stored branch
+bool step_cb(Cell* c, double t, const double* y, double& end_time)
+{
+    const cp_cell_in* in = c->in;
+    bool cont = true;
+    if (in->ev_replicating >= 0 && c->ev[0] != c->ev[0]) {
+        if (y[in->ev_replicating] > 1e-4) c->ev[0] = threshold_crossing_time(c, 1e-4, true, c->previous_integration_step_time);
+    }
+    if (in->ev_replicated >= 0 && c->ev[1] != c->ev[1]) {
+        if (y[in->ev_replicated] > 1.95) c->ev[1] = threshold_crossing_time(c, 1.95, true, c->previous_integration_step_time);
+    }
+    if (in->ev_pcna >= 0 && c->ev[2] != c->ev[2]) {
+        if (y[in->ev_pcna] > 0.5) c->ev[2] = threshold_crossing_time(c, 0.5, true, c->previous_integration_step_time);
+    }
+    if (in->ev_nuclear_envelope >= 0 && c->ev[3] != c->ev[3]) {
+        if (y[in->ev_nuclear_envelope] < 0.5) c->ev[3] = threshold_crossing_time(c, 0.5, false, c->previous_integration_step_time);
+    }
+    if (in->ev_chromatid_separation >= 0 && c->ev[4] != c->ev[4]) {
+        if (y[in->ev_chromatid_separation] > 1e-3) {
+            c->ev[4] = threshold_crossing_time(c, 1e-3, true, c->previous_integration_step_time);
+            c->simulation_end_time = std::max(c->simulation_end_time, c->ev[4] + in->simulate_past_chromatid_separation_time);
+            end_time = c->simulation_end_time;
+        }
+    }
+    if (in->divide_cells && in->ev_cytokinesis >= 0) {
+        if (y[in->ev_cytokinesis] > 1.0) {
+            c->simulation_end_time = t;
+            c->divided = true;
+            cont = false;
+        }
+    }
+    if (in->ev_apoptosis >= 0) {
+        if (y[in->ev_apoptosis] > 1.0) {
+            c->simulation_end_time = t;
+            c->died = true;
+            cont = false;
+        }
+    }
+    c->previous_integration_step_time = t;
+    return cont;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Cell::Simulate with SolveReturnSolution; out_values[M] = the solution at each output time for
+// output_species (NaN where the reference leaves it unset or GetInterpolatedSpeciesValue returns
+// NaN: before creation, after the cell's simulation end); end_y[N] = simulation_end_y.
+int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values, double* end_y)
+{
+    const int N = in->N, M = in->M;
+    Cell c;
+    c.in = in;
+    c.N = N;
+    c.y_copy.assign(N, 0.0);
+    c.work.assign(N, 0.0);
+    c.divided = c.died = false;
+    for (int k = 0; k < 5; k++) c.ev[k] = std::numeric_limits<double>::quiet_NaN();
+    out->nsteps = 0;
+    for (int k = 0; k < M; k++) out_values[k] = std::numeric_limits<double>::quiet_NaN();
+
+    // Cell::Simulate (Cell.cpp:193-210)
+    c.previous_integration_step_time = 0;
+    c.simulation_end_time = in->end_time - in->creation_time;
+    std::vector<double> tp(M);
+    for (int i = 0; i < M; i++) tp[i] = in->output_times[i] - in->creation_time;
+    if (M > 0) c.simulation_end_time = std::max(c.simulation_end_time, tp[M - 1]);
+
+    std::vector<double> sol((size_t)N * M, std::numeric_limits<double>::quiet_NaN());
+    bool result = true;
+    // SolveReturnSolution (ODESolver.cpp:93-134)
+    int ti = 0;
+    bool solve = true;
+    while (ti < M && tp[ti] < std::numeric_limits<double>::epsilon()) {
+        for (int i = 0; i < N; i++) sol[(size_t)ti * N + i] = in->y0[i];
+        ti++;
+    }
+    if (ti == M) solve = false;
+    long nst = 0;
+    if (solve) {
+        double end_time = tp[M - 1];
+        N_Vector y = N_VNew_Serial(N), atol = N_VNew_Serial(N), tmp = N_VNew_Serial(N);
+        for (int i = 0; i < N; i++) {
+            NV_Ith_S(y, i) = in->y0[i];
+            NV_Ith_S(atol, i) = in->atol;
+        }
+        void* mem = CVodeCreate(CV_BDF);
+        c.mem = mem;
+        SUNMatrix J = SUNDenseMatrix(N, N);
+        SUNLinearSolver LS = make_ls(N);
+        SUNNonlinearSolver NLS = SUNNonlinSol_Newton(y);
+        CVodeInit(mem, rhs_fn, 0.0, y);
+        CVodeSetUserData(mem, &c);
+        CVodeSetLinearSolver(mem, LS, J);
+        CVodeSetNonlinearSolver(mem, NLS);
+        CVodeSetJacFn(mem, jac_fn);
+        CVodeSetMinStep(mem, in->hmin);
+        CVodeSetMaxStep(mem, in->hmax);
+        CVodeSetErrHandlerFn(mem, silent_err, nullptr);
+        CVodeSVtolerances(mem, in->rtol, atol);
+        CVodeReInit(mem, 0.0, y);
+        // ODESolverCVODE::Solve (:322-463)
+        long current_step = 0;
+        c.t = 0.0;
+        int tpi = ti;
+        while (1) {
+            double tret;
+            int r = CVode(mem, end_time, y, &tret, CV_ONE_STEP);
+            if (r < 0) {
+                result = false;
+                break;
+            }
+            c.t = tret;
+            current_step++;
+            // the reference reads past the output vector once all outputs are done; stop there
+            while (tpi < M && tret >= tp[tpi]) {
+                if (CVodeGetDky(mem, tp[tpi], 0, tmp) != CV_SUCCESS) {
+                    result = false;
+                    break;
+                }
+                for (int i = 0; i < N; i++) sol[(size_t)tpi * N + i] = NV_Ith_S(tmp, i);
+                tpi++;
+            }
+            if (!result) break;
+            if (!step_cb(&c, c.t, NV_DATA_S(y), end_time)) break;
+            if (c.t >= end_time) break;
+            if (current_step == in->max_steps) {
+                result = false;
+                break;
+            }
+        }
+        nst = current_step;
+        if (!c.divided && !c.died && result)
+            for (int i = 0; i < N; i++) end_y[i] = sol[(size_t)(M - 1) * N + i];
+        if (c.divided || c.died)
+            for (int i = 0; i < N; i++) end_y[i] = NV_Ith_S(y, i);
+        CVodeFree(&mem);
+        SUNNonlinSolFree(NLS);
+        SUNLinSolFree(LS);
+        SUNMatDestroy(J);
+        N_VDestroy(y);
+        N_VDestroy(atol);
+        N_VDestroy(tmp);
+    } else {
+        for (int i = 0; i < N; i++) end_y[i] = sol[(size_t)(M - 1) * N + i];
+    }
+    out->nsteps = nst;
+    out->ok = result ? 1 : 0;
+    out->divided = c.divided;
+    out->died = c.died;
+    double achieved_cell_time;
+    if (c.divided || c.died)
+        achieved_cell_time = c.simulation_end_time;
+    else
+        achieved_cell_time = tp[M - 1];
+    out->sim_end = c.simulation_end_time;
+    out->achieved_time = achieved_cell_time + in->creation_time;
+    for (int k = 0; k < 5; k++) out->event_times[k] = c.ev[k];
+    // GetInterpolatedSpeciesValue (Cell.cpp:280-360), species without synchronisation
+    for (int k = 0; k < M; k++) {
+        const int s = in->output_species[k];
+        if (s < 0 || s >= N) continue;
+        const double cell_time = in->output_times[k] - in->creation_time;
+        if (cell_time < 0.0 || cell_time > c.simulation_end_time) continue;
+        // exact-time lookup: the first stored output with this time
+        for (int i = 0; i < M; i++) {
+            if (tp[i] == cell_time) {
+                out_values[k] = sol[(size_t)i * N + s];
+                break;
+            }
+        }
+    }
+    return result ? 0 : 1;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+"""GPU parity of the cell-population likelihood (config C4) against the oracle: the reference's
+vendored CVODE 5.3.0 with its PartialPivLU per cell (oracle/_ref/libcellpopref.so) under the
+restated Experiment / Cell logic (oracle/cellpop.py).
+
+Parity envelope (stated here, as north_star asks for fp64 work). The device integrates the same BDF
+arithmetic with hardware-reciprocal division, a column-oriented LU solve and ocml's pow/exp; the
+oracle uses Eigen's blocked triangular solves and glibc. An adaptive solver at rtol = atol =
+4*FLT_EPSILON amplifies last-bit differences (a difference-quotient Jacobian with a different
+increment, a corrector that converged one ulp apart) into step sizes that differ at ~1e-7, so the
+reference is not reproducible to more than that even against ITSELF: the same sources built with
+and without FMA contraction (oracle/_ref/libcellpopref_nofma.so) differ by up to ~5e-5 relative in
+logp on these draws. The GPU must sit inside that spread:
+  * identical cell bookkeeping: cell count, division decisions, daughter numbering;
+  * step counts equal for >= 95 % of the cells;
+  * creation and division times within 0.1 h (a step flip moves a division by one step),
+    data values within 1e-3 relative;
+  * logp within 2e-4 * (1 + |logp|) for every draw, the -inf pattern identical, and the median
+    GPU-vs-oracle deviation no larger than 10x the median oracle-vs-oracle(no FMA) deviation."""
+import math
+
+import numpy as np
+import pytest
+
+import cellpop_helpers as CH
+import cellpop as CP
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def setup(tmp_path_factory):
+    from bcm3_amd.likelihood import Likelihood
+    d = tmp_path_factory.mktemp("cellpop_gpu")
+    path = CH.write_likelihood(d, 6, 64)
+    ll = Likelihood(path, CH.PRIOR, device=0)
+    prob = CP.load_problem(path, CH.PRIOR)
+    x = CH.draws(12, 11)
+    ref = CP.simulate(prob, x)
+    ref_nofma = CP.simulate(CP.load_problem(path, CH.PRIOR, variant="nofma"), x)
+    yield ll, prob, x, ref, ref_nofma
+    ll.close()
+
+
+def test_logp_matches_oracle(setup):
+    ll, prob, x, ref, ref_nofma = setup
+    lp, status = ll.evaluate_batch(x)
+    dev, spread = [], []
+    for i in range(len(x)):
+        r = ref["logp"][i]
+        if r == -math.inf:
+            assert lp[i] == -math.inf and status[i] == 1, i
+        else:
+            assert abs(lp[i] - r) <= 2e-4 * (1.0 + abs(r)), (i, lp[i], r)
+            assert status[i] == 0
+            dev.append(abs(lp[i] - r) / (1.0 + abs(r)))
+            spread.append(abs(ref_nofma["logp"][i] - r) / (1.0 + abs(r)))
+    assert np.median(dev) <= 10.0 * np.median(spread) + 1e-12, (np.median(dev), np.median(spread))
+
+
+def test_cells_match_oracle(setup):
+    ll, prob, x, ref, _ = setup
+    ll.evaluate_batch(x)
+    e = prob["experiments"][0]
+    M, NS = len(e["output_times"]), len(e["model"].ode)
+    same_steps = total = 0
+    for i in range(len(x)):
+        cells = ref["detail"][i]["cells"]
+        if not ref["detail"][i]["ok"]:
+            continue
+        rec, vals, endy = ll.cellpop_cells(i, M, NS)
+        assert len(rec) == len(cells), i
+        for k, c in enumerate(cells):
+            assert rec["flags"][k] & 1
+            assert bool(rec["flags"][k] & 2) == c["divided"], (i, k)
+            same_steps += int(rec["nsteps"][k] == c["nsteps"])
+            total += 1
+            # times in hours: within 0.1 h, a few BDF steps near a division (~0.05 h each). A cell
+            # whose step count flips between builds divides one step earlier or later; the
+            # reference flips such cells between its own FMA / no-FMA builds too (0.01-0.025 h)
+            assert abs(rec["creation"][k] - c["creation"]) <= 0.1, (i, k)
+            assert abs(rec["sim_end"][k] - c["sim_end"]) <= 0.1, (i, k)
+            if rec["nsteps"][k] != c["nsteps"] or abs(rec["sim_end"][k] - c["sim_end"]) > 1e-3:
+                continue  # a flipped step moves the end state; the logp envelope covers these cells
+            np.testing.assert_array_equal(np.isnan(vals[k]), np.isnan(c["values"]))
+            ok = ~np.isnan(c["values"])
+            np.testing.assert_allclose(vals[k][ok], c["values"][ok], rtol=1e-3, atol=1e-9)
+            np.testing.assert_allclose(endy[k], c["end_y"], rtol=1e-3, atol=1e-8)
+    assert same_steps >= 0.95 * total, (same_steps, total)
+
+
+def test_batch_invariance(setup):
+    """logp[i] depends on values[i] only: a single evaluation equals the batch entry bit for bit"""
+    ll, prob, x, ref, _ = setup
+    lp, _ = ll.evaluate_batch(x)
+    for i in (0, 3):
+        one, _ = ll.evaluate_batch(x[i:i + 1])
+        assert one[0] == lp[i] or (math.isnan(one[0]) and math.isnan(lp[i]))
+
+
+def test_too_many_cells_is_minus_inf(tmp_path):
+    from bcm3_amd.likelihood import Likelihood
+    path = CH.write_likelihood(tmp_path, 4, 10, name="small_max.xml")
+    ll = Likelihood(path, CH.PRIOR, device=0)
+    lp, status = ll.evaluate_batch(np.array([CH.F.true_values()]))
+    assert lp[0] == -math.inf and status[0] == 1
+    ll.close()
