@@ -22,6 +22,7 @@ using namespace bcm3hip;
 namespace bcm3hip {
 struct CellPopDev;
 int cellpop_create(int device, const bcm3hip_cellpop_model* m, CellPopDev** out);
+int cellpop_precompile(const bcm3hip_cellpop_model* m);
 void cellpop_destroy(CellPopDev* c);
 int cellpop_launch(CellPopDev* c, size_t n, const double* values, double* logp, int32_t* status, hipStream_t s,
                    hipEvent_t e0, hipEvent_t e1);
@@ -262,6 +263,8 @@ int bcm3hip_open_cellpop(int device, const bcm3hip_cellpop_model* m, bcm3hip_ctx
     *out = c;
     return 0;
 }
+
+int bcm3hip_cellpop_precompile(const bcm3hip_cellpop_model* m) { return bcm3hip::cellpop_precompile(m); }
 
 int bcm3hip_cellpop_cells(bcm3hip_ctx* c, size_t item, int32_t* count, bcm3hip_cell_record* records, double* values,
                           double* end_y)

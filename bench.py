@@ -359,6 +359,49 @@ def expm_cpu_baseline(budget_s: float, seed: int):
     return out
 
 
+def cellpop_workload(device, gen, n=64):
+    """Config C4 (BASELINE.json configs[3]): the cell-population likelihood (synthetic cell-cycle SBML
+    model, 15 ODE species, 500 initial heterogeneous cells dividing over 20 h, ~1,500 cell
+    trajectories per evaluation), 64 chains' proposals per launch -- the whole generation loop
+    (init, solve, division bookkeeping, data likelihood) timed with HIP events."""
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.sampler import DevicePrior, load_prior
+    lik, pri = os.path.join(GOLDEN, "cellpop_likelihood.xml"), os.path.join(GOLDEN, "cellpop_prior.xml")
+    ll = Likelihood(lik, pri, device=device.index or 0)
+    x = DevicePrior(load_prior(pri), device).sample(n, gen).contiguous()
+    ms = _rate(ll, n, x, device, reps=2)
+    cells = 0
+    for i in range(n):
+        rec, _, _ = ll.cellpop_cells(i, 21, 15)
+        cells += len(rec)
+    ll.close()
+    return {"chains": n, "kernel_ms": ms, "evals_per_s": n / (ms * 1e-3), "cells_per_eval": cells / n,
+            "cell_trajectories_per_s": cells / (ms * 1e-3), "draws": x.detach().cpu().numpy()}
+
+
+def cellpop_cpu_baseline(draws, budget_s: float):
+    """The reference CPU path of C4: each evaluation's cells integrated by the reference's vendored
+    CVODE 5.3.0 + PartialPivLU (oracle/_ref/libcellpopref.so) in the reference's sequential order,
+    one evaluation per host thread (the sampling threads of TaskManager)."""
+    import concurrent.futures as cf
+    sys.path[:0] = [os.path.join(ROOT, "oracle")]
+    import cellpop as CP
+    prob = CP.load_problem(os.path.join(GOLDEN, "cellpop_likelihood.xml"), os.path.join(GOLDEN, "cellpop_prior.xml"))
+    e = prob["experiments"][0]
+    cores = host_cores()
+    done = 0
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(cores) as pool:
+        while time.perf_counter() - t0 < budget_s and done < len(draws):
+            batch = draws[done:done + cores]
+            list(pool.map(lambda v: CP.simulate_experiment(e, prob, v), batch))
+            done += len(batch)
+    el = time.perf_counter() - t0
+    return {"value": done / el, "unit": "log-likelihood evals/sec", "cores": cores, "kind": "reference",
+            "sample": f"{done} of the GPU line's prior draws, one evaluation per thread on {cores} threads, {el:.1f} s "
+                      "(reference CVODE 5.3.0 + PartialPivLUExtended per cell, experiment logic restated)"}
+
+
 def extra_workloads(device, seed):
     """Secondary lines (not the headline): the P=64 population variant of C3 (256 chains x 64
     patient trajectories per launch) and config C2 (circular ridge, 256 chains)."""
@@ -379,6 +422,7 @@ def extra_workloads(device, seed):
         out[tag] = rec
         ll.close()
     out.update(expm_workloads(device, gen))
+    out["cellpop_c4_64chains"] = cellpop_workload(device, gen)
     return out
 
 
@@ -527,6 +571,11 @@ def main():
                     extra[tag]["cpu_baseline"] = rec
             if "popk_p64_256chains" in extra:
                 extra["popk_p64_256chains"]["cpu_baseline"] = p64_cpu_baseline(6.0, args.seed)
+            if "cellpop_c4_64chains" in extra:
+                extra["cellpop_c4_64chains"]["cpu_baseline"] = cellpop_cpu_baseline(extra["cellpop_c4_64chains"]["draws"], 8.0)
+    for rec in extra.values():
+        if isinstance(rec, dict):
+            rec.pop("draws", None)
 
     acc_mut = loop.acceptance()
     line = {

@@ -47,6 +47,9 @@ int bcm3_likelihood_generated_code(const bcm3_likelihood* ll, char* buf, size_t 
 /* VariabilityPseudoRandomIterator's sequence (boost::random::sobol through uniform_01, restated):
  * points x dims, row-major */
 int bcm3_sobol_points(size_t points, size_t dims, double* out);
+/* cell_population: compile the cell kernel into the code-object cache without a device (build time;
+ * create the likelihood with options "backend=none") */
+int bcm3_likelihood_cellpop_precompile(const bcm3_likelihood* ll);
 /* cell_population: the cells of item `item` of the last batch (bcm3hip_cellpop_cells) */
 int bcm3_likelihood_cellpop_cells(bcm3_likelihood* ll, size_t item, int32_t* count, void* records /*bcm3hip_cell_record*/,
                                   double* values, double* end_y);

@@ -273,6 +273,8 @@ int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* model, bcm3hip
  * ($BCM3_CODEGEN_DIR, default <library dir>/codegen). Per-item status 1 when the experiment fails
  * (solver failure, too many cells): logp = -inf. */
 int bcm3hip_open_cellpop(int device, const bcm3hip_cellpop_model* model, bcm3hip_ctx** out);
+/* compile (or find in the cache) the model's cell kernel without a device (build time) */
+int bcm3hip_cellpop_precompile(const bcm3hip_cellpop_model* model);
 /* cells of item `item` of the last cellpop evaluation: *count cells, records / values[count*M]
  * (the data likelihood's values per output entry) / end_y[count*NS] may be NULL */
 int bcm3hip_cellpop_cells(bcm3hip_ctx* ctx, size_t item, int32_t* count, bcm3hip_cell_record* records,

@@ -52,7 +52,8 @@ class CellIn(C.Structure):
 
 class CellOut(C.Structure):
     _fields_ = [("ok", C.c_int), ("divided", C.c_int), ("died", C.c_int), ("sim_end", C.c_double),
-                ("achieved_time", C.c_double), ("event_times", C.c_double * 5), ("nsteps", C.c_long)]
+                ("achieved_time", C.c_double), ("event_times", C.c_double * 5), ("nsteps", C.c_long),
+                ("nsetups", C.c_long), ("nje", C.c_long), ("nni", C.c_long), ("netf", C.c_long), ("nfe", C.c_long)]
 
 
 _libs = {}
@@ -384,7 +385,8 @@ def simulate_experiment(e, prob, values):
         lib.cp_simulate_cell(C.byref(cin), C.byref(cout), vals.ctypes.data, end_y.ctypes.data)
         c.update(ok=bool(cout.ok), divided=bool(cout.divided), died=bool(cout.died), sim_end=cout.sim_end,
                  achieved=cout.achieved_time, events=list(cout.event_times), values=vals, end_y=end_y,
-                 nsteps=cout.nsteps)
+                 nsteps=cout.nsteps, stats=dict(nsetups=cout.nsetups, nje=cout.nje, nni=cout.nni, netf=cout.netf,
+                                                 nfe=cout.nfe))
         if not cout.ok:
             fail = True
             break

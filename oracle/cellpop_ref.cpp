@@ -20,6 +20,7 @@
  * host and passed in as a function pointer.
  */
 #include <cvode/cvode.h>
+#include <cvode/cvode_ls.h>
 #include <nvector/nvector_serial.h>
 #include <sundials/sundials_linearsolver.h>
 #include <sundials/sundials_math.h>
@@ -70,6 +71,7 @@ typedef struct {
     double achieved_time;
     double event_times[5];  // replication start, replication finish, PCNA increase, NEBD, anaphase onset
     long nsteps;
+    long nsetups, nje, nni, netf, nfe;  // CVODE counters (CVodeGetNum*)
 } cp_cell_out;
 }
 
@@ -258,6 +260,7 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
     c.divided = c.died = false;
     for (int k = 0; k < 5; k++) c.ev[k] = std::numeric_limits<double>::quiet_NaN();
     out->nsteps = 0;
+    out->nsetups = out->nje = out->nni = out->netf = out->nfe = 0;
     for (int k = 0; k < M; k++) out_values[k] = std::numeric_limits<double>::quiet_NaN();
 
     // Cell::Simulate (Cell.cpp:193-210)
@@ -331,6 +334,11 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
             }
         }
         nst = current_step;
+        CVodeGetNumLinSolvSetups(mem, &out->nsetups);
+        CVodeGetNumJacEvals(mem, &out->nje);
+        CVodeGetNumNonlinSolvIters(mem, &out->nni);
+        CVodeGetNumErrTestFails(mem, &out->netf);
+        CVodeGetNumRhsEvals(mem, &out->nfe);
         if (!c.divided && !c.died && result)
             for (int i = 0; i < N; i++) end_y[i] = sol[(size_t)(M - 1) * N + i];
         if (c.divided || c.died)
