@@ -287,6 +287,9 @@ BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
         s.tlast = t_;                      \
         __builtin_amdgcn_sched_barrier(0); \
     } while (0)
+#elif defined(BCM3_MARKS)
+// ISA study build: a comment per phase boundary in the -S output (tools/step_isa.py)
+#define BDF_PH(k) asm volatile("; BDFMARK " #k)
 #else
 #define BDF_PH(k) \
     do {          \

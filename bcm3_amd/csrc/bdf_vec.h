@@ -796,6 +796,9 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
                      int max_steps, Pending& pd)
 {
     for (;;) {
+#ifdef BCM3_MARKS
+        asm volatile("; BDFMARK fast_top Q=%0" ::"i"(Q));
+#endif
         vec::ewt_set(s);
         const double saved_t = s.tn;
         const double eta_eff = (s.hprime != s.h) ? s.eta : 1.0;

@@ -51,6 +51,7 @@ public:
     virtual bool SetBackendOption(int option, int64_t value) { return false; }
 
     size_t GetNumVariables() const { return varset ? varset->GetNumVariables() : 0; }
+    const VariableSet* GetVariableSet() const { return varset.get(); }
 
 protected:
     Likelihood();

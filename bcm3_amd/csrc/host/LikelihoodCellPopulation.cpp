@@ -8,6 +8,7 @@
 #include <fstream>
 #include <limits>
 
+#include "NetCDFClassic.h"
 #include "json.h"
 #include "log.h"
 
@@ -214,7 +215,7 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
     }
     Json doc;
     try {
-        doc = json_load(resolve(data_file, vm));
+        doc = LoadDataFile(resolve(data_file, vm));
     } catch (JsonError& e) {
         LOGERROR("Failed to open data file %s: %s", data_file.c_str(), e.what.c_str());
         return false;

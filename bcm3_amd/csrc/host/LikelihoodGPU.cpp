@@ -6,6 +6,7 @@
 #include <fstream>
 #include <limits>
 
+#include "NetCDFClassic.h"
 #include "json.h"
 #include "log.h"
 
@@ -172,7 +173,8 @@ bool LikelihoodPopPKTrajectory::Initialize(std::shared_ptr<const VariableSet> vs
     }
     Json data;
     try {
-        data = json_load(path);
+        data = LoadDataFile(path);
+        UnwrapDataVariables(data);
     } catch (JsonError& e) {
         LOGERROR("Failed to open data file %s: %s", pkdata_file.c_str(), e.what.c_str());
         return false;
@@ -424,7 +426,8 @@ bool LikelihoodPharmacokineticTrajectory::Initialize(std::shared_ptr<const Varia
     }
     Json data;
     try {
-        data = json_load(path);
+        data = LoadDataFile(path);
+        UnwrapDataVariables(data);
     } catch (JsonError& e) {
         LOGERROR("Failed to open data file %s: %s", pkdata_file.c_str(), e.what.c_str());
         return false;
@@ -660,7 +663,8 @@ static const Json* load_pharmaco_group(const OptionsMap& vm, const std::string& 
         if (file_exists(alt)) path = alt;
     }
     try {
-        data = json_load(path);
+        data = LoadDataFile(path);
+        UnwrapDataVariables(data);
     } catch (JsonError& e) {
         LOGERROR("Failed to open data file %s: %s", pkdata_file.c_str(), e.what.c_str());
         return nullptr;

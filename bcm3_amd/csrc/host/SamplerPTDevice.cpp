@@ -16,6 +16,7 @@
 #include "../../../include/bcm3.h"
 #include "../../../include/bcm3hip.h"
 #include "GMM.h"
+#include "NetCDFClassic.h"
 #include "log.h"
 
 namespace bcm3 {
@@ -261,6 +262,53 @@ struct SamplerPTDevice::Impl {
 
     PTMHCounters cnt;
     int64_t iter = 0, round = 0;
+
+    // sample output: [flush][values C*d | lprior C | llh C] staged on the device
+    std::unique_ptr<SampleFileWriter> out;
+    DevBuf<double> out_buf;
+    int64_t out_samples = 0, out_first = 0, out_pending = 0, emitted = 0;
+    int out_flush = 64;
+    bool out_overflow_logged = false;
+
+    bool Emit()
+    {
+        // SamplerPT::EmitSample (SamplerPT.cpp:321-330): every chain, weight 1
+        const int64_t six = emitted++;
+        if (!out) return true;
+        if (six >= out_samples) {
+            if (!out_overflow_logged) LOGWARNING("More samples than the output file holds (%lld); later samples are not stored", (long long)out_samples);
+            out_overflow_logged = true;
+            return true;
+        }
+        if (out_pending == 0) out_first = six;
+        double* slot = out_buf.p + out_pending * C * (d + 2);
+        if (bcm3hip_memcpy_async(slot, values.p, C * d * sizeof(double), BCM3HIP_D2D, stream) != 0 ||
+            bcm3hip_memcpy_async(slot + C * d, lprior.p, C * sizeof(double), BCM3HIP_D2D, stream) != 0 ||
+            bcm3hip_memcpy_async(slot + C * (d + 1), llh.p, C * sizeof(double), BCM3HIP_D2D, stream) != 0)
+            return false;
+        out_pending++;
+        if (out_pending == out_flush || six + 1 == out_samples) return Flush();
+        return true;
+    }
+
+    bool Flush()
+    {
+        if (!out || out_pending == 0) return true;
+        std::vector<double> h((size_t)(out_pending * C * (d + 2)));
+        if (bcm3hip_memcpy_async(h.data(), out_buf.p, h.size() * sizeof(double), BCM3HIP_D2H, stream) != 0 ||
+            bcm3hip_stream_synchronize(stream) != 0)
+            return false;
+        const std::vector<double> w(C, 1.0);
+        for (int64_t k = 0; k < out_pending; k++) {
+            const double* r = &h[(size_t)(k * C * (d + 2))];
+            if (!out->Write((size_t)(out_first + k), 0, (size_t)C, r, r + C * d, r + C * (d + 1), w.data())) {
+                LOGERROR("Writing sample %lld to the output file failed", (long long)(out_first + k));
+                return false;
+            }
+        }
+        out_pending = 0;
+        return true;
+    }
 
     bool Launch(int rc, const char* what)
     {
@@ -516,6 +564,7 @@ struct SamplerPTDevice::Impl {
         if (!ok) return false;
         const int64_t si = cnt.samples_done++;
         cnt.iterations++;
+        if ((si + 1) % cfg.use_every_nth == 0 && !Emit()) return false;
         if (adaptive && (si + 1) % cfg.use_every_nth == 0) {
             const int64_t sample_ix = si / cfg.use_every_nth;
             if (cfg.adapt_proposal_samples > 0 && (sample_ix + 1) % cfg.adapt_proposal_samples == 0 && !last &&
@@ -593,6 +642,7 @@ SamplerPTDevice::SamplerPTDevice() : p_(new Impl) {}
 
 SamplerPTDevice::~SamplerPTDevice()
 {
+    if (p_ && p_->out && !p_->Flush()) LOGERROR("Flushing the sample output failed");
     if (p_ && p_->stream) bcm3hip_stream_synchronize(p_->stream);
     if (p_ && p_->own_stream) bcm3hip_stream_destroy(p_->stream);
 }
@@ -734,10 +784,36 @@ bool SamplerPTDevice::Run(int64_t num_samples)
         if (!p_->IterationOnce(si + 1 == total)) return false;
         if (p_->cfg.nan_check_every > 0 && (si + 1) % p_->cfg.nan_check_every == 0 && !p_->CheckNaN()) return false;
     }
-    return p_->CheckNaN();
+    return p_->CheckNaN() && FlushOutput();
 }
 
 bool SamplerPTDevice::AdaptProposal() { return p_->Adapt(); }
+
+bool SamplerPTDevice::SetOutput(const std::string& filename, int64_t num_samples, int flush_every)
+{
+    Impl& s = *p_;
+    const VariableSet* vs = s.ll ? s.ll->GetVariableSet() : nullptr;
+    if (!vs || num_samples < 1 || s.emitted != 0) {
+        LOGERROR("SetOutput: needs an initialised sampler before its first sample");
+        return false;
+    }
+    std::vector<std::string> names(vs->GetVariableNames());
+    std::vector<int32_t> tr(names.size());
+    for (size_t i = 0; i < names.size(); i++) tr[i] = (int32_t)vs->GetVariableTransform(i);
+    auto w = std::make_unique<SampleFileWriter>();
+    if (!w->Initialize(filename, (size_t)num_samples, names, tr,
+                       TemperatureLadder(s.Ctot, s.cfg.temperature_power, s.cfg.temperature_max), (size_t)s.g0,
+                       (size_t)s.C))
+        return false;
+    s.out_flush = std::max(1, flush_every);
+    if (!s.out_buf.alloc((size_t)(s.out_flush * s.C * (s.d + 2)))) return false;
+    s.out = std::move(w);
+    s.out_samples = num_samples;
+    s.out_pending = 0;
+    return true;
+}
+
+bool SamplerPTDevice::FlushOutput() { return p_->Flush() && (!p_->out || p_->out->Sync()); }
 bool SamplerPTDevice::CheckNaN() { return p_->CheckNaN(); }
 bool SamplerPTDevice::Synchronize() { return bcm3hip_stream_synchronize(p_->stream) == 0; }
 

@@ -71,6 +71,11 @@ public:
     // num_samples * use_every_nth iterations with the NaN check every nan_check_every
     bool Run(int64_t num_samples);
     bool AdaptProposal();
+    // SampleHandlerNetCDF (SampleHandlerNetCDF.cpp:24-110): every emitted sample of this rank's
+    // temperatures goes to `filename` (netCDF classic, NetCDFClassic.h; all ranks share the file),
+    // staged in HBM and written every `flush_every` samples; call before the first iteration
+    bool SetOutput(const std::string& filename, int64_t num_samples, int flush_every);
+    bool FlushOutput();
     bool CheckNaN();  // synchronises; false (and an error) if a likelihood returned NaN
     bool Synchronize();
     bool GetState(double* values, double* llh, double* lprior, double* lpp);

@@ -126,6 +126,14 @@ int bcm3_ptmh_get_state(bcm3_ptmh* h, double* values, double* llh, double* lprio
     return (h && h->s.GetState(values, llh, lprior, lpp)) ? 0 : -2;
 }
 
+int bcm3_ptmh_set_output(bcm3_ptmh* h, const char* filename, int64_t num_samples, int32_t flush_every)
+{
+    if (!h || !filename) return -1;
+    return h->s.SetOutput(filename, num_samples, flush_every) ? 0 : -2;
+}
+
+int bcm3_ptmh_flush_output(bcm3_ptmh* h) { return (h && h->s.FlushOutput()) ? 0 : -2; }
+
 int bcm3_ptmh_get_components(bcm3_ptmh* h, int32_t* ncomp) { return (h && h->s.GetProposalComponents(ncomp)) ? 0 : -2; }
 
 int bcm3_ptmh_get_counters(bcm3_ptmh* h, int64_t* out)

@@ -65,6 +65,14 @@ def _lib():
         L.bcm3_ptmh_stream.restype = vp
         L.bcm3_ptmh_destroy.argtypes = [vp]
         L.bcm3_ptmh_destroy.restype = None
+        L.bcm3_ptmh_set_output.argtypes = [vp, C.c_char_p, C.c_int64, C.c_int32]
+        L.bcm3_ptmh_flush_output.argtypes = [vp]
+        L.bcm3_samples_open.argtypes = [C.c_char_p, C.c_int64, C.c_int32, C.POINTER(C.c_char_p), vp, C.c_int32, vp,
+                                        C.c_int32, C.c_int32, C.POINTER(vp)]
+        L.bcm3_samples_write.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp]
+        L.bcm3_samples_sync.argtypes = [vp]
+        L.bcm3_samples_close.argtypes = [vp]
+        L.bcm3_samples_close.restype = None
         _bound = True
     return L
 
@@ -128,6 +136,14 @@ class PTMHNative:
         self.d = likelihood.d
         self.C = L.bcm3_ptmh_num_chains(h)
 
+    def set_output(self, filename: str, num_samples: int, flush_every: int = 64):
+        """SampleHandlerNetCDF for this rank's chains (bcm3_ptmh_set_output): the reference's
+        output.nc schema in a netCDF classic file (SampleFile); call before the first iteration."""
+        _check(_lib().bcm3_ptmh_set_output(self.h, filename.encode(), num_samples, flush_every), "bcm3_ptmh_set_output")
+
+    def flush_output(self):
+        _check(_lib().bcm3_ptmh_flush_output(self.h), "bcm3_ptmh_flush_output")
+
     def iterate(self, n: int, last_at_end: bool = False):
         _check(_lib().bcm3_ptmh_iterate(self.h, int(n), int(last_at_end)), "bcm3_ptmh_iterate")
 
@@ -171,3 +187,38 @@ class PTMHNative:
             self.close()
         except Exception:
             pass
+
+
+class SampleFile:
+    """bcm3_samples_*: the reference's output.nc (SampleHandlerNetCDF.cpp:24-110) as a netCDF
+    classic file written by libbcm3 (group members "samples.<name>"); a process writes the
+    temperature columns [first, first + own)."""
+
+    def __init__(self, filename: str, num_samples: int, names, transforms, temperatures, first: int = 0,
+                 own: Optional[int] = None):
+        L = _lib()
+        temps = np.ascontiguousarray(temperatures, dtype=np.float64)
+        tr = np.ascontiguousarray(transforms, dtype=np.int32)
+        own = len(temps) - first if own is None else own
+        arr = (C.c_char_p * len(names))(*[n.encode() for n in names])
+        self.d = len(names)
+        self.h = C.c_void_p()
+        _check(L.bcm3_samples_open(filename.encode(), num_samples, self.d, arr, tr.ctypes.data, len(temps),
+                                   temps.ctypes.data, first, own, C.byref(self.h)), "bcm3_samples_open")
+
+    def write(self, sample_ix: int, t0: int, values, lprior, llh, weight=None):
+        v = np.ascontiguousarray(values, dtype=np.float64).reshape(-1, self.d)
+        nt = v.shape[0]
+        lp = np.ascontiguousarray(lprior, dtype=np.float64).reshape(nt)
+        ll = np.ascontiguousarray(llh, dtype=np.float64).reshape(nt)
+        w = np.ones(nt) if weight is None else np.ascontiguousarray(weight, dtype=np.float64).reshape(nt)
+        _check(_lib().bcm3_samples_write(self.h, sample_ix, t0, nt, v.ctypes.data, lp.ctypes.data, ll.ctypes.data,
+                                         w.ctypes.data), "bcm3_samples_write")
+
+    def close(self):
+        if self.h:
+            _lib().bcm3_samples_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()

@@ -169,6 +169,33 @@ int bcm3_ptmh_get_components(bcm3_ptmh* s, int32_t* ncomp /* [C] */);
 int bcm3_ptmh_get_counters(bcm3_ptmh* s, int64_t* out /* [BCM3_PTMH_NUM_COUNTERS] */);
 void* bcm3_ptmh_stream(const bcm3_ptmh* s);
 void bcm3_ptmh_destroy(bcm3_ptmh* s);
+/* SampleHandlerNetCDF for the rank (SampleHandlerNetCDF.cpp:24-110, SamplerPT::EmitSample
+ * SamplerPT.cpp:321-330): every use_every_nth-th iteration the rank's chains (values, log prior,
+ * log likelihood, weight 1) go to `filename` (bcm3_samples_* format below; the ranks of a sharded
+ * ladder share one file), staged on the device and written every flush_every samples, at the end of
+ * bcm3_ptmh_run and on bcm3_ptmh_flush_output / destroy. Call before the first iteration. */
+int bcm3_ptmh_set_output(bcm3_ptmh* s, const char* filename, int64_t num_samples, int32_t flush_every);
+int bcm3_ptmh_flush_output(bcm3_ptmh* s);
+
+/* ---- netCDF classic files (NetCDFClassic.h): the sampler's output.nc ----
+ * The reference's output.nc schema (group "samples", SampleHandlerNetCDF.cpp:41-58) in a netCDF
+ * classic (CDF-2) file, group members named "samples.<name>": dims sample_ix, temperature,
+ * variable; variables sample_ix, variable (names), temperature, variable_transform,
+ * variable_values[sample_ix][temperature][variable], log_prior / log_likelihood / weights
+ * [sample_ix][temperature], NC_FILL_DOUBLE where no sample was written. A process writes the
+ * temperature columns [first, first + own) (all processes of a sharded ladder open the same file);
+ * the process with first == 0 writes the coordinate variables. tools/nc_convert.py makes the
+ * netCDF-4 group file the reference's R tooling (R/load.r) opens. */
+typedef struct bcm3_samples bcm3_samples;
+int bcm3_samples_open(const char* filename, int64_t num_samples, int32_t d, const char* const* names,
+                      const int32_t* transforms, int32_t num_temperatures, const double* temperatures, int32_t first,
+                      int32_t own, bcm3_samples** out);
+/* sample sample_ix of temperatures [first + t0, first + t0 + nt): values[nt][d], lprior / llh /
+ * weight [nt] */
+int bcm3_samples_write(bcm3_samples* h, int64_t sample_ix, int32_t t0, int32_t nt, const double* values,
+                       const double* lprior, const double* llh, const double* weight);
+int bcm3_samples_sync(bcm3_samples* h);
+void bcm3_samples_close(bcm3_samples* h);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,202 @@
+"""netCDF I/O without libnetcdf: the C++ classic-format reader behind every
+likelihood's data file (NetCDFDataFile::Open / GetValues, src/utils/NetCDFDataFile.cpp) and the
+classic-format output.nc writer (SampleHandlerNetCDF.cpp:24-110), checked against an independent
+implementation of the format (scipy.io.netcdf_file) in both directions.
+
+Parity unpinned: the reference ships no netCDF fixture and its netCDF-4 files need HDF5, which is
+absent here; the files below are the committed JSON sidecars converted by tools/nc_convert.py."""
+import ctypes as C
+import math
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+GOLDEN = H.GOLDEN
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CONVERT = os.path.join(ROOT, "tools", "nc_convert.py")
+netcdf_file = pytest.importorskip("scipy.io").netcdf_file
+
+
+def _convert(cmd, src, dst):
+    subprocess.run([sys.executable, CONVERT, cmd, src, dst], check=True)
+
+
+def _xml_with(tmp_path, name, old, new):
+    text = open(os.path.join(GOLDEN, f"{name}_likelihood.xml")).read().replace(old, new)
+    p = tmp_path / f"{name}_nc_likelihood.xml"
+    p.write_text(text)
+    return str(p)
+
+
+def _lik(xml, prior):
+    from bcm3_amd.likelihood import Likelihood
+    return Likelihood(xml, os.path.join(GOLDEN, f"{prior}_prior.xml"), options="backend=none")
+
+
+def _arr(ptr, n, dt):
+    return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,)).copy()
+
+
+POPK_ARRAYS = (("time", "T", np.float64), ("observed", "PT", np.float64), ("dose", "P", np.float64),
+               ("dosing_interval", "P", np.float64), ("simulate_until", "P", np.int32),
+               ("skipped_days", "P29", np.uint8), ("transforms", "d", np.int32))
+
+
+def _popk_arrays(ll):
+    m = ll.popk_model()  # (arrays owned by ll, alive for this call)
+    n = {"T": m.T, "P": m.P, "PT": m.P * m.T, "P29": m.P * 29, "d": m.d}
+    return {k: _arr(getattr(m, k), n[s], dt) for k, s, dt in POPK_ARRAYS}, (m.rtol, m.atol, m.MW, m.P, m.T, m.d)
+
+
+@pytest.mark.parametrize("name", ["c3", "p64"])
+def test_popk_data_from_classic_file(tmp_path, name):
+    nc = str(tmp_path / f"{name}_pkdata.nc")
+    _convert("to-classic", os.path.join(GOLDEN, f"{name}_pkdata.json"), nc)
+    assert open(nc, "rb").read(4) == b"CDF\x02"
+    ref, ref_s = _popk_arrays(_lik(os.path.join(GOLDEN, f"{name}_likelihood.xml"), name))
+    got, got_s = _popk_arrays(_lik(_xml_with(tmp_path, name, f"{name}_pkdata.json", nc), name))
+    assert got_s == ref_s
+    for k in ref:
+        assert np.array_equal(got[k], ref[k], equal_nan=True), k
+
+
+def test_record_dimension_file(tmp_path):
+    """a classic file whose patients dimension is the record (unlimited) dimension: record
+    variables interleave per record (scipy writes it, the C++ reader reads it)"""
+    import json
+    doc = json.load(open(os.path.join(GOLDEN, "p64_pkdata.json")))
+    (g, grp), = doc.items()
+    P = len(grp["patients"])
+    nc = str(tmp_path / "rec.nc")
+    f = netcdf_file(nc, "w", version=1)
+    f.createDimension(f"{g}.patients", None)
+    T = len(grp["time"])
+    f.createDimension(f"{g}.time", T)
+    f.createDimension(f"{g}.days", 29)
+    f.createDimension(f"{g}.patients_strlen", max(len(str(p)) for p in grp["patients"]))
+    v = f.createVariable(f"{g}.time", "d", (f"{g}.time",))
+    v[:] = np.array(grp["time"], dtype=float)
+    for name, val in grp.items():
+        if name in ("time", "patients"):
+            continue
+        arr = np.array([np.nan if x is None else x for x in np.ravel(np.array(val, dtype=object))], dtype=float)
+        arr = arr.reshape(np.shape(np.array(val, dtype=object)))
+        dims = (f"{g}.patients",) + ((f"{g}.time",) if arr.ndim == 2 and arr.shape[1] == T else
+                                     (f"{g}.days",) if arr.ndim == 2 else ())
+        v = f.createVariable(f"{g}.{name}", "d", dims)
+        v[:P] = arr
+    chars = np.zeros((P, f.dimensions[f"{g}.patients_strlen"]), dtype="S1")
+    for i, p in enumerate(grp["patients"]):
+        for k, ch in enumerate(str(p)):
+            chars[i, k] = ch.encode()
+    v = f.createVariable(f"{g}.patients", "c", (f"{g}.patients", f"{g}.patients_strlen"))
+    v[:P] = chars
+    f.close()
+    ref, ref_s = _popk_arrays(_lik(os.path.join(GOLDEN, "p64_likelihood.xml"), "p64"))
+    got, got_s = _popk_arrays(_lik(_xml_with(tmp_path, "p64", "p64_pkdata.json", nc), "p64"))
+    assert got_s == ref_s
+    for k in ref:
+        assert np.array_equal(got[k], ref[k], equal_nan=True), k
+
+
+def test_pharmaco_data_from_classic_file(tmp_path):
+    nc = str(tmp_path / "pharmaco_pkdata.nc")
+    _convert("to-classic", os.path.join(GOLDEN, "pharmaco_pkdata.json"), nc)
+    la = _lik(os.path.join(GOLDEN, "pharmaco_single_likelihood.xml"), "pharmaco")
+    lb = _lik(_xml_with(tmp_path, "pharmaco_single", "pharmaco_pkdata.json", nc), "pharmaco")
+    a, b = la.expm_pk_model(), lb.expm_pk_model()  # (arrays owned by the likelihoods)
+    assert (a.n_treat, a.n_obs, a.MW, a.d) == (b.n_treat, b.n_obs, b.MW, b.d)
+    for k, n in (("treat_times", a.n_treat), ("treat_doses", a.n_treat), ("obs_times", a.n_obs), ("obs_conc", a.n_obs)):
+        assert np.array_equal(_arr(getattr(a, k), n, np.float64), _arr(getattr(b, k), n, np.float64)), k
+
+
+def test_cellpop_data_from_classic_file(tmp_path):
+    nc = str(tmp_path / "cellpop_data.nc")
+    _convert("to-classic", os.path.join(GOLDEN, "cellpop_data.json"), nc)
+    text = open(os.path.join(GOLDEN, "cellpop_likelihood.xml")).read()
+    text = text.replace('data_file="cellpop_data.json"', f'data_file="{nc}"')
+    text = text.replace('model_file="cellpop_model.xml"', f'model_file="{os.path.join(GOLDEN, "cellpop_model.xml")}"')
+    p = tmp_path / "lik.xml"
+    p.write_text(text)
+    ll = _lik(str(p), "cellpop")
+    assert "generated_derivative" in ll.generated_code() or len(ll.generated_code()) > 0
+    # a missing data variable is reported as in the reference
+    p.write_text(text.replace('data_name="pcna_mean"', 'data_name="nope"'))
+    with pytest.raises(RuntimeError):
+        _lik(str(p), "cellpop")
+
+
+def test_netcdf4_file_is_refused_with_conversion_hint(tmp_path):
+    nc = tmp_path / "pkdata.nc"
+    nc.write_bytes(b"\x89HDF\r\n\x1a\n" + b"\0" * 64)
+    from bcm3_amd.likelihood import Likelihood
+    with pytest.raises(RuntimeError, match="nc_convert"):
+        Likelihood(_xml_with(tmp_path, "c3", "c3_pkdata.json", str(nc)), os.path.join(GOLDEN, "c3_prior.xml"),
+                   options="backend=none")
+
+
+def _read_samples(path):
+    with netcdf_file(path, "r", mmap=False) as f:
+        v = {k.partition(".")[2]: np.array(x[:]) for k, x in f.variables.items()}
+        fill = f.variables["samples.variable_values"]._FillValue
+    return v, fill
+
+
+def test_sample_file_shared_by_two_ranks(tmp_path):
+    from bcm3_amd.ptmh import SampleFile
+    path = str(tmp_path / "output.nc")
+    with open(path, "wb") as f:  # a stale longer file is cut to the exact size
+        f.write(b"x" * 100000)
+    names = ["ka", "CL", "long_variable_name"]
+    temps = [0.0, 0.1, 0.4, 0.7, 1.0]
+    rng = np.random.default_rng(3)
+    N = 6
+    # rank 1 (temperatures 3, 4) opens first and writes before rank 0 exists
+    r1 = SampleFile(path, N, names, [1, 2, 0], temps, first=3, own=2)
+    vals = rng.normal(size=(N, 5, 3))
+    lp, llh = rng.normal(size=(N, 5)), rng.normal(size=(N, 5))
+    for s in range(4):
+        r1.write(s, 0, vals[s, 3:], lp[s, 3:], llh[s, 3:])
+    r0 = SampleFile(path, N, names, [1, 2, 0], temps, first=0, own=3)
+    for s in range(5):
+        r0.write(s, 0, vals[s, :3], lp[s, :3], llh[s, :3], weight=np.full(3, 0.5))
+    r1.close()
+    r0.close()
+    v, fill = _read_samples(path)
+    assert fill == 9.9692099683868690e+36
+    assert [b"".join(r).decode() for r in v["variable"]] == names
+    assert np.array_equal(v["temperature"], temps) and np.array_equal(v["variable_transform"], [1, 2, 0])
+    # sample_ix: 1..N at creation, the 0-based index of each received sample (SampleHandlerNetCDF)
+    assert list(v["sample_ix"]) == [0, 1, 2, 3, 4, 6]
+    assert v["variable_values"].shape == (N, 5, 3)
+    assert np.array_equal(v["variable_values"][:5, :3], vals[:5, :3])
+    assert np.array_equal(v["variable_values"][:4, 3:], vals[:4, 3:])
+    assert np.all(v["variable_values"][5] == fill) and np.all(v["variable_values"][4:, 3:] == fill)
+    assert np.array_equal(v["log_prior"][:4], lp[:4]) and np.array_equal(v["log_likelihood"][:4], llh[:4])
+    assert np.all(v["weights"][:5, :3] == 0.5) and np.all(v["weights"][:4, 3:] == 1.0)
+    # and the converter reads it back into the netCDF-4 layout's JSON form
+    out = str(tmp_path / "output.json")
+    _convert("to-json", path, out)
+    import json
+    doc = json.load(open(out))
+    assert doc["samples"]["variable_values"]["dims"] == ["sample_ix", "temperature", "variable"]
+    assert doc["samples"]["variable_values"]["data"][5][0][0] is None
+    assert doc["samples"]["variable"]["data"] == names
+
+
+def test_sample_file_rejects_bad_geometry(tmp_path):
+    from bcm3_amd.ptmh import SampleFile
+    with pytest.raises(RuntimeError):
+        SampleFile(str(tmp_path / "o.nc"), 4, ["a"], [0], [0.0, 1.0], first=1, own=2)
+    f = SampleFile(str(tmp_path / "o.nc"), 4, ["a"], [0], [0.0, 1.0])
+    with pytest.raises(RuntimeError):
+        f.write(4, 0, [[1.0]], [0.0], [0.0])
+    with pytest.raises(RuntimeError):
+        f.write(0, 1, [[1.0], [2.0]], [0.0, 0.0], [0.0, 0.0])
+    f.close()
+    assert math.isclose(os.path.getsize(str(tmp_path / "o.nc")) % 4, 0)

@@ -123,3 +123,56 @@ def test_native_sharded_ladder_equals_single_rank(world, scheme):
     c1 = one.counters()
     for k, v in tot.items():
         assert v == c1[k], k
+
+
+def _samples(path):
+    from scipy.io import netcdf_file
+    with netcdf_file(path, "r", mmap=False) as f:
+        return {k.partition(".")[2]: np.array(x[:]) for k, x in f.variables.items()}
+
+
+def test_sample_output_file(tmp_path):
+    """SampleHandlerNetCDF: every use_every_nth-th iteration all chains are stored (SamplerPT::
+    EmitSample); the last stored sample equals the final chain state; the sharded ladder's ranks
+    write one shared file identical to the single-rank one"""
+    C, seed, nth, N = 32, 4, 3, 10
+    kw = dict(adapt_proposal_samples=4, adapt_proposal_times=1, use_every_nth=nth)
+    one = _native(*C2, C, seed, 0, **kw)
+    p1 = str(tmp_path / "one.nc")
+    one.set_output(p1, N, flush_every=4)
+    one.run(N)
+    st = one.state()
+    one.close()
+    v = _samples(p1)
+    assert v["variable_values"].shape == (N, C, 2)
+    assert np.array_equal(v["variable_values"][N - 1], st["values"])
+    assert np.array_equal(v["log_prior"][N - 1], st["lprior"]) and np.array_equal(v["log_likelihood"][N - 1], st["llh"])
+    assert np.all(v["weights"] == 1.0) and list(v["sample_ix"]) == list(range(N))
+    from bcm3_amd.pt import temperature_ladder
+    np.testing.assert_allclose(v["temperature"], np.asarray(temperature_ladder(C)), rtol=1e-15, atol=0)
+    # the sharded ladder: 2 ranks, one file
+    from bcm3_amd.ptmh import LocalGroup
+    group = LocalGroup(2)
+    p2 = str(tmp_path / "two.nc")
+    ranks = [_native(*C2, C, seed, 0, rank=r, world=2, group=group, **kw) for r in range(2)]
+    for s in ranks:
+        s.set_output(p2, N, flush_every=3)
+    errors = []
+
+    def go(s):
+        try:
+            s.run(N)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=go, args=(s,)) for s in ranks]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    for s in ranks:
+        s.close()
+    w = _samples(p2)
+    for k in v:
+        assert np.array_equal(v[k], w[k]), k
