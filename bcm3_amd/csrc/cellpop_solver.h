@@ -66,9 +66,29 @@ struct Shared {
     double J[NS * NS];   // saved Jacobian, column-major
     double A[NS * NS];   // I - gamma J -> LU factors, column-major
     int perm[NS];        // (P b)[i] = b[perm[i]]
+    double dinv[NS];     // 1 / u(i, i), correctly rounded (lin_solve's quotients)
+    int dinv_ok;         // every 1 / u(i, i) finite: the quotients through dinv
     double prm[NP > 0 ? NP : 1];
     double cs[NC > 0 ? NC : 1];
+#ifdef CP_PHASES
+    long long ph[8];
+#endif
 };
+
+// CP_PHASES (BCM3_CP_PHASES=1, diagnostic build): clock64 cycles per part of the solve, summed per
+// cell into sh.ph and returned in end_y[0..5] (tools/cellpop_phases.py)
+#ifdef CP_PHASES
+#define CP_PH_BEGIN() const long long ph_t0_ = clock64()
+#define CP_PH_END(sh, k) \
+    if (threadIdx.x == 0) (sh).ph[k] += clock64() - ph_t0_
+#else
+#define CP_PH_BEGIN() \
+    do {              \
+    } while (0)
+#define CP_PH_END(sh, k) \
+    do {                 \
+    } while (0)
+#endif
 
 template <int NS>
 struct GenState {
@@ -83,17 +103,45 @@ struct GenState {
     int nls_jcur;
 };
 
-// sum over the components in component order of a lane value (uniform result)
+// value of lane J of this lane's 16-lane row, in every lane (v_mov_b64_dpp row_newbcast:J; no
+// LDS round trip and no SGPR hop)
+template <int J>
+BDF_INL double rbc(double v)
+{
+    return __builtin_amdgcn_mov_dpp(v, 0x150 + J, 0xf, 0xf, false);
+}
+// value of lane (l - D) of the row in lane l; `old` where l - D leaves the row (row_shr:D)
+template <int D>
+BDF_INL int shr_i(int v, int old)
+{
+    return __builtin_amdgcn_update_dpp(old, v, 0x110 + D, 0xf, 0xf, false);
+}
+template <int D>
+BDF_INL double shr_d(double v, double old)
+{
+    const long long b = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, old);
+    const int lo = shr_i<D>((int)b, (int)o), hi = shr_i<D>((int)(b >> 32), (int)(o >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
+
+// sum over the components in component order of a lane value (uniform result): ((p0 + p1) + p2)
+// ..., the order of nvector_serial's loops
 template <int NS, class SH>
 BDF_INL double lane_sum(SH& sh, double p)
 {
-    wave_sync();
-    sh.red[lane()] = p;
-    wave_sync();
-    double s = sh.red[0];
+    if constexpr (NS <= 16) {
+        double s = rbc<0>(p);
+        cfor<1, NS>([&](auto i) __attribute__((always_inline)) { s = s + rbc<CI(i)>(p); });
+        return wave_uniform(s);
+    } else {
+        wave_sync();
+        sh.red[lane()] = p;
+        wave_sync();
+        double s = sh.red[0];
 #pragma unroll
-    for (int i = 1; i < NS; i++) s += sh.red[i];
-    return s;
+        for (int i = 1; i < NS; i++) s += sh.red[i];
+        return s;
+    }
 }
 
 // N_VWrmsNorm
@@ -145,38 +193,57 @@ BDF_INL void dq_jacobian(SH& sh, const S& s, double y, double fy)
     wave_sync();
 }
 
-// A = I - gamma J (SUNMatCopy + SUNMatScaleAddI), then PartialPivLUExtended::compute_optimized
+// A = I - gamma J (SUNMatCopy + SUNMatScaleAddI), then PartialPivLUExtended::compute_optimized:
+// per column k the first largest |a(i, k)|, i >= k, as pivot (a DPP max-scan over the 16 lanes of
+// row 0), the row swap (lanes = columns), the scaling of column k, and the Schur update of the
+// trailing block element-parallel (lane = (row, column group)), skipping the columns whose pivot-row
+// entry a(k, j) is zero as the reference does. Every element sees the same operations in the same
+// order as the sequential form.
 template <int NS, class SH>
 BDF_INL void lin_setup(SH& sh, double gamma)
 {
     const int ln = lane();
     wave_sync();
-    if (ln < NS) {
-        for (int j = 0; j < NS; j++) {
-            double a = (-gamma) * sh.J[j * NS + ln];
-            if (j == ln) a += 1.0;
-            sh.A[j * NS + ln] = a;
-        }
-        sh.perm[ln] = ln;
+    for (int e = ln; e < NS * NS; e += WAVE) {
+        const int j = e / NS, i = e - j * NS;
+        double a = (-gamma) * sh.J[e];
+        if (i == j) a += 1.0;
+        sh.A[e] = a;
     }
+    if (ln < NS) sh.perm[ln] = ln;
     wave_sync();
     for (int k = 0; k < NS; k++) {
-        // pivot: first row of the largest |A(i, k)|, i >= k (maxCoeff)
-        double v = (ln >= k && ln < NS) ? fabs(sh.A[k * NS + ln]) : -1.0;
-        int ix = ln;
-#pragma unroll
-        for (int off = 1; off < WAVE; off <<= 1) {
-            const double ov = __shfl_xor(v, off);
-            const int oi = __shfl_xor(ix, off);
-            const bool take = (ov > v) || ((ov == v) && (oi < ix));
-            v = take ? ov : v;
-            ix = take ? oi : ix;
+        int p;
+        double biggest;
+        if constexpr (NS <= 16) {
+            // inclusive max-scan, the lower lane winning ties (maxCoeff's first index)
+            double v = (ln >= k && ln < NS) ? fabs(sh.A[k * NS + ln]) : -1.0;
+            int ix = ln;
+            cfor<0, 4>([&](auto r) __attribute__((always_inline)) {
+                constexpr int D = 1 << CI(r);
+                const double ov = shr_d<D>(v, -2.0);
+                const int oi = shr_i<D>(ix, ix);
+                const bool take = ov >= v;
+                v = take ? ov : v;
+                ix = take ? oi : ix;
+            });
+            p = __builtin_amdgcn_readlane(ix, 15);
+            biggest = bcast(v, 15);
+        } else {
+            biggest = -1.0;
+            p = k;
+            for (int i = k; i < NS; i++) {
+                const double v = fabs(sh.A[k * NS + i]);
+                if (v > biggest) {
+                    biggest = v;
+                    p = i;
+                }
+            }
+            p = __builtin_amdgcn_readfirstlane(p);
+            biggest = wave_uniform(biggest);
         }
-        const int p = __builtin_amdgcn_readfirstlane(ix);
-        const double biggest = wave_uniform(v);
         if (biggest != 0.0) {
             if (p != k) {
-                // swap rows k and p: lanes = columns
                 if (ln < NS) {
                     const double a = sh.A[ln * NS + k];
                     const double b = sh.A[ln * NS + p];
@@ -194,19 +261,37 @@ BDF_INL void lin_setup(SH& sh, double gamma)
             if (ln > k && ln < NS) sh.A[k * NS + ln] *= inv;
             wave_sync();
         }
-        // Schur update of the columns with a non-zero pivot-row entry
-        const double lik = (ln > k && ln < NS) ? sh.A[k * NS + ln] : 0.0;
-        for (int j = k + 1; j < NS; j++) {
-            const double akj = sh.A[j * NS + k];
-            if (akj != 0.0) {
-                if (ln > k && ln < NS) sh.A[j * NS + ln] -= akj * lik;
+        for (int i = k + 1 + (ln & 15); i < NS; i += 16) {
+            const double lik = sh.A[k * NS + i];
+            for (int j = k + 1 + (ln >> 4); j < NS; j += 4) {
+                const double akj = sh.A[j * NS + k];
+                if (akj != 0.0) sh.A[j * NS + i] -= akj * lik;
             }
         }
         wave_sync();
     }
+    double r = 1.0;
+    if (ln < NS) {
+        r = 1.0 / sh.A[ln * NS + ln];
+        sh.dinv[ln] = r;
+    }
+    // singular or subnormal pivots keep the IEEE division (x / 0 = inf, not NaN)
+    const bool fin = __builtin_amdgcn_ballot_w64(!(fabs(r) <= 1.7976931348623157e308)) == 0;
+    if (ln == 0) sh.dinv_ok = fin ? 1 : 0;
 }
 
-// x = A^-1 b: P b, unit-lower forward and upper backward substitution (PartialPivLU::solve)
+// x / d from r = RN(1 / d): q = RN(x r), then one residual correction RN(q + (x - d q) r) -- the
+// correctly rounded quotient (Markstein) in three dependent operations instead of the IEEE
+// division sequence, which sits on the critical path of the back substitution
+BDF_INL double div_by(double x, double d, double r)
+{
+    const double q = x * r;
+    const double e = __builtin_fma(-d, q, x);
+    return __builtin_fma(e, r, q);
+}
+
+// x = A^-1 b: P b, unit-lower forward and upper backward substitution (PartialPivLU::solve); the
+// solution component of column j reaches the other lanes by a row broadcast
 template <int NS, class SH>
 BDF_INL double lin_solve(SH& sh, double b)
 {
@@ -215,14 +300,48 @@ BDF_INL double lin_solve(SH& sh, double b)
     if (ln < NS) sh.red[ln] = b;
     wave_sync();
     double x = (ln < NS) ? sh.red[sh.perm[ln]] : 0.0;
-    for (int j = 0; j < NS - 1; j++) {
-        const double xj = bcast(x, j);
-        if (ln > j && ln < NS) x = x - sh.A[j * NS + ln] * xj;
-    }
-    for (int j = NS - 1; j >= 0; j--) {
-        if (ln == j) x = x / sh.A[j * NS + j];
-        const double xj = bcast(x, j);
-        if (ln < j) x = x - sh.A[j * NS + ln] * xj;
+    if (BDF_UNLIKELY(!sh.dinv_ok)) {
+        for (int j = 0; j < NS - 1; j++) {
+            const double xj = bcast(x, j);
+            if (ln > j && ln < NS) x = x - sh.A[j * NS + ln] * xj;
+        }
+        for (int j = NS - 1; j >= 0; j--) {
+            if (ln == j) x = x / sh.A[j * NS + j];
+            const double xj = bcast(x, j);
+            if (ln < j) x = x - sh.A[j * NS + ln] * xj;
+        }
+    } else if constexpr (NS <= 16) {
+        // lane i holds row i of the factors in registers (one batch of LDS loads); the
+        // substitutions are then branch-free: every lane computes, selects keep the lanes a
+        // column does not update
+        double a[NS];
+        const int li = (ln < NS) ? ln : 0;
+        cfor<0, NS>([&](auto J) __attribute__((always_inline)) { a[CI(J)] = sh.A[CI(J) * NS + li]; });
+        const double rinv = sh.dinv[li];
+        cfor<0, NS - 1>([&](auto J) __attribute__((always_inline)) {
+            constexpr int j = CI(J);
+            const double xj = rbc<j>(x);
+            const double t = x - a[j] * xj;
+            x = (ln > j && ln < NS) ? t : x;
+        });
+        cfor_down<NS - 1, 0>([&](auto J) __attribute__((always_inline)) {
+            constexpr int j = CI(J);
+            const double qd = div_by(x, a[j], rinv);
+            x = (ln == j) ? qd : x;
+            const double xj = rbc<j>(x);
+            const double t = x - a[j] * xj;
+            x = (ln < j) ? t : x;
+        });
+    } else {
+        for (int j = 0; j < NS - 1; j++) {
+            const double xj = bcast(x, j);
+            if (ln > j && ln < NS) x = x - sh.A[j * NS + ln] * xj;
+        }
+        for (int j = NS - 1; j >= 0; j--) {
+            if (ln == j) x = div_by(x, sh.A[j * NS + j], sh.dinv[j]);
+            const double xj = bcast(x, j);
+            if (ln < j) x = x - sh.A[j * NS + ln] * xj;
+        }
     }
     return x;
 }
@@ -424,7 +543,12 @@ BDF_INL bool newton(SH& sh, S& s, double rl1, int convfail, bool callSetup)
     int curiter = 0;
     for (;;) {
         const double y = s.zn[0] + s.acor;
-        const double f = rhs_v<NS, NP, NC>(sh, y);
+        double f;
+        {
+            CP_PH_BEGIN();
+            f = rhs_v<NS, NP, NC>(sh, y);
+            CP_PH_END(sh, 0);
+        }
         double delta = __builtin_fma(rl1, s.zn[1], s.acor);
         delta = __builtin_fma(-s.gamma, f, delta);
         if (callSetup) {
@@ -434,9 +558,15 @@ BDF_INL bool newton(SH& sh, S& s, double rl1, int convfail, bool callSetup)
                               ((convfail == CONV_BAD_J) && (dgamma < CVLS_DGMAX)) || (convfail == CONV_OTHER);
             if (jnew) {
                 s.nstlj = s.nst;
+                CP_PH_BEGIN();
                 dq_jacobian<NS, NP, NC>(sh, s, y, f);
+                CP_PH_END(sh, 1);
             }
-            lin_setup<NS>(sh, s.gamma);
+            {
+                CP_PH_BEGIN();
+                lin_setup<NS>(sh, s.gamma);
+                CP_PH_END(sh, 2);
+            }
             s.nls_jcur = jnew;
             s.gamrat = 1.0;
             cscale = 1.0;
@@ -446,7 +576,12 @@ BDF_INL bool newton(SH& sh, S& s, double rl1, int convfail, bool callSetup)
             callSetup = false;
             curiter = 0;
         }
-        double x = lin_solve<NS>(sh, -delta);
+        double x;
+        {
+            CP_PH_BEGIN();
+            x = lin_solve<NS>(sh, -delta);
+            CP_PH_END(sh, 3);
+        }
         if (s.gamrat != 1.0) x *= cscale;
         s.acor += x;
         const double del = wrms<NS>(sh, x, s.ewt);
@@ -729,6 +864,10 @@ extern "C" __global__ __launch_bounds__(64) void cp_solve_kernel(cpk::CpSolveArg
     const int M = MM;
     double* outv = sh.outl;
     for (int k = ln; k < M; k += WAVE) outv[k] = __builtin_nan("");
+#ifdef CP_PHASES
+    if (ln < 8) sh.ph[ln] = 0;
+    const long long ph_kernel0 = clock64();
+#endif
     wave_sync();
 
     // Cell::Simulate (Cell.cpp:193-210)
@@ -779,7 +918,12 @@ extern "C" __global__ __launch_bounds__(64) void cp_solve_kernel(cpk::CpSolveArg
         int tpi = ti;
         for (;;) {
             double tret;
-            const int r = cvode_one_step<NS, NP, NC>(sh, s, end_time, tret);
+            int r;
+            {
+                CP_PH_BEGIN();
+                r = cvode_one_step<NS, NP, NC>(sh, s, end_time, tret);
+                CP_PH_END(sh, 4);
+            }
             if (r < 0) {
                 ok = false;
                 break;
@@ -843,6 +987,11 @@ extern "C" __global__ __launch_bounds__(64) void cp_solve_kernel(cpk::CpSolveArg
         a.out_values[(size_t)slot * M + k] = (ct < 0.0 || ct > sim_end) ? __builtin_nan("") : outv[k];
     }
     if (ln < NS) a.end_y[(size_t)slot * NS + ln] = yend;
+#ifdef CP_PHASES
+    if (ln == 0) sh.ph[5] = clock64() - ph_kernel0;
+    wave_sync();
+    if (ln < 6 && ln < NS) a.end_y[(size_t)slot * NS + ln] = (double)sh.ph[ln];
+#endif
     if (ln == 0) {
         const double achieved_cell_time = (divided || died) ? sim_end : (a.output_times[M - 1] - creation);
         a.sim_end[slot] = sim_end;
