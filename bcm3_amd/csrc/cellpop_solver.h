@@ -847,7 +847,10 @@ BDF_INL double crossing_time(double t, double prev, double threshold, bool above
 // One cell per workgroup (64 lanes): Cell::Simulate -> ODESolver::SolveReturnSolution ->
 // ODESolverCVODE::Solve with the integration-step callback, then the values the experiment's
 // data likelihoods read (GetInterpolatedSpeciesValue) at every output entry.
-extern "C" __global__ __launch_bounds__(64) void cp_solve_kernel(cpk::CpSolveArgs a)
+#ifndef CP_WAVES_PER_EU
+#define CP_WAVES_PER_EU 3  // 168 VGPRs: 3 cells per SIMD (measured best: 2 waves 62 ms, 3 waves 51 ms, 4 waves 61 ms per C4 batch)
+#endif
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CP_WAVES_PER_EU))) void cp_solve_kernel(cpk::CpSolveArgs a)
 {
     using namespace cpk;
     constexpr int NS = CP_NS, NP = CP_NP, NC = CP_NC;
