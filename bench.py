@@ -98,8 +98,9 @@ def issue_rate(ll, x_dev, device):
     smax = int(nst.max())
     return {"kernel_ms": ms, "steps_slowest": smax, "steps_mean": float(nst.mean()),
             "cycles_per_step_slowest": ms * 1e-3 * CLOCK_GHZ * 1e9 / max(1, smax), "clock_ghz": CLOCK_GHZ,
-            "note": "launch time is set by the slowest trajectory; DESIGN.md §7 gives the per-step "
-                    "dependent critical path (~500 cycles) this is compared with"}
+            "issue_bound": issue_bound_from_profiles(len(x), float(nst.mean())),
+            "note": "launch time is set by the slowest trajectory; issue_bound compares the measured "
+                    "cycles per step with 4 cycles per issued instruction (DESIGN.md §7)"}
 
 
 class NativeLoop:
@@ -187,6 +188,36 @@ def traffic_from_profiles(tag: str, n: int):
                 return float(t["bytes_per_launch"])
         except (OSError, ValueError, KeyError):
             continue
+    return None
+
+
+def issue_bound_from_profiles(n: int, steps_mean: float):
+    """The instruction-issue bound of the BDF kernel from the newest committed SQ counters
+    (profiles/<tag>_traffic_c3_<n>.json: SQ_INSTS_VALU / SALU per launch, SQ_WAVE_CYCLES in quad
+    cycles; profiles/<tag>_pmc_sq2.json: SQ_INSTS_BRANCH, SQ_WAIT_ANY, SQ_ACTIVE_INST_ANY). A wavefront
+    issues at most one instruction per 4 cycles (one issue slot per SIMD every 4 cycles, a wave64
+    VALU instruction occupies its SIMD for 4), so 4 x instructions per step is the fastest one
+    trajectory can step; the measured cycles per step are SQ_WAVE_CYCLES over the same waves."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(PROFILES, f"*_traffic_c3_{n}.json")), reverse=True):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+            sq = t["sq_per_launch"]
+            tag = os.path.basename(path).split("_traffic_")[0]
+            with open(os.path.join(PROFILES, f"{tag}_pmc_sq2.json")) as f:
+                sq2 = json.load(f)
+        except (OSError, ValueError, KeyError):
+            continue
+        waves = float(sq["SQ_WAVES"])
+        per_step = lambda c: c / waves / steps_mean  # noqa: E731
+        instr = per_step(sq["SQ_INSTS_VALU"] + sq["SQ_INSTS_SALU"] + sq2["SQ_INSTS_BRANCH"])
+        measured = 4.0 * per_step(sq["SQ_WAVE_CYCLES"])
+        return {"profile": os.path.basename(path), "valu_per_step": per_step(sq["SQ_INSTS_VALU"]),
+                "salu_per_step": per_step(sq["SQ_INSTS_SALU"]), "branch_per_step": per_step(sq2["SQ_INSTS_BRANCH"]),
+                "issue_bound_cycles_per_step": 4.0 * instr, "measured_cycles_per_step_mean": measured,
+                "frac_of_issue_bound": 4.0 * instr / measured,
+                "wait_share": sq2["SQ_WAIT_ANY"] / (sq2["SQ_WAIT_ANY"] + sq2["SQ_ACTIVE_INST_ANY"])}
     return None
 
 

@@ -18,6 +18,8 @@ def main():
     os.makedirs(dst, exist_ok=True)
     copies = {
         os.path.join(src, "kt", "kt_kernel_stats.csv"): f"{tag}_kernel_stats.csv",
+        os.path.join(src, "kt_extras", "kt_kernel_stats.csv"): f"{tag}_kernel_stats_extras.csv",
+        os.path.join(src, "smoke.log"): f"{tag}_smoke.log",
         os.path.join(src, "bench.json"): f"{tag}_bench.json",
         os.path.join(src, "ubench_lat.txt"): f"{tag}_ubench_lat.txt",
         os.path.join(src, "ubench_branch.txt"): f"{tag}_ubench_branch.txt",
