@@ -30,10 +30,16 @@ namespace cpk {
 using namespace bcm3hip;
 
 constexpr int WAVE = 64;
+// A cell's state lives in one ROW of lanes (component i in lane i of the row). With NS <= 16 four
+// cells share a wavefront -- the 16-lane DPP rows -- so every vector instruction advances four
+// cells; with more species one cell takes the whole wavefront. Control flow that depends on a
+// cell's state (step size, order, Newton iterations, failures) diverges between the rows of a
+// wavefront and runs under the execution mask.
+constexpr int ROW = (CP_NS <= 16) ? 16 : 64;
+constexpr int CPW = WAVE / ROW;
 
-
-
-BDF_INL int lane() { return (int)threadIdx.x; }
+BDF_INL int lane() { return (int)threadIdx.x & (ROW - 1); }  // component index within the row
+BDF_INL int row() { return (int)threadIdx.x / ROW; }
 
 BDF_INL double bcast(double v, int k)
 {
@@ -44,6 +50,16 @@ BDF_INL double bcast(double v, int k)
 }
 
 BDF_INL void wave_sync() { __syncthreads(); }
+
+// value of lane k (runtime) of this lane's row (ds_bpermute; the whole row must be active)
+BDF_INL double rowget(double v, int k)
+{
+    const int addr = ((int)(threadIdx.x & ~(unsigned)(ROW - 1)) + k) << 2;
+    const long long b = __builtin_bit_cast(long long, v);
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, (int)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, (int)(b >> 32));
+    return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
+}
 
 struct LdsSpecies {
     const double* y;
@@ -60,9 +76,9 @@ struct PertSpecies {
 template <int NS, int NP, int NC, int M>
 struct Shared {
     double outl[M];      // the cell's values at the output entries
-    double sy[WAVE];     // state broadcast
-    double sf[WAVE];     // f(y) broadcast (Jacobian)
-    double red[WAVE];    // reductions
+    double sy[ROW];      // state broadcast
+    double sf[ROW];      // f(y) broadcast (Jacobian)
+    double red[ROW];     // reductions
     double J[NS * NS];   // saved Jacobian, column-major
     double A[NS * NS];   // I - gamma J -> LU factors, column-major
     int perm[NS];        // (P b)[i] = b[perm[i]]
@@ -80,7 +96,7 @@ struct Shared {
 #ifdef CP_PHASES
 #define CP_PH_BEGIN() const long long ph_t0_ = clock64()
 #define CP_PH_END(sh, k) \
-    if (threadIdx.x == 0) (sh).ph[k] += clock64() - ph_t0_
+    if (lane() == 0) (sh).ph[k] += clock64() - ph_t0_
 #else
 #define CP_PH_BEGIN() \
     do {              \
@@ -132,7 +148,7 @@ BDF_INL double lane_sum(SH& sh, double p)
     if constexpr (NS <= 16) {
         double s = rbc<0>(p);
         cfor<1, NS>([&](auto i) __attribute__((always_inline)) { s = s + rbc<CI(i)>(p); });
-        return wave_uniform(s);
+        return s;
     } else {
         wave_sync();
         sh.red[lane()] = p;
@@ -204,7 +220,7 @@ BDF_INL void lin_setup(SH& sh, double gamma)
 {
     const int ln = lane();
     wave_sync();
-    for (int e = ln; e < NS * NS; e += WAVE) {
+    for (int e = ln; e < NS * NS; e += ROW) {
         const int j = e / NS, i = e - j * NS;
         double a = (-gamma) * sh.J[e];
         if (i == j) a += 1.0;
@@ -227,8 +243,8 @@ BDF_INL void lin_setup(SH& sh, double gamma)
                 v = take ? ov : v;
                 ix = take ? oi : ix;
             });
-            p = __builtin_amdgcn_readlane(ix, 15);
-            biggest = bcast(v, 15);
+            p = __builtin_amdgcn_mov_dpp(ix, 0x15F, 0xf, 0xf, false);  // lane 15 of the row
+            biggest = rbc<15>(v);
         } else {
             biggest = -1.0;
             p = k;
@@ -261,11 +277,23 @@ BDF_INL void lin_setup(SH& sh, double gamma)
             if (ln > k && ln < NS) sh.A[k * NS + ln] *= inv;
             wave_sync();
         }
-        for (int i = k + 1 + (ln & 15); i < NS; i += 16) {
-            const double lik = sh.A[k * NS + i];
-            for (int j = k + 1 + (ln >> 4); j < NS; j += 4) {
-                const double akj = sh.A[j * NS + k];
-                if (akj != 0.0) sh.A[j * NS + i] -= akj * lik;
+        if constexpr (ROW == 16) {
+            // lane i of the row: row i of the trailing block
+            const int i = k + 1 + ln;
+            if (i < NS) {
+                const double lik = sh.A[k * NS + i];
+                for (int j = k + 1; j < NS; j++) {
+                    const double akj = sh.A[j * NS + k];
+                    if (akj != 0.0) sh.A[j * NS + i] -= akj * lik;
+                }
+            }
+        } else {
+            for (int i = k + 1 + (ln & 15); i < NS; i += 16) {
+                const double lik = sh.A[k * NS + i];
+                for (int j = k + 1 + (ln >> 4); j < NS; j += 4) {
+                    const double akj = sh.A[j * NS + k];
+                    if (akj != 0.0) sh.A[j * NS + i] -= akj * lik;
+                }
             }
         }
         wave_sync();
@@ -276,8 +304,9 @@ BDF_INL void lin_setup(SH& sh, double gamma)
         sh.dinv[ln] = r;
     }
     // singular or subnormal pivots keep the IEEE division (x / 0 = inf, not NaN)
-    const bool fin = __builtin_amdgcn_ballot_w64(!(fabs(r) <= 1.7976931348623157e308)) == 0;
-    if (ln == 0) sh.dinv_ok = fin ? 1 : 0;
+    if (ln == 0) sh.dinv_ok = 1;
+    wave_sync();
+    if (!(fabs(r) <= 1.7976931348623157e308)) sh.dinv_ok = 0;
 }
 
 // x / d from r = RN(1 / d): q = RN(x r), then one residual correction RN(q + (x - d q) r) -- the
@@ -302,12 +331,12 @@ BDF_INL double lin_solve(SH& sh, double b)
     double x = (ln < NS) ? sh.red[sh.perm[ln]] : 0.0;
     if (BDF_UNLIKELY(!sh.dinv_ok)) {
         for (int j = 0; j < NS - 1; j++) {
-            const double xj = bcast(x, j);
+            const double xj = rowget(x, j);
             if (ln > j && ln < NS) x = x - sh.A[j * NS + ln] * xj;
         }
         for (int j = NS - 1; j >= 0; j--) {
             if (ln == j) x = x / sh.A[j * NS + j];
-            const double xj = bcast(x, j);
+            const double xj = rowget(x, j);
             if (ln < j) x = x - sh.A[j * NS + ln] * xj;
         }
     } else if constexpr (NS <= 16) {
@@ -848,25 +877,30 @@ BDF_INL double crossing_time(double t, double prev, double threshold, bool above
 // ODESolverCVODE::Solve with the integration-step callback, then the values the experiment's
 // data likelihoods read (GetInterpolatedSpeciesValue) at every output entry.
 #ifndef CP_WAVES_PER_EU
-#define CP_WAVES_PER_EU 3  // 168 VGPRs: 3 cells per SIMD (measured best: 2 waves 62 ms, 3 waves 51 ms, 4 waves 61 ms per C4 batch)
+// occupancy target: four-cell wavefronts hold 4 cells' LDS (~18 KB, so at most 2 per SIMD) and
+// get the full 256 VGPRs; one-cell wavefronts run 3 per SIMD at 168 VGPRs (measured best for
+// NS = 15 in that layout: 2 waves 62 ms, 3 waves 51 ms, 4 waves 61 ms per C4 batch)
+#define CP_WAVES_PER_EU ((CP_NS <= 16) ? 2 : 3)
 #endif
+// CP_CELLS_PER_WAVE cells per workgroup (one wavefront): cell blockIdx.x * CPW + row
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CP_WAVES_PER_EU))) void cp_solve_kernel(cpk::CpSolveArgs a)
 {
     using namespace cpk;
     constexpr int NS = CP_NS, NP = CP_NP, NC = CP_NC;
     constexpr int MM = CP_M;
-    __shared__ Shared<NS, NP, NC, MM> sh;
-    const int wi = (int)blockIdx.x;
-    if (wi >= a.n_work) return;
+    __shared__ Shared<NS, NP, NC, MM> shs[CPW];
+    const int wi = (int)blockIdx.x * CPW + row();
+    if (wi >= a.n_work) return;  // the whole row: rows are cells
+    Shared<NS, NP, NC, MM>& sh = shs[row()];
     const int slot = a.work[wi];
     const int ln = lane();
-    if (ln < NP) sh.prm[ln] = a.params[(size_t)slot * NP + ln];
-    if (ln < NC) sh.cs[ln] = a.constant_species[ln];
+    for (int k = ln; k < NP; k += ROW) sh.prm[k] = a.params[(size_t)slot * NP + k];
+    for (int k = ln; k < NC; k += ROW) sh.cs[k] = a.constant_species[k];
     const double creation = a.creation[slot];
     const double y0 = (ln < NS) ? a.y0[(size_t)slot * NS + ln] : 0.0;
     const int M = MM;
     double* outv = sh.outl;
-    for (int k = ln; k < M; k += WAVE) outv[k] = __builtin_nan("");
+    for (int k = ln; k < M; k += ROW) outv[k] = __builtin_nan("");
 #ifdef CP_PHASES
     if (ln < 8) sh.ph[ln] = 0;
     const long long ph_kernel0 = clock64();
@@ -947,22 +981,22 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
             // Cell::integration_step_cb (Cell.cpp:463-538)
             const double y = s.zn[0];
             bool cont = true;
-            if (a.ev[0] >= 0 && ev[0] != ev[0] && bcast(y, a.ev[0]) > 1e-4) ev[0] = crossing_time(t, previous_step_time, 1e-4, true);
-            if (a.ev[1] >= 0 && ev[1] != ev[1] && bcast(y, a.ev[1]) > 1.95) ev[1] = crossing_time(t, previous_step_time, 1.95, true);
-            if (a.ev[2] >= 0 && ev[2] != ev[2] && bcast(y, a.ev[2]) > 0.5) ev[2] = crossing_time(t, previous_step_time, 0.5, true);
-            if (a.ev[3] >= 0 && ev[3] != ev[3] && bcast(y, a.ev[3]) < 0.5) ev[3] = crossing_time(t, previous_step_time, 0.5, false);
-            if (a.ev[4] >= 0 && ev[4] != ev[4] && bcast(y, a.ev[4]) > 1e-3) {
+            if (a.ev[0] >= 0 && ev[0] != ev[0] && rowget(y, a.ev[0]) > 1e-4) ev[0] = crossing_time(t, previous_step_time, 1e-4, true);
+            if (a.ev[1] >= 0 && ev[1] != ev[1] && rowget(y, a.ev[1]) > 1.95) ev[1] = crossing_time(t, previous_step_time, 1.95, true);
+            if (a.ev[2] >= 0 && ev[2] != ev[2] && rowget(y, a.ev[2]) > 0.5) ev[2] = crossing_time(t, previous_step_time, 0.5, true);
+            if (a.ev[3] >= 0 && ev[3] != ev[3] && rowget(y, a.ev[3]) < 0.5) ev[3] = crossing_time(t, previous_step_time, 0.5, false);
+            if (a.ev[4] >= 0 && ev[4] != ev[4] && rowget(y, a.ev[4]) > 1e-3) {
                 ev[4] = crossing_time(t, previous_step_time, 1e-3, true);
                 sim_end = fmax(sim_end, ev[4] + a.past_cs);
                 end_time = sim_end;
             }
-            if (a.divide_cells && a.ev[5] >= 0 && bcast(y, a.ev[5]) > 1.0) {
+            if (a.divide_cells && a.ev[5] >= 0 && rowget(y, a.ev[5]) > 1.0) {
                 sim_end = t;
                 yend = y;
                 divided = true;
                 cont = false;
             }
-            if (a.ev[6] >= 0 && bcast(y, a.ev[6]) > 1.0) {
+            if (a.ev[6] >= 0 && rowget(y, a.ev[6]) > 1.0) {
                 sim_end = t;
                 yend = y;
                 died = true;
@@ -985,7 +1019,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
     }
     // GetInterpolatedSpeciesValue: NaN outside [0, simulation_end_time] of the cell
     wave_sync();
-    for (int k = ln; k < M; k += WAVE) {
+    for (int k = ln; k < M; k += ROW) {
         const double ct = a.output_times[k] - creation;
         a.out_values[(size_t)slot * M + k] = (ct < 0.0 || ct > sim_end) ? __builtin_nan("") : outv[k];
     }
