@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstring>
 #include <fstream>
+#include <algorithm>
 #include <limits>
 
 #include "log.h"
@@ -652,22 +653,28 @@ bool SampleFileWriter::Initialize(const std::string& filename, size_t num_sample
     const int v_var = h.AddVar("samples.variable", NcChar, {dv, dl});
     const int v_temp = h.AddVar("samples.temperature", NcDouble, {dt});
     const int v_tr = h.AddVar("samples.variable_transform", NcInt, {dv});
-    v_vals_ = h.AddVar("samples.variable_values", NcDouble, {ds, dt, dv});
     v_lp_ = h.AddVar("samples.log_prior", NcDouble, {ds, dt});
     v_llh_ = h.AddVar("samples.log_likelihood", NcDouble, {ds, dt});
     v_w_ = h.AddVar("samples.weights", NcDouble, {ds, dt});
+    // last: CDF-2 lets only the last variable exceed 4 GiB (long runs x large ladders)
+    v_vals_ = h.AddVar("samples.variable_values", NcDouble, {ds, dt, dv});
     for (int v : {v_vals_, v_lp_, v_llh_, v_w_}) h.vars[v].attrs.push_back(NcAttr{"_FillValue", NcDouble, "", {kNcFillDouble}});
     // the process holding temperature 0 writes the shared coordinate variables; every process
     // fills only its own temperature columns (no process truncates: see NcClassicWriter::Create)
     const bool lead = (first_ == 0);
     const std::vector<int> none;
     if (!w_.Create(filename, false, &none)) return false;
-    std::vector<double> fill(n_ * own_ * d_, kNcFillDouble);
-    if (own_ > 0 && (!w_.PutDouble(v_vals_, {0, first_, 0}, {n_, own_, d_}, fill.data()) ||
-                     !w_.PutDouble(v_lp_, {0, first_}, {n_, own_}, fill.data()) ||
-                     !w_.PutDouble(v_llh_, {0, first_}, {n_, own_}, fill.data()) ||
-                     !w_.PutDouble(v_w_, {0, first_}, {n_, own_}, fill.data())))
-        return false;
+    // fill this process's columns in slabs of samples (bounded host memory)
+    const size_t chunk = std::max<size_t>(1, (size_t)(1 << 20) / std::max<size_t>(1, own_ * d_));
+    std::vector<double> fill(std::min(chunk, n_) * own_ * d_, kNcFillDouble);
+    for (size_t s0 = 0; own_ > 0 && s0 < n_; s0 += chunk) {
+        const size_t m = std::min(chunk, n_ - s0);
+        if (!w_.PutDouble(v_vals_, {s0, first_, 0}, {m, own_, d_}, fill.data()) ||
+            !w_.PutDouble(v_lp_, {s0, first_}, {m, own_}, fill.data()) ||
+            !w_.PutDouble(v_llh_, {s0, first_}, {m, own_}, fill.data()) ||
+            !w_.PutDouble(v_w_, {s0, first_}, {m, own_}, fill.data()))
+            return false;
+    }
     if (lead) {
         std::vector<int32_t> six(n_);
         for (size_t i = 0; i < n_; i++) six[i] = (int32_t)(i + 1);

@@ -200,3 +200,20 @@ def test_sample_file_rejects_bad_geometry(tmp_path):
         f.write(0, 1, [[1.0], [2.0]], [0.0, 0.0], [0.0, 0.0])
     f.close()
     assert math.isclose(os.path.getsize(str(tmp_path / "o.nc")) % 4, 0)
+
+
+def test_sample_file_chunked_fill(tmp_path):
+    """more fill values than one slab (the writer fills a process's columns slab by slab)"""
+    from bcm3_amd.ptmh import SampleFile
+    path = str(tmp_path / "big.nc")
+    N, d = 3000, 200
+    names = [f"v{i}" for i in range(d)]
+    f = SampleFile(path, N, names, [0] * d, [0.5, 1.0])
+    x = np.arange(2 * d, dtype=float).reshape(2, d)
+    f.write(N - 1, 0, x, [1.0, 2.0], [3.0, 4.0])
+    f.close()
+    v, fill = _read_samples(path)
+    assert v["variable_values"].shape == (N, 2, d)
+    assert np.all(v["variable_values"][:N - 1] == fill)
+    assert np.array_equal(v["variable_values"][N - 1], x)
+    assert np.array_equal(v["log_likelihood"][N - 1], [3.0, 4.0]) and np.all(v["weights"][:N - 1] == fill)
