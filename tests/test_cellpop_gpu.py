@@ -27,14 +27,17 @@ import cellpop as CP
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(scope="module")
-def setup(tmp_path_factory):
+# (initial cells, max cells, draws): the small case runs many draws; the larger one fills several
+# four-cell wavefronts per generation with cells of different dynamics (rows diverge)
+@pytest.fixture(scope="module", params=[(6, 64, 12), (40, 256, 4)], ids=["6cells", "40cells"])
+def setup(request, tmp_path_factory):
     from bcm3_amd.likelihood import Likelihood
+    nc, mc, nd = request.param
     d = tmp_path_factory.mktemp("cellpop_gpu")
-    path = CH.write_likelihood(d, 6, 64)
+    path = CH.write_likelihood(d, nc, mc)
     ll = Likelihood(path, CH.PRIOR, device=0)
     prob = CP.load_problem(path, CH.PRIOR)
-    x = CH.draws(12, 11)
+    x = CH.draws(nd, 11)
     ref = CP.simulate(prob, x)
     ref_nofma = CP.simulate(CP.load_problem(path, CH.PRIOR, variant="nofma"), x)
     yield ll, prob, x, ref, ref_nofma
