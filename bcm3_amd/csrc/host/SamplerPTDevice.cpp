@@ -793,8 +793,8 @@ bool SamplerPTDevice::SetOutput(const std::string& filename, int64_t num_samples
 {
     Impl& s = *p_;
     const VariableSet* vs = s.ll ? s.ll->GetVariableSet() : nullptr;
-    if (!vs || num_samples < 1 || s.emitted != 0) {
-        LOGERROR("SetOutput: needs an initialised sampler before its first sample");
+    if (!vs || num_samples < 1 || s.emitted != 0 || s.out) {
+        LOGERROR("SetOutput: needs an initialised sampler before its first sample, once");
         return false;
     }
     std::vector<std::string> names(vs->GetVariableNames());
