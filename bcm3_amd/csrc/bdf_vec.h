@@ -337,7 +337,7 @@ struct TqCtx {
     double alpha0, alpha0_hat, xi_inv, xistar_inv, hsum2, lq, A2;  // hsum2: before complete shifts tau
 };
 
-template <int Q, class S>
+template <int Q, bool NSTPOS = false, class S>
 BDF_INL double set_bdf_q(S& s, TqCtx& c)
 {
     constexpr int q = Q;
@@ -377,9 +377,14 @@ BDF_INL double set_bdf_q(S& s, TqCtx& c)
     // estimate (one Newton step, frcp) differs, so the operand is passed through a runtime 1.0
     const double rl1 = frcp((q == 2) ? s.l[1] * s.unity : s.l[1]);
     s.gamma = s.h * rl1;
-    s.gammap = (s.nst == 0) ? s.gamma : s.gammap;
-    const double gr = fdiv(s.gamma, s.gammap);
-    s.gamrat = (s.nst > 0) ? gr : 1.0;
+    if constexpr (NSTPOS) {
+        // fast_run: nst > 0 by its precondition
+        s.gamrat = fdiv(s.gamma, s.gammap);
+    } else {
+        s.gammap = (s.nst == 0) ? s.gamma : s.gammap;
+        const double gr = fdiv(s.gamma, s.gammap);
+        s.gamrat = (s.nst > 0) ? gr : 1.0;
+    }
     return rl1;
 }
 
@@ -476,14 +481,14 @@ BDF_INL bool newton_rest(S& s, const Model& mdl, double rl1, int convfail, bool 
 // correction and the error test passes -- is decided by ONE branch on both tests (the local
 // error dsm = acnrm tq[2] of a first-iteration convergence is del tq[2]); anything else goes on
 // through newton_rest, which repeats the convergence test on the same del.
-template <int Q, int NS, class S, class Model>
+template <int Q, int NS, bool NSTPOS = false, class S, class Model>
 BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, int nflag, double& dsm, TqCtx& tc)
 {
     if (BDF_UNLIKELY(eta_eff != 1.0)) vec::rescale_q<Q>(s, eta_eff);
     BDF_PH(2);
     vec::predict_q<Q>(s);
     BDF_PH(3);
-    const double rl1 = vec::set_bdf_q<Q>(s, tc);
+    const double rl1 = vec::set_bdf_q<Q, NSTPOS>(s, tc);
     BDF_PH(4);
     const int convfail = ((nflag == FIRST_CALL) | (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
     const bool callSetup = (nflag == PREV_CONV_FAIL) | (nflag == PREV_ERR_FAIL) | (s.nst == 0) |
@@ -523,9 +528,11 @@ BDF_INL void complete_head_q(S& s)
     cfor<0, Q + 1>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j)] = __builtin_fma(s.l[CI(j)], s.acor, s.zn[CI(j)]); });
     s.qwait--;
     if constexpr (q != QMAX) {
-        const bool save = (s.qwait == 1);
-        s.zn[QMAX] = save ? s.acor : s.zn[QMAX];
-        s.saved_tq5 = save ? s.tq[5] : s.saved_tq5;
+        // qwait is a scalar counter: a scalar branch instead of four VALU selects every step
+        if (s.qwait == 1) {
+            s.zn[QMAX] = s.acor;
+            s.saved_tq5 = s.tq[5];
+        }
     }
     BDF_PH(7);
 }
@@ -804,7 +811,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         const double eta_eff = (s.hprime != s.h) ? s.eta : 1.0;
         double dsm;
         TqCtx tc;
-        const int r = vec::attempt_q<Q, NS>(s, mdl, eta_eff, saved_t, FIRST_CALL, dsm, tc);
+        const int r = vec::attempt_q<Q, NS, true>(s, mdl, eta_eff, saved_t, FIRST_CALL, dsm, tc);
         if (BDF_UNLIKELY(r != uni::ATTEMPT_OK)) {
             // failed first attempt: the attempt loop takes over from here
             s.tretlast = saved_t;
