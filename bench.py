@@ -401,13 +401,18 @@ def cellpop_workload(device, gen, n=64):
     ll = Likelihood(lik, pri, device=device.index or 0)
     x = DevicePrior(load_prior(pri), device).sample(n, gen).contiguous()
     ms = _rate(ll, n, x, device, reps=2)
-    cells = 0
+    cells = steps = 0
     for i in range(n):
         rec, _, _ = ll.cellpop_cells(i, 21, 15)
         cells += len(rec)
+        steps += int(rec["nsteps"].sum())
     ll.close()
     return {"chains": n, "kernel_ms": ms, "evals_per_s": n / (ms * 1e-3), "cells_per_eval": cells / n,
-            "cell_trajectories_per_s": cells / (ms * 1e-3), "draws": x.detach().cpu().numpy()}
+            "cell_trajectories_per_s": cells / (ms * 1e-3), "bdf_steps_per_cell": steps / max(1, cells),
+            "cell_bdf_steps_per_s": steps / (ms * 1e-3), "cells_per_wavefront": 4,
+            "note": "throughput-bound (every SIMD busy); four cells per wavefront, one 16-lane row each "
+                    "(DESIGN.md §4 'cell population')",
+            "draws": x.detach().cpu().numpy()}
 
 
 def cellpop_cpu_baseline(draws, budget_s: float):
