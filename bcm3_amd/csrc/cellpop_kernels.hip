@@ -141,6 +141,7 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
         const double stdev = cp_ref(dl.stdev, v, m.transforms, 1.0);
         const double offset = cp_ref(dl.offset, v, m.transforms, 0.0);
         const double scale = cp_ref(dl.scale, v, m.transforms, 1.0);
+        const double pstdev = cp_ref(dl.proportional_stdev, v, m.transforms, 0.0);
         const double minus_log_sigma = -log(stdev);
         const double inv2 = 1.0 / (2.0 * stdev * stdev);
         double lp = 0.0;
@@ -151,11 +152,21 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
             for (int j = 0; j < dl.R; j++) {
                 const double o = dl.observed[(size_t)j * dl.T + i];
                 if (o == o) {
-                    if (dl.error_model == 0) {
+                    // DataLikelihoodTimeCourseBase::EvaluateValue(simulated, observed) called as
+                    // EvaluateValue(data, x) by the population average (.cpp:150): the data value
+                    // takes the "simulated" role, so the proportional terms scale with it
+                    if (dl.error_model == BCM3HIP_CP_ERR_NORMAL) {
                         const double dd = x - o;
                         lp += minus_log_sigma - 0.91893853320467274178032973640562 - dd * dd * inv2;
-                    } else {
+                    } else if (dl.error_model == BCM3HIP_CP_ERR_T4) {
                         lp += log_pdf_tnu4(o, x, stdev);
+                    } else {
+                        const double sp = pstdev * fmax(o, 0.0);
+                        const double sigma = (dl.error_model == BCM3HIP_CP_ERR_PROPORTIONAL) ? sp : stdev + sp;
+                        // bcm3::LogPdfNormal(x, o, sigma) (ProbabilityDistributions.cpp:129-138)
+                        const double two_sigma_sq = 2.0 * sigma * sigma;
+                        const double dd = x - o;
+                        lp += -log(sigma) - 0.91893853320467274178032973640562 - dd * dd / two_sigma_sq;
                     }
                 }
             }

@@ -235,10 +235,15 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
         d.data_name = dn->get("data_name");
         d.weight = dn->get_double("weight", 1.0);
         const std::string em = dn->has_attr("error_model") ? dn->get("error_model") : std::string("normal");
+        // DataLikelihoodBase::Load (src/cellpop/DataLikelihoodBase.cpp:51-70)
         if (em == "normal" || em == "additive_normal")
-            d.error_model = 0;
+            d.error_model = BCM3HIP_CP_ERR_NORMAL;
+        else if (em == "proportional_normal")
+            d.error_model = BCM3HIP_CP_ERR_PROPORTIONAL;
+        else if (em == "additive_proportional_normal")
+            d.error_model = BCM3HIP_CP_ERR_ADDITIVE_PROPORTIONAL;
         else if (em == "student_t4" || em == "t4")
-            d.error_model = 1;
+            d.error_model = BCM3HIP_CP_ERR_T4;
         else {
             LOGERROR("cell_population: error model \"%s\" is not supported", em.c_str());
             return false;
@@ -250,6 +255,15 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
             return false;
         }
         if (!ParseRef(dn->get("stdev"), d.stdev)) return false;
+        const std::string ps = dn->has_attr("proportional_stdev") ? dn->get("proportional_stdev") : std::string();
+        if ((d.error_model == BCM3HIP_CP_ERR_PROPORTIONAL || d.error_model == BCM3HIP_CP_ERR_ADDITIVE_PROPORTIONAL) &&
+            ps.empty()) {
+            LOGERROR("Proportional error model is selected, but proportional stdev has not been specified.");
+            return false;
+        }
+        // GetCurrentProportionalSTDev: 0 when not given
+        d.proportional_stdev = bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0};
+        if (!ps.empty() && !ParseRef(ps, d.proportional_stdev)) return false;
         d.offset = bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0};
         d.scale = bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 1.0};
         if (dn->has_attr("offset") && !ParseRef(dn->get("offset"), d.offset)) return false;
@@ -397,7 +411,8 @@ bool LikelihoodCellPopulation::PostInitialize()
     data_flat.clear();
     for (const auto& d : data)
         data_flat.push_back(bcm3hip_cellpop_data{(int32_t)d.times.size(), d.R, d.observed.data(), d.entry.data(), d.stdev,
-                                                 d.offset, d.scale, d.weight, d.error_model});
+                                                 d.offset, d.scale, d.weight, d.error_model,
+                                                 d.proportional_stdev});
     model = bcm3hip_cellpop_model{};
     model.derivative_body = derivative_body.c_str();
     model.NS = (int32_t)NS;

@@ -38,7 +38,7 @@ private:
         std::vector<double> times;
         std::vector<double> observed;  // [R][T]
         int32_t R = 0;
-        bcm3hip_value_ref stdev{}, offset{}, scale{};
+        bcm3hip_value_ref stdev{}, offset{}, scale{}, proportional_stdev{};
         double weight = 1.0;
         int32_t error_model = 0;
         std::vector<int32_t> entry;

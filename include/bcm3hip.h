@@ -199,8 +199,11 @@ typedef struct {
     const int32_t* entry;     /* [T] output entry (sorted simulation time point) of each time point */
     bcm3hip_value_ref stdev, offset, scale;
     double weight;
-    int32_t error_model;      /* 0 normal, 1 student t4 */
+    int32_t error_model;      /* BCM3HIP_CP_ERR_*: DataLikelihoodBase::Load's error_model */
+    bcm3hip_value_ref proportional_stdev; /* proportional_stdev (BCM3HIP_REF_NONE = 0) */
 } bcm3hip_cellpop_data;
+enum { BCM3HIP_CP_ERR_NORMAL = 0, BCM3HIP_CP_ERR_T4 = 1, BCM3HIP_CP_ERR_PROPORTIONAL = 2,
+       BCM3HIP_CP_ERR_ADDITIVE_PROPORTIONAL = 3 };
 
 typedef struct {
     const char* derivative_body; /* SBMLModel::GenerateCode's generated_derivative body */

@@ -229,7 +229,11 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant=""):
                  stdev=_ref_value(dl.get("stdev"), variables),
                  offset=_ref_value(dl.get("offset"), variables) if dl.get("offset") else None,
                  scale=_ref_value(dl.get("scale"), variables) if dl.get("scale") else None,
-                 error_model={"normal": "normal", "additive_normal": "normal", "student_t4": "t4", "t4": "t4"}[em],
+                 error_model={"normal": "normal", "additive_normal": "normal", "student_t4": "t4", "t4": "t4",
+                              "proportional_normal": "proportional",
+                              "additive_proportional_normal": "additive_proportional"}[em],
+                 proportional_stdev=(_ref_value(dl.get("proportional_stdev"), variables)
+                                     if dl.get("proportional_stdev") else None),
                  relative_to_time_average=_bool(dl.get("relative_to_time_average"), False))
         for ti, t in enumerate(times):
             timepoints.append((len(dls), t, ti, six))
@@ -438,6 +442,16 @@ def _popavg_logp(d, avg, tv):
                 if d["error_model"] == "normal":
                     dd = x - o  # EvaluateValue(observed_data, x): d = observed - simulated with the arguments swapped
                     logp += minus_log_sigma - 0.91893853320467274178032973640562 - dd * dd * inv2
+                elif d["error_model"] in ("proportional", "additive_proportional"):
+                    # DataLikelihoodTimeCourseBase.cpp:280-286 with the swapped arguments: the data
+                    # value is "simulated", LogPdfNormal(x, o, sigma) (ProbabilityDistributions.cpp:129-138)
+                    ps = _refval(d["proportional_stdev"], tv) if d["proportional_stdev"] else 0.0
+                    sigma = ps * max(o, 0.0)
+                    if d["error_model"] == "additive_proportional":
+                        sigma = stdev + sigma
+                    two_sigma_sq = 2.0 * sigma * sigma
+                    dd = x - o
+                    logp += -math.log(sigma) - 0.91893853320467274178032973640562 - dd * dd / two_sigma_sq
                 else:
                     z = (o - x) / stdev
                     logp += -0.9808292530117262 - 2.5 * math.log1p(0.25 * z * z) - math.log(stdev)

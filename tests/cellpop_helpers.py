@@ -17,12 +17,13 @@ import make_cellpop_fixtures as F  # noqa: E402
 PRIOR = os.path.join(GOLDEN, "cellpop_prior.xml")
 
 
-def write_likelihood(directory, num_cells, max_cells, name="cellpop_small_likelihood.xml"):
+def write_likelihood(directory, num_cells, max_cells, name="cellpop_small_likelihood.xml", **attrs):
+    """attrs: data_attrs / experiment_attrs of make_cellpop_fixtures.likelihood_text"""
     path = os.path.join(str(directory), name)
     with open(path, "w") as f:
         f.write(F.likelihood_text(num_cells=num_cells, max_cells=max_cells,
                                   data_file=os.path.join(GOLDEN, "cellpop_data.json"),
-                                  model_file=os.path.join(GOLDEN, "cellpop_model.xml")))
+                                  model_file=os.path.join(GOLDEN, "cellpop_model.xml"), **attrs))
     return path
 
 

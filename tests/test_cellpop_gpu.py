@@ -14,8 +14,9 @@ logp on these draws. The GPU must sit inside that spread:
   * step counts equal for >= 95 % of the cells;
   * creation and division times within 0.1 h (a step flip moves a division by one step),
     data values within 1e-3 relative;
-  * logp within 2e-4 * (1 + |logp|) for every draw, the -inf pattern identical, and the median
-    GPU-vs-oracle deviation no larger than 10x the median oracle-vs-oracle(no FMA) deviation."""
+  * logp within 2e-4 * (1 + |logp|) for every draw (or within 3x the two reference builds' own
+    difference on that draw, when larger), the -inf pattern identical, and the median GPU-vs-oracle
+    deviation no larger than 10x the median oracle-vs-oracle(no FMA) deviation."""
 import math
 
 import numpy as np
@@ -27,14 +28,21 @@ import cellpop as CP
 pytestmark = pytest.mark.gpu
 
 
-# (initial cells, max cells, draws): the small case runs many draws; the larger one fills several
-# four-cell wavefronts per generation with cells of different dynamics (rows diverge)
-@pytest.fixture(scope="module", params=[(6, 64, 12), (40, 256, 4)], ids=["6cells", "40cells"])
+# (initial cells, max cells, draws, likelihood options): the small case runs many draws; the larger
+# one fills several four-cell wavefronts per generation with cells of different dynamics (rows
+# diverge); the last two take the other error models (DataLikelihoodBase.cpp:51-70) and a
+# population without division
+CASES = [(6, 64, 12, {}), (40, 256, 4, {}),
+         (8, 64, 6, dict(data_attrs='stdev="stdev" error_model="additive_proportional_normal" proportional_stdev="0.05"')),
+         (6, 32, 6, dict(data_attrs='stdev="stdev" error_model="t4"', experiment_attrs=' divide_cells="false"'))]
+
+
+@pytest.fixture(scope="module", params=CASES, ids=["6cells", "40cells", "addprop", "t4_nodiv"])
 def setup(request, tmp_path_factory):
     from bcm3_amd.likelihood import Likelihood
-    nc, mc, nd = request.param
+    nc, mc, nd, attrs = request.param
     d = tmp_path_factory.mktemp("cellpop_gpu")
-    path = CH.write_likelihood(d, nc, mc)
+    path = CH.write_likelihood(d, nc, mc, **attrs)
     ll = Likelihood(path, CH.PRIOR, device=0)
     prob = CP.load_problem(path, CH.PRIOR)
     x = CH.draws(nd, 11)
@@ -53,7 +61,11 @@ def test_logp_matches_oracle(setup):
         if r == -math.inf:
             assert lp[i] == -math.inf and status[i] == 1, i
         else:
-            assert abs(lp[i] - r) <= 2e-4 * (1.0 + abs(r)), (i, lp[i], r)
+            # per draw: 2e-4 relative, or 3x the reference's own FMA / no-FMA difference on this
+            # draw when that is larger (a division one step earlier moves a small-sigma data
+            # likelihood by more; e.g. addprop draw 2: the two reference builds differ by 6.8e-3)
+            tol = max(2e-4 * (1.0 + abs(r)), 3.0 * abs(ref_nofma["logp"][i] - r))
+            assert abs(lp[i] - r) <= tol, (i, lp[i], r, ref_nofma["logp"][i])
             assert status[i] == 0
             dev.append(abs(lp[i] - r) / (1.0 + abs(r)))
             spread.append(abs(ref_nofma["logp"][i] - r) / (1.0 + abs(r)))
