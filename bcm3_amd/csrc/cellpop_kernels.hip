@@ -144,11 +144,23 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
         const double pstdev = cp_ref(dl.proportional_stdev, v, m.transforms, 0.0);
         const double minus_log_sigma = -log(stdev);
         const double inv2 = 1.0 / (2.0 * stdev * stdev);
+        // relative_to_time_average (DataLikelihoodTimeCoursePopulationAverage.cpp:106-113): add
+        // the offset, divide by the mean over the time points, take the log, then scale
+        double tmean = 0.0;
+        if (dl.relative_to_time_average) {
+            for (int i = 0; i < dl.T; i++) tmean += avg[(size_t)e * m.M + dl.entry[i]] + offset;
+            tmean /= (double)dl.T;
+        }
         double lp = 0.0;
         for (int i = 0; i < dl.T; i++) {
             double x = avg[(size_t)e * m.M + dl.entry[i]];
-            x *= scale;
-            x += offset;
+            if (dl.relative_to_time_average) {
+                x = log((x + offset) / tmean);
+                x *= scale;
+            } else {
+                x *= scale;
+                x += offset;
+            }
             for (int j = 0; j < dl.R; j++) {
                 const double o = dl.observed[(size_t)j * dl.T + i];
                 if (o == o) {

@@ -248,7 +248,8 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
             LOGERROR("cell_population: error model \"%s\" is not supported", em.c_str());
             return false;
         }
-        if (dn->get_bool("relative_to_time_average", false) || dn->get_bool("use_log_ratio", false) ||
+        d.relative_to_time_average = dn->get_bool("relative_to_time_average", false) ? 1 : 0;
+        if (dn->get_bool("use_log_ratio", false) ||
             dn->get_bool("optimize_offset_scale", false) || dn->get_bool("include_only_cells_that_went_through_mitosis", false) ||
             dn->has_attr("saturation_scale")) {
             LOGERROR("cell_population: unsupported option on data \"%s\"", d.data_name.c_str());
@@ -412,7 +413,7 @@ bool LikelihoodCellPopulation::PostInitialize()
     for (const auto& d : data)
         data_flat.push_back(bcm3hip_cellpop_data{(int32_t)d.times.size(), d.R, d.observed.data(), d.entry.data(), d.stdev,
                                                  d.offset, d.scale, d.weight, d.error_model,
-                                                 d.proportional_stdev});
+                                                 d.proportional_stdev, d.relative_to_time_average});
     model = bcm3hip_cellpop_model{};
     model.derivative_body = derivative_body.c_str();
     model.NS = (int32_t)NS;

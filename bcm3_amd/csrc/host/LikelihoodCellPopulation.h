@@ -41,6 +41,7 @@ private:
         bcm3hip_value_ref stdev{}, offset{}, scale{}, proportional_stdev{};
         double weight = 1.0;
         int32_t error_model = 0;
+        int32_t relative_to_time_average = 0;
         std::vector<int32_t> entry;
     };
     bool LoadExperiment(const XmlNode& ex, const OptionsMap& vm);

@@ -201,6 +201,7 @@ typedef struct {
     double weight;
     int32_t error_model;      /* BCM3HIP_CP_ERR_*: DataLikelihoodBase::Load's error_model */
     bcm3hip_value_ref proportional_stdev; /* proportional_stdev (BCM3HIP_REF_NONE = 0) */
+    int32_t relative_to_time_average;     /* log(x / time mean of x) before the data likelihood */
 } bcm3hip_cellpop_data;
 enum { BCM3HIP_CP_ERR_NORMAL = 0, BCM3HIP_CP_ERR_T4 = 1, BCM3HIP_CP_ERR_PROPORTIONAL = 2,
        BCM3HIP_CP_ERR_ADDITIVE_PROPORTIONAL = 3 };

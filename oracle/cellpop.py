@@ -424,9 +424,19 @@ def _popavg_logp(d, avg, tv):
     offset = _refval(d["offset"], tv) if d["offset"] else 0.0
     scale = _refval(d["scale"], tv) if d["scale"] else 1.0
     a = avg.copy()
-    assert not d["relative_to_time_average"]
-    a *= scale
-    a += offset
+    if d["relative_to_time_average"]:
+        # DataLikelihoodTimeCoursePopulationAverage.cpp:106-113 (the time mean summed in time order;
+        # Eigen's vectorised colwise mean may round the last bit differently)
+        a += offset
+        tm = 0.0
+        for i in range(a.shape[0]):
+            tm += a[i, 0]
+        tm /= a.shape[0]
+        a = np.log(a / tm)
+        a *= scale
+    else:
+        a *= scale
+        a += offset
     minus_log_sigma = -math.log(stdev)
     inv2 = 1.0 / (2.0 * stdev * stdev)
     logp = 0.0

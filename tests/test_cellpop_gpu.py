@@ -34,10 +34,11 @@ pytestmark = pytest.mark.gpu
 # population without division
 CASES = [(6, 64, 12, {}), (40, 256, 4, {}),
          (8, 64, 6, dict(data_attrs='stdev="stdev" error_model="additive_proportional_normal" proportional_stdev="0.05"')),
-         (6, 32, 6, dict(data_attrs='stdev="stdev" error_model="t4"', experiment_attrs=' divide_cells="false"'))]
+         (6, 32, 6, dict(data_attrs='stdev="stdev" error_model="t4"', experiment_attrs=' divide_cells="false"')),
+         (6, 64, 6, dict(data_attrs='stdev="stdev" relative_to_time_average="true" offset="0.05"'))]
 
 
-@pytest.fixture(scope="module", params=CASES, ids=["6cells", "40cells", "addprop", "t4_nodiv"])
+@pytest.fixture(scope="module", params=CASES, ids=["6cells", "40cells", "addprop", "t4_nodiv", "reltime"])
 def setup(request, tmp_path_factory):
     from bcm3_amd.likelihood import Likelihood
     nc, mc, nd, attrs = request.param
