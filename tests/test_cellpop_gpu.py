@@ -120,3 +120,25 @@ def test_too_many_cells_is_minus_inf(tmp_path):
     lp, status = ll.evaluate_batch(np.array([CH.F.true_values()]))
     assert lp[0] == -math.inf and status[0] == 1
     ll.close()
+
+
+def test_sampler_drives_cell_population(tmp_path):
+    """config C4 end to end: the C++ PT-MH sampler (bcm3_ptmh_*) with the cell-population likelihood
+    -- proposals, batched evaluation of all chains per mutate step, accept, exchange -- and the
+    final chain states' log-likelihoods equal a fresh evaluation of the same values"""
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.ptmh import PTMHNative
+    path = CH.write_likelihood(tmp_path, 6, 64)
+    ll = Likelihood(path, CH.PRIOR, device=0)
+    s = PTMHNative(ll, CH.PRIOR, 8, seed=3, adapt_proposal_samples=0)
+    s.iterate(6)
+    s.synchronize()
+    st = s.state()
+    c = s.counters()
+    s.close()
+    assert c["attempted_mutate"] == 6 * 8 and c["accepted_mutate"] > 0
+    lp, _ = ll.evaluate_batch(st["values"])
+    fin = np.isfinite(st["llh"])
+    assert fin.any()
+    np.testing.assert_array_equal(lp[fin], st["llh"][fin])
+    ll.close()
