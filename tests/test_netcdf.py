@@ -217,3 +217,15 @@ def test_sample_file_chunked_fill(tmp_path):
     assert np.all(v["variable_values"][:N - 1] == fill)
     assert np.array_equal(v["variable_values"][N - 1], x)
     assert np.array_equal(v["log_likelihood"][N - 1], [3.0, 4.0]) and np.all(v["weights"][:N - 1] == fill)
+
+
+@pytest.mark.parametrize("cut", [3, 40, 200, -64])
+def test_truncated_file_is_an_error(tmp_path, cut):
+    """a damaged data file fails the likelihood's Initialize with an error, never a crash"""
+    nc = str(tmp_path / "c3_pkdata.nc")
+    _convert("to-classic", os.path.join(GOLDEN, "c3_pkdata.json"), nc)
+    data = open(nc, "rb").read()
+    bad = str(tmp_path / "bad.nc")
+    open(bad, "wb").write(data[:cut])
+    with pytest.raises(RuntimeError):
+        _lik(_xml_with(tmp_path, "c3", "c3_pkdata.json", bad), "c3")
