@@ -318,7 +318,7 @@ Json NcClassicRead(const std::string& filename)
     Json doc;
     doc.type = Json::Object;
     auto split = [](const std::string& n, std::string& g, std::string& leaf) {
-        const size_t dot = n.find('.');
+        const size_t dot = n.rfind('.');
         if (dot == std::string::npos) {
             g.clear();
             leaf = n;
@@ -697,6 +697,100 @@ bool SampleFileWriter::Write(size_t sample_ix, size_t t0, size_t nt, const doubl
            w_.PutDouble(v_vals_, {sample_ix, t, 0}, {1, nt, d_}, values) &&
            w_.PutDouble(v_lp_, {sample_ix, t}, {1, nt}, lprior) && w_.PutDouble(v_llh_, {sample_ix, t}, {1, nt}, llh) &&
            w_.PutDouble(v_w_, {sample_ix, t}, {1, nt}, weight);
+}
+
+// ---------------------------------------------------------------------------------------------
+// NetCDFBundler
+
+void BundleFile::AddVector(const std::string& group, const std::string& name, const std::vector<double>& v)
+{
+    Item it;
+    it.group = group;
+    it.name = name;
+    it.rows = v.size();
+    it.d = v;
+    items_.push_back(std::move(it));
+}
+
+void BundleFile::AddVector(const std::string& group, const std::string& name, const std::vector<int32_t>& v)
+{
+    Item it;
+    it.group = group;
+    it.name = name;
+    it.is_int = true;
+    it.rows = v.size();
+    it.i = v;
+    items_.push_back(std::move(it));
+}
+
+void BundleFile::AddMatrix(const std::string& group, const std::string& name, size_t rows, size_t cols,
+                           const std::vector<double>& row_major)
+{
+    Item it;
+    it.group = group;
+    it.name = name;
+    it.rows = rows;
+    it.cols = cols;
+    it.d = row_major;
+    items_.push_back(std::move(it));
+}
+
+bool BundleFile::Write(const std::string& filename) const
+{
+    NcClassicWriter w;
+    std::vector<std::string> groups;
+    for (auto& it : items_)
+        if (std::find(groups.begin(), groups.end(), it.group) == groups.end()) groups.push_back(it.group);
+    std::string gl;
+    for (auto& g : groups) gl += (gl.empty() ? "" : " ") + g;
+    w.h.gattrs.push_back(NcAttr{"bcm3_groups", NcChar, gl, {}});
+    // every dimension gets a coordinate variable 1..n (NetCDFDataFile::CreateDimension)
+    struct Coord {
+        int var;
+        size_t n;
+    };
+    std::vector<Coord> coords;
+    std::vector<int> data_vars;
+    auto flat = [](const std::string& g, const std::string& n) {
+        std::string p = g;
+        for (auto& ch : p)
+            if (ch == '/') ch = '.';
+        return p.empty() ? n : p + "." + n;
+    };
+    auto dim = [&](const std::string& g, const std::string& n, size_t len) {
+        const int d = w.h.AddDim(flat(g, n), len);
+        coords.push_back(Coord{w.h.AddVar(flat(g, n), NcInt, {d}), len});
+        return d;
+    };
+    for (auto& it : items_) {
+        if (it.cols == 0) {
+            const int d = dim(it.group, it.name + "_dim", it.rows);
+            data_vars.push_back(w.h.AddVar(flat(it.group, it.name), it.is_int ? NcInt : NcDouble, {d}));
+        } else {
+            const int d1 = dim(it.group, it.name + "_dim1", it.rows);
+            const int d2 = dim(it.group, it.name + "_dim2", it.cols);
+            data_vars.push_back(w.h.AddVar(flat(it.group, it.name), NcDouble, {d1, d2}));
+        }
+    }
+    if (!w.Create(filename, true)) return false;
+    for (auto& c : coords) {
+        std::vector<int32_t> v(c.n);
+        for (size_t k = 0; k < c.n; k++) v[k] = (int32_t)(k + 1);
+        if (c.n && !w.PutInt(c.var, {0}, {c.n}, v.data())) return false;
+    }
+    for (size_t k = 0; k < items_.size(); k++) {
+        const Item& it = items_[k];
+        bool ok = true;
+        if (it.cols == 0 && it.rows == 0) continue;
+        if (it.cols == 0)
+            ok = it.is_int ? w.PutInt(data_vars[k], {0}, {it.rows}, it.i.data())
+                           : w.PutDouble(data_vars[k], {0}, {it.rows}, it.d.data());
+        else if (it.rows && it.cols)
+            ok = w.PutDouble(data_vars[k], {0, 0}, {it.rows, it.cols}, it.d.data());
+        if (!ok) return false;
+    }
+    w.Close();
+    return true;
 }
 
 }  // namespace bcm3

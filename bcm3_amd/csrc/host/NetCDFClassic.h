@@ -8,8 +8,9 @@
 //     sample_ix / variable / temperature and variables variable_transform, variable_values,
 //     log_prior, log_likelihood, weights).
 // The reference writes netCDF-4 (HDF5) with groups; classic files have no groups, so a group g's
-// dimension or variable n is stored as "g.n" (tools/nc_convert.py converts both ways where the
-// netCDF4 Python module is installed). NC_STRING variables become NC_CHAR [.., g.<dim>_strlen].
+// dimension or variable n is stored as "g.n", nested groups g/h as "g.h.n" (the name after the last
+// '.' is the member; tools/nc_convert.py converts both ways where the netCDF4 Python module is
+// installed). NC_STRING variables become NC_CHAR [.., g.<dim>_strlen].
 #pragma once
 #include <cstdint>
 #include <cstdio>
@@ -64,8 +65,8 @@ size_t NcTypeSize(int type);
 
 // Read: the whole file as the JSON tree the likelihood loaders take,
 // {"<group>": {"<var>": {"dims": [dim names], "data": nested arrays}}} -- numbers, NaN for the
-// variable's _FillValue, char arrays as strings along their last dimension. Names without a
-// group prefix go under the group "". Throws JsonError on malformed input.
+// variable's _FillValue, char arrays as strings along their last dimension. The group is the name
+// up to the last '.'; names without one go under the group "". Throws JsonError on malformed input.
 Json NcClassicRead(const std::string& filename);
 bool NcIsClassic(const std::string& filename);
 
@@ -125,6 +126,29 @@ private:
     NcClassicWriter w_;
     int v_six_ = -1, v_vals_ = -1, v_lp_ = -1, v_llh_ = -1, v_w_ = -1;
     size_t first_ = 0, own_ = 0, d_ = 0, n_ = 0;
+};
+
+// NetCDFBundler (src/utils/NetCDFBundler.cpp:34-80) as a whole-file writer: groups of vectors and
+// matrices, each with the reference's dimension names (<name>_dim, <name>_dim1 / _dim2) and their
+// 1-based coordinate variables; Write() (re)writes the whole file, so records can be added between
+// writes (sampler_adaptation.nc grows by one group per adaptation).
+class BundleFile {
+public:
+    void AddVector(const std::string& group, const std::string& name, const std::vector<double>& v);
+    void AddVector(const std::string& group, const std::string& name, const std::vector<int32_t>& v);
+    void AddMatrix(const std::string& group, const std::string& name, size_t rows, size_t cols,
+                   const std::vector<double>& row_major);
+    bool Write(const std::string& filename) const;
+
+private:
+    struct Item {
+        std::string group, name;
+        bool is_int = false;
+        size_t rows = 0, cols = 0;  // cols == 0: vector
+        std::vector<double> d;
+        std::vector<int32_t> i;
+    };
+    std::vector<Item> items_;
 };
 
 }  // namespace bcm3

@@ -269,6 +269,8 @@ struct SamplerPTDevice::Impl {
     int64_t out_samples = 0, out_first = 0, out_pending = 0, emitted = 0;
     int out_flush = 64;
     bool out_overflow_logged = false;
+    std::string adapt_file;
+    BundleFile adapt_out;
 
     bool Emit()
     {
@@ -633,8 +635,55 @@ struct SamplerPTDevice::Impl {
             !Upload(scale, dsc, stream) || !Upload(ema, dem, stream) ||
             bcm3hip_memset_async(hcount.p, 0, hcount.n * sizeof(int64_t), stream) != 0)
             return false;
+        if (!adapt_file.empty() && g0 + C == Ctot && !WriteAdaptation(C - 1, nc, w, mu, L, h, counts)) return false;
         cnt.adaptations_done++;
         return bcm3hip_stream_synchronize(stream) == 0;
+    }
+
+    bool WriteAdaptation(int64_t c, const std::vector<int32_t>& nc, const std::vector<double>& w,
+                         const std::vector<double>& mu, const std::vector<double>& L, const std::vector<float>& h,
+                         const std::vector<int64_t>& counts)
+    {
+        const std::string g = "adapt" + std::to_string(cnt.adaptations_done) + "/block1";
+        std::vector<int32_t> ix(d);
+        for (int j = 0; j < d; j++) ix[j] = j;
+        adapt_out.AddVector(g, "variable_indices", ix);
+        // covariance of component k = L_k L_k^T (the Cholesky factor the proposal state holds)
+        auto cov = [&](int k) {
+            std::vector<double> S((size_t)d * d, 0.0);
+            const double* Lk = &L[(size_t)((c * kmax + k) * d * d)];
+            for (int i = 0; i < d; i++)
+                for (int j = 0; j < d; j++) {
+                    double s = 0.0;
+                    for (int m = 0; m <= std::min(i, j); m++) s += Lk[i * d + m] * Lk[j * d + m];
+                    S[(size_t)i * d + j] = s;
+                }
+            return S;
+        };
+        if (kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
+            const int K = nc[c];
+            adapt_out.AddVector(g, "gmm_weights", std::vector<double>(w.begin() + c * kmax, w.begin() + c * kmax + K));
+            for (int k = 0; k < K; k++) {
+                const double* m = &mu[(size_t)((c * kmax + k) * d)];
+                adapt_out.AddVector(g, "cluster" + std::to_string(k) + "_mean", std::vector<double>(m, m + d));
+                adapt_out.AddMatrix(g, "cluster" + std::to_string(k) + "_covariance", d, d, cov(k));
+            }
+        } else {
+            adapt_out.AddMatrix(g, "covariance", d, d, cov(0));
+        }
+        if (cnt.adaptations_done >= 1) {
+            // the history this adaptation was fitted to (rows as stored in the device ring)
+            const int64_t rows = std::min<int64_t>(counts[c], H);
+            std::vector<double> hist((size_t)(rows * d));
+            for (int64_t r = 0; r < rows; r++)
+                for (int j = 0; j < d; j++) hist[(size_t)(r * d + j)] = h[(size_t)((c * H + r) * d + j)];
+            adapt_out.AddMatrix(g, "history", (size_t)rows, (size_t)d, hist);
+        }
+        if (!adapt_out.Write(adapt_file)) {
+            LOGERROR("Writing %s failed", adapt_file.c_str());
+            return false;
+        }
+        return true;
     }
 };
 
@@ -810,6 +859,16 @@ bool SamplerPTDevice::SetOutput(const std::string& filename, int64_t num_samples
     s.out = std::move(w);
     s.out_samples = num_samples;
     s.out_pending = 0;
+    return true;
+}
+
+bool SamplerPTDevice::SetAdaptationOutput(const std::string& filename)
+{
+    if (filename.empty() || !p_->adaptive) {
+        LOGERROR("SetAdaptationOutput: needs a file name and an adaptive proposal");
+        return false;
+    }
+    p_->adapt_file = filename;
     return true;
 }
 

@@ -76,6 +76,13 @@ public:
     // staged in HBM and written every `flush_every` samples; call before the first iteration
     bool SetOutput(const std::string& filename, int64_t num_samples, int flush_every);
     bool FlushOutput();
+    // ptmhsampler.output_proposal_adaptation (SamplerPTChain.cpp:149-166): after every adaptation
+    // the highest-temperature chain's proposal -- group adapt<k>/block1 with variable_indices,
+    // gmm_weights and cluster<i>_mean / _covariance (ProposalGaussianMixture::WriteToFile :109-123)
+    // or covariance (ProposalGlobalCovariance::WriteToFile :52-61), and from the second
+    // adaptation on the history it was fitted to -- rewritten into `filename` (NetCDFBundler
+    // layout in the classic format). Only the rank holding that chain writes.
+    bool SetAdaptationOutput(const std::string& filename);
     bool CheckNaN();  // synchronises; false (and an error) if a likelihood returned NaN
     bool Synchronize();
     bool GetState(double* values, double* llh, double* lprior, double* lpp);

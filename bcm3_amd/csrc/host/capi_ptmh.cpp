@@ -134,6 +134,12 @@ int bcm3_ptmh_set_output(bcm3_ptmh* h, const char* filename, int64_t num_samples
 
 int bcm3_ptmh_flush_output(bcm3_ptmh* h) { return (h && h->s.FlushOutput()) ? 0 : -2; }
 
+int bcm3_ptmh_set_adaptation_output(bcm3_ptmh* h, const char* filename)
+{
+    if (!h || !filename) return -1;
+    return h->s.SetAdaptationOutput(filename) ? 0 : -2;
+}
+
 int bcm3_ptmh_get_components(bcm3_ptmh* h, int32_t* ncomp) { return (h && h->s.GetProposalComponents(ncomp)) ? 0 : -2; }
 
 int bcm3_ptmh_get_counters(bcm3_ptmh* h, int64_t* out)

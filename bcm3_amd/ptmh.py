@@ -67,6 +67,7 @@ def _lib():
         L.bcm3_ptmh_destroy.restype = None
         L.bcm3_ptmh_set_output.argtypes = [vp, C.c_char_p, C.c_int64, C.c_int32]
         L.bcm3_ptmh_flush_output.argtypes = [vp]
+        L.bcm3_ptmh_set_adaptation_output.argtypes = [vp, C.c_char_p]
         L.bcm3_samples_open.argtypes = [C.c_char_p, C.c_int64, C.c_int32, C.POINTER(C.c_char_p), vp, C.c_int32, vp,
                                         C.c_int32, C.c_int32, C.POINTER(vp)]
         L.bcm3_samples_write.argtypes = [vp, C.c_int64, C.c_int32, C.c_int32, vp, vp, vp, vp]
@@ -140,6 +141,11 @@ class PTMHNative:
         """SampleHandlerNetCDF for this rank's chains (bcm3_ptmh_set_output): the reference's
         output.nc schema in a netCDF classic file (SampleFile); call before the first iteration."""
         _check(_lib().bcm3_ptmh_set_output(self.h, filename.encode(), num_samples, flush_every), "bcm3_ptmh_set_output")
+
+    def set_adaptation_output(self, filename: str):
+        """ptmhsampler.output_proposal_adaptation: the highest-temperature chain's fitted proposal
+        after every adaptation (bcm3_ptmh_set_adaptation_output)."""
+        _check(_lib().bcm3_ptmh_set_adaptation_output(self.h, filename.encode()), "bcm3_ptmh_set_adaptation_output")
 
     def flush_output(self):
         _check(_lib().bcm3_ptmh_flush_output(self.h), "bcm3_ptmh_flush_output")

@@ -176,6 +176,12 @@ void bcm3_ptmh_destroy(bcm3_ptmh* s);
  * bcm3_ptmh_run and on bcm3_ptmh_flush_output / destroy. Call before the first iteration. */
 int bcm3_ptmh_set_output(bcm3_ptmh* s, const char* filename, int64_t num_samples, int32_t flush_every);
 int bcm3_ptmh_flush_output(bcm3_ptmh* s);
+/* ptmhsampler.output_proposal_adaptation (SamplerPTChain.cpp:149-166): after every adaptation the
+ * highest-temperature chain's proposal (group adapt<k>/block1: variable_indices, gmm_weights,
+ * cluster<i>_mean / cluster<i>_covariance or covariance, and the fitted history from the second
+ * adaptation on) is (re)written to `filename` in the NetCDFBundler layout, netCDF classic
+ * (nested groups named "adapt<k>.block1.<name>"); written by the rank holding that chain. */
+int bcm3_ptmh_set_adaptation_output(bcm3_ptmh* s, const char* filename);
 
 /* ---- netCDF classic files (NetCDFClassic.h): the sampler's output.nc ----
  * The reference's output.nc schema (group "samples", SampleHandlerNetCDF.cpp:41-58) in a netCDF

@@ -176,3 +176,31 @@ def test_sample_output_file(tmp_path):
     w = _samples(p2)
     for k in v:
         assert np.array_equal(v[k], w[k]), k
+
+
+def test_adaptation_output_file(tmp_path):
+    """ptmhsampler.output_proposal_adaptation: one group per adaptation with the hottest chain's
+    mixture (weights, means, covariances) and, from the second adaptation on, its history"""
+    from scipy.io import netcdf_file
+    C, seed = 16, 6
+    s = _native(*C2, C, seed, 0, adapt_proposal_samples=40, adapt_proposal_times=2)
+    path = str(tmp_path / "sampler_adaptation.nc")
+    s.set_adaptation_output(path)
+    s.iterate(130)
+    s.synchronize()
+    nc = s.components()
+    s.close()
+    with netcdf_file(path, "r", mmap=False) as f:
+        v = {k: np.array(x[:]) for k, x in f.variables.items()}
+    for a in (0, 1):
+        g = f"adapt{a}.block1."
+        assert list(v[g + "variable_indices"]) == [0, 1]
+        w = v[g + "gmm_weights"]
+        assert abs(w.sum() - 1.0) < 1e-12 and np.all(w > 0)
+        for k in range(len(w)):
+            S = v[g + f"cluster{k}_covariance"]
+            assert S.shape == (2, 2) and np.allclose(S, S.T) and np.all(np.linalg.eigvalsh(S) > 0)
+            assert v[g + f"cluster{k}_mean"].shape == (2,)
+        assert list(v[g + "gmm_weights_dim"]) == list(range(1, len(w) + 1))
+    assert len(v["adapt1.block1.gmm_weights"]) == nc[-1]
+    assert "adapt0.block1.history" not in v and v["adapt1.block1.history"].shape[1] == 2

@@ -59,8 +59,9 @@ def _from_classic(path):
     out = {}
     with netcdf_file(path, "r", mmap=False) as f:
         for full, v in f.variables.items():
-            g, _, name = full.partition(".") if "." in full else ("", "", full)
-            dims = [d.partition(".")[2] or d for d in v.dimensions]
+            g, _, name = full.rpartition(".") if "." in full else ("", "", full)
+            g = g.replace(".", "/")  # nested groups a.b -> a/b
+            dims = [d.rpartition(".")[2] for d in v.dimensions]
             data = np.array(v[:])
             if data.dtype.kind == "S":
                 data = np.array([b"".join(r).decode() for r in data.reshape(-1, data.shape[-1])]).reshape(data.shape[:-1])
@@ -131,7 +132,7 @@ def _to_classic(doc, path):
         f.bcm3_groups = " ".join(groups)
     made = set()
     for g, vars_ in doc.items():
-        pre = f"{g}." if g else ""
+        pre = (g.replace("/", ".") + ".") if g else ""
         for name, (dims, data) in vars_.items():
             dims = list(dims)
             if data.dtype.kind in "US":
