@@ -341,10 +341,17 @@ Json NcClassicRead(const std::string& filename)
             const uint64_t r = i / per_rec, k = i % per_rec;
             return v.begin + r * recsize + k * sz;
         };
+        // every element must lie inside the file: bounds the element count before anything is
+        // allocated (a corrupt header cannot ask for more elements than the file has bytes)
         uint64_t total = 1;
-        for (auto s : shape) total *= s;
+        for (auto s : shape) {
+            if (s != 0 && total > buf.size() / s) throw JsonError{"netCDF: data beyond end of file"};
+            total *= s;
+        }
+        if (total > 0 && (offset(total - 1) > buf.size() || offset(total - 1) + sz > buf.size()))
+            throw JsonError{"netCDF: data beyond end of file"};
         const bool chars = (v.type == NcChar) && !shape.empty();
-        const uint64_t inner = chars ? shape.back() : 1;
+        const uint64_t inner = chars ? std::max<uint64_t>(shape.back(), 1) : 1;
         std::vector<Json> flat;
         flat.reserve(total / inner);
         for (uint64_t i = 0; i < total; i += inner) {

@@ -229,3 +229,19 @@ def test_truncated_file_is_an_error(tmp_path, cut):
     open(bad, "wb").write(data[:cut])
     with pytest.raises(RuntimeError):
         _lik(_xml_with(tmp_path, "c3", "c3_pkdata.json", bad), "c3")
+
+
+def test_corrupt_dimension_length_is_an_error(tmp_path):
+    """a header whose dimension claims 2^31 - 1 elements fails with an error before any allocation"""
+    import struct
+    nc = str(tmp_path / "c3_pkdata.nc")
+    _convert("to-classic", os.path.join(GOLDEN, "c3_pkdata.json"), nc)
+    data = bytearray(open(nc, "rb").read())
+    assert data[8:12] == b"\x00\x00\x00\x0a"  # NC_DIMENSION
+    nlen = struct.unpack(">I", data[16:20])[0]
+    at = 20 + (nlen + 3) // 4 * 4
+    data[at:at + 4] = struct.pack(">I", 0x7FFFFFFF)
+    bad = str(tmp_path / "bad.nc")
+    open(bad, "wb").write(bytes(data))
+    with pytest.raises(RuntimeError):
+        _lik(_xml_with(tmp_path, "c3", "c3_pkdata.json", bad), "c3")
