@@ -279,13 +279,25 @@ BDF_INL void lin_setup(SH& sh, double gamma)
         }
         if constexpr (ROW == 16) {
             // lane i of the row: row i of the trailing block
+            // (all loads of the row and of the pivot row first, then the updates, then the stores:
+            // one LDS latency per column instead of one per element)
             const int i = k + 1 + ln;
             if (i < NS) {
                 const double lik = sh.A[k * NS + i];
-                for (int j = k + 1; j < NS; j++) {
-                    const double akj = sh.A[j * NS + k];
-                    if (akj != 0.0) sh.A[j * NS + i] -= akj * lik;
-                }
+                double akj[NS], aij[NS];
+                cfor<0, NS>([&](auto jj) __attribute__((always_inline)) {
+                    constexpr int j = CI(jj);
+                    akj[j] = sh.A[j * NS + k];
+                    aij[j] = sh.A[j * NS + i];
+                });
+                cfor<0, NS>([&](auto jj) __attribute__((always_inline)) {
+                    constexpr int j = CI(jj);
+                    if (j > k && akj[j] != 0.0) aij[j] -= akj[j] * lik;
+                });
+                cfor<0, NS>([&](auto jj) __attribute__((always_inline)) {
+                    constexpr int j = CI(jj);
+                    if (j > k) sh.A[j * NS + i] = aij[j];
+                });
             }
         } else {
             for (int i = k + 1 + (ln & 15); i < NS; i += 16) {
