@@ -230,21 +230,26 @@ BDF_INL void lin_setup(SH& sh, double gamma)
     wave_sync();
     for (int k = 0; k < NS; k++) {
         int p;
-        double biggest;
+        double biggest, pivot = 0.0;
         if constexpr (NS <= 16) {
-            // inclusive max-scan, the lower lane winning ties (maxCoeff's first index)
-            double v = (ln >= k && ln < NS) ? fabs(sh.A[k * NS + ln]) : -1.0;
+            // inclusive max-scan, the lower lane winning ties (maxCoeff's first index); the signed
+            // pivot rides along, so the reciprocal needs no read after the row swap
+            const double akk = (ln >= k && ln < NS) ? sh.A[k * NS + ln] : 0.0;
+            double v = (ln >= k && ln < NS) ? fabs(akk) : -1.0, sv = akk;
             int ix = ln;
             cfor<0, 4>([&](auto r) __attribute__((always_inline)) {
                 constexpr int D = 1 << CI(r);
                 const double ov = shr_d<D>(v, -2.0);
+                const double osv = shr_d<D>(sv, 0.0);
                 const int oi = shr_i<D>(ix, ix);
                 const bool take = ov >= v;
                 v = take ? ov : v;
+                sv = take ? osv : sv;
                 ix = take ? oi : ix;
             });
             p = __builtin_amdgcn_mov_dpp(ix, 0x15F, 0xf, 0xf, false);  // lane 15 of the row
             biggest = rbc<15>(v);
+            pivot = rbc<15>(sv);
         } else {
             biggest = -1.0;
             p = k;
@@ -273,17 +278,24 @@ BDF_INL void lin_setup(SH& sh, double gamma)
                 }
                 wave_sync();
             }
-            const double inv = 1.0 / sh.A[k * NS + k];
-            if (ln > k && ln < NS) sh.A[k * NS + ln] *= inv;
-            wave_sync();
+            if constexpr (ROW != 16) {
+                const double inv = 1.0 / sh.A[k * NS + k];
+                if (ln > k && ln < NS) sh.A[k * NS + ln] *= inv;
+                wave_sync();
+            }
         }
         if constexpr (ROW == 16) {
-            // lane i of the row: row i of the trailing block
-            // (all loads of the row and of the pivot row first, then the updates, then the stores:
-            // one LDS latency per column instead of one per element)
+            // lane i of the row: row i of the trailing block. It scales its own column-k entry
+            // (l(i, k) = a(i, k) / u(k, k) through the reciprocal, as above), then loads the row and
+            // the pivot row in one batch, updates, and stores: one LDS latency per column instead of
+            // one per element
             const int i = k + 1 + ln;
             if (i < NS) {
-                const double lik = sh.A[k * NS + i];
+                double lik = sh.A[k * NS + i];
+                if (biggest != 0.0) {
+                    lik *= 1.0 / pivot;
+                    sh.A[k * NS + i] = lik;
+                }
                 double akj[NS], aij[NS];
                 cfor<0, NS>([&](auto jj) __attribute__((always_inline)) {
                     constexpr int j = CI(jj);
