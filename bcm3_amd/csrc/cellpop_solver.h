@@ -774,7 +774,12 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
         const bool callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (s.nst == 0) ||
                                (s.nst >= s.nstlp + MSBP) || (fabs(s.gamrat - 1.0) > DGMAX);
         s.acor = 0.0;
-        const bool conv = newton<NS, NP, NC>(sh, s, rl1, convfail, callSetup);
+        bool conv;
+        {
+            CP_PH_BEGIN();
+            conv = newton<NS, NP, NC>(sh, s, rl1, convfail, callSetup);
+            CP_PH_END(sh, 6);
+        }
         if (conv) {
             dsm = s.acnrm * s.tq[2];
             if (dsm <= 1.0) break;
@@ -834,6 +839,7 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
         s.saved_tq5 = s.tq[5];
     }
     // cvPrepareNextStep
+    CP_PH_BEGIN();
     if (s.etamax == 1.0) {
         s.qwait = SUNMAX(s.qwait, 2);
         s.qprime = s.q;
@@ -874,6 +880,7 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
             s.hprime = s.h * s.eta;
         }
     }
+    CP_PH_END(sh, 7);
     s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
     s.acor *= s.tq[2];
     s.tretlast = tret = s.tn;
@@ -1051,7 +1058,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
 #ifdef CP_PHASES
     if (ln == 0) sh.ph[5] = clock64() - ph_kernel0;
     wave_sync();
-    if (ln < 6 && ln < NS) a.end_y[(size_t)slot * NS + ln] = (double)sh.ph[ln];
+    if (ln < 8 && ln < NS) a.end_y[(size_t)slot * NS + ln] = (double)sh.ph[ln];
 #endif
     if (ln == 0) {
         const double achieved_cell_time = (divided || died) ? sim_end : (a.output_times[M - 1] - creation);
