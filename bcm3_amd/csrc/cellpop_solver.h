@@ -889,6 +889,16 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
 
 // get_threshold_crossing_time in the non-stored mode (see oracle/cellpop_ref.cpp): the
 // interpolant of the unused buffer is 0, so the bisection only walks to one end
+// component J of the row's state in every lane of the row (the event species' value)
+template <int J>
+BDF_INL double ev_value(double y)
+{
+    if constexpr (ROW == 16)
+        return rbc<J>(y);
+    else
+        return rowget(y, J);
+}
+
 BDF_INL double crossing_time(double t, double prev, double threshold, bool above)
 {
     double dt = (t - prev) * 0.5;
@@ -984,6 +994,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
         double end_time = a.output_times[M - 1] - creation;
         double t = 0.0;
         int tpi = ti;
+        // the next output time in a register: no global load on every step's critical path
+        double next_out = a.output_times[tpi] - creation;
         for (;;) {
             double tret;
             int r;
@@ -998,40 +1010,51 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
             }
             t = tret;
             nst++;
-            while (tpi < M && tret >= a.output_times[tpi] - creation) {
+            while (tpi < M && tret >= next_out) {
                 double dky;
-                if (get_dky(s, a.output_times[tpi] - creation, dky) != CV_SUCCESS) {
+                if (get_dky(s, next_out, dky) != CV_SUCCESS) {
                     ok = false;
                     break;
                 }
                 const int sp = a.output_species[tpi];
                 if (sp >= 0 && ln == sp) outv[tpi] = dky;
                 tpi++;
+                if (tpi < M) next_out = a.output_times[tpi] - creation;
             }
             if (!ok) break;
             // Cell::integration_step_cb (Cell.cpp:463-538)
             const double y = s.zn[0];
             bool cont = true;
-            if (a.ev[0] >= 0 && ev[0] != ev[0] && rowget(y, a.ev[0]) > 1e-4) ev[0] = crossing_time(t, previous_step_time, 1e-4, true);
-            if (a.ev[1] >= 0 && ev[1] != ev[1] && rowget(y, a.ev[1]) > 1.95) ev[1] = crossing_time(t, previous_step_time, 1.95, true);
-            if (a.ev[2] >= 0 && ev[2] != ev[2] && rowget(y, a.ev[2]) > 0.5) ev[2] = crossing_time(t, previous_step_time, 0.5, true);
-            if (a.ev[3] >= 0 && ev[3] != ev[3] && rowget(y, a.ev[3]) < 0.5) ev[3] = crossing_time(t, previous_step_time, 0.5, false);
-            if (a.ev[4] >= 0 && ev[4] != ev[4] && rowget(y, a.ev[4]) > 1e-3) {
-                ev[4] = crossing_time(t, previous_step_time, 1e-3, true);
-                sim_end = fmax(sim_end, ev[4] + a.past_cs);
-                end_time = sim_end;
+            if constexpr (CP_EV0 >= 0)
+                if (ev[0] != ev[0] && ev_value<CP_EV0>(y) > 1e-4) ev[0] = crossing_time(t, previous_step_time, 1e-4, true);
+            if constexpr (CP_EV1 >= 0)
+                if (ev[1] != ev[1] && ev_value<CP_EV1>(y) > 1.95) ev[1] = crossing_time(t, previous_step_time, 1.95, true);
+            if constexpr (CP_EV2 >= 0)
+                if (ev[2] != ev[2] && ev_value<CP_EV2>(y) > 0.5) ev[2] = crossing_time(t, previous_step_time, 0.5, true);
+            if constexpr (CP_EV3 >= 0)
+                if (ev[3] != ev[3] && ev_value<CP_EV3>(y) < 0.5) ev[3] = crossing_time(t, previous_step_time, 0.5, false);
+            if constexpr (CP_EV4 >= 0) {
+                if (ev[4] != ev[4] && ev_value<CP_EV4>(y) > 1e-3) {
+                    ev[4] = crossing_time(t, previous_step_time, 1e-3, true);
+                    sim_end = fmax(sim_end, ev[4] + a.past_cs);
+                    end_time = sim_end;
+                }
             }
-            if (a.divide_cells && a.ev[5] >= 0 && rowget(y, a.ev[5]) > 1.0) {
-                sim_end = t;
-                yend = y;
-                divided = true;
-                cont = false;
+            if constexpr (CP_EV5 >= 0) {
+                if (a.divide_cells && ev_value<CP_EV5>(y) > 1.0) {
+                    sim_end = t;
+                    yend = y;
+                    divided = true;
+                    cont = false;
+                }
             }
-            if (a.ev[6] >= 0 && rowget(y, a.ev[6]) > 1.0) {
-                sim_end = t;
-                yend = y;
-                died = true;
-                cont = false;
+            if constexpr (CP_EV6 >= 0) {
+                if (ev_value<CP_EV6>(y) > 1.0) {
+                    sim_end = t;
+                    yend = y;
+                    died = true;
+                    cont = false;
+                }
             }
             previous_step_time = t;
             if (!cont) break;
