@@ -220,11 +220,28 @@ BDF_INL void lin_setup(SH& sh, double gamma)
 {
     const int ln = lane();
     wave_sync();
-    for (int e = ln; e < NS * NS; e += ROW) {
-        const int j = e / NS, i = e - j * NS;
-        double a = (-gamma) * sh.J[e];
-        if (i == j) a += 1.0;
-        sh.A[e] = a;
+    if constexpr (ROW == 16) {
+        // all loads of the saved Jacobian first, then the stores (one LDS latency, not one per element)
+        constexpr int NE = (NS * NS + ROW - 1) / ROW;
+        double jv[NE];
+        cfor<0, NE>([&](auto kk) __attribute__((always_inline)) {
+            const int e = ln + CI(kk) * ROW;
+            jv[CI(kk)] = (e < NS * NS) ? sh.J[e] : 0.0;
+        });
+        cfor<0, NE>([&](auto kk) __attribute__((always_inline)) {
+            const int e = ln + CI(kk) * ROW;
+            const int j = e / NS, i = e - j * NS;
+            double a = (-gamma) * jv[CI(kk)];
+            if (i == j) a += 1.0;
+            if (e < NS * NS) sh.A[e] = a;
+        });
+    } else {
+        for (int e = ln; e < NS * NS; e += ROW) {
+            const int j = e / NS, i = e - j * NS;
+            double a = (-gamma) * sh.J[e];
+            if (i == j) a += 1.0;
+            sh.A[e] = a;
+        }
     }
     if (ln < NS) sh.perm[ln] = ln;
     wave_sync();
@@ -746,8 +763,19 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
     }
     {
         const double p = s.zn[0] * s.ewt;
-        const double ss = lane_sum<NS>(sh, p * p);
-        if (ss > (double)NS * (1.0 / (UROUND * UROUND))) {
+        constexpr double thr = (double)NS * (1.0 / (UROUND * UROUND));
+        bool too_much;
+        if constexpr (NS <= 16) {
+            // NS * max p^2 bounds the sum: far below the threshold (every step in practice) the
+            // component-order sum is not needed to decide; near or above it, it decides
+            double m = (lane() < NS) ? p * p : 0.0;
+            cfor<0, 4>([&](auto r) __attribute__((always_inline)) { m = fmax(m, shr_d<(1 << CI(r))>(m, 0.0)); });
+            m = rbc<15>(m);
+            too_much = !((double)NS * m <= 0.5 * thr) && (lane_sum<NS>(sh, p * p) > thr);
+        } else {
+            too_much = lane_sum<NS>(sh, p * p) > thr;
+        }
+        if (too_much) {
             s.tretlast = tret = s.tn;
             return CV_TOO_MUCH_ACC;
         }
