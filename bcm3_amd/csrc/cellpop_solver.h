@@ -65,6 +65,12 @@ struct LdsSpecies {
     const double* y;
     BDF_INL double operator[](int k) const { return y[k]; }
 };
+// the row's state in registers: component k broadcast from lane k of the row (row_newbcast, NS <= 16)
+template <int NS>
+struct RegSpecies {
+    double v[NS];
+    BDF_INL double operator[](int k) const { return v[k]; }
+};
 // lane j: the state with component j perturbed (DifferenceQuotientJacobian's y_copy)
 struct PertSpecies {
     const double* y;
@@ -172,11 +178,18 @@ BDF_INL double wrms(SH& sh, double x, double w)
 template <int NS, int NP, int NC, class SH>
 BDF_INL double rhs_v(SH& sh, double y)
 {
-    wave_sync();
-    if (lane() < NS) sh.sy[lane()] = y;
-    wave_sync();
     double o[NS];
-    generated_derivative(o, LdsSpecies{sh.sy}, sh.cs, sh.prm, (const double*)nullptr);
+    if constexpr (NS <= 16) {
+        // the state reaches every lane of the row by DPP broadcasts: no LDS round trip
+        RegSpecies<NS> sp;
+        cfor<0, NS>([&](auto k) __attribute__((always_inline)) { sp.v[CI(k)] = rbc<CI(k)>(y); });
+        generated_derivative(o, sp, sh.cs, sh.prm, (const double*)nullptr);
+    } else {
+        wave_sync();
+        if (lane() < NS) sh.sy[lane()] = y;
+        wave_sync();
+        generated_derivative(o, LdsSpecies{sh.sy}, sh.cs, sh.prm, (const double*)nullptr);
+    }
     double r = o[NS - 1];
 #pragma unroll
     for (int k = NS - 2; k >= 0; k--) r = (lane() == k) ? o[k] : r;
@@ -366,10 +379,18 @@ template <int NS, class SH>
 BDF_INL double lin_solve(SH& sh, double b)
 {
     const int ln = lane();
-    wave_sync();
-    if (ln < NS) sh.red[ln] = b;
-    wave_sync();
-    double x = (ln < NS) ? sh.red[sh.perm[ln]] : 0.0;
+    double x;
+    if constexpr (NS <= 16) {
+        // P b by one ds_bpermute within the row (the permutation is read independently of b)
+        const int pl = sh.perm[(ln < NS) ? ln : 0];
+        x = rowget(b, pl);
+        x = (ln < NS) ? x : 0.0;
+    } else {
+        wave_sync();
+        if (ln < NS) sh.red[ln] = b;
+        wave_sync();
+        x = (ln < NS) ? sh.red[sh.perm[ln]] : 0.0;
+    }
     if (BDF_UNLIKELY(!sh.dinv_ok)) {
         for (int j = 0; j < NS - 1; j++) {
             const double xj = rowget(x, j);
