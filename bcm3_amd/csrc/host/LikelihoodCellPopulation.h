@@ -5,11 +5,13 @@
 // the per-model ODE kernel compiled with hipRTC, generation-by-generation division).
 //
 // Supported (the reference's options this path uses): one <experiment> with model_file, data_file
-// (a JSON sidecar with the netCDF group's variables), num_cells, max_cells, divide_cells,
-// entry_time, trailing_simulation_time, simulate_past_chromatid_separation_time, solver_* settings
-// (solver_type CVODE); <set_parameter>; <cell_variability distribution="diagonal_gaussian">;
-// <data type="time_course_population_average"> with the normal / additive_normal / student_t4
-// error models, stdev / offset / scale / weight. Not built: treatment trajectories (time-varying
+// (netCDF classic, or a JSON sidecar with the netCDF group's variables), num_cells, max_cells,
+// divide_cells, entry_time, trailing_simulation_time, simulate_past_chromatid_separation_time,
+// solver_* settings (solver_type CVODE); <set_parameter>; <cell_variability
+// distribution="diagonal_gaussian">; <data type="time_course_population_average"> with the normal /
+// additive_normal / proportional_normal / additive_proportional_normal / student_t4 error models,
+// stdev / proportional_stdev / offset / scale / weight / relative_to_time_average. Not built:
+// treatment trajectories (time-varying
 // constant species), synchronised data (time_course, time_points, duration likelihoods), the DP5
 // solver, full_gaussian variability, several experiments in one likelihood, non-sampled parameters.
 #pragma once
