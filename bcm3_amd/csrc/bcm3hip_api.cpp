@@ -27,12 +27,18 @@ void cellpop_destroy(CellPopDev* c);
 int cellpop_launch(CellPopDev* c, size_t n, const double* values, double* logp, int32_t* status, hipStream_t s,
                    hipEvent_t e0, hipEvent_t e1);
 int cellpop_cells(CellPopDev* c, size_t item, int32_t* count, bcm3hip_cell_record* rec, double* values, double* end_y);
+hipError_t launch_cp_accumulate(int32_t n, double* logp, int32_t* status, const double* x, const int32_t* xstatus,
+                                hipStream_t s);
 }  // namespace bcm3hip
 
 struct bcm3hip_ctx {
     int device = 0;
     int kind = 0;  // 1 popk, 2 analytic, 3 expm pk, 4 cell population
     bcm3hip::CellPopDev* cp = nullptr;
+    std::vector<bcm3hip::CellPopDev*> cp_more;  // experiments 1.. of a cell-population likelihood
+    double* cp_logp = nullptr;                  // their per-experiment logp / status
+    int32_t *cp_status = nullptr, *cp_status0 = nullptr;
+    size_t cap_cp = 0, cap_cp_status = 0, cap_cp_status0 = 0;
     int d = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -246,22 +252,34 @@ int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* m, bcm3hip_c
     return 0;
 }
 
-int bcm3hip_open_cellpop(int device, const bcm3hip_cellpop_model* m, bcm3hip_ctx** out)
+int bcm3hip_open_cellpop_experiments(int device, const bcm3hip_cellpop_model* m, int n_experiments, bcm3hip_ctx** out)
 {
-    if (!m || !out) return BCM3HIP_ERR_ARG;
+    if (!m || !out || n_experiments < 1) return BCM3HIP_ERR_ARG;
     *out = nullptr;
+    for (int k = 1; k < n_experiments; k++)
+        if (m[k].d != m[0].d) return BCM3HIP_ERR_ARG;  // one parameter vector for every experiment
     bcm3hip_ctx* c = new (std::nothrow) bcm3hip_ctx();
     if (!c) return BCM3HIP_ERR_ALLOC;
     int r = ctx_common_init(c, device);
-    if (r == 0) r = bcm3hip::cellpop_create(device, m, &c->cp);
+    if (r == 0) r = bcm3hip::cellpop_create(device, &m[0], &c->cp);
+    for (int k = 1; k < n_experiments && r == 0; k++) {
+        bcm3hip::CellPopDev* e = nullptr;
+        r = bcm3hip::cellpop_create(device, &m[k], &e);
+        if (r == 0) c->cp_more.push_back(e);
+    }
     if (r) {
         bcm3hip_close(c);
         return r;
     }
     c->kind = 4;
-    c->d = m->d;
+    c->d = m[0].d;
     *out = c;
     return 0;
+}
+
+int bcm3hip_open_cellpop(int device, const bcm3hip_cellpop_model* m, bcm3hip_ctx** out)
+{
+    return bcm3hip_open_cellpop_experiments(device, m, 1, out);
 }
 
 int bcm3hip_cellpop_precompile(const bcm3hip_cellpop_model* m) { return bcm3hip::cellpop_precompile(m); }
@@ -412,6 +430,10 @@ int bcm3hip_close(bcm3hip_ctx* c)
     if (!c) return 0;
     if (c->stream) hipSetDevice(c->device);
     if (c->cp) bcm3hip::cellpop_destroy(c->cp);
+    for (auto* e : c->cp_more) bcm3hip::cellpop_destroy(e);
+    hipFree(c->cp_logp);
+    hipFree(c->cp_status);
+    hipFree(c->cp_status0);
     for (void* p : c->model_allocs) hipFree(p);
     hipFree(c->values);
     hipFree(c->logp);
@@ -516,9 +538,22 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
                                c->exps, s, i0 == 0 ? e0 : nullptr, i0 + m >= n ? e1 : nullptr);
         }
     } else if (c->kind == 4) {
-        const int r = bcm3hip::cellpop_launch(c->cp, n, dvalues, dlogp, dstatus, s, e0, e1);
+        // experiment 0 into logp, every further one into scratch, summed in experiment order
+        int32_t* st = dstatus;
+        if (!c->cp_more.empty()) {
+            if (!st && grow(c->cp_status0, c->cap_cp_status0, n)) return BCM3HIP_ERR_ALLOC;
+            if (!st) st = c->cp_status0;
+            if (grow(c->cp_logp, c->cap_cp, n) || grow(c->cp_status, c->cap_cp_status, n)) return BCM3HIP_ERR_ALLOC;
+        }
+        int r = bcm3hip::cellpop_launch(c->cp, n, dvalues, dlogp, st, s, e0, c->cp_more.empty() ? e1 : nullptr);
         if (r) return r;
         e = hipSuccess;
+        for (size_t k = 0; k < c->cp_more.size() && e == hipSuccess; k++) {
+            r = bcm3hip::cellpop_launch(c->cp_more[k], n, dvalues, c->cp_logp, c->cp_status, s, nullptr, nullptr);
+            if (r) return r;
+            e = bcm3hip::launch_cp_accumulate((int32_t)n, dlogp, st, c->cp_logp, c->cp_status, s);
+        }
+        if (e == hipSuccess && e1 && !c->cp_more.empty()) e = hipEventRecord(e1, s);
     } else {
         e = launch_analytic(c->am, (int64_t)n, dvalues, dlogp, dstatus, s, e0, e1);
     }

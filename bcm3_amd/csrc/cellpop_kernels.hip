@@ -222,4 +222,26 @@ hipError_t launch_cp_gather(const int32_t* work, int32_t n, const int32_t* flags
     return hipGetLastError();
 }
 
+// logp += the next experiment's; the reference stops at the first experiment that fails (logp =
+// -inf, later experiments not evaluated), so a failed sum stays as it is
+__global__ void cp_accumulate_kernel(int32_t n, double* logp, int32_t* status, const double* x, const int32_t* xstatus)
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || status[i] != BCM3HIP_STATUS_OK) return;
+    if (xstatus[i] != BCM3HIP_STATUS_OK) {
+        logp[i] = -__builtin_inf();
+        status[i] = xstatus[i];
+    } else {
+        logp[i] = logp[i] + x[i];
+    }
+}
+
+hipError_t launch_cp_accumulate(int32_t n, double* logp, int32_t* status, const double* x, const int32_t* xstatus,
+                                hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cp_accumulate_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, logp, status, x, xstatus);
+    return hipGetLastError();
+}
+
 }  // namespace bcm3hip

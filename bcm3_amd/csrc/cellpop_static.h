@@ -40,5 +40,9 @@ hipError_t launch_cp_popavg(const CpStatic& m, int32_t n, const double* values, 
                             const double* sim_end, double* avg, double* logp, int32_t* status, hipStream_t s);
 // out[w] = flags[work[w]]
 hipError_t launch_cp_gather(const int32_t* work, int32_t n, const int32_t* flags, int32_t* out, hipStream_t s);
+// the next experiment's (x, xstatus) into the running sum (logp, status) of
+// CellPopulationLikelihood::EvaluateLogProbability (CellPopulationLikelihood.cpp:90-98)
+hipError_t launch_cp_accumulate(int32_t n, double* logp, int32_t* status, const double* x, const int32_t* xstatus,
+                                hipStream_t s);
 
 }  // namespace bcm3hip

@@ -108,12 +108,19 @@ bool LikelihoodCellPopulation::Initialize(std::shared_ptr<const VariableSet> vs,
     varset = vs;
     host_only = option_get(vm, "backend", "") == "none";
     std::vector<const XmlNode*> exps = likelihood_node.children_named("experiment");
-    if (exps.size() != 1) {
-        LOGERROR("cell_population: exactly one <experiment> is supported (got %zu)", exps.size());
+    if (exps.empty()) {
+        LOGERROR("cell_population: no <experiment> in the likelihood");
         return false;
     }
     try {
         if (!LoadExperiment(*exps[0], vm)) return false;
+        for (size_t k = 1; k < exps.size(); k++) {
+            auto e = std::make_unique<LikelihoodCellPopulation>(1, 1);
+            e->varset = vs;
+            e->host_only = true;
+            if (!e->LoadExperiment(*exps[k], vm)) return false;
+            more_experiments.push_back(std::move(e));
+        }
     } catch (XmlError& e) {
         LOGERROR("Error parsing likelihood file: %s", e.what.c_str());
         return false;
@@ -304,8 +311,17 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
 }
 
 // Experiment::PostInitialize (Experiment.cpp:145-237) + the flat device model
+std::vector<const bcm3hip_cellpop_model*> LikelihoodCellPopulation::GetDeviceModels() const
+{
+    std::vector<const bcm3hip_cellpop_model*> v{&model};
+    for (const auto& e : more_experiments) v.push_back(&e->model);
+    return v;
+}
+
 bool LikelihoodCellPopulation::PostInitialize()
 {
+    for (auto& e : more_experiments)
+        if (!e->PostInitialize()) return false;
     std::string err;
     if (!sbml.GenerateDerivative(varset->GetVariableNames(), forced, derivative_body, err)) {
         LOGERROR("%s", err.c_str());
@@ -448,7 +464,9 @@ bool LikelihoodCellPopulation::PostInitialize()
     model.n_data = (int32_t)data_flat.size();
     model.data = data_flat.data();
     if (host_only) return true;
-    const int r = bcm3hip_open_cellpop(device, &model, &ctx);
+    std::vector<bcm3hip_cellpop_model> models{model};
+    for (const auto& e : more_experiments) models.push_back(e->model);
+    const int r = bcm3hip_open_cellpop_experiments(device, models.data(), (int)models.size(), &ctx);
     if (r) {
         LOGERROR("bcm3hip_open_cellpop failed: %s", bcm3hip_error_string(r));
         return false;

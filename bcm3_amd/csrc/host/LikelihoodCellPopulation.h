@@ -4,7 +4,8 @@
 // the host; the cells are simulated by libbcm3hip's cell-population context (bcm3hip_open_cellpop:
 // the per-model ODE kernel compiled with hipRTC, generation-by-generation division).
 //
-// Supported (the reference's options this path uses): one <experiment> with model_file, data_file
+// Supported (the reference's options this path uses): one or more <experiment>s (their
+// log-likelihoods summed in order, CellPopulationLikelihood.cpp:82-101), each with model_file, data_file
 // (netCDF classic, or a JSON sidecar with the netCDF group's variables), num_cells, max_cells,
 // divide_cells, entry_time, trailing_simulation_time, simulate_past_chromatid_separation_time,
 // solver_* settings (solver_type CVODE); <set_parameter>; <cell_variability
@@ -15,6 +16,7 @@
 // constant species), synchronised data (time_course, time_points, duration likelihoods), the DP5
 // solver, full_gaussian variability, several experiments in one likelihood, non-sampled parameters.
 #pragma once
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -32,6 +34,8 @@ public:
 
     const std::string& GetGeneratedCode() const { return derivative_body; }
     const bcm3hip_cellpop_model& GetDeviceModel() const { return model; }
+    // every experiment's device model, in <experiment> order
+    std::vector<const bcm3hip_cellpop_model*> GetDeviceModels() const;
 
 private:
     struct DataLikelihood {
@@ -74,6 +78,8 @@ private:
     std::vector<bcm3hip_cellpop_data> data_flat;
     bcm3hip_cellpop_model model{};
     bool host_only = false;
+    // the second and later <experiment>s (host-side descriptions; one device context sums them)
+    std::vector<std::unique_ptr<LikelihoodCellPopulation>> more_experiments;
 };
 
 // boost::random::sobol (Joe & Kuo 2008 direction numbers, first point skipped) through

@@ -79,7 +79,11 @@ int bcm3_likelihood_cellpop_precompile(const bcm3_likelihood* h)
     if (!h || !h->ll) return -1;
     auto* p = dynamic_cast<bcm3::LikelihoodCellPopulation*>(h->ll.get());
     if (!p) return -2;
-    return bcm3hip_cellpop_precompile(&p->GetDeviceModel());
+    for (const bcm3hip_cellpop_model* m : p->GetDeviceModels()) {
+        const int r = bcm3hip_cellpop_precompile(m);
+        if (r) return r;
+    }
+    return 0;
 }
 
 int bcm3_likelihood_cellpop_cells(bcm3_likelihood* h, size_t item, int32_t* count, void* records, double* values,

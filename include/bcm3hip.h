@@ -277,6 +277,13 @@ int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* model, bcm3hip
  * ($BCM3_CODEGEN_DIR, default <library dir>/codegen). Per-item status 1 when the experiment fails
  * (solver failure, too many cells): logp = -inf. */
 int bcm3hip_open_cellpop(int device, const bcm3hip_cellpop_model* model, bcm3hip_ctx** out);
+/* cell_population with several <experiment>s (CellPopulationLikelihood::EvaluateLogProbability,
+ * src/cellpop/CellPopulationLikelihood.cpp:82-101): one compiled cell kernel per experiment model,
+ * logp = the sum of the experiments' log-likelihoods in experiment order; -inf (status 1) from
+ * the first experiment that fails, as the reference returns there. bcm3hip_cellpop_cells reads
+ * experiment 0. */
+int bcm3hip_open_cellpop_experiments(int device, const bcm3hip_cellpop_model* models, int n_experiments,
+                                     bcm3hip_ctx** out);
 /* compile (or find in the cache) the model's cell kernel without a device (build time) */
 int bcm3hip_cellpop_precompile(const bcm3hip_cellpop_model* model);
 /* cells of item `item` of the last cellpop evaluation: *count cells, records / values[count*M]

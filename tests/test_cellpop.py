@@ -182,3 +182,17 @@ def test_proportional_error_oracle_formula(tmp_path):
         s = 0.2 + 0.1 * max(o, 0.0)
         want += -math.log(s) - 0.91893853320467274178032973640562 - (x - o) ** 2 / (2 * s * s)
     assert abs(got - want) < 1e-14
+
+
+def test_several_experiments_load(tmp_path):
+    """CellPopulationLikelihood::Initialize loads every <experiment> (CellPopulationLikelihood.cpp:
+    24-35); a likelihood without one is an error"""
+    import test_cellpop_experiments_gpu as TE
+    from bcm3_amd.likelihood import Likelihood
+    _, _, ab = TE.two_experiments(tmp_path)
+    Likelihood(ab, CH.PRIOR, options="backend=none").close()
+    assert len(CP.load_problem(ab, CH.PRIOR)["experiments"]) == 2
+    none = tmp_path / "none.xml"
+    none.write_text('<bcm_likelihood type="cell_population">\n</bcm_likelihood>\n')
+    with pytest.raises(RuntimeError):
+        Likelihood(str(none), CH.PRIOR, options="backend=none")
