@@ -576,12 +576,6 @@ __global__ void __launch_bounds__(256) popk_reduce_kernel(int64_t n, int P, cons
     if (status) status[e] = st;
 }
 
-__global__ void copy_status_kernel(int64_t n, const int32_t* __restrict__ src, int32_t* __restrict__ dst)
-{
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) dst[e] = src[e];
-}
-
 hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
                        double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
                        bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, int uni_solver,
@@ -598,20 +592,22 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
     const bool uni = (lpw == 1) && ntraj < (int64_t)1 << 30;
     const bool vec_state = uni && (uni_solver == 0);
     double* logp_direct = direct ? logp : nullptr;
+    // one patient: the trajectory status is the evaluation status, written in place (no copy kernel)
+    int32_t* tstat = (direct && status) ? status : traj_status_scratch;
     if (ev_start) hipEventRecord(ev_start, stream);
 #define LAUNCH(PKT)                                                                                           \
     if (vec_state && !stats_out)                                                                              \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, false>), grid, block, 0, stream, m, ntraj, lpw,     \
-                           values, logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, nullptr);   \
+                           values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr);   \
     else if (vec_state)                                                                                       \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, true>), grid, block, 0, stream, m, ntraj, lpw,      \
-                           values, logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out); \
+                           values, logp_direct, patient_llh_scratch, tstat, traj_out, stats_out); \
     else if (uni)                                                                                             \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_UNI, true>), grid, block, 0, stream, m, ntraj, lpw, values, \
-                           logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out);         \
+                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out);         \
     else                                                                                                      \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_LANES, true>), grid, block, 0, stream, m, ntraj, lpw, values,  \
-                           logp_direct, patient_llh_scratch, traj_status_scratch, traj_out, stats_out)
+                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out)
     switch (m.pk_type) {
     case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;
     case BCM3HIP_PK_TWO: LAUNCH(BCM3HIP_PK_TWO); break;
@@ -630,8 +626,6 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
     if (!direct) {
         hipLaunchKernelGGL(popk_reduce_kernel, dim3(rb), dim3(tb), 0, stream, n, m.P, patient_llh_scratch,
                            traj_status_scratch, logp, status);
-    } else if (status) {
-        hipLaunchKernelGGL(copy_status_kernel, dim3(rb), dim3(tb), 0, stream, n, traj_status_scratch, status);
     }
     return hipGetLastError();
 }
