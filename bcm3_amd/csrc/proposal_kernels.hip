@@ -268,8 +268,8 @@ __device__ __forceinline__ double lane_bcast(double x, int j)  // x of lane j (j
     return __builtin_bit_cast(double, ((long long)hi << 32) | (unsigned)lo);
 }
 
-// lane i (< d) holds v_i and row i of L (Lrow); returns s_i of L s = v
-__device__ __forceinline__ double wave_lower_solve(int d, const double* Lrow, double v, int lane)
+// generic form, any d <= 64
+__device__ __forceinline__ double wave_lower_solve_any(int d, const double* Lrow, double v, int lane)
 {
     double acc = 0.0, s = 0.0;
     for (int j = 0; j < d; j++) {
@@ -278,6 +278,34 @@ __device__ __forceinline__ double wave_lower_solve(int d, const double* Lrow, do
         if (lane > j && lane < d) acc += Lrow[j] * sj;
     }
     return s;
+}
+
+// d <= MD: the lane's row is loaded into registers first (every row pointer is valid -- lanes >= d
+// read row 0 -- and indices are clamped, so the loads are unconditional and issue back to back),
+// so the dependent division -> broadcast chain waits on memory once, not once per column. The same
+// arithmetic, in the same order, as wave_lower_solve_any.
+template <int MD>
+__device__ __forceinline__ double wave_lower_solve_reg(int d, const double* Lrow, double v, int lane)
+{
+    double L[MD];
+#pragma unroll
+    for (int j = 0; j < MD; j++) L[j] = Lrow[(j < d) ? j : d - 1];
+    double acc = 0.0, s = 0.0;
+#pragma unroll
+    for (int j = 0; j < MD; j++) {
+        if (j >= d) break;
+        if (lane == j) s = (v - acc) / L[j];
+        const double sj = lane_bcast(s, j);
+        if (lane > j && lane < d) acc += L[j] * sj;
+    }
+    return s;
+}
+
+// lane i (< d) holds v_i and row i of L (Lrow); returns s_i of L s = v
+__device__ __forceinline__ double wave_lower_solve(int d, const double* Lrow, double v, int lane)
+{
+    if (d <= 16) return wave_lower_solve_reg<16>(d, Lrow, v, lane);
+    return wave_lower_solve_any(d, Lrow, v, lane);
 }
 
 // sum_{i<n} x_i in lane order (uniform result)
@@ -430,7 +458,8 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
         double x = 0.0;
         for (int j = 0; j < d; j++) {
             const double zj = lane_bcast(z, j);
-            if (j <= lane) x += Ls[j] * zj;
+            const double a = x + Ls[j] * zj;  // Ls: this lane's row (row 0 for lanes >= d)
+            x = (j <= lane) ? a : x;
         }
         nxt = reflect(x * f + cur, P.lower[li], P.upper[li]);
         if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
