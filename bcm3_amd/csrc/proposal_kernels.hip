@@ -301,6 +301,35 @@ __device__ __forceinline__ double wave_lower_solve_reg(int d, const double* Lrow
     return s;
 }
 
+// two right-hand sides with the same L (the proposal's reverse-responsibility and MH solves of
+// one component): two independent division -> broadcast chains in one pass over the columns,
+// each with exactly the arithmetic of wave_lower_solve
+template <int MD>
+__device__ __forceinline__ void wave_lower_solve2_reg(int d, const double* Lrow, double va, double vb, int lane,
+                                                      double& sa_out, double& sb_out)
+{
+    double L[MD];
+#pragma unroll
+    for (int j = 0; j < MD; j++) L[j] = Lrow[(j < d) ? j : d - 1];
+    double acca = 0.0, accb = 0.0, sa = 0.0, sb = 0.0;
+#pragma unroll
+    for (int j = 0; j < MD; j++) {
+        if (j >= d) break;
+        if (lane == j) {
+            sa = (va - acca) / L[j];
+            sb = (vb - accb) / L[j];
+        }
+        const double saj = lane_bcast(sa, j);
+        const double sbj = lane_bcast(sb, j);
+        if (lane > j && lane < d) {
+            acca += L[j] * saj;
+            accb += L[j] * sbj;
+        }
+    }
+    sa_out = sa;
+    sb_out = sb;
+}
+
 // lane i (< d) holds v_i and row i of L (Lrow); returns s_i of L s = v
 __device__ __forceinline__ double wave_lower_solve(int d, const double* Lrow, double v, int lane)
 {
@@ -314,6 +343,24 @@ __device__ __forceinline__ double wave_seq_sum(int n, double x)
     double s = 0.0;
     for (int i = 0; i < n; i++) s += lane_bcast(x, i);
     return s;
+}
+
+// lane k holds log(w_k N_k(x)); returns the responsibility r_k in lane k and the mixture's
+// log-density in lsum_out (GMM::CalculateResponsibilities' log-sum-exp, components in order)
+__device__ __forceinline__ double wave_normalize_resp(int K, double r, double& lsum_out)
+{
+    double m = lane_bcast(r, 0);
+    for (int k = 1; k < K; k++) {
+        const double rk = lane_bcast(r, k);
+        m = (rk > m) ? rk : m;
+    }
+    double sum = 0.0;
+    for (int k = 0; k < K; k++) sum += exp(lane_bcast(r, k) - m);
+    const double lsum = log(sum) + m;
+    const double e = exp(r - lsum);
+    const double tot = wave_seq_sum(K, e);
+    lsum_out = lsum;
+    return e / tot;
 }
 
 // responsibilities of the point x (lane i = x_i); lane k of the result = r_k; lsum = the mixture's
@@ -330,18 +377,7 @@ __device__ __forceinline__ double wave_responsibilities_lsum(int K, int d, doubl
         const double rk = (logc[k] - 0.5 * wave_seq_sum(d, (lane < d) ? t * t : 0.0)) + log(w[k]);
         r = (lane == k) ? rk : r;
     }
-    double m = lane_bcast(r, 0);
-    for (int k = 1; k < K; k++) {
-        const double rk = lane_bcast(r, k);
-        m = (rk > m) ? rk : m;
-    }
-    double sum = 0.0;
-    for (int k = 0; k < K; k++) sum += exp(lane_bcast(r, k) - m);
-    const double lsum = log(sum) + m;
-    const double e = exp(r - lsum);
-    const double tot = wave_seq_sum(K, e);
-    lsum_out = lsum;
-    return e / tot;
+    return wave_normalize_resp(K, r, lsum_out);
 }
 
 __device__ __forceinline__ double wave_responsibilities(int K, int d, double x, const double* mean,
@@ -462,7 +498,33 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
             x = (j <= lane) ? a : x;
         }
         nxt = reflect(x * f + cur, P.lower[li], P.upper[li]);
-        if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
+        if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE && d <= 16) {
+            // the reverse responsibilities at nxt and the MH solve of component k use the same
+            // L_k: one pass solves both (values as in the branch below, bit for bit)
+            double r = 0.0, qv = 0.0;
+            for (int k = 0; k < K; k++) {
+                const double sk = (k == upd) ? sc : scale[k];
+                const double ta0 = on ? nxt - mean[k * d + lane] : 0.0;
+                const double tb0 = on ? (nxt - cur) / sk : 0.0;
+                double ta, tb;
+                wave_lower_solve2_reg<16>(d, chol + (int64_t)k * d * d + (int64_t)li * d, ta0, tb0, lane, ta, tb);
+                const double rk = (logc[k] - 0.5 * wave_seq_sum(d, on ? ta * ta : 0.0)) + log(w[k]);
+                r = (lane == k) ? rk : r;
+                const double q = 0.5 * wave_seq_sum(d, on ? tb * tb : 0.0);
+                qv = (lane == k) ? q : qv;
+            }
+            double lsum;
+            const double rr = wave_normalize_resp(K, r, lsum);
+            double fwd = -INFINITY, rev = -INFINITY;
+            for (int k = 0; k < K; k++) {
+                const double sk = (k == upd) ? sc : scale[k];
+                const double base = -log(sk * sk) + logc[k];
+                const double q = lane_bcast(qv, k);
+                fwd = logsum2(fwd, (base - q) + log(lane_bcast(rf, k)));
+                rev = logsum2(rev, (base - q) + log(lane_bcast(rr, k)));
+            }
+            lmh = rev - fwd;
+        } else if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
             const double rr = wave_responsibilities(K, d, nxt, mean, chol, logc, w, lane);
             double fwd = -INFINITY, rev = -INFINITY;
             for (int k = 0; k < K; k++) {
