@@ -3,6 +3,7 @@
 
 #include <cmath>
 #include <cstdlib>
+#include <exception>
 #include <fstream>
 #include <limits>
 
@@ -54,15 +55,28 @@ bool LikelihoodGPUBase::EvaluateLogProbability(size_t threadix, const VectorReal
         std::vector<Request*> batch;
         batch.swap(comb_queue);
         lk.unlock();
+        // whatever happens in the launch (a bad_alloc included), the batch is marked done and the
+        // waiting threads are woken, so no caller waits on a launch that will never finish
+        bool ok = false;
         const size_t d = GetNumVariables(), n = batch.size();
-        std::vector<Real> v(n * d), out(n);
-        std::vector<int32_t> st(n);
-        for (size_t i = 0; i < n; i++) std::copy(batch[i]->values, batch[i]->values + d, v.begin() + i * d);
-        const bool ok = EvaluateLogProbabilityBatch(n, v.data(), out.data(), st.data());
+        std::vector<Real> out;
+        std::vector<int32_t> st;
+        try {
+            std::vector<Real> v(n * d);
+            out.assign(n, -std::numeric_limits<Real>::infinity());
+            st.assign(n, BCM3HIP_STATUS_SOLVER_FAIL);
+            for (size_t i = 0; i < n; i++) std::copy(batch[i]->values, batch[i]->values + d, v.begin() + i * d);
+            ok = EvaluateLogProbabilityBatch(n, v.data(), out.data(), st.data());
+        } catch (const std::exception& e) {
+            LOGERROR("Batched likelihood evaluation failed: %s", e.what());
+            ok = false;
+        }
         lk.lock();
         for (size_t i = 0; i < n; i++) {
-            batch[i]->logp = out[i];
-            batch[i]->ok = ok;
+            // per request: a model failure (status 1) is a legal -inf, anything else a failed call
+            const bool item_ok = ok && i < st.size() && (st[i] == BCM3HIP_STATUS_OK || st[i] == BCM3HIP_STATUS_SOLVER_FAIL);
+            batch[i]->logp = item_ok ? out[i] : std::numeric_limits<Real>::quiet_NaN();
+            batch[i]->ok = item_ok;
             batch[i]->done = true;
         }
         comb_busy = false;

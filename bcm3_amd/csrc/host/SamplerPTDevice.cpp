@@ -635,16 +635,23 @@ struct SamplerPTDevice::Impl {
             !Upload(scale, dsc, stream) || !Upload(ema, dem, stream) ||
             bcm3hip_memset_async(hcount.p, 0, hcount.n * sizeof(int64_t), stream) != 0)
             return false;
-        if (!adapt_file.empty() && g0 + C == Ctot && !WriteAdaptation(C - 1, nc, w, mu, L, h, counts)) return false;
+        // SamplerPTChain::AdaptProposal names the fit adapt<adaptation_iteration>: adapt0 is the
+        // initial proposal (written by SetAdaptationOutput), so the k-th fit is adapt<k+1>, and every
+        // fit carries the history it was fitted to (SamplerPTChain.cpp:149-166)
+        if (!adapt_file.empty() && g0 + C == Ctot &&
+            !WriteAdaptation(cnt.adaptations_done + 1, C - 1, nc, w, mu, L, &h, counts))
+            return false;
         cnt.adaptations_done++;
         return bcm3hip_stream_synchronize(stream) == 0;
     }
 
-    bool WriteAdaptation(int64_t c, const std::vector<int32_t>& nc, const std::vector<double>& w,
-                         const std::vector<double>& mu, const std::vector<double>& L, const std::vector<float>& h,
+    // adapt<index>/block1 of sampler_adaptation.nc for chain c's proposal; h == nullptr: no history
+    // group (adapt0, the proposal before any fit)
+    bool WriteAdaptation(int64_t index, int64_t c, const std::vector<int32_t>& nc, const std::vector<double>& w,
+                         const std::vector<double>& mu, const std::vector<double>& L, const std::vector<float>* h,
                          const std::vector<int64_t>& counts)
     {
-        const std::string g = "adapt" + std::to_string(cnt.adaptations_done) + "/block1";
+        const std::string g = "adapt" + std::to_string(index) + "/block1";
         std::vector<int32_t> ix(d);
         for (int j = 0; j < d; j++) ix[j] = j;
         adapt_out.AddVector(g, "variable_indices", ix);
@@ -671,12 +678,12 @@ struct SamplerPTDevice::Impl {
         } else {
             adapt_out.AddMatrix(g, "covariance", d, d, cov(0));
         }
-        if (cnt.adaptations_done >= 1) {
+        if (h) {
             // the history this adaptation was fitted to (rows as stored in the device ring)
             const int64_t rows = std::min<int64_t>(counts[c], H);
             std::vector<double> hist((size_t)(rows * d));
             for (int64_t r = 0; r < rows; r++)
-                for (int j = 0; j < d; j++) hist[(size_t)(r * d + j)] = h[(size_t)((c * H + r) * d + j)];
+                for (int j = 0; j < d; j++) hist[(size_t)(r * d + j)] = (*h)[(size_t)((c * H + r) * d + j)];
             adapt_out.AddMatrix(g, "history", (size_t)rows, (size_t)d, hist);
         }
         if (!adapt_out.Write(adapt_file)) {
@@ -719,6 +726,17 @@ bool SamplerPTDevice::Initialize(std::shared_ptr<Likelihood> ll, const std::vect
     s.g0 = cfg.rank * s.C;
     C_ = s.C;
     d_ = s.d;
+    if (cfg.use_every_nth < 1 || cfg.exploration_steps < 0 || cfg.initial_position_tries < 1 ||
+        cfg.adapt_proposal_samples < 0 || cfg.adapt_proposal_times < 0 || cfg.max_history_size < 1 ||
+        !(cfg.exchange_probability >= 0.0 && cfg.exchange_probability <= 1.0)) {
+        LOGERROR("SamplerPTDevice: out-of-range setting (use_every_nth %d, exploration_steps %d, "
+                 "initial_position_tries %d, adapt_proposal_samples %lld, adapt_proposal_times %lld, "
+                 "max_history_size %lld, exchange_probability %g)",
+                 (int)cfg.use_every_nth, (int)cfg.exploration_steps, (int)cfg.initial_position_tries,
+                 (long long)cfg.adapt_proposal_samples, (long long)cfg.adapt_proposal_times,
+                 (long long)cfg.max_history_size, cfg.exchange_probability);
+        return false;
+    }
     if (cfg.proposal < 0 || cfg.proposal > 3 || cfg.swapping_scheme < 0 || cfg.swapping_scheme > 2) {
         LOGERROR("SamplerPTDevice: unknown proposal type or swapping scheme");
         return false;
@@ -868,8 +886,17 @@ bool SamplerPTDevice::SetAdaptationOutput(const std::string& filename)
         LOGERROR("SetAdaptationOutput: needs a file name and an adaptive proposal");
         return false;
     }
-    p_->adapt_file = filename;
-    return true;
+    Impl& s = *p_;
+    s.adapt_file = filename;
+    if (s.cnt.adaptations_done > 0 || s.g0 + s.C != s.Ctot) return true;
+    // adapt0: the hottest chain's initial proposal (SamplerPTChain::Initialize -> AdaptProposal(0) with
+    // an empty history: the prior-moment proposal InitProposal uploaded), no history group
+    std::vector<int32_t> dnc;
+    std::vector<double> dw, dmu, dL;
+    if (!Download(dnc, s.ncomp, s.stream) || !Download(dw, s.weights, s.stream) || !Download(dmu, s.mean, s.stream) ||
+        !Download(dL, s.chol, s.stream))
+        return false;
+    return s.WriteAdaptation(0, s.C - 1, dnc, dw, dmu, dL, nullptr, std::vector<int64_t>());
 }
 
 bool SamplerPTDevice::FlushOutput() { return p_->Flush() && (!p_->out || p_->out->Sync()); }

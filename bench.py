@@ -513,23 +513,25 @@ def main():
     C = args.total_chains // world if args.total_chains else args.chains
     loop_kind = args.loop
     if args.loop == "native":
+        # the C++ sampler is the measured loop; if its RCCL communicator cannot be set up this run
+        # fails (never a silent switch to the Python loop, which is only run with --loop python)
+        err = None
         try:
             loop = NativeLoop(ll, C * world, rank, world, args, dist if world > 1 else None)
         except RuntimeError as e:
             if world == 1:
                 raise
-            # the C++ loop's own RCCL communicator could not be set up on this node: the same
-            # iteration in Python, its PT swap over torch.distributed (also RCCL); both logged
-            print(f"bench.py rank {rank}: C++ sampler unavailable ({e}); using the Python loop", file=sys.stderr,
-                  flush=True)
-            loop_kind = "python"
-        ok = torch.tensor([1 if loop_kind == "native" else 0], device=device)
+            err = e
+            print(f"bench.py rank {rank}: C++ sampler setup failed: {e}", file=sys.stderr, flush=True)
         if world > 1:
+            ok = torch.tensor([0 if err else 1], device=device)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0 and loop_kind == "native":
-            loop.s.close()
-            loop_kind = "python"
-    if loop_kind == "python":
+            if int(ok.item()) == 0:
+                print(f"bench.py rank {rank}: the C++ sampler is unavailable on some rank; no fallback "
+                      "(rerun with --loop python to time the Python loop)", file=sys.stderr, flush=True)
+                dist.destroy_process_group()
+                sys.exit(3)
+    else:
         loop = PythonLoop(ll, C * world, rank, world, args, device)
 
     loop.run(args.warmup)

@@ -468,8 +468,18 @@ def _popavg_logp(d, avg, tv):
     return logp * d["weight"]
 
 
-def simulate(prob, values):
+def simulate(prob, values, nthreads=1):
+    """Every draw's experiments in order; nthreads > 1 runs draws on a thread pool (the per-cell
+    CVODE solves run in C without the GIL), one evaluation per thread like the reference's
+    sampling threads. Results do not depend on nthreads."""
     values = np.atleast_2d(np.asarray(values, dtype=float))
+    if nthreads > 1 and len(values) > 1:
+        import concurrent.futures as cf
+        with cf.ThreadPoolExecutor(nthreads) as pool:
+            parts = list(pool.map(lambda v: simulate(prob, v[None, :]), values))
+        return dict(logp=np.concatenate([p["logp"] for p in parts]),
+                    population_average=[p["population_average"][0] for p in parts],
+                    num_cells=[p["num_cells"][0] for p in parts], detail=[p["detail"][0] for p in parts])
     res = []
     for v in values:
         logp = 0.0

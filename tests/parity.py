@@ -6,14 +6,20 @@ without FMA contraction (oracle/_ref/libbcm3ref.so vs libbcm3ref_nofma.so) diffe
     y1 max rel err per draw:  <=1e-9 for 93.0%, <=1e-6 for 99.0%, <=2e-5 for 99.65%
     llh |d|/(1+|llh|):        <=1e-8 for 99.2%, max 1.4e-5
     BDF step counts equal:    99.3%;  ok/fail status identical for 100%.
-The contract asserts the GPU is inside that envelope (with a small margin):
+The contract asserts the GPU is inside that envelope, at the reference's own FMA on/off spread
+minus a small margin (VERDICT r02 "Next round" 1): y1 >=92% at 1e-9, >=98.5% at 1e-6, >=99.5% at
+2e-5; llh >=99% at 1e-8. Every assert_parity call appends its measured fractions to the JSON-lines
+file named by $BCM3_PARITY_LOG (committed under profiles/ per round).
 """
 from __future__ import annotations
 
+import json
+import os
+
 import numpy as np
 
-Y1_TIERS = ((1e-9, 0.90), (1e-6, 0.97), (2e-5, 0.985))  # (tolerance, min fraction of draws)
-LLH_T1, LLH_T1_FRAC = 1e-8, 0.975
+Y1_TIERS = ((1e-9, 0.92), (1e-6, 0.985), (2e-5, 0.995))  # (tolerance, min fraction of draws)
+LLH_T1, LLH_T1_FRAC = 1e-8, 0.99
 LLH_T2 = 1e-3  # every draw whose ok/fail status agrees
 STEPS_FRACTION = 0.98
 
@@ -47,9 +53,21 @@ def summarize(y1_err, llh_e, steps_a, steps_b) -> dict:
     return out
 
 
+def log_summary(s: dict, **extra):
+    """Append one JSON line {test, fractions...} to $BCM3_PARITY_LOG (no-op when unset)."""
+    path = os.environ.get("BCM3_PARITY_LOG")
+    if not path:
+        return
+    rec = {"test": os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0], **s, **extra}
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "a") as f:
+        f.write(json.dumps(rec) + "\n")
+
+
 def assert_parity(y1_err, llh_e, steps_a, steps_b, ok_a, ok_b, near_cap=None):
     """Assert the GPU-vs-oracle differences are inside the reference's self-parity envelope."""
     s = summarize(y1_err, llh_e, steps_a, steps_b)
+    log_summary(s, n=int(np.asarray(llh_e).size))
     ok_a, ok_b = np.asarray(ok_a), np.asarray(ok_b)
     differ = ok_a != ok_b
     if near_cap is not None:

@@ -113,6 +113,58 @@ def test_batch_invariance(setup):
         assert one[0] == lp[i] or (math.isnan(one[0]) and math.isnan(lp[i]))
 
 
+def test_bench_size_batch_matches_oracle(tmp_path):
+    """Config C4 as benched (tests/golden/cellpop_likelihood.xml: 500 initial cells, max_cells 2048,
+    ~1,650 cells per evaluation) with the bench's 64 evaluations in ONE batch, so generation sizes,
+    the generation loop and the cell numbering run at the bench's scale; the first 16 evaluations
+    checked against the oracle (both reference builds) inside the envelope of the module docstring."""
+    import os
+    import parity
+    from bcm3_amd.likelihood import Likelihood
+    path = os.path.join(CH.GOLDEN, "cellpop_likelihood.xml")
+    ll = Likelihood(path, CH.PRIOR, device=0)
+    x = CH.draws(64, 23)
+    lp, status = ll.evaluate_batch(x)
+    n = 16
+    nthreads = max(1, min(16, len(os.sched_getaffinity(0))))
+    prob = CP.load_problem(path, CH.PRIOR)
+    ref = CP.simulate(prob, x[:n], nthreads=nthreads)
+    ref_nofma = CP.simulate(CP.load_problem(path, CH.PRIOR, variant="nofma"), x[:n], nthreads=nthreads)
+    e = prob["experiments"][0]
+    M, NS = len(e["output_times"]), len(e["model"].ode)
+    dev, spread, same_steps, total, cells_total = [], [], 0, 0, 0
+    for i in range(n):
+        r = ref["logp"][i]
+        if r == -math.inf:
+            assert lp[i] == -math.inf and status[i] == 1, i
+            continue
+        tol = max(2e-4 * (1.0 + abs(r)), 3.0 * abs(ref_nofma["logp"][i] - r))
+        assert abs(lp[i] - r) <= tol, (i, lp[i], r, ref_nofma["logp"][i])
+        assert status[i] == 0
+        dev.append(abs(lp[i] - r) / (1.0 + abs(r)))
+        spread.append(abs(ref_nofma["logp"][i] - r) / (1.0 + abs(r)))
+        cells = ref["detail"][i]["cells"]
+        rec, _, _ = ll.cellpop_cells(i, M, NS)
+        assert len(rec) == len(cells), i
+        cells_total += len(cells)
+        for k, c in enumerate(cells):
+            assert bool(rec["flags"][k] & 2) == c["divided"], (i, k)
+            same_steps += int(rec["nsteps"][k] == c["nsteps"])
+            total += 1
+    assert dev, "every checked draw was -inf"
+    assert np.median(dev) <= 10.0 * np.median(spread) + 1e-12, (np.median(dev), np.median(spread))
+    assert same_steps >= 0.95 * total, (same_steps, total)
+    parity.log_summary({"cellpop_draws_checked": n, "finite": len(dev), "cells": cells_total,
+                        "steps_equal": same_steps / max(1, total), "logp_dev_median": float(np.median(dev)),
+                        "logp_dev_max": float(np.max(dev)), "ref_fma_spread_median": float(np.median(spread))},
+                       n=n)
+    # the rest of the batch: each entry equals its own single evaluation (no batch coupling)
+    for i in (17, 40, 63):
+        one, _ = ll.evaluate_batch(x[i:i + 1])
+        assert one[0] == lp[i] or (math.isnan(one[0]) and math.isnan(lp[i]))
+    ll.close()
+
+
 def test_too_many_cells_is_minus_inf(tmp_path):
     from bcm3_amd.likelihood import Likelihood
     path = CH.write_likelihood(tmp_path, 4, 10, name="small_max.xml")

@@ -308,7 +308,8 @@ def test_c5_2048_chains_on_one_gpu():
     mism = np.isfinite(got) != np.isfinite(ref)
     assert np.all(r["stats"][mism, 0, 0] >= 1980)
     err = parity.llh_err(got[~mism], ref[~mism])
-    assert np.mean(err <= parity.LLH_T1) >= 0.97 and np.all(err <= parity.LLH_T2)
+    parity.log_summary({"llh_t1": float(np.mean(err <= parity.LLH_T1)), "llh_max": float(err.max())}, n=int(err.size))
+    assert np.mean(err <= parity.LLH_T1) >= parity.LLH_T1_FRAC and np.all(err <= parity.LLH_T2)
     # one exchange round of the whole ladder
     snap = [t.cpu().numpy().copy() for t in (loop.values, loop.llh, loop.lprior, loop.lpp)]
     rnd = loop.round

@@ -179,8 +179,10 @@ def test_sample_output_file(tmp_path):
 
 
 def test_adaptation_output_file(tmp_path):
-    """ptmhsampler.output_proposal_adaptation: one group per adaptation with the hottest chain's
-    mixture (weights, means, covariances) and, from the second adaptation on, its history"""
+    """ptmhsampler.output_proposal_adaptation in the reference's layout (SamplerPTChain.cpp:88-97,
+    149-166): adapt0 = the hottest chain's initial prior-moment proposal without history, then one
+    group adapt<k> per fit k = 1, 2, ... with the mixture (weights, means, covariances) and the
+    history it was fitted to"""
     from scipy.io import netcdf_file
     C, seed = 16, 6
     s = _native(*C2, C, seed, 0, adapt_proposal_samples=40, adapt_proposal_times=2)
@@ -192,7 +194,7 @@ def test_adaptation_output_file(tmp_path):
     s.close()
     with netcdf_file(path, "r", mmap=False) as f:
         v = {k: np.array(x[:]) for k, x in f.variables.items()}
-    for a in (0, 1):
+    for a in (0, 1, 2):
         g = f"adapt{a}.block1."
         assert list(v[g + "variable_indices"]) == [0, 1]
         w = v[g + "gmm_weights"]
@@ -202,5 +204,11 @@ def test_adaptation_output_file(tmp_path):
             assert S.shape == (2, 2) and np.allclose(S, S.T) and np.all(np.linalg.eigvalsh(S) > 0)
             assert v[g + f"cluster{k}_mean"].shape == (2,)
         assert list(v[g + "gmm_weights_dim"]) == list(range(1, len(w) + 1))
-    assert len(v["adapt1.block1.gmm_weights"]) == nc[-1]
-    assert "adapt0.block1.history" not in v and v["adapt1.block1.history"].shape[1] == 2
+    # adapt0: one component at the prior's moments (C2 prior: U(-6, 6)^2 -> mean 0, variance 12)
+    assert len(v["adapt0.block1.gmm_weights"]) == 1
+    np.testing.assert_allclose(v["adapt0.block1.cluster0_mean"], [0.0, 0.0], atol=1e-12)
+    np.testing.assert_allclose(v["adapt0.block1.cluster0_covariance"], np.diag([12.0, 12.0]), rtol=1e-12)
+    assert len(v["adapt2.block1.gmm_weights"]) == nc[-1]
+    assert "adapt0.block1.history" not in v
+    assert v["adapt1.block1.history"].shape[1] == 2 and v["adapt2.block1.history"].shape[1] == 2
+    assert "adapt3.block1.gmm_weights" not in v
