@@ -4,6 +4,7 @@
 
 #include "../../../include/bcm3.h"
 #include "../../../include/bcm3hip.h"
+#include "Config.h"
 #include "Likelihood.h"
 #include "Prior.h"
 #include "SamplerPTDevice.h"
@@ -48,6 +49,66 @@ void bcm3_ptmh_config_default(bcm3_ptmh_config* c)
     c->nan_check_every = d.nan_check_every;
     c->host_threads = 0;
     c->transport = BCM3_PTMH_TRANSPORT_NONE;
+}
+
+static bool CopyString(char* dst, size_t cap, const std::string& src, const char* what)
+{
+    if (src.size() + 1 > cap) {
+        LOGERROR("config: %s is longer than %zu characters", what, cap - 1);
+        return false;
+    }
+    std::memcpy(dst, src.c_str(), src.size() + 1);
+    return true;
+}
+
+int bcm3_run_config_from_file(const char* path, bcm3_run_config* out)
+{
+    if (!path || !out) return -1;
+    bcm3::RunConfig rc;
+    if (!bcm3::LoadRunConfig(path, rc)) return -2;
+    bcm3_run_config r;
+    std::memset(&r, 0, sizeof(r));
+    bcm3_ptmh_config_default(&r.ptmh);
+    const bcm3::PTMHConfig& p = rc.ptmh;
+    r.ptmh.num_chains = p.num_chains;
+    r.ptmh.temperature_power = p.temperature_power;
+    r.ptmh.temperature_max = p.temperature_max;
+    r.ptmh.seed = p.seed;
+    r.ptmh.learning_rate = p.learning_rate;
+    r.ptmh.exploration_steps = p.exploration_steps;
+    r.ptmh.proposal = p.proposal;
+    r.ptmh.t_dof = p.t_dof;
+    r.ptmh.adapt_proposal_samples = p.adapt_proposal_samples;
+    r.ptmh.adapt_proposal_times = p.adapt_proposal_times;
+    r.ptmh.max_history_size = p.max_history_size;
+    r.ptmh.adapt_proposal_max_history_samples = p.adapt_proposal_max_history_samples;
+    r.ptmh.use_every_nth = p.use_every_nth;
+    r.ptmh.swapping_scheme = p.swapping_scheme;
+    r.ptmh.exchange_probability = p.exchange_probability;
+    r.ptmh.initial_position_tries = p.initial_position_tries;
+    r.ptmh.host_threads = p.host_threads;
+    r.num_samples = rc.num_samples;
+    r.output_proposal_adaptation = rc.output_proposal_adaptation ? 1 : 0;
+    r.sampling_threads = rc.sampling_threads;
+    r.evaluation_threads = rc.evaluation_threads;
+    if (!CopyString(r.sampler_type, sizeof(r.sampler_type), rc.sampler_type, "sampler.type") ||
+        !CopyString(r.prior, sizeof(r.prior), rc.prior, "prior") ||
+        !CopyString(r.likelihood, sizeof(r.likelihood), rc.likelihood, "likelihood") ||
+        !CopyString(r.output_folder, sizeof(r.output_folder), rc.output_folder, "output.folder") ||
+        !CopyString(r.likelihood_options, sizeof(r.likelihood_options), rc.likelihood_options, "likelihood options"))
+        return -2;
+    *out = r;
+    return 0;
+}
+
+int bcm3_ptmh_config_from_file(const char* path, bcm3_ptmh_config* cfg)
+{
+    if (!path || !cfg) return -1;
+    bcm3_run_config r;
+    const int rc = bcm3_run_config_from_file(path, &r);
+    if (rc != 0) return rc;
+    *cfg = r.ptmh;
+    return 0;
 }
 
 int bcm3_ptmh_nccl_unique_id(void* id) { return bcm3hip_nccl_get_unique_id(id) == 0 ? 0 : -2; }

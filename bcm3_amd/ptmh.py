@@ -38,6 +38,16 @@ class PTMHConfig(C.Structure):
     ]
 
 
+class RunConfig(C.Structure):
+    """bcm3_run_config (include/bcm3.h): bcminf's config.txt as the PT-MH path reads it."""
+    _fields_ = [
+        ("ptmh", PTMHConfig), ("num_samples", C.c_int64), ("output_proposal_adaptation", C.c_int32),
+        ("pad_", C.c_int32), ("sampling_threads", C.c_int64), ("evaluation_threads", C.c_int64),
+        ("sampler_type", C.c_char * 64), ("prior", C.c_char * 1024), ("likelihood", C.c_char * 1024),
+        ("output_folder", C.c_char * 1024), ("likelihood_options", C.c_char * 2048),
+    ]
+
+
 _bound = False
 
 
@@ -48,6 +58,8 @@ def _lib():
         vp = C.c_void_p
         L.bcm3_ptmh_config_default.argtypes = [C.POINTER(PTMHConfig)]
         L.bcm3_ptmh_config_default.restype = None
+        L.bcm3_run_config_from_file.argtypes = [C.c_char_p, C.POINTER(RunConfig)]
+        L.bcm3_ptmh_config_from_file.argtypes = [C.c_char_p, C.POINTER(PTMHConfig)]
         L.bcm3_ptmh_nccl_unique_id.argtypes = [vp]
         L.bcm3_ptmh_group_create.argtypes = [C.c_int, C.POINTER(vp)]
         L.bcm3_ptmh_group_destroy.argtypes = [vp]
@@ -82,6 +94,22 @@ def _check(r: int, what: str):
     if r != 0:
         msg = host_lib().bcm3_last_error()
         raise RuntimeError(f"{what} failed ({r}): {msg.decode() if msg else ''}")
+
+
+def load_config(path: str) -> dict:
+    """config.txt through bcm3_run_config_from_file: {"ptmh": {field: value}, "num_samples": ...,
+    "prior": ..., ...}; raises RuntimeError with the reader's message on a file the reference
+    would reject."""
+    rc = RunConfig()
+    _check(_lib().bcm3_run_config_from_file(path.encode(), C.byref(rc)), "bcm3_run_config_from_file")
+    ptmh = {k: getattr(rc.ptmh, k) for k, _ in PTMHConfig._fields_ if k not in ("nccl_id", "group")}
+    out = {"ptmh": ptmh}
+    for k, _ in RunConfig._fields_:
+        if k in ("ptmh", "pad_"):
+            continue
+        v = getattr(rc, k)
+        out[k] = v.decode() if isinstance(v, bytes) else v
+    return out
 
 
 def nccl_unique_id() -> bytes:

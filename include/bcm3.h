@@ -183,6 +183,29 @@ int bcm3_ptmh_flush_output(bcm3_ptmh* s);
  * (nested groups named "adapt<k>.block1.<name>"); written by the rank holding that chain. */
 int bcm3_ptmh_set_adaptation_output(bcm3_ptmh* s, const char* filename);
 
+/* ---- config.txt (bcminf's configuration file) ----
+ * boost::program_options::parse_config_file over the options bcminf registers
+ * (src/bcminf/main.cpp:293-320; Sampler.cpp:142-149; SamplerPT.cpp:147-171;
+ * LikelihoodFactory.cpp:103-111), read as Sampler::LoadSettings / SamplerPT::LoadSettings do
+ * (SamplerPT.cpp:40-95): "[section]" lines prefix "section.", '#' comments, the registered
+ * defaults for every key the file omits; an unknown or repeated key, a value of the wrong type, an
+ * unknown swapping scheme or proposal type (e.g. "parametric_mixture": SamplerPTChain.cpp:428-444)
+ * fail (< 0, message in bcm3_last_error). sampler.rngseed = 0 becomes a time-based seed
+ * (Sampler.cpp:91-94). rank / world / transport are left at their defaults. */
+typedef struct {
+    bcm3_ptmh_config ptmh;
+    int64_t num_samples;                /* sampler.num_samples (2500): bcm3_ptmh_run's argument */
+    int32_t output_proposal_adaptation; /* ptmhsampler.output_proposal_adaptation */
+    int32_t pad_;
+    int64_t sampling_threads, evaluation_threads;
+    char sampler_type[64];
+    char prior[1024], likelihood[1024], output_folder[1024];
+    char likelihood_options[2048];      /* "key=value;..." for bcm3_likelihood_create_ex */
+} bcm3_run_config;
+int bcm3_run_config_from_file(const char* path, bcm3_run_config* out);
+/* the sampler part of the same file (bcm3_ptmh_config_default, then the file's settings) */
+int bcm3_ptmh_config_from_file(const char* path, bcm3_ptmh_config* cfg);
+
 /* ---- netCDF classic files (NetCDFClassic.h): the sampler's output.nc ----
  * The reference's output.nc schema (group "samples", SampleHandlerNetCDF.cpp:41-58) in a netCDF
  * classic (CDF-2) file, group members named "samples.<name>": dims sample_ix, temperature,

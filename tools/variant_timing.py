@@ -26,11 +26,11 @@ for n in (256, 2048):
         ctx.eval_device(n, v.data_ptr(), lp.data_ptr(), None, None)
         ms.append(ctx.last_kernel_ms())
     out.append(f"n={n}: {min(ms):.3f} ms")
-vals = S.prior_draws(1, 512, 11)
+vals = S.prior_draws(1, int(os.environ.get("NPAR", "512")), 20251019)
 g = ctx.eval(vals)
 o = O.Oracle('restated').popk_eval(prob, vals, nthreads=8, want_traj=False)
 e = parity.llh_err(g[0] if isinstance(g, tuple) else g['logp'], o['logp'])
-print(LIB, ' '.join(out), f"llh<=1e-8 {np.mean(e <= 1e-8):.3f} max {np.max(e):.2e}", flush=True)
+print(LIB, ' '.join(out), f"llh<=1e-8 {np.mean(e <= 1e-8):.4f} max {np.max(e):.2e}", flush=True)
 """
 
 
