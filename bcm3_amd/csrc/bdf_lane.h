@@ -129,6 +129,14 @@ BDF_INL void cfor_down(F&& f)
 // value. The GPU-vs-CPU llh parity envelope (tests/parity.py) holds for both (512 C3 draws:
 // 99.6 % within 1e-8 fast, 99.4 % correctly rounded).
 
+// Default (round 3): the correctly rounded forms -- the reference's IEEE quotients, and the GPU's
+// llh agreement with the reference CVODE then meets the reference's own FMA on/off spread (4,096
+// C3 draws: 99.05 % within 1e-8 vs 98.88 % with the one-step forms; profiles/r03_parity_variants.txt).
+// -DBCM3_FAST_DIV selects the one-Newton-step forms (tools/build_variant.sh).
+#if !defined(BCM3_FAST_DIV) && !defined(BCM3_CORRECTLY_ROUNDED)
+#define BCM3_CORRECTLY_ROUNDED
+#endif
+
 // reciprocal
 BDF_INL double frcp(double b)
 {

@@ -128,17 +128,87 @@ bool LoadPriorMarginals(const XmlNode& root, std::vector<Marginal>& out)
         return false;
     }
     out.clear();
+    // multivariate (Dirichlet) groups by id: first variable index and member alphas
+    // (PriorIndependence::LoadFromXML, PriorIndependence.cpp:20-115)
+    struct Group {
+        long first = -1;
+        std::vector<double> alpha;
+    };
+    std::vector<Group> groups;
+    std::vector<long> member_group;  // per variable, -1 for univariate
     try {
         for (auto& var : node->children) {
             if (var->name != "variable") continue;
-            Marginal m;
-            if (!ParseMarginal(*var, m)) return false;
+            const bool multivariate = var->get_bool("multivariate", false);
             const long repeat = var->get_long("repeat", 1);
-            for (long i = 0; i < repeat; i++) out.push_back(m);
+            if (multivariate) {
+                if (repeat > 1) {
+                    LOGERROR("Multivariate prior with repeat not supported");
+                    return false;
+                }
+                const long id = var->get_long("id", 0);  // missing: the reference throws; 0 is refused below
+                if (id <= 0) {
+                    LOGERROR("Multivariate distribution IDs should start at 1.");
+                    return false;
+                }
+                const long vix = (long)out.size();
+                if (id > (long)groups.size()) {
+                    groups.resize(id);
+                    // only dirichlet (PriorIndependence.cpp:47-51)
+                    if (var->get("distribution") != "dirichlet") {
+                        LOGERROR("Multivariate distribution of unknown type (only dirichlet supported).");
+                        return false;
+                    }
+                }
+                Group& g = groups[id - 1];
+                if (g.first < 0) g.first = vix;
+                g.alpha.push_back(var->get_double("alpha"));
+                if (vix != g.first + (long)g.alpha.size() - 1) {
+                    LOGERROR("All variables in a multivariate distribution should follow each other directly");
+                    return false;
+                }
+                Marginal m;
+                m.kind = BCM3HIP_PRIOR_DIRICHLET;
+                m.p0 = g.alpha.back();
+                m.p1 = (double)g.first;
+                m.lower = 0.0;  // MultivariateMarginal::GetLowerBound / GetUpperBound (:160-180)
+                m.upper = 1.0;
+                out.push_back(m);
+                member_group.push_back(id - 1);
+            } else {
+                Marginal m;
+                if (!ParseMarginal(*var, m)) return false;
+                for (long i = 0; i < repeat; i++) {
+                    out.push_back(m);
+                    member_group.push_back(-1);
+                }
+            }
         }
     } catch (XmlError& e) {
         LOGERROR("Error parsing UnivariateMarginal: %s", e.what.c_str());
         return false;
+    }
+    // MultivariateMarginal::Initialize (:47-64): log normalisation constant; EvaluateMarginalMean /
+    // EvaluateMarginalVariance (:120-158) for the proposals' starting moments. lgamma: glibc here,
+    // boost::math::lgamma in the reference (parity of this constant unpinned, Boost absent)
+    for (size_t gi = 0; gi < groups.size(); gi++) {
+        const Group& g = groups[gi];
+        if (g.first < 0) {
+            LOGERROR("Multivariate distribution id %zu has no variables", gi + 1);
+            return false;
+        }
+        double sum = 0.0, lprod = 0.0;
+        for (double a : g.alpha) {
+            sum += a;
+            lprod += std::lgamma(a);
+        }
+        const double lnc = std::lgamma(sum) - lprod;
+        for (size_t k = 0; k < g.alpha.size(); k++) {
+            Marginal& m = out[g.first + k];
+            m.p2 = lnc;
+            m.mean = g.alpha[k] / sum;
+            m.var = g.alpha[k] * (sum - g.alpha[k]) / (sum * sum * (sum + 1.0));
+        }
     }
     return true;
 }

@@ -7,6 +7,7 @@
 #include "../../../include/bcm3hip.h"
 #include "Likelihood.h"
 #include "LikelihoodGPU.h"
+#include "Prior.h"
 #include "log.h"
 
 #include "capi_internal.h"
@@ -124,6 +125,32 @@ int bcm3_likelihood_expm_pk_model(const bcm3_likelihood* h, void* model)
 }
 
 void bcm3_likelihood_destroy(bcm3_likelihood* h) { delete h; }
+
+int bcm3_prior_marginals(const char* prior_xml, int max_vars, int32_t* kind, double* params /*[max][3]*/,
+                         double* bounds /*[max][2]*/, double* moments /*[max][2]*/)
+{
+    if (!prior_xml) return -1;
+    std::vector<bcm3::Marginal> m;
+    if (!bcm3::LoadPriorMarginals(prior_xml, m)) return -2;
+    const int d = (int)m.size();
+    for (int i = 0; i < d && i < max_vars; i++) {
+        if (kind) kind[i] = m[i].kind;
+        if (params) {
+            params[3 * i] = m[i].p0;
+            params[3 * i + 1] = m[i].p1;
+            params[3 * i + 2] = m[i].p2;
+        }
+        if (bounds) {
+            bounds[2 * i] = m[i].lower;
+            bounds[2 * i + 1] = m[i].upper;
+        }
+        if (moments) {
+            moments[2 * i] = m[i].mean;
+            moments[2 * i + 1] = m[i].var;
+        }
+    }
+    return d;
+}
 
 int bcm3_likelihood_num_variables(const bcm3_likelihood* h) { return h ? (int)h->varset->GetNumVariables() : -1; }
 

@@ -91,6 +91,9 @@ __device__ inline double sample(int kind, double p0, double p1, double p2, uint6
         const double p = s.uniform();
         return (p < p2) ? exponential(1.0 / p0, s) : exponential(1.0 / p1, s);
     }
+    // a Dirichlet member's Gamma(alpha_i, 1) draw; the caller divides by the group's sum
+    // (MultivariateMarginal::Sample, MultivariateMarginal.cpp:66-84)
+    case BCM3HIP_PRIOR_DIRICHLET: return gamma(p0, 1.0, s);
     default: return NAN;
     }
 }
@@ -151,6 +154,39 @@ __device__ inline double log_pdf(int kind, double p0, double p1, double p2, doub
         return logsum(log(p2) + log_pdf_exponential(x, p0), log(1.0 - p2) + log_pdf_exponential(x, p1));
     default: return NAN;
     }
+}
+
+// Dirichlet group of variables [first, last] (BCM3HIP_PRIOR_DIRICHLET): the last member of the
+// group starting at `first`
+__device__ inline int dirichlet_last(int d, const int32_t* kind, const double* p1, int first)
+{
+    int l = first;
+    while (l + 1 < d && kind[l + 1] == BCM3HIP_PRIOR_DIRICHLET && (int)p1[l + 1] == first) l++;
+    return l;
+}
+
+__device__ inline bool has_dirichlet(int d, const int32_t* kind)
+{
+    for (int i = 0; i < d; i++)
+        if (kind[i] == BCM3HIP_PRIOR_DIRICHLET) return true;
+    return false;
+}
+
+// MultivariateMarginal::EvaluateLogPDF (MultivariateMarginal.cpp:86-118) of the group
+// [first, last]; x(j) returns variable j's value
+template <class X>
+__device__ inline double dirichlet_log_pdf(int first, int last, const double* alpha, double lnc, X&& x)
+{
+    double sum = 0.0;
+    for (int j = first; j <= last; j++) {
+        const double v = x(j);
+        if (v < 0.0 || v > 1.0) return -INFINITY;
+        sum += v;
+    }
+    if (fabs(sum - 1.0) > 1e-15) return -INFINITY;
+    double lp = 0.0;
+    for (int j = first; j <= last; j++) lp += (alpha[j] - 1) * log(x(j));
+    return lp + lnc;
 }
 
 }  // namespace prior

@@ -155,9 +155,20 @@ __device__ __forceinline__ void propose_chain(int c, int d, const int32_t* __res
     const double* cur = values + (int64_t)c * d;
     double* nxt = prop + (int64_t)c * d;
     double lmh = 0.0;
+    const bool dir = prior::has_dirichlet(d, kind);
     if (temps[c] == 0.0) {
-        // PriorIndependence::Sample
+        // PriorIndependence::Sample (PriorIndependence.cpp:158-178)
         for (int i = 0; i < d; i++) nxt[i] = prior::sample(kind[i], p0[i], p1[i], p2[i], seed, iter, gc, i);
+        if (dir) {
+            for (int f = 0; f < d; f++) {
+                if (kind[f] != BCM3HIP_PRIOR_DIRICHLET || (int)p1[f] != f) continue;
+                const int l = prior::dirichlet_last(d, kind, p1, f);
+                double sum = 0.0;
+                for (int j = f; j <= l; j++) sum += nxt[j];
+                const double inv = 1.0 / sum;
+                for (int j = f; j <= l; j++) nxt[j] *= inv;
+            }
+        }
     } else {
         const int Km = P.kmax;
         int K = (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) ? P.ncomp[c] : 1;
@@ -246,10 +257,30 @@ __device__ __forceinline__ void propose_chain(int c, int d, const int32_t* __res
             lmh = rev - fwd;
         }
         for (int i = 0; i < d; i++) nxt[i] = v[i];
+        // Dirichlet residual: the group's last member := 1 - sum(others) after the MH ratio of the
+        // unmodified proposal (SamplerPTChain.cpp:270-278, 295)
+        if (dir) {
+            for (int f = 0; f < d; f++) {
+                if (kind[f] != BCM3HIP_PRIOR_DIRICHLET || (int)p1[f] != f) continue;
+                const int l = prior::dirichlet_last(d, kind, p1, f);
+                double sum = 0.0;
+                for (int j = f; j < l; j++) sum += nxt[j];
+                nxt[l] = 1.0 - sum;
+            }
+        }
         P.selected[c] = sel;
     }
+    // PriorIndependence::EvaluateLogPDF (PriorIndependence.cpp:129-157): multivariate groups first,
+    // then the univariate marginals in variable order
     double lp = 0.0;
-    for (int i = 0; i < d; i++) lp += prior::log_pdf(kind[i], p0[i], p1[i], p2[i], nxt[i]);
+    if (dir) {
+        for (int f = 0; f < d; f++)
+            if (kind[f] == BCM3HIP_PRIOR_DIRICHLET && (int)p1[f] == f)
+                lp += prior::dirichlet_log_pdf(f, prior::dirichlet_last(d, kind, p1, f), p0, p2[f],
+                                               [&](int j) { return nxt[j]; });
+    }
+    for (int i = 0; i < d; i++)
+        if (kind[i] != BCM3HIP_PRIOR_DIRICHLET) lp += prior::log_pdf(kind[i], p0[i], p1[i], p2[i], nxt[i]);
     lprior_prop[c] = lp;
     log_mh[c] = lmh;
 }
@@ -423,8 +454,20 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
     const double cur = values[(int64_t)c * d + li];
     double nxt;
     double lmh = 0.0;
+    const bool dir = prior::has_dirichlet(d, kind);
     if (temps[c] == 0.0) {
         nxt = prior::sample(kind[li], p0[li], p1[li], p2[li], seed, iter, gc, li);
+        if (dir) {
+            // MultivariateMarginal::Sample: each member's Gamma draw over the group's sum
+            for (int f = 0; f < d; f++) {
+                if (kind[f] != BCM3HIP_PRIOR_DIRICHLET || (int)p1[f] != f) continue;
+                const int l = prior::dirichlet_last(d, kind, p1, f);
+                double sum = 0.0;
+                for (int j = f; j <= l; j++) sum += lane_bcast(nxt, j);
+                const double inv = 1.0 / sum;
+                if (lane >= f && lane <= l) nxt *= inv;
+            }
+        }
     } else {
         const int Km = P.kmax;
         int K = (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) ? P.ncomp[c] : 1;
@@ -538,10 +581,35 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
             }
             lmh = rev - fwd;
         }
+        if (dir) {
+            // Dirichlet residual after the MH ratio of the unmodified proposal (SamplerPTChain.cpp:270-278)
+            for (int f = 0; f < d; f++) {
+                if (kind[f] != BCM3HIP_PRIOR_DIRICHLET || (int)p1[f] != f) continue;
+                const int l = prior::dirichlet_last(d, kind, p1, f);
+                double sum = 0.0;
+                for (int j = f; j < l; j++) sum += lane_bcast(nxt, j);
+                if (lane == l) nxt = 1.0 - sum;
+            }
+        }
         if (lane == 0) P.selected[c] = sel;
     }
     if (on) prop[(int64_t)c * d + lane] = nxt;
-    const double lp = wave_seq_sum(d, on ? prior::log_pdf(kind[li], p0[li], p1[li], p2[li], nxt) : 0.0);
+    double lp;
+    if (!dir) {
+        lp = wave_seq_sum(d, on ? prior::log_pdf(kind[li], p0[li], p1[li], p2[li], nxt) : 0.0);
+    } else {
+        // PriorIndependence::EvaluateLogPDF: multivariate groups first, then the univariate
+        // marginals in variable order
+        const double ul = (on && kind[li] != BCM3HIP_PRIOR_DIRICHLET) ? prior::log_pdf(kind[li], p0[li], p1[li], p2[li], nxt)
+                                                                        : 0.0;
+        lp = 0.0;
+        for (int f = 0; f < d; f++)
+            if (kind[f] == BCM3HIP_PRIOR_DIRICHLET && (int)p1[f] == f)
+                lp += prior::dirichlet_log_pdf(f, prior::dirichlet_last(d, kind, p1, f), p0, p2[f],
+                                               [&](int j) { return lane_bcast(nxt, j); });
+        for (int i = 0; i < d; i++)
+            if (kind[i] != BCM3HIP_PRIOR_DIRICHLET) lp += lane_bcast(ul, i);
+    }
     if (lane == 0) {
         lprior_prop[c] = lp;
         log_mh[c] = lmh;

@@ -35,7 +35,7 @@ from .pt import PTExchange, move_uniform, random_pair
 
 
 PRIOR_KINDS = {"uniform": 0, "normal": 1, "exponential": 2, "gamma": 3, "beta": 4, "half_cauchy": 5, "beta_prime": 6,
-               "exponential_mix": 7}
+               "exponential_mix": 7, "dirichlet": 8}
 
 
 @dataclass
@@ -52,14 +52,16 @@ class Marginal:
     def bounds(self):
         """GetLowerBound / GetUpperBound (UnivariateMarginal.cpp:627-647)."""
         lo = self.a if self.kind == "uniform" else (
-            0.0 if self.kind in ("beta", "exponential", "gamma", "half_cauchy", "beta_prime") else -math.inf)
-        hi = self.b if self.kind == "uniform" else (1.0 if self.kind == "beta" else math.inf)
+            0.0 if self.kind in ("beta", "exponential", "gamma", "half_cauchy", "beta_prime", "dirichlet") else -math.inf)
+        hi = self.b if self.kind == "uniform" else (1.0 if self.kind in ("beta", "dirichlet") else math.inf)
         return lo, hi
 
     def moments(self):
         """EvaluateMean / EvaluateVariance (UnivariateMarginal.cpp:448-540)."""
         p0, p1, p2 = self.p
         k = self.kind
+        if k == "dirichlet":
+            return self.mu, self.sigma  # set from the whole group by load_prior
         if k == "uniform":
             d = p1 - p0
             return 0.5 * (p1 + p0), (d * d) / 12.0
@@ -130,11 +132,41 @@ def _marginal(v) -> Marginal:
 
 
 def load_prior(path: str) -> List[Marginal]:
-    """Univariate marginals of a prior.xml in variable order (VariableSet::LoadFromXML repeat rule)."""
+    """Marginals of a prior.xml in variable order (VariableSet::LoadFromXML repeat rule). Members of a
+    multivariate (Dirichlet) group (PriorIndependence.cpp:20-77) become Marginal("dirichlet",
+    p=(alpha_i, index of the group's first variable, log normalisation constant)), moments in
+    mu / sigma (MultivariateMarginal.cpp:47-158), as csrc/host/Prior.cpp does."""
     root = ET.parse(path).getroot()
     out = []
+    groups = {}
     for v in root.iter("variable"):
-        out += [_marginal(v)] * int(v.get("repeat", "1"))
+        if v.get("multivariate", "false").lower() in ("true", "1"):
+            if int(v.get("repeat", "1")) > 1:
+                raise ValueError("Multivariate prior with repeat not supported")
+            gid = int(v.get("id", "0"))
+            if gid <= 0:
+                raise ValueError("Multivariate distribution IDs should start at 1.")
+            if gid not in groups:
+                if v.get("distribution") != "dirichlet":
+                    raise ValueError("Multivariate distribution of unknown type (only dirichlet supported).")
+                groups[gid] = (len(out), [])
+            first, alphas = groups[gid]
+            if len(out) != first + len(alphas):
+                raise ValueError("All variables in a multivariate distribution should follow each other directly")
+            alphas.append(float(v.get("alpha")))
+            out.append(Marginal("dirichlet", p=(alphas[-1], float(first), 0.0)))
+        else:
+            out += [_marginal(v)] * int(v.get("repeat", "1"))
+    for first, alphas in groups.values():
+        s = 0.0
+        lprod = 0.0
+        for a in alphas:
+            s += a
+            lprod += math.lgamma(a)
+        lnc = math.lgamma(s) - lprod
+        for k, a in enumerate(alphas):
+            out[first + k] = Marginal("dirichlet", mu=a / s, sigma=a * (s - a) / (s * s * (s + 1.0)),
+                                      p=(a, float(first), lnc))
     return out
 
 

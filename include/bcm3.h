@@ -55,6 +55,12 @@ int bcm3_likelihood_cellpop_cells(bcm3_likelihood* ll, size_t item, int32_t* cou
                                   double* values, double* end_y);
 void bcm3_likelihood_destroy(bcm3_likelihood* ll);
 int bcm3_likelihood_num_variables(const bcm3_likelihood* ll);
+/* PriorIndependence::LoadFromXML (src/sampler/PriorIndependence.cpp:20-115) as the device sampler
+ * holds it: per variable the BCM3HIP_PRIOR_* kind, (p0, p1, p2), (lower, upper) bounds and the
+ * marginal (mean, variance) (Dirichlet groups: MultivariateMarginal.cpp:47-180). Fills up to
+ * max_vars entries (any array may be NULL); returns the number of variables or < 0. */
+int bcm3_prior_marginals(const char* prior_xml, int max_vars, int32_t* kind, double* params, double* bounds,
+                         double* moments);
 /* name of variable i (prior.xml order, repeat-expanded); returns the name length or < 0 */
 int bcm3_likelihood_variable_name(const bcm3_likelihood* ll, int i, char* buf, size_t buflen);
 /* VariableSet::TransformVariable code of variable i (0 none, 1 log, 2 log10, 3 logit) */

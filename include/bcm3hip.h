@@ -330,7 +330,13 @@ enum {
     BCM3HIP_PRIOR_BETA = 4,
     BCM3HIP_PRIOR_HALF_CAUCHY = 5,
     BCM3HIP_PRIOR_BETA_PRIME = 6,
-    BCM3HIP_PRIOR_EXPONENTIAL_MIX = 7
+    BCM3HIP_PRIOR_EXPONENTIAL_MIX = 7,
+    /* member of a Dirichlet group (MultivariateMarginal, src/sampler/MultivariateMarginal.cpp:23-180;
+     * PriorIndependence.cpp:40-77): p0 = alpha_i, p1 = index of the group's first variable, p2 =
+     * the group's log normalisation constant lgamma(sum alpha) - sum lgamma(alpha_i). Members are
+     * consecutive; the last one is the residual 1 - sum(others) the proposals overwrite
+     * (SamplerPTChain.cpp:270-278). Adaptive proposal kernels only. */
+    BCM3HIP_PRIOR_DIRICHLET = 8
 };
 /* prior_kind[d], prior_p0[d] (lower | mu), prior_p1[d] (upper | sigma), scale[d] random-walk sd,
  * temps[C], values[C*d] -> prop[C*d], lprior_prop[C]. T == 0 chains draw from the prior. */

@@ -220,9 +220,50 @@ def prior_sample(kind, p0, p1, p2, seed, it, gc, i):
     if kind == 6:
         x = _beta(p0, p1, s)
         return p2 * (x / (1.0 - x))
+    if kind == 8:  # Dirichlet member: Gamma(alpha, 1), divided by the group sum by the caller
+        return _gamma(p0, 1.0, s)
     p = s.uniform()
     lam = p0 if p < p2 else p1
     return -(1.0 / lam) * math.log1p(-s.uniform())
+
+
+def dirichlet_groups(kind, p1):
+    """[(first, last)] of the Dirichlet groups (kind 8, p1 = first index), in variable order."""
+    d = len(kind)
+    out = []
+    for f in range(d):
+        if kind[f] == 8 and int(p1[f]) == f:
+            last = f
+            while last + 1 < d and kind[last + 1] == 8 and int(p1[last + 1]) == f:
+                last += 1
+            out.append((f, last))
+    return out
+
+
+def dirichlet_logpdf(x, first, last, alpha, lnc):
+    """MultivariateMarginal::EvaluateLogPDF (MultivariateMarginal.cpp:86-118)."""
+    s = 0.0
+    for j in range(first, last + 1):
+        if x[j] < 0.0 or x[j] > 1.0:
+            return -math.inf
+        s += x[j]
+    if abs(s - 1.0) > 1e-15:
+        return -math.inf
+    lp = 0.0
+    for j in range(first, last + 1):
+        lp += (alpha[j] - 1) * math.log(x[j])
+    return lp + lnc
+
+
+def prior_total(kind, p0, p1, p2, x):
+    """PriorIndependence::EvaluateLogPDF (PriorIndependence.cpp:129-157): groups, then univariates."""
+    lp = 0.0
+    for f, last in dirichlet_groups(kind, p1):
+        lp += dirichlet_logpdf(x, f, last, p0, p2[f])
+    for i in range(len(kind)):
+        if kind[i] != 8:
+            lp += prior_logpdf(kind[i], p0[i], p1[i], x[i], p2[i])
+    return lp
 
 
 def propose(P, kind, p0, p1, temps, values, chain0, seed, it, p2=None):
@@ -238,9 +279,17 @@ def propose(P, kind, p0, p1, temps, values, chain0, seed, it, p2=None):
         gc = chain0 + c
         cur = [float(v) for v in values[c]]
         nxt = [0.0] * d
+        groups = dirichlet_groups(kind, p1)
         if temps[c] == 0.0:
             for i in range(d):
                 nxt[i] = prior_sample(kind[i], p0[i], p1[i], p2[i], seed, it, gc, i)
+            for f, last in groups:  # MultivariateMarginal::Sample
+                s = 0.0
+                for j in range(f, last + 1):
+                    s += nxt[j]
+                inv = 1.0 / s
+                for j in range(f, last + 1):
+                    nxt[j] *= inv
         else:
             gmm = P["kind"] == GAUSSIAN_MIXTURE
             K = int(P["ncomp"][c]) if gmm else 1
@@ -299,12 +348,14 @@ def propose(P, kind, p0, p1, temps, values, chain0, seed, it, p2=None):
                     fwd = logsum2(fwd, (base - 0.5 * dot(s1)) + math.log(rf[k]))
                     rev = logsum2(rev, (base - 0.5 * dot(s2)) + math.log(rr[k]))
                 lmh[c] = rev - fwd
+            for f, last in groups:  # Dirichlet residual (SamplerPTChain.cpp:270-278)
+                s = 0.0
+                for j in range(f, last):
+                    s += nxt[j]
+                nxt[last] = 1.0 - s
             P["selected"][c] = sel
         prop[c] = nxt
-        lp = 0.0
-        for i in range(d):
-            lp += prior_logpdf(kind[i], p0[i], p1[i], nxt[i], p2[i])
-        lprior[c] = lp
+        lprior[c] = prior_total(kind, p0, p1, p2, nxt)
     return prop, lprior, lmh
 
 

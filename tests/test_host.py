@@ -101,3 +101,68 @@ def test_repeat_and_transforms(tmp_path):
     ll = Likelihood(str(lik), str(prior), options="backend=none")
     assert ll.variable_names == ["a_0", "a_1", "a_2", "b"]
     assert ll.variable_transforms == [2, 2, 2, 3]
+
+
+DIRICHLET_PRIOR = """<?xml version="1.0" encoding="utf-8"?>
+<variableset>
+  <variable name="x" distribution="uniform" lower="-1.0" upper="2.0"/>
+  <variable name="w0" multivariate="true" id="1" distribution="dirichlet" alpha="2.0"/>
+  <variable name="w1" multivariate="true" id="1" distribution="dirichlet" alpha="3.0"/>
+  <variable name="w2" multivariate="true" id="1" distribution="dirichlet" alpha="4.5"/>
+  <variable name="y" distribution="normal" mu="0.5" sigma="2.0"/>
+  <variable name="v0" multivariate="true" id="2" distribution="dirichlet" alpha="0.5"/>
+  <variable name="v1" multivariate="true" id="2" distribution="dirichlet" alpha="1.5"/>
+</variableset>
+"""
+
+
+def _host_prior(path, d_max=16):
+    import ctypes as C
+    from bcm3_amd.likelihood import lib
+    L = lib()
+    L.bcm3_prior_marginals.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    kind = np.zeros(d_max, dtype=np.int32)
+    par, bnd, mom = np.zeros((d_max, 3)), np.zeros((d_max, 2)), np.zeros((d_max, 2))
+    d = L.bcm3_prior_marginals(str(path).encode(), d_max, kind.ctypes.data, par.ctypes.data, bnd.ctypes.data,
+                               mom.ctypes.data)
+    return d, kind[:max(d, 0)], par[:max(d, 0)], bnd[:max(d, 0)], mom[:max(d, 0)]
+
+
+def test_dirichlet_prior_host_parse(tmp_path):
+    """PriorIndependence's multivariate groups (PriorIndependence.cpp:20-115, MultivariateMarginal.cpp):
+    libbcm3's parse equals the Python one the GPU tests restate, with the reference's moments, bounds
+    and log normalisation constant lgamma(sum a) - sum lgamma(a_i)"""
+    import math
+    from bcm3_amd.sampler import PRIOR_KINDS, load_prior
+    p = tmp_path / "prior.xml"
+    p.write_text(DIRICHLET_PRIOR)
+    d, kind, par, bnd, mom = _host_prior(p)
+    assert d == 7 and kind.tolist() == [0, 8, 8, 8, 1, 8, 8]
+    py = load_prior(str(p))
+    for i, m in enumerate(py):
+        assert PRIOR_KINDS[m.kind] == kind[i]
+        # (p2 of a Dirichlet member is lgamma-based: glibc's lgamma here, CPython's own in load_prior)
+        np.testing.assert_allclose(par[i], m.p, rtol=4e-16, atol=0)
+        assert tuple(bnd[i]) == m.bounds() and tuple(mom[i]) == m.moments()
+    a = [2.0, 3.0, 4.5]
+    lnc = math.lgamma(sum(a)) - sum(math.lgamma(x) for x in a)
+    assert par[1, 2] == par[3, 2] and abs(par[1, 2] - lnc) < 1e-13
+    assert par[5, 1] == 5.0 and par[6, 1] == 5.0 and tuple(bnd[6]) == (0.0, 1.0)
+    s = sum(a)
+    assert abs(mom[2, 0] - 3.0 / s) < 1e-16 and abs(mom[2, 1] - 3.0 * (s - 3.0) / (s * s * (s + 1))) < 1e-16
+
+
+@pytest.mark.parametrize("body,msg", [
+    ('<variable name="w0" multivariate="true" id="1" distribution="dirichlet" alpha="2"/>'
+     '<variable name="x" distribution="uniform" lower="0" upper="1"/>'
+     '<variable name="w1" multivariate="true" id="1" distribution="dirichlet" alpha="2"/>', "follow each other"),
+    ('<variable name="w0" multivariate="true" id="1" distribution="wishart" alpha="2"/>', "only dirichlet"),
+    ('<variable name="w0" multivariate="true" id="0" distribution="dirichlet" alpha="2"/>', "start at 1"),
+    ('<variable name="w0" multivariate="true" id="1" repeat="2" distribution="dirichlet" alpha="2"/>', "repeat"),
+])
+def test_dirichlet_prior_errors(tmp_path, body, msg):
+    from bcm3_amd.likelihood import lib
+    p = tmp_path / "prior.xml"
+    p.write_text(f'<?xml version="1.0"?>\n<variableset>{body}</variableset>\n')
+    d = _host_prior(p)[0]
+    assert d < 0 and msg in lib().bcm3_last_error().decode()

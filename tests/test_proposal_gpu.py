@@ -298,3 +298,85 @@ def test_circular_ridge_adapts_to_a_mixture():
     assert (loop.proposal.selected.cpu().numpy() >= -1).all()
     acc = int(loop.accepted_mutate.item()) / loop.attempted_mutate
     assert 0.05 < acc < 0.9
+
+
+DIRICHLET_PRIOR = """<?xml version="1.0" encoding="utf-8"?>
+<variableset>
+  <variable name="x" distribution="uniform" lower="-1.0" upper="2.0"/>
+  <variable name="w0" multivariate="true" id="1" distribution="dirichlet" alpha="2.0"/>
+  <variable name="w1" multivariate="true" id="1" distribution="dirichlet" alpha="3.0"/>
+  <variable name="w2" multivariate="true" id="1" distribution="dirichlet" alpha="4.5"/>
+  <variable name="y" distribution="normal" mu="0.5" sigma="2.0"/>
+</variableset>
+"""
+
+
+def _dirichlet_prior(tmp_path):
+    from bcm3_amd.sampler import DevicePrior, load_prior
+    path = tmp_path / "dirichlet_prior.xml"
+    path.write_text(DIRICHLET_PRIOR)
+    return str(path), DevicePrior(load_prior(str(path)), "cuda")
+
+
+@pytest.mark.parametrize("K", [1, 2])
+def test_dirichlet_prior_propose(tmp_path, K):
+    """A 3-component Dirichlet prior (MultivariateMarginal, PriorIndependence.cpp:40-77): T = 0 draws
+    (Gamma draws over their sum), the residual fix-up of T > 0 proposals after the MH ratio of the
+    unmodified proposal (SamplerPTChain.cpp:270-278) and the group-first prior density
+    (PriorIndependence.cpp:129-157) of the kernels against the restatement, over several iterations"""
+    _, prior = _dirichlet_prior(tmp_path)
+    assert prior.kind_codes.tolist() == [0, 8, 8, 8, 1]
+    assert prior.p1.cpu().numpy()[1:4].tolist() == [1.0, 1.0, 1.0]
+    _check_propose("gaussian_mixture", K, 0.0, its=(0, 9, 2**40), prior_xml=prior, C=40)
+
+
+def test_dirichlet_prior_draws(tmp_path):
+    from bcm3_amd import _hip
+    from bcm3_amd.proposal import DeviceProposal
+    _, prior = _dirichlet_prior(tmp_path)
+    C, d = 4000, prior.d
+    temps = torch.zeros(C, dtype=torch.float64, device="cuda")
+    Q = DeviceProposal("global_covariance", prior, temps)
+    vals = torch.zeros((C, d), dtype=torch.float64, device="cuda")
+    prop = torch.empty_like(vals)
+    lp = torch.empty(C, dtype=torch.float64, device="cuda")
+    lmh = torch.empty(C, dtype=torch.float64, device="cuda")
+    _hip.ptmh_propose_adaptive(C, d, prior.kind_codes.data_ptr(), prior.p0.data_ptr(), prior.p1.data_ptr(),
+                               prior.p2.data_ptr(), temps.data_ptr(), vals.data_ptr(), prop.data_ptr(), lp.data_ptr(),
+                               lmh.data_ptr(), Q.struct, 0, 5, 1)
+    torch.cuda.synchronize()
+    x = prop.cpu().numpy()
+    w = x[:, 1:4]
+    assert np.all((w >= 0) & (w <= 1)) and np.all(np.abs(w.sum(axis=1) - 1.0) <= 1e-15)
+    assert np.all(np.isfinite(lp.cpu().numpy()))
+    a = np.array([2.0, 3.0, 4.5])
+    mean, var = a / a.sum(), a * (a.sum() - a) / (a.sum() ** 2 * (a.sum() + 1))
+    assert np.all(np.abs(w.mean(axis=0) - mean) < 5 * np.sqrt(var / C))
+    np.testing.assert_allclose(prior.mean.cpu().numpy()[1:4], mean, rtol=1e-15)
+    np.testing.assert_allclose(prior.var.cpu().numpy()[1:4], var, rtol=1e-15)
+
+
+def test_sampler_runs_with_dirichlet_prior(tmp_path):
+    """The C++ sampler (bcm3_ptmh_*) on a banana likelihood over a prior with a Dirichlet group: every
+    chain's group stays on the simplex (sum 1 within the reference's 1e-15), and each chain's log prior
+    equals the restated PriorIndependence density of its values"""
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.ptmh import PTMHNative
+    prior_xml, prior = _dirichlet_prior(tmp_path)
+    lik = tmp_path / "banana5.xml"
+    lik.write_text('<bcm_likelihood type="banana" dimension="5" sd1="2.0" sd2="1.0"></bcm_likelihood>\n')
+    ll = Likelihood(str(lik), prior_xml, device=0)
+    s = PTMHNative(ll, prior_xml, 16, seed=4, adapt_proposal_samples=30, adapt_proposal_times=1)
+    s.iterate(80)
+    s.synchronize()
+    st = s.state()
+    c = s.counters()
+    s.close()
+    assert c["accepted_mutate"] > 16 and c["adaptations_done"] == 1
+    w = st["values"][:, 1:4]
+    assert np.all((w >= 0) & (w <= 1)) and np.all(np.abs(w.sum(axis=1) - 1.0) <= 1e-15)
+    kd, p0, p1, p2 = (t.cpu().numpy() for t in _prior_arrays(prior))
+    for i in range(len(w)):
+        ref = R.prior_total(kd, p0, p1, p2, [float(v) for v in st["values"][i]])
+        assert abs(st["lprior"][i] - ref) <= 1e-12 * (1 + abs(ref)), (i, st["lprior"][i], ref)
+    ll.close()

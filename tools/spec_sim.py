@@ -1,0 +1,77 @@
+"""Speculative evaluation, measured before it is built (VERDICT r02 "Next round" 5).
+
+The C3 launch holds 256 trajectories on 1,024 SIMDs and lasts as long as the slowest of them. If
+iteration r's launch also evaluated every proposal iteration r+1 can make -- for each chain, one per
+outcome of its own accept at r and of its exchange partner's (the state after exchange r+1 is one of
+old_i, prop_i, old_p, prop_p: 4 candidates, T = 0 chains 1) -- the accept of r+1 would need no launch
+of its own: two iterations per launch. Counter-based random numbers make the candidates' proposals
+exactly the ones the sequential sampler would make, so only committed evaluations count.
+
+This script measures the kernel time of one launch of n = k x 256 realistic C3 proposals (chain
+states of a running C++ sampler over consecutive iterations) for k = 1..8, with one trajectory per
+wavefront (lanes_per_wave 1) and with the library's automatic choice, and prints the committed
+evals/s that a 1 + 4 speculative launch would give against the plain loop.
+
+    python tools/spec_sim.py [iterations_warmup]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from bcm3_amd import _hip  # noqa: E402
+from bcm3_amd.likelihood import Likelihood  # noqa: E402
+from bcm3_amd.ptmh import PTMHNative  # noqa: E402
+
+G = os.path.join(ROOT, "tests", "golden")
+LIK, PRI = os.path.join(G, "c3_likelihood.xml"), os.path.join(G, "c3_prior.xml")
+
+
+def kernel_ms(ll, x, lpw, reps=5):
+    n = len(x)
+    xd = torch.tensor(x, dtype=torch.float64, device="cuda")
+    out = torch.empty(n, dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    ll.set_option(_hip.OPT_LANES_PER_WAVE, lpw)
+    ll.evaluate_batch_device(n, xd.data_ptr(), out.data_ptr(), None, stream)
+    torch.cuda.synchronize()
+    best = []
+    for _ in range(reps):
+        ll.set_option(_hip.OPT_TIMING_LOG, 1)
+        ll.evaluate_batch_device(n, xd.data_ptr(), out.data_ptr(), None, stream)
+        torch.cuda.synchronize()
+        tt, nl, _ = ll.kernel_time_log()
+        ll.set_option(_hip.OPT_TIMING_LOG, 0)
+        best.append(tt / nl)
+    return float(np.median(best))
+
+
+def main():
+    warm = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+    ll = Likelihood(LIK, PRI, device=0)
+    s = PTMHNative(ll, PRI, 256, seed=20251016, proposal="gaussian_mixture")
+    s.iterate(warm)
+    states = []
+    for _ in range(8):
+        s.iterate(1)
+        states.append(s.state()["values"].copy())
+    s.close()
+    res = {}
+    for k in range(1, 9):
+        x = np.concatenate(states[:k])
+        res[k] = {lpw: kernel_ms(ll, x, lpw) for lpw in (1, 0)}
+        print(f"n={256 * k:5d}  lpw=1 {res[k][1]:.3f} ms   auto {res[k][0]:.3f} ms", flush=True)
+    base = res[1][1]
+    for k, label in ((5, "1 + 4 candidates"), (7, "1 + 6 candidates")):
+        t = min(res[k].values())
+        print(f"{label}: launch {t:.3f} ms for 2 committed iterations vs 2 x {base:.3f} ms -> "
+              f"{2 * base / t:.2f}x committed evals/s (kernel time only)")
+    ll.close()
+
+
+if __name__ == "__main__":
+    main()
