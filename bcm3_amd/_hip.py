@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("BCM3HIP_LIB") or os.path.join(_HERE, "lib", "libbcm3h
 
 PK_TYPES = {"one": 0, "two": 1, "one_biphasic": 2, "two_biphasic": 3, "one_transit": 4, "two_transit": 5}
 ANALYTIC_BANANA, ANALYTIC_CIRCULAR = 1, 2
-OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES, OPT_TIMING_LOG, OPT_UNI_SOLVER = 1, 2, 3, 4
+OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES, OPT_TIMING_LOG, OPT_UNI_SOLVER, OPT_BLOCK_LDS = 1, 2, 3, 4, 5
 PRIOR_UNIFORM, PRIOR_NORMAL = 0, 1
 PROPOSAL_GLOBAL_COVARIANCE, PROPOSAL_GAUSSIAN_MIXTURE = 0, 1
 PROPOSAL_KMAX = 16

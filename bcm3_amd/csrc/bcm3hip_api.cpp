@@ -76,6 +76,7 @@ struct bcm3hip_ctx {
     int lanes_per_wave = 0;  // 0 = auto (auto_lanes_per_wave)
     int uni_solver = 0;      // BCM3HIP_OPT_UNI_SOLVER
     int block_waves = 1;
+    int block_lds = 0;  // BCM3HIP_OPT_BLOCK_LDS
 };
 
 #define HIPCHK(x)                                                                                          \
@@ -473,6 +474,10 @@ int bcm3hip_set_option(bcm3hip_ctx* c, int option, int64_t value)
         if (value != 0 && value != 1) return BCM3HIP_ERR_ARG;
         c->uni_solver = (int)value;
         return 0;
+    case BCM3HIP_OPT_BLOCK_LDS:
+        if (value < 0 || value > 65536) return BCM3HIP_ERR_ARG;
+        c->block_lds = (int)value;
+        return 0;
     default: return BCM3HIP_ERR_ARG;
     }
 }
@@ -525,7 +530,7 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
         if (r) return r;
         e = launch_popk(c->pm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, dtraj, dstats,
                         c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
-                        c->block_waves, c->uni_solver, s, e0, e1);
+                        c->block_waves, c->uni_solver, s, e0, e1, c->block_lds);
     } else if (c->kind == 3) {
         const size_t per_eval = (size_t)c->xm.n_jobs * (size_t)(c->xm.n * c->xm.n);
         const size_t chunk = per_eval == 0 ? n : std::max<size_t>(1, kExpmScratchBytes / (per_eval * sizeof(double)));

@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(256) popk_reduce_kernel(int64_t n, int P, cons
 hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
                        double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
                        bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, int uni_solver,
-                       hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop)
+                       hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop, int block_lds)
 {
     const int64_t ntraj = n * (int64_t)m.P;
     if (ntraj == 0) return hipSuccess;
@@ -597,16 +597,16 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
     if (ev_start) hipEventRecord(ev_start, stream);
 #define LAUNCH(PKT)                                                                                           \
     if (vec_state && !stats_out)                                                                              \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, false>), grid, block, 0, stream, m, ntraj, lpw,     \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, false>), grid, block, block_lds, stream, m, ntraj, lpw,     \
                            values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr);   \
     else if (vec_state)                                                                                       \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, true>), grid, block, 0, stream, m, ntraj, lpw,      \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, true>), grid, block, block_lds, stream, m, ntraj, lpw,      \
                            values, logp_direct, patient_llh_scratch, tstat, traj_out, stats_out); \
     else if (uni)                                                                                             \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_UNI, true>), grid, block, 0, stream, m, ntraj, lpw, values, \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_UNI, true>), grid, block, block_lds, stream, m, ntraj, lpw, values, \
                            logp_direct, patient_llh_scratch, tstat, traj_out, stats_out);         \
     else                                                                                                      \
-        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_LANES, true>), grid, block, 0, stream, m, ntraj, lpw, values,  \
+        hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_LANES, true>), grid, block, block_lds, stream, m, ntraj, lpw, values,  \
                            logp_direct, patient_llh_scratch, tstat, traj_out, stats_out)
     switch (m.pk_type) {
     case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;

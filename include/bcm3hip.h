@@ -257,9 +257,13 @@ enum {
     BCM3HIP_OPT_LANES_PER_WAVE = 1, /* trajectories per wavefront: 1..64, 0 = auto (default) */
     BCM3HIP_OPT_BLOCK_WAVES = 2,    /* wavefronts per workgroup: 1..4 (default 1) */
     BCM3HIP_OPT_TIMING_LOG = 3,     /* 1: keep one HIP event pair per launch (see kernel_time_log) */
-    BCM3HIP_OPT_UNI_SOLVER = 4      /* one-trajectory-per-wavefront launches: 0 = state vectors across
+    BCM3HIP_OPT_UNI_SOLVER = 4,     /* one-trajectory-per-wavefront launches: 0 = state vectors across
                                        lanes (bdf_vec.h, default), 1 = scalar state (bdf_uni.h);
                                        same results */
+    BCM3HIP_OPT_BLOCK_LDS = 5       /* bytes of LDS reserved per workgroup of the PopPK launch (0..65536,
+                                       default 0): caps the workgroups resident per CU, so a launch
+                                       with more wavefronts than SIMDs queues the rest instead of
+                                       sharing a SIMD (see bcm3hip_eval_batch_device_ordered) */
 };
 
 int bcm3hip_device_count(void);

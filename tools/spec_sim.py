@@ -65,6 +65,25 @@ def main():
         x = np.concatenate(states[:k])
         res[k] = {lpw: kernel_ms(ll, x, lpw) for lpw in (1, 0)}
         print(f"n={256 * k:5d}  lpw=1 {res[k][1]:.3f} ms   auto {res[k][0]:.3f} ms", flush=True)
+    # launch order and residency: one wavefront per SIMD (LDS reservation: 4 one-wave workgroups per
+    # CU), trajectories dispatched longest first (predicted by their own step counts here, by the
+    # step count of the state they start from in the sampler) -- the workgroups beyond 1,024 wait
+    # for the first SIMDs to free up instead of sharing one
+    ctx = _hip.Context.from_popk_model(ll.popk_model(), 0)
+    for k in (4, 5, 6, 7, 8):
+        x = np.concatenate(states[:k])
+        nst = ctx.eval(x, detail=True)["stats"]["nst"].reshape(len(x), -1).sum(axis=1)
+        order = np.argsort(-nst, kind="stable")
+        xs = np.ascontiguousarray(x[order])
+        row = []
+        for lds in (0, 40960):
+            ll.set_option(_hip.OPT_BLOCK_LDS, lds)
+            row.append((lds, kernel_ms(ll, x, 1), kernel_ms(ll, xs, 1)))
+        ll.set_option(_hip.OPT_BLOCK_LDS, 0)
+        print(f"n={256 * k:5d} steps max {nst.max()} mean {nst.mean():.0f}: " +
+              "; ".join(f"lds {l}: as is {a:.3f} ms, longest first {b:.3f} ms" for l, a, b in row), flush=True)
+        res[k]["ordered"] = min(b for _, _, b in row)
+    ctx.close()
     base = res[1][1]
     for k, label in ((5, "1 + 4 candidates"), (7, "1 + 6 candidates")):
         t = min(res[k].values())
