@@ -508,8 +508,10 @@ static int auto_lanes_per_wave(size_t ntraj)
 static const size_t kExpmScratchBytes = (size_t)1 << 30;
 
 static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp, int32_t* dstatus,
-                  double* dtraj, bcm3hip_traj_stats* dstats, hipStream_t s)
+                  double* dtraj, bcm3hip_traj_stats* dstats, hipStream_t s, const int32_t* n_dev = nullptr,
+                  int32_t* dsteps = nullptr)
 {
+    if ((n_dev || dsteps) && c->kind != 1) return BCM3HIP_ERR_ARG;  // PopPK launches only
     hipError_t e;
     if (c->scratch_used && c->scratch_stream != s) HIPCHK(hipStreamWaitEvent(s, c->scratch_ev, 0));
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
@@ -530,7 +532,7 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
         if (r) return r;
         e = launch_popk(c->pm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, dtraj, dstats,
                         c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
-                        c->block_waves, c->uni_solver, s, e0, e1, c->block_lds);
+                        c->block_waves, c->uni_solver, s, e0, e1, c->block_lds, n_dev, dsteps);
     } else if (c->kind == 3) {
         const size_t per_eval = (size_t)c->xm.n_jobs * (size_t)(c->xm.n * c->xm.n);
         const size_t chunk = per_eval == 0 ? n : std::max<size_t>(1, kExpmScratchBytes / (per_eval * sizeof(double)));
@@ -582,6 +584,15 @@ int bcm3hip_eval_batch_device(bcm3hip_ctx* c, size_t n, const double* values_dev
     HIPCHK(hipSetDevice(c->device));
     // the caller's stream as given (NULL = the null/default stream, e.g. torch's default stream)
     return launch(c, n, values_dev, logp_dev, status_dev, nullptr, nullptr, (hipStream_t)stream);
+}
+
+int bcm3hip_eval_batch_device_counted(bcm3hip_ctx* c, size_t n_max, const int32_t* n_dev, const double* values_dev,
+                                      double* logp_dev, int32_t* status_dev, int32_t* steps_dev, void* stream)
+{
+    if (!c || !n_dev || (n_max > 0 && (!values_dev || !logp_dev))) return BCM3HIP_ERR_ARG;
+    if (c->kind != 1) return BCM3HIP_ERR_ARG;
+    HIPCHK(hipSetDevice(c->device));
+    return launch(c, n_max, values_dev, logp_dev, status_dev, nullptr, nullptr, (hipStream_t)stream, n_dev, steps_dev);
 }
 
 int bcm3hip_last_kernel_ms(bcm3hip_ctx* c, float* ms)

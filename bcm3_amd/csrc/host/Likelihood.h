@@ -43,6 +43,16 @@ public:
     //! Device-resident batch on a HIP stream (void* hipStream_t); false if unsupported.
     virtual bool EvaluateLogProbabilityBatchDevice(size_t n, const Real* values_dev, Real* logp_dev,
                                                    int32_t* status_dev, void* stream);
+    //! Device-resident batch whose size *n_dev (<= n_max) is a device value, with the solver steps
+    //! of each item in steps_dev (may be null): the speculative iteration pairs of SamplerPTDevice.
+    //! False if unsupported (only latency-bound likelihoods -- the PopPK BDF kernel -- provide it).
+    virtual bool EvaluateLogProbabilityBatchDeviceCounted(size_t n_max, const int32_t* n_dev, const Real* values_dev,
+                                                          Real* logp_dev, int32_t* status_dev, int32_t* steps_dev,
+                                                          void* stream)
+    {
+        return false;
+    }
+    virtual bool SupportsCountedBatch() const { return false; }
     //! Duration of the last kernel launch (HIP events), < 0 if unknown.
     virtual float LastKernelMilliseconds() { return -1.0f; }
     //! Summed / max kernel time and launch count since the last call (BCM3HIP_OPT_TIMING_LOG).

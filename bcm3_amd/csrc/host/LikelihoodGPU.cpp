@@ -120,6 +120,20 @@ bool LikelihoodGPUBase::EvaluateLogProbabilityBatchDevice(size_t n, const Real* 
     return true;
 }
 
+bool LikelihoodGPUBase::EvaluateLogProbabilityBatchDeviceCounted(size_t n_max, const int32_t* n_dev,
+                                                                 const Real* values_dev, Real* logp_dev,
+                                                                 int32_t* status_dev, int32_t* steps_dev, void* stream)
+{
+    if (!SupportsCountedBatch() || !CheckEvaluable() || !ctx) return false;
+    std::lock_guard<std::mutex> lock(mutex);
+    int r = bcm3hip_eval_batch_device_counted(ctx, n_max, n_dev, values_dev, logp_dev, status_dev, steps_dev, stream);
+    if (r != 0) {
+        LOGERROR("GPU likelihood evaluation failed: %s", bcm3hip_error_string(r));
+        return false;
+    }
+    return true;
+}
+
 float LikelihoodGPUBase::LastKernelMilliseconds()
 {
     float ms = -1.0f;

@@ -33,6 +33,9 @@ public:
     bool EvaluateLogProbabilityBatch(size_t n, const Real* values, Real* logp, int32_t* status) override;
     bool EvaluateLogProbabilityBatchDevice(size_t n, const Real* values_dev, Real* logp_dev, int32_t* status_dev,
                                            void* stream) override;
+    bool EvaluateLogProbabilityBatchDeviceCounted(size_t n_max, const int32_t* n_dev, const Real* values_dev,
+                                                  Real* logp_dev, int32_t* status_dev, int32_t* steps_dev,
+                                                  void* stream) override;
     float LastKernelMilliseconds() override;
     bool KernelTimeLog(double& total_ms, int64_t& launches, double& max_ms) override;
     bool SetBackendOption(int option, int64_t value) override;
@@ -63,6 +66,7 @@ public:
     bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
                     const OptionsMap& vm) override;
     bool PostInitialize() override { return true; }
+    bool SupportsCountedBatch() const override { return ctx != nullptr; }
 
     size_t GetNumPatients() const { return patient_ids.size(); }
     const std::vector<Real>& GetTimepoints() const { return time; }
@@ -104,6 +108,7 @@ public:
     bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
                     const OptionsMap& vm) override;
     bool PostInitialize() override { return true; }
+    bool SupportsCountedBatch() const override { return ctx != nullptr; }
     const std::string& GetPatientID() const { return patient_id; }
     const bcm3hip_popk_model& GetDeviceModel() const { return model; }
 

@@ -263,6 +263,17 @@ struct SamplerPTDevice::Impl {
     PTMHCounters cnt;
     int64_t iter = 0, round = 0;
 
+    // speculative iteration pairs (bcm3hip_ptmh_spec_*): candidate / batch buffers, per round parity
+    // the exchange partner and the first chain of each chain's pair, accept flags of both moves
+    bool spec_on = false;
+    DevBuf<double> sp_cand_x, sp_cand_lp, sp_cand_lmh, sp_cand_llh, sp_cand_sc, sp_batch_x, sp_batch_llh;
+    DevBuf<int32_t> sp_cand_sel, sp_cand_upd, sp_cand_steps, sp_steps_hint, sp_steps_prop, sp_batch_status,
+        sp_batch_steps, sp_batch_src, sp_batch_n, sp_err;
+    DevBuf<uint8_t> sp_cand_active, acc_mut, acc_exc;
+    DevBuf<int32_t> partner[2], pair_first[2];
+    bcm3hip_spec S{};
+    int64_t spec_pairs = 0;
+
     // sample output: [flush][values C*d | lprior C | llh C] staged on the device
     std::unique_ptr<SampleFileWriter> out;
     DevBuf<double> out_buf;
@@ -483,7 +494,7 @@ struct SamplerPTDevice::Impl {
                       "pt_cross_accept");
     }
 
-    bool Exchange()
+    bool Exchange(uint8_t* acc_mask = nullptr)
     {
         // DoExchangeMove (SamplerPT.cpp:277-298): pairs inside the slice on the GPU, the two
         // slice-boundary pairs over the transport (sampler.sharded_exchange_round)
@@ -491,7 +502,7 @@ struct SamplerPTDevice::Impl {
         const int start = (int)(round % 2);
         const bool wrap_local = cfg.world == 1 && (Ctot - 1 - start) % 2 == 0;
         if (!Launch(bcm3hip_pt_exchange_local((int)C, d, g0, start, wrap_local ? 1 : 0, temps.p, values.p, llh.p,
-                                              lprior.p, lpp.p, nullptr, acc_exchange.p, cfg.seed, (uint64_t)round,
+                                              lprior.p, lpp.p, acc_mask, acc_exchange.p, cfg.seed, (uint64_t)round,
                                               stream),
                     "pt_exchange_local"))
             return false;
@@ -563,16 +574,163 @@ struct SamplerPTDevice::Impl {
         } else {
             ok = Mutate();
         }
-        if (!ok) return false;
+        return ok && PostIteration(last);
+    }
+
+    // does the end of iteration si (0-based sample index) adapt the proposals (SamplerPT.cpp:229-248)
+    bool AdaptDue(int64_t si, bool last) const
+    {
+        if (!adaptive || (si + 1) % cfg.use_every_nth != 0) return false;
+        const int64_t sample_ix = si / cfg.use_every_nth;
+        return cfg.adapt_proposal_samples > 0 && (sample_ix + 1) % cfg.adapt_proposal_samples == 0 && !last &&
+               cnt.adaptations_done < cfg.adapt_proposal_times;
+    }
+
+    // the end of SamplerPT::Run's loop body: sample emission, proposal adaptation when due
+    bool PostIteration(bool last)
+    {
         const int64_t si = cnt.samples_done++;
         cnt.iterations++;
         if ((si + 1) % cfg.use_every_nth == 0 && !Emit()) return false;
-        if (adaptive && (si + 1) % cfg.use_every_nth == 0) {
-            const int64_t sample_ix = si / cfg.use_every_nth;
-            if (cfg.adapt_proposal_samples > 0 && (sample_ix + 1) % cfg.adapt_proposal_samples == 0 && !last &&
-                cnt.adaptations_done < cfg.adapt_proposal_times)
-                return Adapt();
+        if (AdaptDue(si, last)) return Adapt();
+        return true;
+    }
+
+    // can the next two iterations run as a speculative pair (the first must not adapt: the second's
+    // proposals are made before it ends)
+    bool PairPossible() const { return spec_on && !AdaptDue(cnt.samples_done, false); }
+
+    // Two DeterministicEvenOdd iterations r, r+1 with ONE likelihood launch (include/bcm3hip.h
+    // "speculative iteration pairs"): exchange r, propose r, the candidates of r+1 (every state
+    // exchange r+1 can leave in each slot), one launch over r's proposals and the candidates, accept
+    // r; exchange r+1, select the candidate that happened, accept r+1. The same kernels' arithmetic
+    // on the same counter-based random numbers as two IterationOnce calls.
+    bool IterationPair(bool last)
+    {
+        if (!Exchange()) return false;
+        const int nxt = (int)(round % 2);  // start parity of exchange round r + 1
+        if (!Launch(bcm3hip_ptmh_propose_adaptive((int)C, d, pkind.p, p0.p, p1.p, p2.p, temps.p, values.p, prop.p,
+                                                  lprior_prop.p, log_mh.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
+                    "ptmh_propose_adaptive") ||
+            !Launch(bcm3hip_ptmh_spec_candidates((int)C, d, pkind.p, p0.p, p1.p, p2.p, temps.p, values.p, prop.p,
+                                                 partner[nxt].p, &P, &S, g0, cfg.seed, (uint64_t)iter + 1, stream),
+                    "ptmh_spec_candidates") ||
+            !Launch(bcm3hip_ptmh_spec_batch((int)C, d, prop.p, partner[nxt].p, &S, stream), "ptmh_spec_batch"))
+            return false;
+        if (!ll->EvaluateLogProbabilityBatchDeviceCounted((size_t)C * (1 + BCM3HIP_SPEC_SLOTS), S.batch_n, S.batch_x,
+                                                          S.batch_llh, S.batch_status, S.batch_steps, stream)) {
+            LOGERROR("EvaluateLogProbabilityBatchDeviceCounted failed");
+            return false;
         }
+        if (!Launch(bcm3hip_ptmh_spec_scatter((int)C, &S, llh_prop.p, stream), "ptmh_spec_scatter") ||
+            !Launch(bcm3hip_ptmh_accept_adaptive((int)C, d, temps.p, prop.p, lprior_prop.p, llh_prop.p, log_mh.p,
+                                                 cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, acc_mut.p,
+                                                 acc_mutate.p, nan_flag.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
+                    "ptmh_accept_adaptive") ||
+            !HistoryAdd(nullptr))
+            return false;
+        cnt.attempted_mutate += C;
+        iter++;
+        if (!PostIteration(false)) return false;
+        // iteration r + 1
+        if (!Exchange(acc_exc.p)) return false;
+        if (!Launch(bcm3hip_ptmh_spec_select((int)C, d, temps.p, partner[nxt].p, pair_first[nxt].p, acc_mut.p,
+                                             acc_exc.p, &S, prop.p, lprior_prop.p, log_mh.p, llh_prop.p, &P, sp_err.p,
+                                             stream),
+                    "ptmh_spec_select") ||
+            !Launch(bcm3hip_ptmh_accept_adaptive((int)C, d, temps.p, prop.p, lprior_prop.p, llh_prop.p, log_mh.p,
+                                                 cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, nullptr,
+                                                 acc_mutate.p, nan_flag.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
+                    "ptmh_accept_adaptive") ||
+            !HistoryAdd(nullptr))
+            return false;
+        cnt.attempted_mutate += C;
+        iter++;
+        spec_pairs++;
+        return PostIteration(last);
+    }
+
+    // n iterations: speculative pairs where possible, single iterations otherwise
+    bool Iterations(int64_t n, bool last_at_end, int64_t nan_every)
+    {
+        int64_t since_check = 0;
+        for (int64_t i = 0; i < n;) {
+            int64_t k;
+            if (i + 2 <= n && PairPossible()) {
+                if (!IterationPair(last_at_end && i + 2 == n)) return false;
+                k = 2;
+            } else {
+                if (!IterationOnce(last_at_end && i + 1 == n)) return false;
+                k = 1;
+            }
+            i += k;
+            since_check += k;
+            if (nan_every > 0 && since_check >= nan_every) {
+                since_check = 0;
+                if (!CheckNaN()) return false;
+            }
+        }
+        return true;
+    }
+
+    bool SetupSpeculation()
+    {
+        spec_on = cfg.speculate != 0 && adaptive && cfg.world == 1 && cfg.swapping_scheme == 0 &&
+                  cfg.exploration_steps == 1 && Ctot >= 2 && d <= 64 && C * (1 + BCM3HIP_SPEC_SLOTS) <= 4096 &&
+                  ll->SupportsCountedBatch();
+        if (!spec_on) return true;
+        const int64_t K = BCM3HIP_SPEC_SLOTS, N = C * (1 + K);
+        bool ok = sp_cand_x.alloc(C * K * d) && sp_cand_lp.alloc(C * K) && sp_cand_lmh.alloc(C * K) &&
+                  sp_cand_llh.alloc(C * K) && sp_cand_sc.alloc(C * K) && sp_cand_sel.alloc(C * K) &&
+                  sp_cand_upd.alloc(C * K) && sp_cand_steps.alloc(C * K) && sp_cand_active.alloc(C * K) &&
+                  sp_steps_hint.alloc(C) && sp_steps_prop.alloc(C) && sp_batch_x.alloc(N * d) &&
+                  sp_batch_llh.alloc(N) && sp_batch_status.alloc(N) && sp_batch_steps.alloc(N) &&
+                  sp_batch_src.alloc(N) && sp_batch_n.alloc(1) && sp_err.alloc(1) && acc_mut.alloc(C) &&
+                  acc_exc.alloc(C);
+        for (int st = 0; st < 2 && ok; st++) ok = partner[st].alloc(C) && pair_first[st].alloc(C);
+        if (!ok) {
+            LOGERROR("SamplerPTDevice: speculative buffers could not be allocated");
+            return false;
+        }
+        // exchange pairs of a round with start parity st (pt_exchange_kernel: first chains i with
+        // (g0 + i - st) even, i + 1 < C, then the wrap pair (C-1, 0) on one rank)
+        for (int st = 0; st < 2; st++) {
+            std::vector<int32_t> pa(C, -1), pf(C, -1);
+            const int par = (int)(((g0 - st) % 2 + 2) % 2);
+            for (int64_t i = par; i + 1 < C; i += 2) {
+                pa[i] = (int32_t)(i + 1);
+                pa[i + 1] = (int32_t)i;
+                pf[i] = pf[i + 1] = (int32_t)i;
+            }
+            if (cfg.world == 1 && (Ctot - 1 - st) % 2 == 0) {
+                pa[C - 1] = 0;
+                pa[0] = (int32_t)(C - 1);
+                pf[C - 1] = pf[0] = (int32_t)(C - 1);
+            }
+            if (!Upload(partner[st], pa, stream) || !Upload(pair_first[st], pf, stream)) return false;
+        }
+        if (bcm3hip_memset_async(sp_steps_hint.p, 0, C * sizeof(int32_t), stream) != 0 ||
+            bcm3hip_memset_async(sp_batch_steps.p, 0, N * sizeof(int32_t), stream) != 0 ||
+            bcm3hip_memset_async(sp_cand_steps.p, 0, C * K * sizeof(int32_t), stream) != 0 ||
+            bcm3hip_memset_async(sp_err.p, 0, sizeof(int32_t), stream) != 0)
+            return false;
+        S.cand_x = sp_cand_x.p;
+        S.cand_lp = sp_cand_lp.p;
+        S.cand_lmh = sp_cand_lmh.p;
+        S.cand_llh = sp_cand_llh.p;
+        S.cand_sel = sp_cand_sel.p;
+        S.cand_upd = sp_cand_upd.p;
+        S.cand_sc = sp_cand_sc.p;
+        S.cand_active = sp_cand_active.p;
+        S.cand_steps = sp_cand_steps.p;
+        S.steps_hint = sp_steps_hint.p;
+        S.steps_prop = sp_steps_prop.p;
+        S.batch_x = sp_batch_x.p;
+        S.batch_llh = sp_batch_llh.p;
+        S.batch_status = sp_batch_status.p;
+        S.batch_steps = sp_batch_steps.p;
+        S.batch_src = sp_batch_src.p;
+        S.batch_n = sp_batch_n.p;
         return true;
     }
 
@@ -583,6 +741,13 @@ struct SamplerPTDevice::Impl {
         if (f[0] != 0) {
             LOGERROR("Likelihood evaluation returned NaN (Sampler::EvaluateLikelihood, fatal)");
             return false;
+        }
+        if (spec_on) {
+            if (!Download(f, sp_err, stream)) return false;
+            if (f[0] != 0) {
+                LOGERROR("Speculative iteration: the candidate that happened was not evaluated (internal error)");
+                return false;
+            }
         }
         return true;
     }
@@ -834,24 +999,16 @@ bool SamplerPTDevice::Initialize(std::shared_ptr<Likelihood> ll, const std::vect
             if (!s.masks[start].back()->alloc(C) || !Upload(*s.masks[start].back(), v, s.stream)) return false;
         }
     }
+    if (!s.SetupSpeculation()) return false;
     return s.InitialPositions() && bcm3hip_stream_synchronize(s.stream) == 0;
 }
 
-bool SamplerPTDevice::Iterate(int64_t n, bool last_at_end)
-{
-    for (int64_t i = 0; i < n; i++)
-        if (!p_->IterationOnce(last_at_end && i + 1 == n)) return false;
-    return true;
-}
+bool SamplerPTDevice::Iterate(int64_t n, bool last_at_end) { return p_->Iterations(n, last_at_end, 0); }
 
 bool SamplerPTDevice::Run(int64_t num_samples)
 {
     const int64_t total = num_samples * p_->cfg.use_every_nth;
-    for (int64_t si = 0; si < total; si++) {
-        if (!p_->IterationOnce(si + 1 == total)) return false;
-        if (p_->cfg.nan_check_every > 0 && (si + 1) % p_->cfg.nan_check_every == 0 && !p_->CheckNaN()) return false;
-    }
-    return p_->CheckNaN() && FlushOutput();
+    return p_->Iterations(total, true, p_->cfg.nan_check_every) && p_->CheckNaN() && FlushOutput();
 }
 
 bool SamplerPTDevice::AdaptProposal() { return p_->Adapt(); }

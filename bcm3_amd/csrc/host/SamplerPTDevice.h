@@ -53,6 +53,11 @@ struct PTMHConfig {
     int initial_position_tries = 100;
     int nan_check_every = 100;
     int host_threads = 0;  // proposal adaptation threads, 0 = hardware concurrency (max 16)
+    // speculative iteration pairs: iteration r's likelihood launch also evaluates every proposal
+    // iteration r + 1 can make (own / exchange partner's state, accepted or not), so the pair needs
+    // one launch; bit-identical results. Used when the likelihood supports counted device batches
+    // (the PopPK kernel), one rank, deterministic_even_odd, one exploration step, adaptive proposals.
+    int speculate = 1;
 };
 
 struct PTMHCounters {

@@ -48,6 +48,7 @@ void bcm3_ptmh_config_default(bcm3_ptmh_config* c)
     c->initial_position_tries = d.initial_position_tries;
     c->nan_check_every = d.nan_check_every;
     c->host_threads = 0;
+    c->speculate = d.speculate;
     c->transport = BCM3_PTMH_TRANSPORT_NONE;
 }
 
@@ -151,6 +152,7 @@ int bcm3_ptmh_create(bcm3_likelihood* ll, const char* prior_xml, const bcm3_ptmh
     cfg.initial_position_tries = c->initial_position_tries;
     cfg.nan_check_every = c->nan_check_every;
     cfg.host_threads = c->host_threads;
+    cfg.speculate = c->speculate;
     std::unique_ptr<bcm3::Transport> tr;
     if (c->world > 1) {
         if (c->transport == BCM3_PTMH_TRANSPORT_RCCL) {

@@ -225,13 +225,18 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                                                         double* __restrict__ patient_llh,
                                                         int32_t* __restrict__ traj_status,
                                                         double* __restrict__ traj_out,
-                                                        bcm3hip_traj_stats* __restrict__ stats_out)
+                                                        bcm3hip_traj_stats* __restrict__ stats_out,
+                                                        const int32_t* __restrict__ n_dev,
+                                                        int32_t* __restrict__ steps_out)
 {
     using TR = PKTraits<PKT>;
     constexpr int NS = TR::NS;
     constexpr bool UNI = (MODE != POPK_LANES);
     constexpr bool VEC = (MODE == POPK_VEC);
     const int lane = threadIdx.x & 63;
+    // n_dev: the number of evaluations is a device value (the speculative batches of the sampler
+    // size themselves on the device); the grid covers the maximum and the rest return here
+    if (n_dev) ntraj = (int64_t)__builtin_amdgcn_readfirstlane(*n_dev) * m.P;
     int64_t g;
     if constexpr (UNI) {
         g = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
@@ -341,6 +346,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     double* tro = traj_out ? traj_out + g * (int64_t)NS * T : nullptr;
 
     double llh = 0.0;
+    int nsteps = 0;         // BDF steps of the solve (steps_out: the sampler's dispatch-order hint)
     bool llh_done = false;  // NaN concentration seen: llh = -inf, stop accumulating
     int status = BCM3HIP_STATUS_OK;
 
@@ -531,6 +537,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                     s.tstopset = 1;
                 }
             }
+            nsteps = current_step;
         }
     }
     if (status != BCM3HIP_STATUS_OK) llh = -INFINITY;
@@ -542,6 +549,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     if (logp_direct) logp_direct[e] = 0.0 + llh;  // P == 1: logp = 0 + patient term
     if (patient_llh) patient_llh[g] = llh;
     if (traj_status) traj_status[g] = status;
+    if (steps_out && m.P == 1) steps_out[g] = nsteps;
     if (STATS && stats_out) {
         bcm3hip_traj_stats st;
         st.nst = s.cnt.nst_total;
@@ -560,8 +568,10 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
 // (LikelihoodPopPKTrajectory.cpp:427-440); status = max over patients.
 __global__ void __launch_bounds__(256) popk_reduce_kernel(int64_t n, int P, const double* __restrict__ patient_llh,
                                                           const int32_t* __restrict__ traj_status,
-                                                          double* __restrict__ logp, int32_t* __restrict__ status)
+                                                          double* __restrict__ logp, int32_t* __restrict__ status,
+                                                          const int32_t* __restrict__ n_dev)
 {
+    if (n_dev) n = *n_dev;
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
     double acc = 0.0;
@@ -579,7 +589,8 @@ __global__ void __launch_bounds__(256) popk_reduce_kernel(int64_t n, int P, cons
 hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
                        double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
                        bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, int uni_solver,
-                       hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop, int block_lds)
+                       hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop, int block_lds,
+                       const int32_t* n_dev, int32_t* steps_out)
 {
     const int64_t ntraj = n * (int64_t)m.P;
     if (ntraj == 0) return hipSuccess;
@@ -598,16 +609,16 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
 #define LAUNCH(PKT)                                                                                           \
     if (vec_state && !stats_out)                                                                              \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, false>), grid, block, block_lds, stream, m, ntraj, lpw,     \
-                           values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr);   \
+                           values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr, n_dev, steps_out);   \
     else if (vec_state)                                                                                       \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, true>), grid, block, block_lds, stream, m, ntraj, lpw,      \
-                           values, logp_direct, patient_llh_scratch, tstat, traj_out, stats_out); \
+                           values, logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out); \
     else if (uni)                                                                                             \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_UNI, true>), grid, block, block_lds, stream, m, ntraj, lpw, values, \
-                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out);         \
+                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out);         \
     else                                                                                                      \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_LANES, true>), grid, block, block_lds, stream, m, ntraj, lpw, values,  \
-                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out)
+                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out)
     switch (m.pk_type) {
     case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;
     case BCM3HIP_PK_TWO: LAUNCH(BCM3HIP_PK_TWO); break;
@@ -625,7 +636,7 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
     const unsigned rb = (unsigned)((n + tb - 1) / tb);
     if (!direct) {
         hipLaunchKernelGGL(popk_reduce_kernel, dim3(rb), dim3(tb), 0, stream, n, m.P, patient_llh_scratch,
-                           traj_status_scratch, logp, status);
+                           traj_status_scratch, logp, status, n_dev);
     }
     return hipGetLastError();
 }

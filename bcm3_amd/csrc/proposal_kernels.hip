@@ -439,19 +439,27 @@ __global__ void __launch_bounds__(64) gmm_eval_wave_kernel(int n, int d, int K, 
     if (logpdf && lane == 0) logpdf[p] = lsum;
 }
 
-__global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
-    int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0, const double* __restrict__ p1,
-    const double* __restrict__ p2, const double* __restrict__ temps, const double* __restrict__ values, double* __restrict__ prop,
-    double* __restrict__ lprior_prop, double* __restrict__ log_mh, bcm3hip_proposal P, int64_t chain0,
-    uint64_t seed, uint64_t iter)
+// One chain's proposal (see ptmh_propose_wave_kernel). cur_row: the point proposed from. SPEC = false:
+// the proposal state is updated in place (Proposal::Update's scale, the selected component), the
+// results go to out_row / *lprior_out / *log_mh_out. SPEC = true (speculative candidates for the next
+// iteration, ptmh_spec_candidates_kernel): the acceptance EMA of the component Update reads is
+// ema_last (the value the accept step leaves for an assumed outcome), and instead of writing the
+// proposal state the kernel reports what the sequential propose would write: *sel_out (selected
+// component), *upd_out / *sc_out (the scale Update's component, -1 for none, and its new value).
+template <bool SPEC>
+__device__ __forceinline__ void propose_wave_one(int c, int d, const int32_t* __restrict__ kind,
+                                                 const double* __restrict__ p0, const double* __restrict__ p1,
+                                                 const double* __restrict__ p2, const double* __restrict__ temps,
+                                                 const double* __restrict__ cur_row, double ema_last,
+                                                 double* __restrict__ out_row, double* __restrict__ lprior_out,
+                                                 double* __restrict__ log_mh_out, const bcm3hip_proposal& P,
+                                                 uint64_t gc, uint64_t seed, uint64_t iter, int32_t* sel_out,
+                                                 int32_t* upd_out, double* sc_out)
 {
     const int lane = threadIdx.x & 63;
-    const int c = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
-    if (c >= C) return;
-    const uint64_t gc = (uint64_t)(chain0 + c);
     const bool on = lane < d;
     const int li = on ? lane : 0;
-    const double cur = values[(int64_t)c * d + li];
+    const double cur = cur_row[li];
     double nxt;
     double lmh = 0.0;
     const bool dir = prior::has_dirichlet(d, kind);
@@ -491,14 +499,15 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
             if (last != -1) {
                 const double lrate = 1.0 + u01(rng_key(seed, iter, gc, rng::KEY_UPDATE)) * slr * K;
                 sc = scale[last];
-                if (ema[last] < target / (1.0 - slr)) {
+                const double e = SPEC ? ema_last : ema[last];
+                if (e < target / (1.0 - slr)) {
                     sc /= lrate;
                     sc = (sc > 1e-4) ? sc : 1e-4;
-                } else if (ema[last] > (1 + slr) * target) {
+                } else if (e > (1 + slr) * target) {
                     sc *= lrate;
                     sc = (sc < 10.0) ? sc : 10.0;
                 }
-                if (lane == 0) scale[last] = sc;
+                if (!SPEC && lane == 0) scale[last] = sc;
                 upd = last;
             }
             rf = wave_responsibilities(K, d, cur, mean, chol, logc, w, lane);
@@ -515,14 +524,15 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
         } else {
             const double lrate = 1.0 + u01(rng_key(seed, iter, gc, rng::KEY_UPDATE)) * slr;
             sc = scale[0];
-            if (ema[0] < 0.952381 * target) {
+            const double e = SPEC ? ema_last : ema[0];
+            if (e < 0.952381 * target) {
                 sc /= lrate;
                 sc = (sc > 1e-4) ? sc : 1e-4;
-            } else if (ema[0] > 1.05 * target) {
+            } else if (e > 1.05 * target) {
                 sc *= lrate;
                 sc = (sc < 10.0) ? sc : 10.0;
             }
-            if (lane == 0) scale[0] = sc;
+            if (!SPEC && lane == 0) scale[0] = sc;
             upd = 0;
             sel = 0;
         }
@@ -591,9 +601,17 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
                 if (lane == l) nxt = 1.0 - sum;
             }
         }
-        if (lane == 0) P.selected[c] = sel;
+        if (SPEC) {
+            if (lane == 0) {
+                *sel_out = sel;
+                *upd_out = upd;
+                *sc_out = sc;
+            }
+        } else if (lane == 0) {
+            P.selected[c] = sel;
+        }
     }
-    if (on) prop[(int64_t)c * d + lane] = nxt;
+    if (on) out_row[lane] = nxt;
     double lp;
     if (!dir) {
         lp = wave_seq_sum(d, on ? prior::log_pdf(kind[li], p0[li], p1[li], p2[li], nxt) : 0.0);
@@ -611,9 +629,22 @@ __global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
             if (kind[i] != BCM3HIP_PRIOR_DIRICHLET) lp += lane_bcast(ul, i);
     }
     if (lane == 0) {
-        lprior_prop[c] = lp;
-        log_mh[c] = lmh;
+        *lprior_out = lp;
+        *log_mh_out = lmh;
     }
+}
+
+__global__ void __launch_bounds__(64) ptmh_propose_wave_kernel(
+    int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0, const double* __restrict__ p1,
+    const double* __restrict__ p2, const double* __restrict__ temps, const double* __restrict__ values, double* __restrict__ prop,
+    double* __restrict__ lprior_prop, double* __restrict__ log_mh, bcm3hip_proposal P, int64_t chain0,
+    uint64_t seed, uint64_t iter)
+{
+    const int c = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    if (c >= C) return;
+    propose_wave_one<false>(c, d, kind, p0, p1, p2, temps, values + (int64_t)c * d, 0.0, prop + (int64_t)c * d,
+                            lprior_prop + c, log_mh + c, P, (uint64_t)(chain0 + c), seed, iter, nullptr, nullptr,
+                            nullptr);
 }
 
 // generic path (d > 64): one thread per chain, its vectors in the global work buffer
@@ -701,6 +732,187 @@ __global__ void history_add_kernel(int C, int d, int H, int subsampling, const d
     }
 }
 
+// ---- speculative iteration pairs (include/bcm3hip.h "speculative iteration pairs") ----
+
+// Proposal::Update's branch for an acceptance EMA e: 0 shrink, 1 keep, 2 grow (the comparisons of
+// propose_wave_one, in the same form)
+__device__ __forceinline__ int update_branch(const bcm3hip_proposal& P, double e)
+{
+    const double slr = P.scaling_learning_rate, target = P.target_acceptance;
+    if (P.kind == BCM3HIP_PROPOSAL_GAUSSIAN_MIXTURE) {
+        if (e < target / (1.0 - slr)) return 0;
+        if (e > (1 + slr) * target) return 2;
+        return 1;
+    }
+    if (e < 0.952381 * target) return 0;
+    if (e > 1.05 * target) return 2;
+    return 1;
+}
+
+// one wavefront per (chain c, slot k): candidate k of c for iteration `iter` (= r + 1)
+__global__ void __launch_bounds__(64) ptmh_spec_candidates_kernel(
+    int C, int d, const int32_t* __restrict__ kind, const double* __restrict__ p0, const double* __restrict__ p1,
+    const double* __restrict__ p2, const double* __restrict__ temps, const double* __restrict__ values,
+    const double* __restrict__ prop, const int32_t* __restrict__ partner, bcm3hip_proposal P, bcm3hip_spec S,
+    int64_t chain0, uint64_t seed, uint64_t iter)
+{
+    const int w = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    const int c = w / BCM3HIP_SPEC_SLOTS, k = w - c * BCM3HIP_SPEC_SLOTS;
+    if (c >= C) return;
+    const int lane = threadIdx.x & 63;
+    const int pc = partner[c];
+    const double* row = values + (int64_t)c * d;
+    double ema_last = 0.0;
+    bool active;
+    if (temps[c] == 0.0) {
+        active = (k == 0);  // a prior draw: the state does not matter
+    } else {
+        // the EMA NotifyAccepted leaves for component selected[c] (ptmh_accept_adaptive_kernel's
+        // arithmetic) after a reject (e0) or an accept (e1) of iteration r
+        const int sel = P.selected[c];
+        const double e = P.ema[(int64_t)c * P.kmax + (sel < 0 ? 0 : sel)];
+        const double alpha = 2.0 / (P.scaling_ema_period + 1);
+        const double e0 = e + (0.0 - e) * alpha;
+        const double e1 = e + (1.0 - e) * alpha;
+        const bool two = update_branch(P, e0) != update_branch(P, e1);
+        int a = 0;
+        switch (k) {
+        case 0: active = true; a = 0; break;
+        case 1: active = true; row = prop + (int64_t)c * d; a = 1; break;
+        case 2: active = pc >= 0; row = values + (int64_t)(pc < 0 ? c : pc) * d; a = 0; break;
+        case 3: active = pc >= 0; row = prop + (int64_t)(pc < 0 ? c : pc) * d; a = 0; break;
+        case 4: active = pc >= 0 && two; row = values + (int64_t)(pc < 0 ? c : pc) * d; a = 1; break;
+        default: active = pc >= 0 && two; row = prop + (int64_t)(pc < 0 ? c : pc) * d; a = 1; break;
+        }
+        ema_last = a ? e1 : e0;
+    }
+    if (lane == 0) {
+        S.cand_active[w] = active ? 1 : 0;
+        S.cand_sel[w] = -1;
+        S.cand_upd[w] = -1;
+        S.cand_sc[w] = 0.0;
+    }
+    if (!active) return;
+    propose_wave_one<true>(c, d, kind, p0, p1, p2, temps, row, ema_last, S.cand_x + (int64_t)w * d, S.cand_lp + w,
+                           S.cand_lmh + w, P, (uint64_t)(chain0 + c), seed, iter, S.cand_sel + w, S.cand_upd + w,
+                           S.cand_sc + w);
+}
+
+// one workgroup: the batch of iteration r's proposals and the active candidates, sorted by the
+// predicted solve length (the steps of the last evaluation of the chain whose state an entry starts
+// from), longest first, ties by entry id; the hardware dispatches wavefronts in this order, so the
+// long solves start first and the short ones fill the SIMDs they free (tools/spec_sim.py)
+constexpr int kSpecSortMax = 4096;
+__global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, const double* __restrict__ prop,
+                                                               const int32_t* __restrict__ partner, bcm3hip_spec S)
+{
+    __shared__ unsigned long long key[kSpecSortMax];
+    const int tid = threadIdx.x;
+    const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
+    int N = 1;
+    while (N < n_all) N <<= 1;
+    for (int i = tid; i < N; i += blockDim.x) {
+        unsigned long long kv = ~0ull;
+        int src = -1;
+        if (i < C) {
+            src = i;
+        } else if (i < n_all) {
+            const int sl = i - C, c = sl / BCM3HIP_SPEC_SLOTS, k = sl - c * BCM3HIP_SPEC_SLOTS;
+            if (S.cand_active[sl]) src = (k <= 1 || partner[c] < 0) ? c : partner[c];
+        }
+        if (src >= 0) {
+            int h = S.steps_hint[src];
+            h = h < 0 ? 0 : h;
+            kv = ((unsigned long long)(0x7fffffffu - (unsigned)h) << 32) | (unsigned)i;
+        }
+        key[i] = kv;
+    }
+    __syncthreads();
+    for (int size = 2; size <= N; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < N; i += blockDim.x) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const unsigned long long a = key[i], b = key[j];
+                    const bool up = (i & size) == 0;
+                    if ((a > b) == up) {
+                        key[i] = b;
+                        key[j] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // the active entries are the prefix before the first ~0 key
+    for (int i = tid; i < N; i += blockDim.x)
+        if (key[i] != ~0ull && (i + 1 == N || key[i + 1] == ~0ull)) S.batch_n[0] = i + 1;
+    for (int i = tid; i < N; i += blockDim.x)
+        if (key[i] != ~0ull) S.batch_src[i] = (int)(key[i] & 0xffffffffull);
+    for (int t = tid; t < N * d; t += blockDim.x) {
+        const int pos = t / d, j = t - pos * d;
+        if (key[pos] == ~0ull) continue;
+        const int id = (int)(key[pos] & 0xffffffffull);
+        const double* src = (id < C) ? prop + (int64_t)id * d : S.cand_x + (int64_t)(id - C) * d;
+        S.batch_x[(int64_t)pos * d + j] = src[j];
+    }
+}
+
+__global__ void ptmh_spec_scatter_kernel(int C, bcm3hip_spec S, double* __restrict__ llh_prop)
+{
+    const int pos = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pos >= S.batch_n[0]) return;
+    const int id = S.batch_src[pos];
+    if (id < C) {
+        llh_prop[id] = S.batch_llh[pos];
+        S.steps_prop[id] = S.batch_steps[pos];
+        S.steps_hint[id] = S.batch_steps[pos];
+    } else {
+        S.cand_llh[id - C] = S.batch_llh[pos];
+        S.cand_steps[id - C] = S.batch_steps[pos];
+    }
+}
+
+// one thread per chain: the candidate that the accept of r and the exchange of r + 1 made real
+__global__ void ptmh_spec_select_kernel(int C, int d, const double* __restrict__ temps,
+                                        const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first,
+                                        const uint8_t* __restrict__ acc_mut, const uint8_t* __restrict__ acc_exc,
+                                        bcm3hip_spec S, double* __restrict__ prop, double* __restrict__ lprior_prop,
+                                        double* __restrict__ log_mh, double* __restrict__ llh_prop, bcm3hip_proposal P,
+                                        int32_t* __restrict__ error)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    int k = 0;
+    const bool hot = temps[c] != 0.0;
+    if (hot) {
+        const int pc = partner[c];
+        const bool swapped = pc >= 0 && acc_exc[pair_first[c]] != 0;
+        const bool own = acc_mut[c] != 0;
+        if (!swapped) {
+            k = own ? 1 : 0;
+        } else {
+            k = acc_mut[pc] ? 3 : 2;
+            if (own && S.cand_active[c * BCM3HIP_SPEC_SLOTS + k + 2]) k += 2;
+        }
+    }
+    const int sl = c * BCM3HIP_SPEC_SLOTS + k;
+    if (!S.cand_active[sl]) {
+        if (error) *error = 1;
+        return;
+    }
+    for (int i = 0; i < d; i++) prop[(int64_t)c * d + i] = S.cand_x[(int64_t)sl * d + i];
+    lprior_prop[c] = S.cand_lp[sl];
+    log_mh[c] = S.cand_lmh[sl];
+    llh_prop[c] = S.cand_llh[sl];
+    S.steps_hint[c] = S.cand_steps[sl];
+    if (hot) {
+        const int upd = S.cand_upd[sl];
+        if (upd >= 0) P.scale[(int64_t)c * P.kmax + upd] = S.cand_sc[sl];
+        P.selected[c] = S.cand_sel[sl];
+    }
+}
+
 bool proposal_ok(const bcm3hip_proposal* P, int C, int d)
 {
     if (!P || P->kmax < 1 || P->kmax > BCM3HIP_PROPOSAL_KMAX) return false;
@@ -755,6 +967,61 @@ int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double
     hipLaunchKernelGGL(ptmh_accept_adaptive_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d,
                        temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values, lprior, llh, lpp, accept_out,
                        (unsigned long long*)accepted, nan_llh, *proposal, chain0, seed, iter);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+static bool spec_ok(const bcm3hip_spec* S)
+{
+    return S && S->cand_x && S->cand_lp && S->cand_lmh && S->cand_llh && S->cand_sel && S->cand_upd && S->cand_sc &&
+           S->cand_active && S->cand_steps && S->steps_hint && S->steps_prop && S->batch_x && S->batch_llh &&
+           S->batch_status && S->batch_steps && S->batch_src && S->batch_n;
+}
+
+int bcm3hip_ptmh_spec_candidates(int C, int d, const int32_t* prior_kind, const double* prior_p0,
+                                 const double* prior_p1, const double* prior_p2, const double* temps,
+                                 const double* values, const double* prop, const int32_t* partner,
+                                 const bcm3hip_proposal* proposal, const bcm3hip_spec* spec, int64_t chain0,
+                                 uint64_t seed, uint64_t iter_next, void* stream)
+{
+    if (C < 0 || d <= 0 || d > 64 || !proposal_ok(proposal, C, d) || !spec_ok(spec) ||
+        (C > 0 && (!prior_kind || !prior_p0 || !prior_p1 || !prior_p2 || !temps || !values || !prop || !partner)))
+        return BCM3HIP_ERR_ARG;
+    if (C == 0) return 0;
+    hipLaunchKernelGGL(ptmh_spec_candidates_kernel, dim3(C * BCM3HIP_SPEC_SLOTS), dim3(64), 0, (hipStream_t)stream, C,
+                       d, prior_kind, prior_p0, prior_p1, prior_p2, temps, values, prop, partner, *proposal, *spec,
+                       chain0, seed, iter_next);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* partner, const bcm3hip_spec* spec,
+                            void* stream)
+{
+    if (C <= 0 || d <= 0 || C * (1 + BCM3HIP_SPEC_SLOTS) > kSpecSortMax || !prop || !partner || !spec_ok(spec))
+        return BCM3HIP_ERR_ARG;
+    hipLaunchKernelGGL(ptmh_spec_batch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, prop, partner, *spec);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_spec_scatter(int C, const bcm3hip_spec* spec, double* llh_prop, void* stream)
+{
+    if (C <= 0 || !spec_ok(spec) || !llh_prop) return BCM3HIP_ERR_ARG;
+    const int n = C * (1 + BCM3HIP_SPEC_SLOTS);
+    hipLaunchKernelGGL(ptmh_spec_scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, C, *spec,
+                       llh_prop);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_spec_select(int C, int d, const double* temps, const int32_t* partner, const int32_t* pair_first,
+                             const uint8_t* acc_mutate, const uint8_t* acc_exchange, const bcm3hip_spec* spec,
+                             double* prop, double* lprior_prop, double* log_mh, double* llh_prop,
+                             const bcm3hip_proposal* proposal, int32_t* error, void* stream)
+{
+    if (C <= 0 || d <= 0 || !temps || !partner || !pair_first || !acc_mutate || !acc_exchange || !spec_ok(spec) ||
+        !prop || !lprior_prop || !log_mh || !llh_prop || !proposal_ok(proposal, C, d))
+        return BCM3HIP_ERR_ARG;
+    hipLaunchKernelGGL(ptmh_spec_select_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d, temps,
+                       partner, pair_first, acc_mutate, acc_exchange, *spec, prop, lprior_prop, log_mh, llh_prop,
+                       *proposal, error);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -34,6 +34,7 @@ class PTMHConfig(C.Structure):
         ("adapt_proposal_max_history_samples", C.c_int32), ("use_every_nth", C.c_int32),
         ("swapping_scheme", C.c_int32), ("exchange_probability", C.c_double),
         ("initial_position_tries", C.c_int32), ("nan_check_every", C.c_int32), ("host_threads", C.c_int32),
+        ("speculate", C.c_int32),
         ("transport", C.c_int32), ("nccl_id", C.c_uint8 * 128), ("group", C.c_void_p),
     ]
 

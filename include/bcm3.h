@@ -144,6 +144,9 @@ typedef struct {
     int32_t initial_position_tries;
     int32_t nan_check_every;     /* bcm3_ptmh_run checks for NaN likelihoods every n iterations */
     int32_t host_threads;        /* proposal adaptation threads, 0 = all cores (max 16) */
+    int32_t speculate;           /* 1 (default): pairs of iterations in one likelihood launch when the
+                                    likelihood supports it (SamplerPTDevice, bcm3hip_ptmh_spec_*);
+                                    bit-identical to 0, the one-launch-per-iteration loop */
     int32_t transport;           /* BCM3_PTMH_TRANSPORT_*, world > 1 */
     uint8_t nccl_id[128];        /* BCM3_PTMH_TRANSPORT_RCCL: bcm3_ptmh_nccl_unique_id of rank 0 */
     bcm3_ptmh_group* group;      /* BCM3_PTMH_TRANSPORT_LOCAL */

@@ -263,7 +263,7 @@ enum {
     BCM3HIP_OPT_BLOCK_LDS = 5       /* bytes of LDS reserved per workgroup of the PopPK launch (0..65536,
                                        default 0): caps the workgroups resident per CU, so a launch
                                        with more wavefronts than SIMDs queues the rest instead of
-                                       sharing a SIMD (see bcm3hip_eval_batch_device_ordered) */
+                                       sharing a SIMD */
 };
 
 int bcm3hip_device_count(void);
@@ -309,6 +309,12 @@ int bcm3hip_eval_batch(bcm3hip_ctx* ctx, size_t n, size_t d, const double* value
  * stream has synchronised. */
 int bcm3hip_eval_batch_device(bcm3hip_ctx* ctx, size_t n, const double* values_dev, double* logp_dev,
                               int32_t* status_dev, void* stream);
+/* PopPK only: as bcm3hip_eval_batch_device for the first *n_dev (a device int32, <= n_max) items of
+ * values_dev, the count read on the device (the launch covers n_max; the items beyond *n_dev return
+ * at once), so a batch sized by a kernel needs no host round trip; steps_dev[i] (may be NULL) =
+ * BDF steps of item i's solve (one patient per evaluation; left unwritten for P > 1). SamplerPTDevice's speculative iteration pairs. */
+int bcm3hip_eval_batch_device_counted(bcm3hip_ctx* ctx, size_t n_max, const int32_t* n_dev, const double* values_dev,
+                                      double* logp_dev, int32_t* status_dev, int32_t* steps_dev, void* stream);
 int bcm3hip_last_kernel_ms(bcm3hip_ctx* ctx, float* ms);
 /* With BCM3HIP_OPT_TIMING_LOG on: synchronises on every launch logged since the last call and
  * returns the summed / maximum kernel time (HIP events recorded on each launch's own stream) and
@@ -402,6 +408,60 @@ int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double
                                  double* lprior, double* llh, double* lpp, uint8_t* accept_out, uint64_t* accepted,
                                  int32_t* nan_llh, const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed,
                                  uint64_t iter, void* stream);
+/* ---- speculative iteration pairs (SamplerPTDevice) ----
+ * Iteration r+1's proposal of chain c starts from the state exchange round r+1 leaves in slot c: its
+ * own state after iteration r (old = values[c], or prop[c] if accepted) or its exchange partner's
+ * (values[p] / prop[p]), with the acceptance EMA the accept of r leaves (it decides Proposal::Update's
+ * scale branch). With counter-based random numbers every such proposal is determined now, so one
+ * launch evaluates iteration r's proposals AND every candidate of r+1; after accept r and exchange
+ * r+1, bcm3hip_ptmh_spec_select picks the candidate that happened and its log-likelihood, so the
+ * accept of r+1 needs no launch -- bit-identical to the sequential iteration.
+ * Candidate slots per chain (k): 0 old_c (own reject), 1 prop_c (own accept), 2 old_p, 3 prop_p
+ * (swapped; own reject -- or either outcome when Update's branch does not depend on it), 4 old_p,
+ * 5 prop_p (swapped, own accept; only when the branch differs). T == 0 chains: slot 0 (a prior
+ * draw). All pointers are device pointers sized for C chains (slots [C][6]). */
+enum { BCM3HIP_SPEC_SLOTS = 6 };
+typedef struct {
+    double* cand_x;       /* [C][6][d] candidate proposals */
+    double* cand_lp;      /* [C][6] their log prior */
+    double* cand_lmh;     /* [C][6] log MH ratio */
+    double* cand_llh;     /* [C][6] log-likelihood (scattered from the batch) */
+    int32_t* cand_sel;    /* [C][6] selected component */
+    int32_t* cand_upd;    /* [C][6] component whose scale Update changed (-1 none) */
+    double* cand_sc;      /* [C][6] its new scale */
+    uint8_t* cand_active; /* [C][6] */
+    int32_t* cand_steps;  /* [C][6] BDF steps of the candidate's solve */
+    int32_t* steps_hint;  /* [C] BDF steps of the last evaluation of the chain (dispatch order) */
+    int32_t* steps_prop;  /* [C] steps of iteration r's proposals */
+    double* batch_x;      /* [7C][d] the launch's vectors, longest predicted solve first */
+    double* batch_llh;    /* [7C] */
+    int32_t* batch_status;/* [7C] */
+    int32_t* batch_steps; /* [7C] */
+    int32_t* batch_src;   /* [7C] source of each batch entry: c < C proposal of chain c, C + 6c + k candidate */
+    int32_t* batch_n;     /* [1] entries in use */
+} bcm3hip_spec;
+/* candidates of iteration iter_next = r + 1 (after bcm3hip_ptmh_propose_adaptive of iteration r, whose
+ * proposals are in prop); partner[c] = exchange partner of chain c in round r + 1 (-1 none) */
+int bcm3hip_ptmh_spec_candidates(int C, int d, const int32_t* prior_kind, const double* prior_p0,
+                                 const double* prior_p1, const double* prior_p2, const double* temps,
+                                 const double* values, const double* prop, const int32_t* partner,
+                                 const bcm3hip_proposal* proposal, const bcm3hip_spec* spec, int64_t chain0,
+                                 uint64_t seed, uint64_t iter_next, void* stream);
+/* the launch's batch: iteration r's C proposals + the active candidates, ordered by the predicted
+ * length of their solves (steps_hint of the chain whose state they start from), longest first (C <= 1024) */
+int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* partner, const bcm3hip_spec* spec,
+                            void* stream);
+/* batch results back: llh_prop[c] (iteration r), cand_llh / cand_steps, steps_prop */
+int bcm3hip_ptmh_spec_scatter(int C, const bcm3hip_spec* spec, double* llh_prop, void* stream);
+/* after accept r (accept_out = acc_mutate[C]) and exchange r + 1 (accept_out = acc_exchange, indexed
+ * by the first chain of each pair; pair_first[c] = that chain for c's pair in round r + 1): iteration
+ * r + 1's proposal, log prior, MH ratio and log-likelihood of each chain, and the proposal state
+ * writes its propose would have made (scale Update, selected component). *error != 0 if a needed
+ * candidate was not evaluated (never expected). */
+int bcm3hip_ptmh_spec_select(int C, int d, const double* temps, const int32_t* partner, const int32_t* pair_first,
+                             const uint8_t* acc_mutate, const uint8_t* acc_exchange, const bcm3hip_spec* spec,
+                             double* prop, double* lprior_prop, double* log_mh, double* llh_prop,
+                             const bcm3hip_proposal* proposal, int32_t* error, void* stream);
 /* The propose kernel's mixture arithmetic (GMM::CalculateResponsibilities, src/stats/GMM.cpp:172-186,
  * with the component densities of GMM::LogPdfMVN :392-398) at n points x[n][d] (device buffers,
  * d <= 64, K <= 64): logpdf[n] = log sum_k w_k N(x; mean_k, L_k L_k^T), resp[n][K]; either may be

@@ -11,6 +11,11 @@ Outputs (all data; no reference source text):
   c3_golden.npz                      512 prior draws (seed 20251016) with the reference-built
                                      oracle's logp, per-patient llh, trajectories, step counters
   analytic_golden.npz                banana / circular draws with reference-formula outputs
+  c3_golden_llh.npz                  8,192 prior draws (seed 20251021, regenerated from the seed by
+                                     synthetic.prior_draws) with the reference-built oracle's logp,
+                                     step counts and ok flags, and the same from the reference built
+                                     without FMA contraction (its self-spread); `--llh-only` writes
+                                     just this file
 """
 from __future__ import annotations
 
@@ -62,7 +67,24 @@ def make_pkdata(P: int, seed: int) -> dict:
     return pk
 
 
+LLH_SEED, LLH_N = 20251021, 8192
+
+
+def make_llh_fixture():
+    pk = O.load_pkdata(os.path.join(HERE, "c3_pkdata.json"))
+    prob = O.build_problem(pk, S.TRIAL, S.DRUG, S.PK_TYPE, variables(1))
+    draws = S.prior_draws(1, LLH_N, LLH_SEED)
+    ref = O.Oracle("ref").popk_eval(prob, draws, nthreads=8, want_traj=False)
+    nof = O.Oracle("ref_nofma").popk_eval(prob, draws, nthreads=8, want_traj=False)
+    np.savez_compressed(os.path.join(HERE, "c3_golden_llh.npz"), seed=LLH_SEED, n=LLH_N,
+                        values_sum=draws.sum(), logp=ref["logp"], nst=ref["stats"][:, 0, 0], ok=ref["ok"][:, 0],
+                        logp_nofma=nof["logp"], nst_nofma=nof["stats"][:, 0, 0])
+
+
 def main():
+    if "--llh-only" in sys.argv:
+        make_llh_fixture()
+        return
     for P, name, seed in ((1, "c3", 20251015), (64, "p64", 20251017)):
         pk = make_pkdata(P, seed)
         with open(os.path.join(HERE, f"{name}_pkdata.json"), "w") as f:
@@ -88,6 +110,7 @@ def main():
     np.savez_compressed(os.path.join(HERE, "analytic_golden.npz"), banana_values=b,
                         banana_logp=r.banana(b, 2, 2.0, 1.0), circular_values=c,
                         circular_logp=r.circular(c, 2, 2.0, 3.5, 0.1))
+    make_llh_fixture()
     print("fixtures written to", HERE)
 
 

@@ -21,6 +21,20 @@ import numpy as np
 Y1_TIERS = ((1e-9, 0.92), (1e-6, 0.985), (2e-5, 0.995))  # (tolerance, min fraction of draws)
 LLH_T1, LLH_T1_FRAC = 1e-8, 0.99
 LLH_T2 = 1e-3  # every draw whose ok/fail status agrees
+# The llh tier is a rate near 99 %: on fewer than LLH_FULL_N draws its sampling noise (sigma = 0.44 %
+# at 512 draws) exceeds the margin, so smaller samples are held to the binomial bound of a 99 %
+# process (expected misses + 2 sigma); the >= 99 % rate itself is asserted on the large samples
+# (8,192 golden draws, 4,096 prior draws, 12,288 P64 trajectories, 2,048 C5 chains). The
+# reference's own two builds differ on 4 of the 512 c3_golden draws (99.2 %).
+LLH_FULL_N = 2048
+
+
+def llh_min_fraction(n: int) -> float:
+    if n >= LLH_FULL_N:
+        return LLH_T1_FRAC
+    p = 1.0 - LLH_T1_FRAC
+    allowed = int(np.floor(n * p + 2.0 * np.sqrt(n * p * (1.0 - p))))
+    return 1.0 - allowed / max(1, n)
 STEPS_FRACTION = 0.98
 
 
@@ -76,7 +90,7 @@ def assert_parity(y1_err, llh_e, steps_a, steps_b, ok_a, ok_b, near_cap=None):
     both_ok = (ok_a == 1) & (ok_b == 1)
     for t, frac in Y1_TIERS:
         assert np.mean(y1_err[both_ok] <= t) >= frac, (t, frac, s)
-    assert np.mean(llh_e <= LLH_T1) >= LLH_T1_FRAC, s
+    assert np.mean(llh_e <= LLH_T1) >= llh_min_fraction(np.asarray(llh_e).size), s
     assert np.all(llh_e[both_ok] <= LLH_T2), s
     assert s["steps_equal"] >= STEPS_FRACTION, s
     return s

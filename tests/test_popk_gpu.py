@@ -51,6 +51,30 @@ def test_c3_golden_fixture(c3, golden_dir):
                          gold["ok"][:, 0], near)
 
 
+def test_c3_golden_llh_8192(c3):
+    """8,192 prior draws against the reference-built CVODE (tests/golden/c3_golden_llh.npz): identical
+    ok / fail status, llh within 1e-8 (1 + |llh|) for >= 99 % of the draws (the reference's own FMA /
+    no-FMA builds: 99.21 % on the same draws), within 1e-3 for all, step counts equal for >= 98 %"""
+    prob, ctx = c3
+    z = np.load(os.path.join(H.GOLDEN, "c3_golden_llh.npz"))
+    vals = H.S.prior_draws(1, int(z["n"]), int(z["seed"]))
+    assert vals.sum() == z["values_sum"]
+    g = ctx.eval(vals, detail=True)
+    ok_g = g["status"] == 0
+    ok_r = z["ok"].astype(bool)
+    near = z["nst"] >= 0.99 * prob.max_steps
+    assert np.all((ok_g == ok_r) | near)
+    e = parity.llh_err(g["logp"], z["logp"])
+    self_spread = parity.llh_err(z["logp_nofma"], z["logp"])
+    s = {"llh_t1": float(np.mean(e <= parity.LLH_T1)), "llh_max": float(e[ok_g & ok_r].max()),
+         "ref_self_llh_t1": float(np.mean(self_spread <= parity.LLH_T1)),
+         "steps_equal": float(np.mean(g["stats"]["nst"][:, 0] == z["nst"]))}
+    parity.log_summary(s, n=len(vals))
+    assert s["llh_t1"] >= parity.LLH_T1_FRAC, s
+    assert np.all(e[ok_g & ok_r] <= parity.LLH_T2), s
+    assert s["steps_equal"] >= parity.STEPS_FRACTION, s
+
+
 def test_c3_prior_draws_vs_oracle(c3, orc):
     prob, ctx = c3
     vals = H.S.prior_draws(1, 4096, 20251019)

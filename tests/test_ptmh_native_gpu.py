@@ -212,3 +212,51 @@ def test_adaptation_output_file(tmp_path):
     assert "adapt0.block1.history" not in v
     assert v["adapt1.block1.history"].shape[1] == 2 and v["adapt2.block1.history"].shape[1] == 2
     assert "adapt3.block1.gmm_weights" not in v
+
+
+@pytest.mark.parametrize("proposal,C,t_dof", [("gaussian_mixture", 64, 0.0), ("global_covariance", 64, 0.0),
+                                              ("gaussian_mixture_adjustedAIC", 63, 0.0), ("gaussian_mixture", 32, 5.0)])
+def test_speculative_pairs_bit_identical(tmp_path, proposal, C, t_dof):
+    """SamplerPTDevice's speculative iteration pairs (one likelihood launch per two iterations, the
+    second iteration's proposal picked from the candidates after accept / exchange) against the
+    one-launch-per-iteration loop: the same chains, counters, fitted mixtures and sample file bit for
+    bit, with adaptations falling on either iteration of a pair (use_every_nth 1 and 3),
+    an odd ladder (one chain without an exchange partner in alternate rounds) and t proposals"""
+    from scipy.io import netcdf_file
+    res = []
+    for spec in (0, 1):
+        for every in (1, 3):
+            # adaptation after si = 14 (the first iteration of a pair: that pair is not formed) or after
+            # si = 47 (the second iteration of a pair)
+            s = _native(*C3, C, 17, 0, proposal=proposal, adapt_proposal_samples=15 if every == 1 else 16,
+                        adapt_proposal_times=2, t_dof=t_dof, speculate=spec, use_every_nth=every)
+            out = str(tmp_path / f"out_{spec}_{every}.nc")
+            s.set_output(out, 90 // every, flush_every=7)
+            s.iterate(91 if every == 1 else 90)
+            s.synchronize()
+            s.flush_output()
+            st, c, nc = s.state(), s.counters(), s.components()
+            s.close()
+            with netcdf_file(out, "r", mmap=False) as f:
+                vv = np.array(f.variables["samples.variable_values"][:])
+            res.append((spec, every, st, c, nc, vv))
+    for (s0, e0, st0, c0, nc0, v0), (s1, e1, st1, c1, nc1, v1) in zip(res[:2], res[2:]):
+        assert (s0, s1, e0) == (0, 1, e1)
+        _compare(st0, st1)
+        assert c0 == c1 and c0["adaptations_done"] == 2
+        assert np.array_equal(nc0, nc1)
+        assert _same(v0, v1)
+
+
+def test_speculation_is_used_for_popk():
+    """the C3 sampler runs its iterations as speculative pairs: one likelihood launch per two
+    iterations (the timing log counts launches)"""
+    from bcm3_amd import _hip
+    s = _native(*C3, 64, 3, 0)
+    s.ll.set_option(_hip.OPT_TIMING_LOG, 1)
+    s.iterate(20)
+    s.synchronize()
+    _, launches, _ = s.ll.kernel_time_log()
+    s.ll.set_option(_hip.OPT_TIMING_LOG, 0)
+    s.close()
+    assert launches == 10
