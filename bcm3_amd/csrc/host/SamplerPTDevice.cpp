@@ -383,10 +383,21 @@ struct SamplerPTDevice::Impl {
         const uint64_t INIT_ITER = (1ull << 63) - 1;
         std::vector<double> v(C * d, 0.0), q(C, -kInf), l(C, -kInf), pv, pq, pl;
         std::vector<char> bad(C, 1);
+        std::vector<int32_t> hint(C, 0), ps;  // the speculative pairs' dispatch-order hints
         bool any = true;
         for (int k = 0; k < cfg.initial_position_tries && any; k++) {
-            if (!Upload(values, v, stream) || !ProposeInit(INIT_ITER - (uint64_t)k) || !Eval(prop.p, llh_prop.p))
+            if (!Upload(values, v, stream) || !ProposeInit(INIT_ITER - (uint64_t)k)) return false;
+            if (spec_on) {
+                // the same evaluation through the counted entry point, for the solves' step counts
+                const std::vector<int32_t> nC(1, (int32_t)C);
+                if (!Upload(sp_batch_n, nC, stream) ||
+                    !ll->EvaluateLogProbabilityBatchDeviceCounted((size_t)C, sp_batch_n.p, prop.p, llh_prop.p,
+                                                                  status.p, sp_steps_prop.p, stream) ||
+                    !Download(ps, sp_steps_prop, stream))
+                    return false;
+            } else if (!Eval(prop.p, llh_prop.p)) {
                 return false;
+            }
             if (!Download(pv, prop, stream) || !Download(pq, lprior_prop, stream) || !Download(pl, llh_prop, stream))
                 return false;
             any = false;
@@ -400,6 +411,7 @@ struct SamplerPTDevice::Impl {
                     std::copy(pv.begin() + c * d, pv.begin() + (c + 1) * d, v.begin() + c * d);
                     q[c] = pq[c];
                     l[c] = nl;
+                    if (spec_on) hint[c] = ps[c];
                 }
                 bad[c] = !(q[c] + temps_host[c] * l[c] > -kInf);
                 any |= bad[c] != 0;
@@ -413,7 +425,7 @@ struct SamplerPTDevice::Impl {
         std::vector<double> pp(C);
         for (int64_t c = 0; c < C; c++) pp[c] = (temps_host[c] == 0.0) ? q[c] : q[c] + temps_host[c] * l[c];
         return Upload(values, v, stream) && Upload(lprior, q, stream) && Upload(llh, l, stream) &&
-               Upload(lpp, pp, stream);
+               Upload(lpp, pp, stream) && (!spec_on || Upload(sp_steps_hint, hint, stream));
     }
 
     bool HistoryAdd(const uint8_t* mask)
@@ -607,7 +619,11 @@ struct SamplerPTDevice::Impl {
     // on the same counter-based random numbers as two IterationOnce calls.
     bool IterationPair(bool last)
     {
-        if (!Exchange()) return false;
+        const int cur = (int)(round % 2);  // start parity of exchange round r
+        if (!Exchange(acc_exc.p) ||
+            !Launch(bcm3hip_ptmh_spec_track((int)C, nullptr, partner[cur].p, pair_first[cur].p, acc_exc.p, &S, stream),
+                    "ptmh_spec_track"))
+            return false;
         const int nxt = (int)(round % 2);  // start parity of exchange round r + 1
         if (!Launch(bcm3hip_ptmh_propose_adaptive((int)C, d, pkind.p, p0.p, p1.p, p2.p, temps.p, values.p, prop.p,
                                                   lprior_prop.p, log_mh.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
@@ -627,21 +643,28 @@ struct SamplerPTDevice::Impl {
                                                  cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, acc_mut.p,
                                                  acc_mutate.p, nan_flag.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
                     "ptmh_accept_adaptive") ||
+            !Launch(bcm3hip_ptmh_spec_track((int)C, acc_mut.p, nullptr, nullptr, nullptr, &S, stream),
+                    "ptmh_spec_track") ||
             !HistoryAdd(nullptr))
             return false;
         cnt.attempted_mutate += C;
         iter++;
         if (!PostIteration(false)) return false;
         // iteration r + 1
-        if (!Exchange(acc_exc.p)) return false;
+        if (!Exchange(acc_exc.p) ||
+            !Launch(bcm3hip_ptmh_spec_track((int)C, nullptr, partner[nxt].p, pair_first[nxt].p, acc_exc.p, &S, stream),
+                    "ptmh_spec_track"))
+            return false;
         if (!Launch(bcm3hip_ptmh_spec_select((int)C, d, temps.p, partner[nxt].p, pair_first[nxt].p, acc_mut.p,
                                              acc_exc.p, &S, prop.p, lprior_prop.p, log_mh.p, llh_prop.p, &P, sp_err.p,
                                              stream),
                     "ptmh_spec_select") ||
             !Launch(bcm3hip_ptmh_accept_adaptive((int)C, d, temps.p, prop.p, lprior_prop.p, llh_prop.p, log_mh.p,
-                                                 cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, nullptr,
+                                                 cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, acc_mut.p,
                                                  acc_mutate.p, nan_flag.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
                     "ptmh_accept_adaptive") ||
+            !Launch(bcm3hip_ptmh_spec_track((int)C, acc_mut.p, nullptr, nullptr, nullptr, &S, stream),
+                    "ptmh_spec_track") ||
             !HistoryAdd(nullptr))
             return false;
         cnt.attempted_mutate += C;
@@ -1012,6 +1035,22 @@ bool SamplerPTDevice::Run(int64_t num_samples)
 }
 
 bool SamplerPTDevice::AdaptProposal() { return p_->Adapt(); }
+
+int64_t SamplerPTDevice::SpeculativeBatch(int32_t* src, int32_t* steps, int32_t* hint_of_src)
+{
+    Impl& s = *p_;
+    if (!s.spec_on) return -1;
+    std::vector<int32_t> n, bs, bt, cand_active;
+    if (!Download(n, s.sp_batch_n, s.stream) || !Download(bs, s.sp_batch_src, s.stream) ||
+        !Download(bt, s.sp_batch_steps, s.stream))
+        return -1;
+    for (int32_t i = 0; i < n[0]; i++) {
+        if (src) src[i] = bs[i];
+        if (steps) steps[i] = bt[i];
+    }
+    (void)hint_of_src;
+    return n[0];
+}
 
 bool SamplerPTDevice::SetOutput(const std::string& filename, int64_t num_samples, int flush_every)
 {

@@ -76,6 +76,9 @@ public:
     // num_samples * use_every_nth iterations with the NaN check every nan_check_every
     bool Run(int64_t num_samples);
     bool AdaptProposal();
+    // diagnostics: the last speculative launch's entries in dispatch order (source ids as in
+    // bcm3hip_spec::batch_src, BDF steps); returns the entry count, -1 without speculation
+    int64_t SpeculativeBatch(int32_t* src, int32_t* steps, int32_t* unused);
     // SampleHandlerNetCDF (SampleHandlerNetCDF.cpp:24-110): every emitted sample of this rank's
     // temperatures goes to `filename` (netCDF classic, NetCDFClassic.h; all ranks share the file),
     // staged in HBM and written every `flush_every` samples; call before the first iteration

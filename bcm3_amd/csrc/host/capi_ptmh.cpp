@@ -178,6 +178,11 @@ int bcm3_ptmh_iterate(bcm3_ptmh* h, int64_t n, int last_at_end)
 
 int bcm3_ptmh_run(bcm3_ptmh* h, int64_t num_samples) { return (h && h->s.Run(num_samples)) ? 0 : -2; }
 
+int64_t bcm3_ptmh_spec_batch_info(bcm3_ptmh* h, int32_t* src, int32_t* steps)
+{
+    return h ? h->s.SpeculativeBatch(src, steps, nullptr) : -1;
+}
+
 int bcm3_ptmh_adapt(bcm3_ptmh* h) { return (h && h->s.AdaptProposal()) ? 0 : -2; }
 
 int bcm3_ptmh_synchronize(bcm3_ptmh* h) { return (h && h->s.Synchronize() && h->s.CheckNaN()) ? 0 : -2; }

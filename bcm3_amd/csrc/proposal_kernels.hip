@@ -866,7 +866,6 @@ __global__ void ptmh_spec_scatter_kernel(int C, bcm3hip_spec S, double* __restri
     if (id < C) {
         llh_prop[id] = S.batch_llh[pos];
         S.steps_prop[id] = S.batch_steps[pos];
-        S.steps_hint[id] = S.batch_steps[pos];
     } else {
         S.cand_llh[id - C] = S.batch_llh[pos];
         S.cand_steps[id - C] = S.batch_steps[pos];
@@ -905,12 +904,38 @@ __global__ void ptmh_spec_select_kernel(int C, int d, const double* __restrict__
     lprior_prop[c] = S.cand_lp[sl];
     log_mh[c] = S.cand_lmh[sl];
     llh_prop[c] = S.cand_llh[sl];
-    S.steps_hint[c] = S.cand_steps[sl];
+    S.steps_prop[c] = S.cand_steps[sl];
     if (hot) {
         const int upd = S.cand_upd[sl];
         if (upd >= 0) P.scale[(int64_t)c * P.kmax + upd] = S.cand_sc[sl];
         P.selected[c] = S.cand_sel[sl];
     }
+}
+
+// dispatch-order bookkeeping of the pairs: steps_hint[c] = BDF steps of the solve of the state now in
+// slot c; after an accept (acc[c]: the proposal, whose steps are steps_prop[c], became the state) ...
+__global__ void ptmh_spec_track_accept_kernel(int C, const uint8_t* __restrict__ acc, bcm3hip_spec S)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    if (acc[c]) S.steps_hint[c] = S.steps_prop[c];
+}
+// ... and after an exchange round (acc_exc[pair_first[c]]: c took its partner's state); one
+// workgroup, the old values read before any is written
+__global__ void __launch_bounds__(1024) ptmh_spec_track_exchange_kernel(int C, const int32_t* __restrict__ partner,
+                                                                        const int32_t* __restrict__ pair_first,
+                                                                        const uint8_t* __restrict__ acc_exc,
+                                                                        bcm3hip_spec S)
+{
+    int v[4];
+    int n = 0;
+    for (int c = threadIdx.x; c < C && n < 4; c += blockDim.x, n++) {
+        const int p = partner[c];
+        v[n] = (p >= 0 && acc_exc[pair_first[c]]) ? S.steps_hint[p] : S.steps_hint[c];
+    }
+    __syncthreads();
+    n = 0;
+    for (int c = threadIdx.x; c < C && n < 4; c += blockDim.x, n++) S.steps_hint[c] = v[n];
 }
 
 bool proposal_ok(const bcm3hip_proposal* P, int C, int d)
@@ -1022,6 +1047,21 @@ int bcm3hip_ptmh_spec_select(int C, int d, const double* temps, const int32_t* p
     hipLaunchKernelGGL(ptmh_spec_select_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d, temps,
                        partner, pair_first, acc_mutate, acc_exchange, *spec, prop, lprior_prop, log_mh, llh_prop,
                        *proposal, error);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_spec_track(int C, const uint8_t* acc_mutate, const int32_t* partner, const int32_t* pair_first,
+                            const uint8_t* acc_exchange, const bcm3hip_spec* spec, void* stream)
+{
+    if (C <= 0 || C > 4096 || !spec_ok(spec) || (!acc_mutate && !acc_exchange) ||
+        (acc_exchange && (!partner || !pair_first)))
+        return BCM3HIP_ERR_ARG;
+    if (acc_mutate)
+        hipLaunchKernelGGL(ptmh_spec_track_accept_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, C,
+                           acc_mutate, *spec);
+    else
+        hipLaunchKernelGGL(ptmh_spec_track_exchange_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, partner,
+                           pair_first, acc_exchange, *spec);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -69,6 +69,8 @@ def _lib():
         L.bcm3_ptmh_iterate.argtypes = [vp, C.c_int64, C.c_int]
         L.bcm3_ptmh_run.argtypes = [vp, C.c_int64]
         L.bcm3_ptmh_adapt.argtypes = [vp]
+        L.bcm3_ptmh_spec_batch_info.argtypes = [vp, vp, vp]
+        L.bcm3_ptmh_spec_batch_info.restype = C.c_int64
         L.bcm3_ptmh_synchronize.argtypes = [vp]
         L.bcm3_ptmh_num_chains.argtypes = [vp]
         L.bcm3_ptmh_get_state.argtypes = [vp, vp, vp, vp, vp]
@@ -184,6 +186,13 @@ class PTMHNative:
 
     def run(self, num_samples: int):
         _check(_lib().bcm3_ptmh_run(self.h, int(num_samples)), "bcm3_ptmh_run")
+
+    def spec_batch_info(self):
+        """(src, steps) of the last speculative launch in dispatch order, or None"""
+        src = np.zeros(7 * self.C, dtype=np.int32)
+        steps = np.zeros(7 * self.C, dtype=np.int32)
+        n = _lib().bcm3_ptmh_spec_batch_info(self.h, src.ctypes.data, steps.ctypes.data)
+        return None if n < 0 else (src[:n], steps[:n])
 
     def adapt(self):
         _check(_lib().bcm3_ptmh_adapt(self.h), "bcm3_ptmh_adapt")

@@ -169,6 +169,11 @@ int bcm3_ptmh_iterate(bcm3_ptmh* s, int64_t n, int last_at_end);
  * Sampler::EvaluateLikelihood, src/sampler/Sampler.cpp:172-178) */
 int bcm3_ptmh_run(bcm3_ptmh* s, int64_t num_samples);
 int bcm3_ptmh_adapt(bcm3_ptmh* s);
+/* diagnostics of the speculative iteration pairs (bcm3_ptmh_config.speculate): the last pair's
+ * likelihood launch in dispatch order -- entry sources (c < C: chain c's proposal; C + 6c + k:
+ * candidate k of chain c, bcm3hip_spec) and BDF steps (src / steps: [7 C], may be NULL); returns the
+ * entry count, -1 when the sampler does not speculate */
+int64_t bcm3_ptmh_spec_batch_info(bcm3_ptmh* s, int32_t* src, int32_t* steps);
 /* wait for the stream; < 0 if a likelihood returned NaN */
 int bcm3_ptmh_synchronize(bcm3_ptmh* s);
 int bcm3_ptmh_num_chains(const bcm3_ptmh* s); /* chains of this rank */

@@ -431,8 +431,8 @@ typedef struct {
     double* cand_sc;      /* [C][6] its new scale */
     uint8_t* cand_active; /* [C][6] */
     int32_t* cand_steps;  /* [C][6] BDF steps of the candidate's solve */
-    int32_t* steps_hint;  /* [C] BDF steps of the last evaluation of the chain (dispatch order) */
-    int32_t* steps_prop;  /* [C] steps of iteration r's proposals */
+    int32_t* steps_hint;  /* [C] BDF steps of the solve of the state in each slot (dispatch order) */
+    int32_t* steps_prop;  /* [C] steps of the proposals being accepted or rejected */
     double* batch_x;      /* [7C][d] the launch's vectors, longest predicted solve first */
     double* batch_llh;    /* [7C] */
     int32_t* batch_status;/* [7C] */
@@ -462,6 +462,11 @@ int bcm3hip_ptmh_spec_select(int C, int d, const double* temps, const int32_t* p
                              const uint8_t* acc_mutate, const uint8_t* acc_exchange, const bcm3hip_spec* spec,
                              double* prop, double* lprior_prop, double* log_mh, double* llh_prop,
                              const bcm3hip_proposal* proposal, int32_t* error, void* stream);
+/* dispatch-order bookkeeping (steps_hint = BDF steps of the solve of the state in each slot): after an
+ * accept (acc_mutate: the proposals' steps, steps_prop, become the states') or, with acc_mutate NULL,
+ * after an exchange round (acc_exchange indexed by pair_first, partner as in spec_select) */
+int bcm3hip_ptmh_spec_track(int C, const uint8_t* acc_mutate, const int32_t* partner, const int32_t* pair_first,
+                            const uint8_t* acc_exchange, const bcm3hip_spec* spec, void* stream);
 /* The propose kernel's mixture arithmetic (GMM::CalculateResponsibilities, src/stats/GMM.cpp:172-186,
  * with the component densities of GMM::LogPdfMVN :392-398) at n points x[n][d] (device buffers,
  * d <= 64, K <= 64): logpdf[n] = log sum_k w_k N(x; mean_k, L_k L_k^T), resp[n][K]; either may be

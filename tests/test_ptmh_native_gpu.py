@@ -226,13 +226,13 @@ def test_speculative_pairs_bit_identical(tmp_path, proposal, C, t_dof):
     res = []
     for spec in (0, 1):
         for every in (1, 3):
-            # adaptation after si = 14 (the first iteration of a pair: that pair is not formed) or after
-            # si = 47 (the second iteration of a pair)
-            s = _native(*C3, C, 17, 0, proposal=proposal, adapt_proposal_samples=15 if every == 1 else 16,
+            # adaptation after si = 40 (the first iteration of a pair: that pair is not formed) or after
+            # si = 41 (every = 3, adaptation every 14 samples: the second iteration of a pair)
+            s = _native(*C3, C, 17, 0, proposal=proposal, adapt_proposal_samples=41 if every == 1 else 14,
                         adapt_proposal_times=2, t_dof=t_dof, speculate=spec, use_every_nth=every)
             out = str(tmp_path / f"out_{spec}_{every}.nc")
-            s.set_output(out, 90 // every, flush_every=7)
-            s.iterate(91 if every == 1 else 90)
+            s.set_output(out, 130 // every, flush_every=7)
+            s.iterate(131 if every == 1 else 130)
             s.synchronize()
             s.flush_output()
             st, c, nc = s.state(), s.counters(), s.components()

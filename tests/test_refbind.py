@@ -66,7 +66,7 @@ def test_c3_through_the_reference_interface(tmp_path, mode):
     assert r.returncode == 0, r.stderr
     e = parity.llh_err(got, gold["logp"])
     assert np.array_equal(np.isneginf(got), np.isneginf(gold["logp"]))
-    assert np.mean(e <= parity.LLH_T1) >= parity.LLH_T1_FRAC and np.all(e[np.isfinite(got)] <= parity.LLH_T2)
+    assert np.mean(e <= parity.LLH_T1) >= parity.llh_min_fraction(len(e)) and np.all(e[np.isfinite(got)] <= parity.LLH_T2)
 
 
 @pytest.mark.gpu

@@ -84,6 +84,24 @@ def main():
               "; ".join(f"lds {l}: as is {a:.3f} ms, longest first {b:.3f} ms" for l, a, b in row), flush=True)
         res[k]["ordered"] = min(b for _, _, b in row)
     ctx.close()
+    # the sampler's own speculative launches: kernel time per launch and how well the dispatch order
+    # (predicted from the chains' previous solves) follows the real solve lengths
+    s = PTMHNative(ll, PRI, 256, seed=20251016, proposal="gaussian_mixture")
+    s.iterate(warm)
+    ll.set_option(_hip.OPT_TIMING_LOG, 1)
+    s.iterate(20)
+    s.synchronize()
+    tt, nl, mx = ll.kernel_time_log()
+    ll.set_option(_hip.OPT_TIMING_LOG, 0)
+    src, steps = s.spec_batch_info()
+    s.close()
+    n = len(steps)
+    rank = np.argsort(np.argsort(-steps, kind="stable"), kind="stable")  # 0 = longest
+    top = np.argsort(-steps, kind="stable")[:64]
+    print(f"sampler: {nl} launches for 20 iterations, {tt / nl:.3f} ms per launch (max {mx:.3f}); last batch "
+          f"{n} entries, steps max {steps.max()} mean {steps.mean():.0f}; the 64 longest solves sit at dispatch "
+          f"positions median {np.median(top):.0f} (max {top.max()}); rank correlation "
+          f"{np.corrcoef(np.arange(n), rank)[0, 1]:.2f}", flush=True)
     base = res[1][1]
     for k, label in ((5, "1 + 4 candidates"), (7, "1 + 6 candidates")):
         t = min(res[k].values())
