@@ -271,6 +271,11 @@ struct SamplerPTDevice::Impl {
         sp_batch_steps, sp_batch_src, sp_batch_n, sp_err;
     DevBuf<uint8_t> sp_cand_active, acc_mut, acc_exc;
     DevBuf<int32_t> partner[2], pair_first[2];
+    DevBuf<double> sp_send_last, sp_send_first, sp_remote;  // boundary rows [state | proposal] of a sharded ladder
+    DevBuf<uint8_t> cross_acc;
+    DevBuf<int32_t> sp_pred;
+    DevBuf<double> sp_inv_scale;  // 1 / prior sd per variable (the predictor's distance)
+    bool cross_round[2] = {false, false};  // do the slice-boundary pairs exchange in rounds of this parity
     bcm3hip_spec S{};
     int64_t spec_pairs = 0;
 
@@ -424,8 +429,11 @@ struct SamplerPTDevice::Impl {
         }
         std::vector<double> pp(C);
         for (int64_t c = 0; c < C; c++) pp[c] = (temps_host[c] == 0.0) ? q[c] : q[c] + temps_host[c] * l[c];
+        // (the counted evaluations above used batch_n: reset, so the first pair predicts from hints)
         return Upload(values, v, stream) && Upload(lprior, q, stream) && Upload(llh, l, stream) &&
-               Upload(lpp, pp, stream) && (!spec_on || Upload(sp_steps_hint, hint, stream));
+               Upload(lpp, pp, stream) &&
+               (!spec_on || (Upload(sp_steps_hint, hint, stream) &&
+                             bcm3hip_memset_async(sp_batch_n.p, 0, sizeof(int32_t), stream) == 0));
     }
 
     bool HistoryAdd(const uint8_t* mask)
@@ -470,7 +478,7 @@ struct SamplerPTDevice::Impl {
     int Next() const { return (cfg.rank + 1) % cfg.world; }
     int Prev() const { return (cfg.rank - 1 + cfg.world) % cfg.world; }
 
-    bool Cross(bool do_next, bool do_prev, int64_t gp)
+    bool Cross(bool do_next, bool do_prev, int64_t gp, uint8_t* acc_out = nullptr)
     {
         const size_t n = (size_t)d + 4;
         if (!Launch(bcm3hip_pt_pack_boundary((int)C, d, temps.p, values.p, llh.p, lprior.p, lpp.p,
@@ -501,12 +509,12 @@ struct SamplerPTDevice::Impl {
             return false;
         }
         return Launch(bcm3hip_pt_cross_accept((int)C, d, g0, gp, do_next, do_prev, temps.p, values.p, llh.p,
-                                              lprior.p, lpp.p, recv_next.p, recv_prev.p, nullptr,
+                                              lprior.p, lpp.p, recv_next.p, recv_prev.p, acc_out,
                                               do_next ? acc_exchange.p : nullptr, cfg.seed, (uint64_t)round, stream),
                       "pt_cross_accept");
     }
 
-    bool Exchange(uint8_t* acc_mask = nullptr)
+    bool Exchange(uint8_t* acc_mask = nullptr, uint8_t* cross_out = nullptr)
     {
         // DoExchangeMove (SamplerPT.cpp:277-298): pairs inside the slice on the GPU, the two
         // slice-boundary pairs over the transport (sampler.sharded_exchange_round)
@@ -522,7 +530,7 @@ struct SamplerPTDevice::Impl {
         for (int64_t i = 0; i + 1 < C; i++)
             if (((g0 + i - start) % 2 + 2) % 2 == 0) attempted++;
         if (cfg.world > 1 && ((g0 + C - 1 - start) % 2 + 2) % 2 == 0) {
-            if (!Cross(true, true, (int64_t)Prev() * C + C - 1)) return false;
+            if (!Cross(true, true, (int64_t)Prev() * C + C - 1, cross_out)) return false;
             attempted++;
         }
         cnt.attempted_exchange += attempted;
@@ -620,18 +628,39 @@ struct SamplerPTDevice::Impl {
     bool IterationPair(bool last)
     {
         const int cur = (int)(round % 2);  // start parity of exchange round r
-        if (!Exchange(acc_exc.p) ||
+        if (!Exchange(acc_exc.p, cross_acc.p) ||
             !Launch(bcm3hip_ptmh_spec_track((int)C, nullptr, partner[cur].p, pair_first[cur].p, acc_exc.p, &S, stream),
                     "ptmh_spec_track"))
             return false;
         const int nxt = (int)(round % 2);  // start parity of exchange round r + 1
         if (!Launch(bcm3hip_ptmh_propose_adaptive((int)C, d, pkind.p, p0.p, p1.p, p2.p, temps.p, values.p, prop.p,
                                                   lprior_prop.p, log_mh.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
-                    "ptmh_propose_adaptive") ||
-            !Launch(bcm3hip_ptmh_spec_candidates((int)C, d, pkind.p, p0.p, p1.p, p2.p, temps.p, values.p, prop.p,
-                                                 partner[nxt].p, &P, &S, g0, cfg.seed, (uint64_t)iter + 1, stream),
+                    "ptmh_propose_adaptive"))
+            return false;
+        if (cross_round[nxt]) {
+            // a sharded ladder whose boundary pairs exchange in round r + 1: the neighbours' boundary
+            // chains' (state, proposal) rows, for the candidates that start from them
+            const size_t row = (size_t)d * sizeof(double);
+            if (bcm3hip_memcpy_async(sp_send_last.p, values.p + (C - 1) * d, row, BCM3HIP_D2D, stream) != 0 ||
+                bcm3hip_memcpy_async(sp_send_last.p + d, prop.p + (C - 1) * d, row, BCM3HIP_D2D, stream) != 0 ||
+                bcm3hip_memcpy_async(sp_send_first.p, values.p, row, BCM3HIP_D2D, stream) != 0 ||
+                bcm3hip_memcpy_async(sp_send_first.p + d, prop.p, row, BCM3HIP_D2D, stream) != 0)
+                return false;
+            const double* sends[2] = {sp_send_last.p, sp_send_first.p};
+            const int speer[2] = {Next(), Prev()};
+            double* recvs[2] = {sp_remote.p + 2 * d, sp_remote.p};  // from prev -> PREV slot, from next -> NEXT slot
+            const int rpeer[2] = {Prev(), Next()};
+            if (!transport || !transport->Exchange(2, sends, speer, 2, recvs, rpeer, (size_t)(2 * d), stream)) {
+                LOGERROR("speculative boundary rows: transport failed (rank %d)", cfg.rank);
+                return false;
+            }
+        }
+        if (!Launch(bcm3hip_ptmh_spec_candidates((int)C, d, pkind.p, p0.p, p1.p, p2.p, temps.p, values.p, prop.p,
+                                                 partner[nxt].p, sp_remote.p, &P, &S, g0, cfg.seed, (uint64_t)iter + 1,
+                                                 stream),
                     "ptmh_spec_candidates") ||
-            !Launch(bcm3hip_ptmh_spec_batch((int)C, d, prop.p, partner[nxt].p, &S, stream), "ptmh_spec_batch"))
+            !Launch(bcm3hip_ptmh_spec_batch((int)C, d, prop.p, partner[nxt].p, sp_inv_scale.p, &S, stream),
+                    "ptmh_spec_batch"))
             return false;
         if (!ll->EvaluateLogProbabilityBatchDeviceCounted((size_t)C * (1 + BCM3HIP_SPEC_SLOTS), S.batch_n, S.batch_x,
                                                           S.batch_llh, S.batch_status, S.batch_steps, stream)) {
@@ -651,13 +680,13 @@ struct SamplerPTDevice::Impl {
         iter++;
         if (!PostIteration(false)) return false;
         // iteration r + 1
-        if (!Exchange(acc_exc.p) ||
+        if (!Exchange(acc_exc.p, cross_acc.p) ||
             !Launch(bcm3hip_ptmh_spec_track((int)C, nullptr, partner[nxt].p, pair_first[nxt].p, acc_exc.p, &S, stream),
                     "ptmh_spec_track"))
             return false;
         if (!Launch(bcm3hip_ptmh_spec_select((int)C, d, temps.p, partner[nxt].p, pair_first[nxt].p, acc_mut.p,
-                                             acc_exc.p, &S, prop.p, lprior_prop.p, log_mh.p, llh_prop.p, &P, sp_err.p,
-                                             stream),
+                                             acc_exc.p, cross_acc.p, sp_remote.p, values.p, &S, prop.p, lprior_prop.p,
+                                             log_mh.p, llh_prop.p, &P, sp_err.p, stream),
                     "ptmh_spec_select") ||
             !Launch(bcm3hip_ptmh_accept_adaptive((int)C, d, temps.p, prop.p, lprior_prop.p, llh_prop.p, log_mh.p,
                                                  cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, acc_mut.p,
@@ -698,7 +727,7 @@ struct SamplerPTDevice::Impl {
 
     bool SetupSpeculation()
     {
-        spec_on = cfg.speculate != 0 && adaptive && cfg.world == 1 && cfg.swapping_scheme == 0 &&
+        spec_on = cfg.speculate != 0 && adaptive && (cfg.world == 1 || transport) && cfg.swapping_scheme == 0 &&
                   cfg.exploration_steps == 1 && Ctot >= 2 && d <= 64 && C * (1 + BCM3HIP_SPEC_SLOTS) <= 4096 &&
                   ll->SupportsCountedBatch();
         if (!spec_on) return true;
@@ -709,7 +738,8 @@ struct SamplerPTDevice::Impl {
                   sp_steps_hint.alloc(C) && sp_steps_prop.alloc(C) && sp_batch_x.alloc(N * d) &&
                   sp_batch_llh.alloc(N) && sp_batch_status.alloc(N) && sp_batch_steps.alloc(N) &&
                   sp_batch_src.alloc(N) && sp_batch_n.alloc(1) && sp_err.alloc(1) && acc_mut.alloc(C) &&
-                  acc_exc.alloc(C);
+                  acc_exc.alloc(C) && sp_send_last.alloc(2 * d) && sp_send_first.alloc(2 * d) &&
+                  sp_remote.alloc(4 * d) && cross_acc.alloc(2) && sp_pred.alloc(N) && sp_inv_scale.alloc(d);
         for (int st = 0; st < 2 && ok; st++) ok = partner[st].alloc(C) && pair_first[st].alloc(C);
         if (!ok) {
             LOGERROR("SamplerPTDevice: speculative buffers could not be allocated");
@@ -730,9 +760,21 @@ struct SamplerPTDevice::Impl {
                 pa[0] = (int32_t)(C - 1);
                 pf[C - 1] = pf[0] = (int32_t)(C - 1);
             }
+            // sharded: the slice-boundary pairs over the transport (Exchange: both cross pairs of a
+            // rank exchange in the same rounds, C being even)
+            cross_round[st] = cfg.world > 1 && ((g0 + C - 1 - st) % 2 + 2) % 2 == 0;
+            if (cross_round[st]) {
+                pa[C - 1] = BCM3HIP_SPEC_REMOTE_NEXT;
+                pa[0] = BCM3HIP_SPEC_REMOTE_PREV;
+            }
             if (!Upload(partner[st], pa, stream) || !Upload(pair_first[st], pf, stream)) return false;
         }
-        if (bcm3hip_memset_async(sp_steps_hint.p, 0, C * sizeof(int32_t), stream) != 0 ||
+        std::vector<double> isc(d);
+        for (int j = 0; j < d; j++)
+            isc[j] = (prior_var[j] > 0.0 && std::isfinite(prior_var[j])) ? 1.0 / std::sqrt(prior_var[j]) : 1.0;
+        if (!Upload(sp_inv_scale, isc, stream) ||
+            bcm3hip_memset_async(sp_batch_n.p, 0, sizeof(int32_t), stream) != 0 ||
+            bcm3hip_memset_async(sp_steps_hint.p, 0, C * sizeof(int32_t), stream) != 0 ||
             bcm3hip_memset_async(sp_batch_steps.p, 0, N * sizeof(int32_t), stream) != 0 ||
             bcm3hip_memset_async(sp_cand_steps.p, 0, C * K * sizeof(int32_t), stream) != 0 ||
             bcm3hip_memset_async(sp_err.p, 0, sizeof(int32_t), stream) != 0)
@@ -754,6 +796,7 @@ struct SamplerPTDevice::Impl {
         S.batch_steps = sp_batch_steps.p;
         S.batch_src = sp_batch_src.p;
         S.batch_n = sp_batch_n.p;
+        S.pred_steps = sp_pred.p;
         return true;
     }
 

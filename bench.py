@@ -52,6 +52,9 @@ def parse():
     ap.add_argument("--seed", type=int, default=20251016)
     ap.add_argument("--loop", default="native", choices=("native", "python"),
                     help="native: the C++ sampler (bcm3_ptmh_*); python: bcm3_amd.sampler.PTMHDevice")
+    ap.add_argument("--speculate", type=int, default=1,
+                    help="C++ loop: 1 = speculative iteration pairs (one likelihood launch per two iterations, "
+                         "bit-identical chains), 0 = one launch per iteration")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--throughput-batch", type=int, default=16384,
                     help="extra: evals/s of one large batch (0 = skip); not the headline value")
@@ -115,7 +118,7 @@ class NativeLoop:
             dist.broadcast_object_list(obj, src=0)
             kw = dict(transport=TRANSPORT_RCCL, nccl_id=obj[0])
         self.s = PTMHNative(ll, PRIOR_XML, num_chains, rank=rank, world=world, seed=args.seed,
-                            proposal=args.proposal, **kw)
+                            proposal=args.proposal, speculate=args.speculate, **kw)
         self.exploration_steps = 1
 
     def run(self, n):
@@ -564,11 +567,15 @@ def main():
 
     evals = C * world * args.steps * loop.exploration_steps
     value = evals / dt
+    # committed evaluations per likelihood launch on this rank: C for one launch per iteration, 2C when
+    # the C++ sampler runs speculative iteration pairs (one launch for two iterations; the launch also
+    # evaluates the candidates that did not happen, which are not counted anywhere)
+    per_launch = C * args.steps * loop.exploration_steps / max(1, k_launches)
     b_eval = algorithmic_bytes_per_eval(m)
-    achieved_gbs = b_eval * C / (k_avg * 1e-3) / 1e9
+    achieved_gbs = b_eval * per_launch / (k_avg * 1e-3) / 1e9
     tb = traffic_from_profiles("c3_256", C)
     f_alg = flops_per_eval()
-    achieved_tf = f_alg * C / (k_avg * 1e-3) / 1e12  # the kernel's own rate, like achieved_gbs
+    achieved_tf = f_alg * per_launch / (k_avg * 1e-3) / 1e12  # the kernel's own rate, like achieved_gbs
     issue = issue_rate(ll, loop.values(), device) if rank == 0 else None
 
     extra = {}
@@ -642,8 +649,10 @@ def main():
             "lanes_per_wave": args.lanes_per_wave or "auto",
             "parallelism": f"chains sharded over {world} rank(s); PT swap = RCCL neighbour send/recv",
             "proposal": args.proposal,
-            "sampler_loop": "C++ host loop (libbcm3.so bcm3_ptmh_iterate)" if loop_kind == "native"
-            else "Python loop (bcm3_amd.sampler.PTMHDevice)",
+            "sampler_loop": ("C++ host loop (libbcm3.so bcm3_ptmh_iterate), speculative iteration pairs"
+                             if loop_kind == "native" and k_launches < args.steps else
+                             "C++ host loop (libbcm3.so bcm3_ptmh_iterate)" if loop_kind == "native"
+                             else "Python loop (bcm3_amd.sampler.PTMHDevice)"),
         },
         "roofline": {
             "bound": "hbm",
@@ -654,6 +663,8 @@ def main():
             "traffic": tb,
             "kernel": "popk_traj_kernel<TWO>",
             "kernel_ms_avg": k_avg,
+            "committed_evals_per_launch": per_launch,
+            "launches_per_step": k_launches / max(1, args.steps),
             "algorithmic_bytes_per_eval": b_eval,
             "achieved_fp64": achieved_tf,
             "peak_fp64": FP64_VECTOR_PEAK_TFLOPS,

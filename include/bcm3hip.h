@@ -421,6 +421,10 @@ int bcm3hip_ptmh_accept_adaptive(int C, int d, const double* temps, const double
  * 5 prop_p (swapped, own accept; only when the branch differs). T == 0 chains: slot 0 (a prior
  * draw). All pointers are device pointers sized for C chains (slots [C][6]). */
 enum { BCM3HIP_SPEC_SLOTS = 6 };
+/* partner codes besides local chain indices: -1 none, and the neighbour ranks' boundary chains of a
+ * sharded ladder (my last chain pairs with the next rank's first, my first with the previous rank's
+ * last) whose (state, proposal) rows arrive in `remote` = [next: state d | proposal d][prev: ...] */
+enum { BCM3HIP_SPEC_REMOTE_NEXT = -2, BCM3HIP_SPEC_REMOTE_PREV = -3 };
 typedef struct {
     double* cand_x;       /* [C][6][d] candidate proposals */
     double* cand_lp;      /* [C][6] their log prior */
@@ -445,8 +449,8 @@ typedef struct {
 int bcm3hip_ptmh_spec_candidates(int C, int d, const int32_t* prior_kind, const double* prior_p0,
                                  const double* prior_p1, const double* prior_p2, const double* temps,
                                  const double* values, const double* prop, const int32_t* partner,
-                                 const bcm3hip_proposal* proposal, const bcm3hip_spec* spec, int64_t chain0,
-                                 uint64_t seed, uint64_t iter_next, void* stream);
+                                 const double* remote, const bcm3hip_proposal* proposal, const bcm3hip_spec* spec,
+                                 int64_t chain0, uint64_t seed, uint64_t iter_next, void* stream);
 /* the launch's batch: iteration r's C proposals + the active candidates, ordered by the predicted
  * length of their solves (steps_hint of the chain whose state they start from), longest first (C <= 1024) */
 int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* partner, const bcm3hip_spec* spec,
@@ -454,14 +458,17 @@ int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* par
 /* batch results back: llh_prop[c] (iteration r), cand_llh / cand_steps, steps_prop */
 int bcm3hip_ptmh_spec_scatter(int C, const bcm3hip_spec* spec, double* llh_prop, void* stream);
 /* after accept r (accept_out = acc_mutate[C]) and exchange r + 1 (accept_out = acc_exchange, indexed
- * by the first chain of each pair; pair_first[c] = that chain for c's pair in round r + 1): iteration
+ * by the first chain of each pair; pair_first[c] = that chain for c's pair in round r + 1; for a
+ * sharded ladder cross_acc[2] = pt_cross_accept's flags, remote / values as in spec_candidates and
+ * after the exchange): iteration
  * r + 1's proposal, log prior, MH ratio and log-likelihood of each chain, and the proposal state
  * writes its propose would have made (scale Update, selected component). *error != 0 if a needed
  * candidate was not evaluated (never expected). */
 int bcm3hip_ptmh_spec_select(int C, int d, const double* temps, const int32_t* partner, const int32_t* pair_first,
-                             const uint8_t* acc_mutate, const uint8_t* acc_exchange, const bcm3hip_spec* spec,
-                             double* prop, double* lprior_prop, double* log_mh, double* llh_prop,
-                             const bcm3hip_proposal* proposal, int32_t* error, void* stream);
+                             const uint8_t* acc_mutate, const uint8_t* acc_exchange, const uint8_t* cross_acc,
+                             const double* remote, const double* values, const bcm3hip_spec* spec, double* prop,
+                             double* lprior_prop, double* log_mh, double* llh_prop, const bcm3hip_proposal* proposal,
+                             int32_t* error, void* stream);
 /* dispatch-order bookkeeping (steps_hint = BDF steps of the solve of the state in each slot): after an
  * accept (acc_mutate: the proposals' steps, steps_prop, become the states') or, with acc_mutate NULL,
  * after an exchange round (acc_exchange indexed by pair_first, partner as in spec_select) */

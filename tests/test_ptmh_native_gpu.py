@@ -260,3 +260,45 @@ def test_speculation_is_used_for_popk():
     s.ll.set_option(_hip.OPT_TIMING_LOG, 0)
     s.close()
     assert launches == 10
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_speculative_pairs_sharded_ladder(world):
+    """speculative pairs on a sharded C3 ladder (in-process ranks, host-staged transport): the boundary
+    chains' candidates start from the neighbour rank's (state, proposal) rows, the cross-rank swap
+    picks among them -- bit-identical to the single-rank loop without speculation"""
+    C, seed, steps = 32, 13, 61
+    kw = dict(adapt_proposal_samples=25, adapt_proposal_times=1)
+    one = _native(*C3, C, seed, steps, speculate=0, **kw)
+    one.iterate(steps)
+    one.synchronize()
+    ref, cref = one.state(), one.counters()
+    one.close()
+    from bcm3_amd.ptmh import LocalGroup
+    group = LocalGroup(world)
+    ranks = [_native(*C3, C, seed, steps, rank=r, world=world, group=group, speculate=1, **kw)
+             for r in range(world)]
+    errors = []
+
+    def go(s):
+        try:
+            s.iterate(steps)
+            s.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=go, args=(s,)) for s in ranks]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    got = [s.state() for s in ranks]
+    infos = [s.spec_batch_info() for s in ranks]
+    acc = sum(s.counters()["accepted_mutate"] for s in ranks)
+    for s in ranks:
+        s.close()
+    assert all(i is not None for i in infos), "speculation not used"
+    for k in ("values", "llh", "lprior", "lpp"):
+        assert _same(np.concatenate([g[k] for g in got]), ref[k]), k
+    assert acc == cref["accepted_mutate"]
