@@ -442,7 +442,8 @@ typedef struct {
     int32_t* batch_status;/* [7C] */
     int32_t* batch_steps; /* [7C] */
     int32_t* batch_src;   /* [7C] source of each batch entry: c < C proposal of chain c, C + 6c + k candidate */
-    int32_t* batch_n;     /* [1] entries in use */
+    int32_t* batch_n;     /* [1] entries in use (0 before the first launch) */
+    int32_t* pred_steps;  /* [7C] predicted solve length of each entry (batch order key) */
 } bcm3hip_spec;
 /* candidates of iteration iter_next = r + 1 (after bcm3hip_ptmh_propose_adaptive of iteration r, whose
  * proposals are in prop); partner[c] = exchange partner of chain c in round r + 1 (-1 none) */
@@ -452,9 +453,11 @@ int bcm3hip_ptmh_spec_candidates(int C, int d, const int32_t* prior_kind, const 
                                  const double* remote, const bcm3hip_proposal* proposal, const bcm3hip_spec* spec,
                                  int64_t chain0, uint64_t seed, uint64_t iter_next, void* stream);
 /* the launch's batch: iteration r's C proposals + the active candidates, ordered by the predicted
- * length of their solves (steps_hint of the chain whose state they start from), longest first (C <= 1024) */
-int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* partner, const bcm3hip_spec* spec,
-                            void* stream);
+ * length of their solves, longest first (C <= 585): the mean BDF steps of the entry's 4 nearest
+ * neighbours among the previous launch's entries, distances scaled by inv_scale[d] (1 / prior sd);
+ * before any launch, the steps_hint of the slot the entry starts from */
+int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* partner, const double* inv_scale,
+                            const bcm3hip_spec* spec, void* stream);
 /* batch results back: llh_prop[c] (iteration r), cand_llh / cand_steps, steps_prop */
 int bcm3hip_ptmh_spec_scatter(int C, const bcm3hip_spec* spec, double* llh_prop, void* stream);
 /* after accept r (accept_out = acc_mutate[C]) and exchange r + 1 (accept_out = acc_exchange, indexed
