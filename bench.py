@@ -410,7 +410,16 @@ def cellpop_workload(device, gen, n=64):
         cells += len(rec)
         steps += int(rec["nsteps"].sum())
     ll.close()
-    return {"chains": n, "kernel_ms": ms, "evals_per_s": n / (ms * 1e-3), "cells_per_eval": cells / n,
+    # FP64 roofline: F_alg per cell BDF step from the operation-count model over the reference CVODE's
+    # own per-cell counters (tests/golden/make_c4_falg.py), times the cell steps this launch took
+    with open(os.path.join(GOLDEN, "c4_falg.json")) as fh:
+        falg = json.load(fh)
+    tf = falg["flops_per_cell_step"] * steps / (ms * 1e-3) / 1e12
+    roof = {"bound": "fp64-vector (latency-limited chains)", "achieved": tf, "peak": FP64_VECTOR_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": tf / FP64_VECTOR_PEAK_TFLOPS,
+            "flops_per_cell_step": falg["flops_per_cell_step"], "cell_steps_per_launch": steps,
+            "method": falg["method"]}
+    return {"chains": n, "kernel_ms": ms, "evals_per_s": n / (ms * 1e-3), "cells_per_eval": cells / n, "roofline": roof,
             "cell_trajectories_per_s": cells / (ms * 1e-3), "bdf_steps_per_cell": steps / max(1, cells),
             "cell_bdf_steps_per_s": steps / (ms * 1e-3), "cells_per_wavefront": 4,
             "note": "throughput-bound (every SIMD busy); four cells per wavefront, one 16-lane row each "

@@ -33,6 +33,15 @@ def main():
     imax = int(np.argmax(tot))
     print(f"n={n} lpw={lpw} kernel {ms:.3f} ms; slowest traj {tot[imax]:.3e} cycles, {nst[imax]:.0f} steps "
           f"-> {tot[imax] / nst[imax]:.0f} cycles/step; implied clock {tot[imax] / (ms * 1e-3) / 1e9:.2f} GHz")
+    # the slowest trajectory (the one the launch waits for) and the 10 slowest
+    slow = np.argsort(-tot)[:10]
+    print(f"slowest trajectory: {nst[imax]:.0f} steps, nfe {g['stats']['nfe'][imax, 0]}, netf {g['stats']['netf'][imax, 0]}, "
+          f"ncfn {g['stats']['ncfn'][imax, 0]}, nsetups {g['stats']['nsetups'][imax, 0]}; its cycles per step by phase:")
+    for k, name in enumerate(NAMES):
+        print(f"  {name:24s} {ph[imax, k] / nst[imax]:8.0f}")
+    print(f"10 slowest: steps {nst[slow].astype(int).tolist()}, cycles/step {(tot[slow] / nst[slow]).round(0).tolist()}")
+    print(f"all: steps mean {nst.mean():.0f}, cycles/step mean {(tot / nst).mean():.0f}; "
+          f"corr(steps, cycles/step) {np.corrcoef(nst, tot / nst)[0, 1]:.2f}")
     per = ph.sum(axis=0) / nst.sum()
     print(f"mean cycles per step {per.sum():.0f}:")
     for k, name in enumerate(NAMES):
