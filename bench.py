@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--throughput-batch", type=int, default=16384,
                     help="extra: evals/s of one large batch (0 = skip); not the headline value")
+    ap.add_argument("--issue-probe", type=int, default=1,
+                    help="measure cycles per BDF step on a plain 256-proposal launch after the timed region "
+                         "(0 = skip, so a kernel trace holds only the sampler's launches)")
     ap.add_argument("--extras", type=int, default=1, help="extra: P=64 and circular workloads (0 = skip)")
     return ap.parse_args()
 
@@ -585,7 +588,7 @@ def main():
     tb = traffic_from_profiles("c3_256", C)
     f_alg = flops_per_eval()
     achieved_tf = f_alg * per_launch / (k_avg * 1e-3) / 1e12  # the kernel's own rate, like achieved_gbs
-    issue = issue_rate(ll, loop.values(), device) if rank == 0 else None
+    issue = issue_rate(ll, loop.values(), device) if rank == 0 and args.issue_probe else None
 
     extra = {}
     if rank == 0 and args.throughput_batch > 0:
@@ -687,7 +690,7 @@ def main():
         },
         "nan_llh_detected": nan_flag,
         "cpu_baseline": cpu,
-        "kernel_share_of_step": k_avg / (dt / args.steps * 1e3),
+        "kernel_share_of_step": k_avg * k_launches / max(1, args.steps) / (dt / args.steps * 1e3),
         "mutate_acceptance": acc_mut,
         **extra,
     }

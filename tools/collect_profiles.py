@@ -32,6 +32,21 @@ def main():
             print("copied", b)
     subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_traffic.py"), src, dst, tag, "256"], check=True,
                    stdout=subprocess.DEVNULL)
+    # per-dispatch durations of the BDF kernel by launch size (kernel trace of the bench): the
+    # speculative-pair launches are the largest grid; the bench's own HIP-event average is over them
+    tr = os.path.join(src, "kt", "kt_kernel_trace.csv")
+    if os.path.exists(tr):
+        import collections
+        import csv
+        by = collections.defaultdict(list)
+        for r in csv.DictReader(open(tr)):
+            if "popk_traj_kernel" in r["Kernel_Name"]:
+                by[r.get("Grid_Size_X", r.get("Grid_Size", "?"))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+        summ = {g: {"dispatches": len(v), "avg_ms": sum(v) / len(v), "min_ms": min(v), "max_ms": max(v)}
+                for g, v in by.items()}
+        with open(os.path.join(dst, f"{tag}_popk_dispatch_durations.json"), "w") as f:
+            json.dump(summ, f, indent=1)
+        print("wrote", f"{tag}_popk_dispatch_durations.json")
     # second SQ pass
     import collections
     import csv

@@ -17,18 +17,25 @@ KERNEL = "popk_traj_kernel"
 
 
 def per_launch(path, counter):
+    """mean over the dispatches of the most frequent grid size (the bench's speculative-pair launches;
+    the few plain launches of its start and of the issue-rate probe are left out), and that grid"""
     vals = collections.defaultdict(float)
+    grid = {}
     for r in csv.DictReader(open(path)):
         if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
-    v = list(vals.values())
-    return (sum(v) / len(v), len(v)) if v else (None, 0)
+            grid[r["Dispatch_Id"]] = r.get("Grid_Size", "?")
+    if not vals:
+        return None, 0, None
+    g = collections.Counter(grid.values()).most_common(1)[0][0]
+    v = [x for d, x in vals.items() if grid[d] == g]
+    return sum(v) / len(v), len(v), g
 
 
 def main():
     src, dst, tag, n = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
-    fetch_kb, nf = per_launch(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv"), "FETCH_SIZE")
-    write_kb, nw = per_launch(os.path.join(src, "pmc_write", "pmc_counter_collection.csv"), "WRITE_SIZE")
+    fetch_kb, nf, grid = per_launch(os.path.join(src, "pmc_fetch", "pmc_counter_collection.csv"), "FETCH_SIZE")
+    write_kb, nw, _ = per_launch(os.path.join(src, "pmc_write", "pmc_counter_collection.csv"), "WRITE_SIZE")
     sq = {}
     sq_path = os.path.join(src, "pmc_sq", "pmc_counter_collection.csv")
     for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES"):
@@ -37,6 +44,7 @@ def main():
         "n": n,
         "kernel": KERNEL,
         "launches_fetch_pass": nf,
+        "grid_size": grid,
         "launches_write_pass": nw,
         "fetch_kb_per_launch": fetch_kb,
         "write_kb_per_launch": write_kb,
