@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("BCM3HIP_LIB") or os.path.join(_HERE, "lib", "libbcm3h
 PK_TYPES = {"one": 0, "two": 1, "one_biphasic": 2, "two_biphasic": 3, "one_transit": 4, "two_transit": 5}
 ANALYTIC_BANANA, ANALYTIC_CIRCULAR = 1, 2
 OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES, OPT_TIMING_LOG, OPT_UNI_SOLVER, OPT_BLOCK_LDS = 1, 2, 3, 4, 5
+OPT_PLACEMENT_LOG = 6
 PRIOR_UNIFORM, PRIOR_NORMAL = 0, 1
 PROPOSAL_GLOBAL_COVARIANCE, PROPOSAL_GAUSSIAN_MIXTURE = 0, 1
 PROPOSAL_KMAX = 16
@@ -126,6 +127,9 @@ def lib() -> C.CDLL:
     L.bcm3hip_eval_batch.argtypes = [vp, sz, sz, vp, vp, vp]
     L.bcm3hip_eval_batch_device.argtypes = [vp, sz, vp, vp, vp, vp]
     L.bcm3hip_last_kernel_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    if hasattr(L, "bcm3hip_placement_log"):  # (absent from libraries built before it: tools/variant_timing.py)
+        L.bcm3hip_placement_log.argtypes = [vp, i64, vp]
+        L.bcm3hip_placement_log.restype = i64
     L.bcm3hip_eval_batch_detail.argtypes = [vp, sz, sz, vp, vp, vp, vp, vp, vp]
     for f in ("bcm3hip_open_popk", "bcm3hip_open_analytic", "bcm3hip_open_expm_pk", "bcm3hip_close", "bcm3hip_set_option",
               "bcm3hip_num_variables", "bcm3hip_eval_batch", "bcm3hip_eval_batch_device",
@@ -241,6 +245,16 @@ class Context:
         ms = C.c_float()
         check(lib().bcm3hip_last_kernel_ms(self.h, C.byref(ms)), "last_kernel_ms")
         return float(ms.value)
+
+    def placement_log(self, n_max: int):
+        """(n, 4) uint64 rows of the last PopPK launch with OPT_PLACEMENT_LOG on: HW_ID, XCC_ID,
+        wall clock (100 MHz) at start and at end of each trajectory."""
+        import numpy as np
+        out = np.zeros((n_max, 4), dtype=np.uint64)
+        m = lib().bcm3hip_placement_log(self.h, n_max, out.ctypes.data)
+        if m < 0:
+            check(int(m), "placement_log")
+        return out[:m]
 
     def kernel_time_log(self):
         """(total_ms, launches, max_ms) of the launches logged since the last call (OPT_TIMING_LOG)."""

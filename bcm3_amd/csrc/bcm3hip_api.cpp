@@ -77,6 +77,11 @@ struct bcm3hip_ctx {
     int uni_solver = 0;      // BCM3HIP_OPT_UNI_SOLVER
     int block_waves = 1;
     int block_lds = 0;  // BCM3HIP_OPT_BLOCK_LDS
+    bool place_log = false;  // BCM3HIP_OPT_PLACEMENT_LOG
+    uint64_t* place = nullptr;
+    size_t cap_place = 0;
+    int64_t place_n = 0;
+    hipStream_t place_stream = nullptr;
 };
 
 #define HIPCHK(x)                                                                                          \
@@ -136,6 +141,14 @@ int bcm3hip_device_count(void)
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess) return 0;
     return count;
+}
+
+int bcm3hip_current_device_simds(void)
+{
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    return 4 * cus;
 }
 
 const char* bcm3hip_error_string(int code)
@@ -444,6 +457,7 @@ int bcm3hip_close(bcm3hip_ctx* c)
     hipFree(c->tstatus);
     hipFree(c->traj);
     hipFree(c->stats);
+    hipFree(c->place);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->scratch_ev) hipEventDestroy(c->scratch_ev);
@@ -478,11 +492,26 @@ int bcm3hip_set_option(bcm3hip_ctx* c, int option, int64_t value)
         if (value < 0 || value > 65536) return BCM3HIP_ERR_ARG;
         c->block_lds = (int)value;
         return 0;
+    case BCM3HIP_OPT_PLACEMENT_LOG:
+        if (value != 0 && value != 1) return BCM3HIP_ERR_ARG;
+        c->place_log = value != 0;
+        return 0;
     default: return BCM3HIP_ERR_ARG;
     }
 }
 
 int bcm3hip_num_variables(const bcm3hip_ctx* c) { return c ? c->d : -1; }
+
+int64_t bcm3hip_placement_log(bcm3hip_ctx* c, int64_t n_max, uint64_t* host_out)
+{
+    if (!c || n_max < 0 || (n_max > 0 && !host_out)) return BCM3HIP_ERR_ARG;
+    if (!c->place || c->place_n == 0) return 0;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->place_stream));
+    const int64_t m = n_max < c->place_n ? n_max : c->place_n;
+    if (m > 0) HIPCHK(hipMemcpy(host_out, c->place, (size_t)m * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return m;
+}
 
 static int ensure_traj_scratch(bcm3hip_ctx* c, size_t n)
 {
@@ -530,9 +559,17 @@ static int launch(bcm3hip_ctx* c, size_t n, const double* dvalues, double* dlogp
     if (c->kind == 1) {
         int r = ensure_traj_scratch(c, n);
         if (r) return r;
+        uint64_t* place = nullptr;
+        if (c->place_log) {
+            if (grow(c->place, c->cap_place, 4 * n * (size_t)c->pm.P)) return BCM3HIP_ERR_ALLOC;
+            HIPCHK(hipMemsetAsync(c->place, 0, 4 * n * (size_t)c->pm.P * sizeof(uint64_t), s));
+            place = c->place;
+            c->place_n = (int64_t)(n * (size_t)c->pm.P);
+            c->place_stream = s;
+        }
         e = launch_popk(c->pm, (int64_t)n, dvalues, dlogp, dstatus, c->pllh, c->tstatus, dtraj, dstats,
                         c->lanes_per_wave ? c->lanes_per_wave : auto_lanes_per_wave(n * (size_t)c->pm.P),
-                        c->block_waves, c->uni_solver, s, e0, e1, c->block_lds, n_dev, dsteps);
+                        c->block_waves, c->uni_solver, s, e0, e1, c->block_lds, n_dev, dsteps, place);
     } else if (c->kind == 3) {
         const size_t per_eval = (size_t)c->xm.n_jobs * (size_t)(c->xm.n * c->xm.n);
         const size_t chunk = per_eval == 0 ? n : std::max<size_t>(1, kExpmScratchBytes / (per_eval * sizeof(double)));

@@ -512,43 +512,11 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
     return conv ? uni::ATTEMPT_ERR_FAIL : uni::ATTEMPT_CONV_FAIL;
 }
 
-// The first attempt of a fast_run step. cvSet's coefficients (l, tq[2], tq[5], the tq[1]/tq[3]
-// intermediates, gamma, gamrat) depend on h, tau[1..Q] and gammap only. After Q completed steps
-// at an unchanged h, tau[1..Q] all equal h, so every later step at that h with no linear-solver
-// setup in between recomputes exactly the values it already holds (52 % of the steps on C3 prior
-// draws, measured in the oracle): `reuse` skips the recomputation and keeps them -- the same
-// bits as computing them again.
-template <int Q, int NS, class S, class Model>
-BDF_INL int attempt_fast_q(S& s, const Model& mdl, double eta_eff, double saved_t, double& dsm, TqCtx& tc, double& rl1,
-                           bool reuse, bool& setup)
-{
-    if (BDF_UNLIKELY(eta_eff != 1.0)) vec::rescale_q<Q>(s, eta_eff);
-    BDF_PH(2);
-    vec::predict_q<Q>(s);
-    BDF_PH(3);
-    if (!reuse) rl1 = vec::set_bdf_q<Q, true>(s, tc);
-    BDF_PH(4);
-    const int convfail = CONV_NONE;  // nflag == FIRST_CALL
-    const bool callSetup = (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);  // nst > 0 here
-    setup = callSetup;
-    s.acor = 0.0;
-    double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
-    const double del = vec::newton_correction<NS>(s, mdl, rl1, cscale, callSetup, false, convfail);
-    const double dsm1 = del * s.tq[2];
-    if (BDF_LIKELY((del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) & (dsm1 <= 1.0))) {
-        s.acnrm = del;
-        s.nls_jcur = 0;
-        dsm = dsm1;
-        BDF_PH(5);
-        return uni::ATTEMPT_OK;
-    }
-    const bool conv = vec::newton_rest<NS>(s, mdl, rl1, convfail, callSetup, cscale, del);
-    BDF_PH(5);
-    dsm = s.acnrm * s.tq[2];
-    if (BDF_LIKELY(conv & (dsm <= 1.0))) return uni::ATTEMPT_OK;
-    vec::restore_q<Q>(s, saved_t);
-    return conv ? uni::ATTEMPT_ERR_FAIL : uni::ATTEMPT_CONV_FAIL;
-}
+// cvSet's coefficients (l, tq[2], tq[5], the tq[1]/tq[3] intermediates, gamma, gamrat) depend on
+// h, tau[1..Q] and gammap only. After Q completed steps at an unchanged h, tau[1..Q] all equal h, so
+// every later step at that h with no linear-solver setup in between recomputes exactly the values
+// it already holds (52 % of the steps on C3 prior draws, measured in the oracle): fast_run keeps
+// them instead -- the same bits as computing them again (see fast_run).
 
 // FAST: called from fast_run, where the step's first attempt passed, so etamax is the value the
 // previous completion set (ETAMX2 / ETAMX3) or ReInit's ETAMX1 -- never 1
@@ -842,11 +810,12 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
 {
     // run: completed steps of this loop since h last changed (tau[1..run] == h); have: the
     // coefficients held in s / tc / rl1 were computed with tau[1..Q] == h at the current h and no
-    // setup has changed gammap since (see attempt_fast_q)
+    // setup has changed gammap since. cscale_h is the Newton scale 2 / (1 + gamrat) computed from
+    // gamrat_h, the gamrat it was computed with.
     int run = 0;
     bool have = false;
     TqCtx tc;
-    double rl1 = 0.0;
+    double rl1 = 0.0, cscale_h = 1.0, gamrat_h = 0.0;
     for (;;) {
 #ifdef BCM3_MARKS
         asm volatile("; BDFMARK fast_top Q=%0" ::"i"(Q));
@@ -858,20 +827,65 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             run = 0;
             have = false;
         }
-        double dsm;
-        bool setup;
         const bool reuse = have;
-        const int r = vec::attempt_fast_q<Q, NS>(s, mdl, eta_eff, saved_t, dsm, tc, rl1, reuse, setup);
+        // A plain step: the coefficients are held (so h is unchanged: no rescale), gamrat is the
+        // one the held Newton scale was computed with, and no linear-solver setup is due -- the
+        // callSetup test of the attempt (nst >= nstlp + MSBP | |gamrat - 1| > DGMAX) is false
+        // because its gamrat part was false when the coefficients were computed (a setup then
+        // clears `have`) and gamrat has not changed. One branch instead of the rescale, cvSet,
+        // setup and scale tests.
+        const bool plain = reuse & (s.nst < s.nstlp + MSBP) & (s.gamrat == gamrat_h);
+        bool setup = false;
+        double cscale, del;
+        BDF_PH(2);
+        if (BDF_LIKELY(plain)) {
+            vec::predict_q<Q>(s);
+            BDF_PH(3);
+            BDF_PH(4);
+            cscale = cscale_h;
+            s.acor = 0.0;
+            del = vec::newton_correction<NS>(s, mdl, rl1, cscale, false, false, CONV_NONE);
+        } else {
+            // cvStep's attempt at order Q (attempt_q with nflag == FIRST_CALL, nst > 0)
+#ifdef BCM3_MARKS
+            asm volatile("; BDFMARK general");
+#endif
+            if (eta_eff != 1.0) vec::rescale_q<Q>(s, eta_eff);
+            vec::predict_q<Q>(s);
+            BDF_PH(3);
+            if (!reuse) rl1 = vec::set_bdf_q<Q, true>(s, tc);
+            BDF_PH(4);
+            setup = (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);
+            cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
+            gamrat_h = s.gamrat;
+            cscale_h = cscale;
+            s.acor = 0.0;
+            del = vec::newton_correction<NS>(s, mdl, rl1, cscale, setup, false, CONV_NONE);
+        }
         have = (reuse | (run >= Q)) & !setup;
         run++;
-        if (BDF_UNLIKELY(r != uni::ATTEMPT_OK)) {
-            // failed first attempt: the attempt loop takes over from here
-            s.tretlast = saved_t;
-            pd.saved_t = saved_t;
-            pd.eta_eff = eta_eff;
-            pd.r = r;
-            pd.dsm = dsm;
-            return NEED_ATTEMPTS;
+        // the usual outcome -- Newton converges on its first correction and the error test passes
+        // (a first-iteration convergence has local error dsm = acnrm tq[2] = del tq[2]) -- is ONE
+        // branch; anything else goes on through newton_rest, which repeats the convergence test
+        double dsm = del * s.tq[2];
+        if (BDF_LIKELY((del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) & (dsm <= 1.0))) {
+            s.acnrm = del;
+            s.nls_jcur = 0;
+            BDF_PH(5);
+        } else {
+            const bool conv = vec::newton_rest<NS>(s, mdl, rl1, CONV_NONE, setup, cscale, del);
+            BDF_PH(5);
+            dsm = s.acnrm * s.tq[2];
+            if (BDF_UNLIKELY(!(conv & (dsm <= 1.0)))) {
+                // failed first attempt: the attempt loop takes over from here
+                vec::restore_q<Q>(s, saved_t);
+                s.tretlast = saved_t;
+                pd.saved_t = saved_t;
+                pd.eta_eff = eta_eff;
+                pd.r = conv ? uni::ATTEMPT_ERR_FAIL : uni::ATTEMPT_CONV_FAIL;
+                pd.dsm = dsm;
+                return NEED_ATTEMPTS;
+            }
         }
         vec::complete_q<Q, NS, true>(s, dsm, tc);
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));

@@ -278,6 +278,7 @@ struct SamplerPTDevice::Impl {
     bool cross_round[2] = {false, false};  // do the slice-boundary pairs exchange in rounds of this parity
     bcm3hip_spec S{};
     int64_t spec_pairs = 0;
+    int spec_first_round = 0;  // the device's SIMDs: batch positions p and p + this share a SIMD
 
     // sample output: [flush][values C*d | lprior C | llh C] staged on the device
     std::unique_ptr<SampleFileWriter> out;
@@ -659,7 +660,8 @@ struct SamplerPTDevice::Impl {
                                                  partner[nxt].p, sp_remote.p, &P, &S, g0, cfg.seed, (uint64_t)iter + 1,
                                                  stream),
                     "ptmh_spec_candidates") ||
-            !Launch(bcm3hip_ptmh_spec_batch((int)C, d, prop.p, partner[nxt].p, sp_inv_scale.p, &S, stream),
+            !Launch(bcm3hip_ptmh_spec_batch((int)C, d, prop.p, partner[nxt].p, sp_inv_scale.p, spec_first_round, &S,
+                                            stream),
                     "ptmh_spec_batch"))
             return false;
         if (!ll->EvaluateLogProbabilityBatchDeviceCounted((size_t)C * (1 + BCM3HIP_SPEC_SLOTS), S.batch_n, S.batch_x,
@@ -731,6 +733,7 @@ struct SamplerPTDevice::Impl {
                   cfg.exploration_steps == 1 && Ctot >= 2 && d <= 64 && C * (1 + BCM3HIP_SPEC_SLOTS) <= 4096 &&
                   ll->SupportsCountedBatch();
         if (!spec_on) return true;
+        spec_first_round = bcm3hip_current_device_simds();
         const int64_t K = BCM3HIP_SPEC_SLOTS, N = C * (1 + K);
         bool ok = sp_cand_x.alloc(C * K * d) && sp_cand_lp.alloc(C * K) && sp_cand_lmh.alloc(C * K) &&
                   sp_cand_llh.alloc(C * K) && sp_cand_sc.alloc(C * K) && sp_cand_sel.alloc(C * K) &&

@@ -30,7 +30,7 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
                        double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
                        bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, int uni_solver,
                        hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop, int block_lds = 0,
-                       const int32_t* n_dev = nullptr, int32_t* steps_out = nullptr);
+                       const int32_t* n_dev = nullptr, int32_t* steps_out = nullptr, uint64_t* place_out = nullptr);
 
 struct AnalyticDevModel {
     int32_t kind, d;

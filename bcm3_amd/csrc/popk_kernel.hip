@@ -227,7 +227,8 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
                                                         double* __restrict__ traj_out,
                                                         bcm3hip_traj_stats* __restrict__ stats_out,
                                                         const int32_t* __restrict__ n_dev,
-                                                        int32_t* __restrict__ steps_out)
+                                                        int32_t* __restrict__ steps_out,
+                                                        uint64_t* __restrict__ place_out)
 {
     using TR = PKTraits<PKT>;
     constexpr int NS = TR::NS;
@@ -247,6 +248,9 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         g = gwave * lpw + lane;
         if (g >= ntraj) return;
     }
+    // placement diagnostics (BCM3HIP_OPT_PLACEMENT_LOG): where (HW_ID, XCC_ID) and when (100 MHz
+    // wall clock) this trajectory ran; read from hardware registers, written by lane 0
+    const uint64_t place_t0 = place_out ? wall_clock64() : 0;
     const int P = m.P;
     const int64_t e = g / P;
     const int j = (int)(g - e * P);
@@ -550,6 +554,15 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     if (patient_llh) patient_llh[g] = llh;
     if (traj_status) traj_status[g] = status;
     if (steps_out && m.P == 1) steps_out[g] = nsteps;
+    if (UNI && place_out && lane == 0) {
+        // HW_ID (hwreg 4, all 32 bits) and XCC_ID (hwreg 20, bits 0..3)
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);
+        place_out[4 * g + 0] = hw;
+        place_out[4 * g + 1] = xcc;
+        place_out[4 * g + 2] = place_t0;
+        place_out[4 * g + 3] = wall_clock64();
+    }
     if (STATS && stats_out) {
         bcm3hip_traj_stats st;
         st.nst = s.cnt.nst_total;
@@ -590,7 +603,7 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
                        double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
                        bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, int uni_solver,
                        hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop, int block_lds,
-                       const int32_t* n_dev, int32_t* steps_out)
+                       const int32_t* n_dev, int32_t* steps_out, uint64_t* place_out)
 {
     const int64_t ntraj = n * (int64_t)m.P;
     if (ntraj == 0) return hipSuccess;
@@ -609,16 +622,16 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
 #define LAUNCH(PKT)                                                                                           \
     if (vec_state && !stats_out)                                                                              \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, false>), grid, block, block_lds, stream, m, ntraj, lpw,     \
-                           values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr, n_dev, steps_out);   \
+                           values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr, n_dev, steps_out, place_out); \
     else if (vec_state)                                                                                       \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, true>), grid, block, block_lds, stream, m, ntraj, lpw,      \
-                           values, logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out); \
+                           values, logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out, place_out); \
     else if (uni)                                                                                             \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_UNI, true>), grid, block, block_lds, stream, m, ntraj, lpw, values, \
-                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out);         \
+                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out, place_out); \
     else                                                                                                      \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_LANES, true>), grid, block, block_lds, stream, m, ntraj, lpw, values,  \
-                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out)
+                           logp_direct, patient_llh_scratch, tstat, traj_out, stats_out, n_dev, steps_out, place_out)
     switch (m.pk_type) {
     case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;
     case BCM3HIP_PK_TWO: LAUNCH(BCM3HIP_PK_TWO); break;

@@ -807,17 +807,22 @@ __global__ void __launch_bounds__(64) ptmh_spec_candidates_kernel(
 // The solve length of an entry, predicted from the previous launch's entries (batch_x / batch_steps
 // before this pair's batch overwrites them): the mean steps of its 4 nearest neighbours in parameter
 // space, coordinates scaled by 1 / (prior sd). On C3 prior draws this ranks solve lengths with a
-// Spearman correlation of 0.93 (the state's own last solve: 0.58). One wavefront per entry; entries
-// with nothing to compare against (first pair) keep the steps_hint of their source.
+// Spearman correlation of 0.93 (the state's own last solve: 0.58). One workgroup of 4 wavefronts
+// per entry, each scanning a quarter of the previous entries; entries with nothing to compare
+// against (first pair) keep the steps_hint of their source.
 constexpr int kKnn = 4;
-__global__ void __launch_bounds__(64) ptmh_spec_predict_kernel(int C, int d, const double* __restrict__ prop,
-                                                               const int32_t* __restrict__ partner,
-                                                               const double* __restrict__ inv_scale, bcm3hip_spec S)
+constexpr int kKnnWaves = 4;
+__global__ void __launch_bounds__(64 * kKnnWaves) ptmh_spec_predict_kernel(int C, int d, const double* __restrict__ prop,
+                                                                           const int32_t* __restrict__ partner,
+                                                                           const double* __restrict__ inv_scale,
+                                                                           bcm3hip_spec S)
 {
+    __shared__ double wd[kKnnWaves * kKnn];
+    __shared__ int ws[kKnnWaves * kKnn];
     const int e = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
     const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
     if (e >= n_all) return;
-    const int lane = threadIdx.x & 63;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const double* x;
     int src;
     if (e < C) {
@@ -831,7 +836,7 @@ __global__ void __launch_bounds__(64) ptmh_spec_predict_kernel(int C, int d, con
     }
     const int mem_n = S.batch_n[0];
     if (mem_n <= 0) {
-        if (lane == 0) S.pred_steps[e] = S.steps_hint[src];
+        if (tid == 0) S.pred_steps[e] = S.steps_hint[src];
         return;
     }
     double bd[kKnn];
@@ -840,7 +845,7 @@ __global__ void __launch_bounds__(64) ptmh_spec_predict_kernel(int C, int d, con
         bd[q] = INFINITY;
         bs[q] = 0;
     }
-    for (int m = lane; m < mem_n; m += 64) {
+    for (int m = tid; m < mem_n; m += 64 * kKnnWaves) {
         const double* y = S.batch_x + (int64_t)m * d;
         double dist = 0.0;
         for (int j = 0; j < d; j++) {
@@ -859,83 +864,126 @@ __global__ void __launch_bounds__(64) ptmh_spec_predict_kernel(int C, int d, con
             bs[q] = st;
         }
     }
-    // the kKnn smallest over the wavefront: repeatedly take the minimum head
-    int sum = 0, got = 0;
+    // the kKnn smallest of each wavefront: repeatedly take the minimum head
     for (int r = 0; r < kKnn; r++) {
         double mn = bd[0];
         for (int off = 32; off >= 1; off >>= 1) {
             const double o = __shfl_xor(mn, off);
             mn = (o < mn) ? o : mn;
         }
-        if (mn == INFINITY) break;
-        // the lowest lane holding the minimum pops it
-        const unsigned long long who = __ballot(bd[0] == mn);
-        const int owner = __builtin_ctzll(who);
-        const int st = __shfl(bs[0], owner);
-        if (lane == owner) {
-            for (int q = 0; q < kKnn - 1; q++) {
-                bd[q] = bd[q + 1];
-                bs[q] = bs[q + 1];
+        int st = 0;
+        if (mn != INFINITY) {
+            // the lowest lane holding the minimum pops it
+            const unsigned long long who = __ballot(bd[0] == mn);
+            const int owner = __builtin_ctzll(who);
+            st = __shfl(bs[0], owner);
+            if (lane == owner) {
+                for (int q = 0; q < kKnn - 1; q++) {
+                    bd[q] = bd[q + 1];
+                    bs[q] = bs[q + 1];
+                }
+                bd[kKnn - 1] = INFINITY;
             }
-            bd[kKnn - 1] = INFINITY;
         }
-        sum += st;
-        got++;
-    }
-    if (lane == 0) S.pred_steps[e] = got ? sum / got : S.steps_hint[src];
-}
-
-// one workgroup: the batch of iteration r's proposals and the active candidates, sorted by the
-// predicted solve length (the steps of the last evaluation of the chain whose state an entry starts
-// from), longest first, ties by entry id; the hardware dispatches wavefronts in this order, so the
-// long solves start first and the short ones fill the SIMDs they free (tools/spec_sim.py)
-constexpr int kSpecSortMax = 4096;
-__global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, const double* __restrict__ prop,
-                                                               const int32_t* __restrict__ partner, bcm3hip_spec S)
-{
-    __shared__ unsigned long long key[kSpecSortMax];
-    const int tid = threadIdx.x;
-    const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
-    int N = 1;
-    while (N < n_all) N <<= 1;
-    for (int i = tid; i < N; i += blockDim.x) {
-        unsigned long long kv = ~0ull;
-        const bool on = (i < C) || (i < n_all && S.cand_active[i - C]);
-        if (on) {
-            int h = S.pred_steps[i];  // ptmh_spec_predict_kernel
-            h = h < 0 ? 0 : h;
-            kv = ((unsigned long long)(0x7fffffffu - (unsigned)h) << 32) | (unsigned)i;
+        if (lane == 0) {
+            wd[wv * kKnn + r] = mn;
+            ws[wv * kKnn + r] = st;
         }
-        key[i] = kv;
     }
     __syncthreads();
-    for (int size = 2; size <= N; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = tid; i < N; i += blockDim.x) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const unsigned long long a = key[i], b = key[j];
-                    const bool up = (i & size) == 0;
-                    if ((a > b) == up) {
-                        key[i] = b;
-                        key[j] = a;
-                    }
-                }
-            }
-            __syncthreads();
+    if (tid == 0) {
+        // the kKnn smallest of the wavefronts' lists
+        int sum = 0, got = 0;
+        for (int r = 0; r < kKnn; r++) {
+            int best = -1;
+            for (int i = 0; i < kKnnWaves * kKnn; i++)
+                if (wd[i] != INFINITY && (best < 0 || wd[i] < wd[best])) best = i;
+            if (best < 0) break;
+            sum += ws[best];
+            got++;
+            wd[best] = INFINITY;
+        }
+        S.pred_steps[e] = got ? sum / got : S.steps_hint[src];
+    }
+}
+
+// one workgroup: the batch of iteration r's proposals and the active candidates, ordered by the
+// predicted solve length (ptmh_spec_predict_kernel), longest first. A counting sort over buckets of
+// 2 steps (atomic ranks inside a bucket: the order of equal keys is arbitrary, which changes timing
+// only -- every entry's result is its own). Layout for a batch of M > R wavefronts, R = the
+// wavefronts the device runs at once one per SIMD (first_round): the hardware gives batch
+// positions p and p + R the same SIMD (measured, tools/placement.py), so the M - R shortest go to
+// positions R.., the next M - R shortest to positions 0.. (they share SIMDs with each other), and
+// the 2R - M longest run alone at positions M - R .. R - 1; first_round = 0: plain longest first.
+constexpr int kSpecSortMax = 4096;
+constexpr int kSpecBuckets = 2048;
+__global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, const double* __restrict__ prop,
+                                                               const int32_t* __restrict__ partner, int first_round,
+                                                               bcm3hip_spec S)
+{
+    __shared__ int cnt[kSpecBuckets];
+    __shared__ int wsum[16];
+    __shared__ int pos_of[kSpecSortMax];  // entry id -> batch position (-1 inactive)
+    const int tid = threadIdx.x;
+    const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
+    for (int b = tid; b < kSpecBuckets; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    constexpr int kPer = kSpecSortMax / 1024;
+    int bk[kPer], rk[kPer];
+    for (int q = 0; q < kPer; q++) {
+        const int i = tid + q * 1024;
+        bk[q] = -1;
+        const bool on = (i < C) || (i < n_all && S.cand_active[i - C]);
+        if (on) {
+            int h = S.pred_steps[i];
+            h = h < 0 ? 0 : (h >> 1);
+            h = h > kSpecBuckets - 1 ? kSpecBuckets - 1 : h;
+            bk[q] = kSpecBuckets - 1 - h;  // longest first
+            rk[q] = atomicAdd(&cnt[bk[q]], 1);
         }
     }
-    // the active entries are the prefix before the first ~0 key
-    for (int i = tid; i < N; i += blockDim.x)
-        if (key[i] != ~0ull && (i + 1 == N || key[i + 1] == ~0ull)) S.batch_n[0] = i + 1;
-    for (int i = tid; i < N; i += blockDim.x)
-        if (key[i] != ~0ull) S.batch_src[i] = (int)(key[i] & 0xffffffffull);
-    for (int t = tid; t < N * d; t += blockDim.x) {
-        const int pos = t / d, j = t - pos * d;
-        if (key[pos] == ~0ull) continue;
-        const int id = (int)(key[pos] & 0xffffffffull);
+    __syncthreads();
+    // exclusive prefix sum of the bucket counts: two buckets per thread, then a scan over the
+    // 16 wavefronts' totals
+    const int lane = tid & 63, wv = tid >> 6;
+    const int c0 = cnt[2 * tid], c1 = cnt[2 * tid + 1];
+    int incl = c0 + c1;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wv; w++) before += wsum[w];
+    int M = 0;
+    for (int w = 0; w < 16; w++) M += wsum[w];
+    const int ex = before + incl - c0 - c1;
+    __syncthreads();
+    cnt[2 * tid] = ex;
+    cnt[2 * tid + 1] = ex + c0;
+    for (int i = tid; i < kSpecSortMax; i += blockDim.x) pos_of[i] = -1;
+    __syncthreads();
+    const int R = first_round;
+    const int S2 = (R > 0 && M > R) ? M - R : 0;  // entries of the second round
+    const int L = M - 2 * S2;                      // entries that run alone
+    for (int q = 0; q < kPer; q++) {
+        if (bk[q] < 0) continue;
+        const int r = cnt[bk[q]] + rk[q];
+        int p = r;
+        if (S2 > 0) p = (r < L) ? S2 + r : (r < L + S2) ? r - L : R + (r - L - S2);
+        pos_of[tid + q * 1024] = p;
+    }
+    if (tid == 0) S.batch_n[0] = M;
+    __syncthreads();
+    for (int i = tid; i < n_all; i += blockDim.x)
+        if (pos_of[i] >= 0) S.batch_src[pos_of[i]] = i;
+    for (int t = tid; t < n_all * d; t += blockDim.x) {
+        const int id = t / d, j = t - id * d;
+        const int p = pos_of[id];
+        if (p < 0) continue;
         const double* src = (id < C) ? prop + (int64_t)id * d : S.cand_x + (int64_t)(id - C) * d;
-        S.batch_x[(int64_t)pos * d + j] = src[j];
+        S.batch_x[(int64_t)p * d + j] = src[j];
     }
 }
 
@@ -1115,14 +1163,16 @@ int bcm3hip_ptmh_spec_candidates(int C, int d, const int32_t* prior_kind, const 
 }
 
 int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* partner, const double* inv_scale,
-                            const bcm3hip_spec* spec, void* stream)
+                            int first_round, const bcm3hip_spec* spec, void* stream)
 {
     if (C <= 0 || d <= 0 || C * (1 + BCM3HIP_SPEC_SLOTS) > kSpecSortMax || !prop || !partner || !inv_scale ||
-        !spec_ok(spec) || !spec->pred_steps)
+        first_round < 0 || !spec_ok(spec) || !spec->pred_steps)
         return BCM3HIP_ERR_ARG;
-    hipLaunchKernelGGL(ptmh_spec_predict_kernel, dim3(C * (1 + BCM3HIP_SPEC_SLOTS)), dim3(64), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(ptmh_spec_predict_kernel, dim3(C * (1 + BCM3HIP_SPEC_SLOTS)), dim3(64 * kKnnWaves), 0,
+                       (hipStream_t)stream,
                        C, d, prop, partner, inv_scale, *spec);
-    hipLaunchKernelGGL(ptmh_spec_batch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, prop, partner, *spec);
+    hipLaunchKernelGGL(ptmh_spec_batch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, prop, partner,
+                       first_round, *spec);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -260,13 +260,18 @@ enum {
     BCM3HIP_OPT_UNI_SOLVER = 4,     /* one-trajectory-per-wavefront launches: 0 = state vectors across
                                        lanes (bdf_vec.h, default), 1 = scalar state (bdf_uni.h);
                                        same results */
-    BCM3HIP_OPT_BLOCK_LDS = 5       /* bytes of LDS reserved per workgroup of the PopPK launch (0..65536,
+    BCM3HIP_OPT_BLOCK_LDS = 5,      /* bytes of LDS reserved per workgroup of the PopPK launch (0..65536,
                                        default 0): caps the workgroups resident per CU, so a launch
                                        with more wavefronts than SIMDs queues the rest instead of
                                        sharing a SIMD */
+    BCM3HIP_OPT_PLACEMENT_LOG = 6   /* diagnostics, PopPK one-trajectory-per-wavefront launches: 1 = each
+                                       trajectory records where and when it ran (see placement_log) */
 };
 
 int bcm3hip_device_count(void);
+/* SIMDs of the calling thread's current device (compute units x 4), 0 on error: the wavefronts a
+ * launch of one-wavefront workgroups runs one per SIMD */
+int bcm3hip_current_device_simds(void);
 const char* bcm3hip_error_string(int code);
 
 int bcm3hip_open_popk(int device, const bcm3hip_popk_model* model, bcm3hip_ctx** out);
@@ -316,6 +321,12 @@ int bcm3hip_eval_batch_device(bcm3hip_ctx* ctx, size_t n, const double* values_d
 int bcm3hip_eval_batch_device_counted(bcm3hip_ctx* ctx, size_t n_max, const int32_t* n_dev, const double* values_dev,
                                       double* logp_dev, int32_t* status_dev, int32_t* steps_dev, void* stream);
 int bcm3hip_last_kernel_ms(bcm3hip_ctx* ctx, float* ms);
+/* With BCM3HIP_OPT_PLACEMENT_LOG on: the placement of the trajectories of the most recent PopPK
+ * launch, 4 words per trajectory in launch order: the wavefront's HW_ID register (wave, SIMD, CU,
+ * shader array, shader engine fields), its XCC_ID register, and the constant-rate wall clock
+ * (100 MHz) when the trajectory started and when it finished. Copies min(n_max, trajectories) rows
+ * (synchronises with the launch) and returns that count, or a negative error. */
+int64_t bcm3hip_placement_log(bcm3hip_ctx* ctx, int64_t n_max, uint64_t* host_out);
 /* With BCM3HIP_OPT_TIMING_LOG on: synchronises on every launch logged since the last call and
  * returns the summed / maximum kernel time (HIP events recorded on each launch's own stream) and
  * the number of launches, then clears the log. Lets a timed loop run without host syncs. */
@@ -455,9 +466,12 @@ int bcm3hip_ptmh_spec_candidates(int C, int d, const int32_t* prior_kind, const 
 /* the launch's batch: iteration r's C proposals + the active candidates, ordered by the predicted
  * length of their solves, longest first (C <= 585): the mean BDF steps of the entry's 4 nearest
  * neighbours among the previous launch's entries, distances scaled by inv_scale[d] (1 / prior sd);
- * before any launch, the steps_hint of the slot the entry starts from */
+ * before any launch, the steps_hint of the slot the entry starts from. first_round > 0: the
+ * wavefronts the device runs one per SIMD (its SIMD count); a batch larger than that puts its
+ * shortest entries on the SIMDs that take two wavefronts (positions p and p + first_round), so the
+ * longest run alone; 0: plain longest-first order */
 int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* partner, const double* inv_scale,
-                            const bcm3hip_spec* spec, void* stream);
+                            int first_round, const bcm3hip_spec* spec, void* stream);
 /* batch results back: llh_prop[c] (iteration r), cand_llh / cand_steps, steps_prop */
 int bcm3hip_ptmh_spec_scatter(int C, const bcm3hip_spec* spec, double* llh_prop, void* stream);
 /* after accept r (accept_out = acc_mutate[C]) and exchange r + 1 (accept_out = acc_exchange, indexed

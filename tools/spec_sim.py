@@ -96,11 +96,19 @@ def main():
     src, steps = s.spec_batch_info()
     s.close()
     n = len(steps)
+    # the batch layout (ptmh_spec_batch_kernel): predicted rank r -> position; invert it with the
+    # device's SIMD count R (positions p and p + R share a SIMD)
+    R = _hip.lib().bcm3hip_current_device_simds() if hasattr(_hip.lib(), "bcm3hip_current_device_simds") else 0
+    S2 = n - R if 0 < R < n else 0
+    L = n - 2 * S2
+    p = np.arange(n)
+    pred_rank = np.where(p < S2, L + p, np.where(p < R, p - S2, L + S2 + (p - R))) if S2 else p
+    steps = steps[np.argsort(pred_rank)]  # in predicted order, longest first
     rank = np.argsort(np.argsort(-steps, kind="stable"), kind="stable")  # 0 = longest
     top = np.argsort(-steps, kind="stable")[:64]
     print(f"sampler: {nl} launches for 20 iterations, {tt / nl:.3f} ms per launch (max {mx:.3f}); last batch "
-          f"{n} entries, steps max {steps.max()} mean {steps.mean():.0f}; the 64 longest solves sit at dispatch "
-          f"positions median {np.median(top):.0f} (max {top.max()}); rank correlation "
+          f"{n} entries, steps max {steps.max()} mean {steps.mean():.0f}; the 64 longest solves sit at predicted "
+          f"ranks median {np.median(top):.0f} (max {top.max()}); rank correlation "
           f"{np.corrcoef(np.arange(n), rank)[0, 1]:.2f}", flush=True)
     base = res[1][1]
     for k, label in ((5, "1 + 4 candidates"), (7, "1 + 6 candidates")):

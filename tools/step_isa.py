@@ -160,14 +160,15 @@ def marked(blocks, order, name):
     return [l for l in order if any(k == "mark" and t == name for k, t, *_ in blocks[l].items)]
 
 
-def step_path(blocks, order, top, seq, set_bdf):
+def step_path(blocks, order, top, seq, set_bdf, avoid=()):
     """Shortest cycle top -> (a block marked seq[0]) -> ... -> top, passing the phase markers in the
     order a plain step passes them. Consecutive markers in one block are one stop. The structurised
     control flow branches on exec (s_cbranch_execz skips a region no lane enters); a wave-uniform
     step enters a region exactly when its condition holds, so the markers pin the regions a plain
     step runs. set_bdf: the step recomputes the BDF coefficients (the region between markers 3 and
     4 is entered) or reuses them (skipped)."""
-    banned = {l for l in order if any(k == "mark" and t.startswith("fast_top") for k, t, *_ in blocks[l].items)}
+    banned = {l for l in order if any(k == "mark" and (t.startswith("fast_top") or t in avoid)
+                                      for k, t, *_ in blocks[l].items)}
     stops = [[top]]
     for name in seq:
         stops.append(marked(blocks, order, name))
@@ -274,8 +275,14 @@ def main():
             continue
         top = tops[0]
         print(f"Q={q}  fast_top block {top}")
-        for label, sb in (("step reusing the BDF coefficients", False), ("step recomputing them (set_bdf)", True)):
-            p = step_path(blocks, order, top, ["2", "3", "4", "5", "7", "8"], sb)
+        # fast_run's plain step (one branch on `plain`) and its general attempt ("general" marker:
+        # rescale, cvSet, setup and scale tests), the latter with the cvSet region entered
+        general = bool(marked(blocks, order, "general"))
+        for label, sb, seq, avoid in (
+                ("plain step (coefficients held)", False, ["2", "3", "4", "5", "7", "8"], ("general",)),
+                ("general attempt recomputing them (set_bdf)", True,
+                 (["general", "3", "4", "5", "7", "8"] if general else ["2", "3", "4", "5", "7", "8"]), ())):
+            p = step_path(blocks, order, top, seq, sb, avoid)
             if not p:
                 print(f"  {label}: no path")
                 continue
