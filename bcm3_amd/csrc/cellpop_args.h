@@ -21,6 +21,8 @@ struct CpSolveArgs {
     int32_t divide_cells;
     double past_cs;               // simulate_past_chromatid_separation_time
     int32_t ev[7];                // event species (simulated-species index applied to the ODE state), -1 = none
+    const double* treat_times;    // pulse start times of the treatment trajectories, concatenated (CP_NTREAT)
+    const int32_t* treat_offset;  // [CP_NTREAT + 1]
     // outputs
     double* out_values;           // [slot][M]
     double* end_y;                // [slot][NS]

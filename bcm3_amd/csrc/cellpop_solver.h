@@ -29,6 +29,9 @@
 namespace cpk {
 using namespace bcm3hip;
 
+#ifndef CP_NTREAT
+#define CP_NTREAT 0
+#endif
 constexpr int WAVE = 64;
 // A cell's state lives in one ROW of lanes (component i in lane i of the row). With NS <= 16 four
 // cells share a wavefront -- the 16-lane DPP rows -- so every vector instruction advances four
@@ -92,6 +95,11 @@ struct Shared {
     int dinv_ok;         // every 1 / u(i, i) finite: the quotients through dinv
     double prm[NP > 0 ? NP : 1];
     double cs[NC > 0 ? NC : 1];
+#if CP_NTREAT > 0
+    const double* treat_times;     // the pulse start times (a.treat_times)
+    int treat_off[CP_NTREAT + 1];
+    double creation;               // the cell's creation time (treatment times are experiment times)
+#endif
 #ifdef CP_PHASES
     long long ph[8];
 #endif
@@ -123,6 +131,8 @@ struct GenState {
     int q, qprime, qwait, L;
     int nst, nstlp, nstlj;
     int nls_jcur;
+    double tstop;  // CVodeSetStopTime (treatment discontinuities)
+    int tstopset;
 };
 
 // value of lane J of this lane's 16-lane row, in every lane (v_mov_b64_dpp row_newbcast:J; no
@@ -174,21 +184,85 @@ BDF_INL double wrms(SH& sh, double x, double w)
     return fsqrt(fdiv_c(lane_sum<NS>(sh, p * p), (double)NS, 1.0 / NS));
 }
 
+// ---- treatment trajectories (TreatmentTrajectoryPulses.cpp) --------------------------------------
+// pulses starting at times tp[0..n) (sorted): 0 until start + 2, linear up to 1 over 2, 1 until
+// start + 10, linear down over 4 (GetConcentration, :22-41)
+BDF_INL double pulse_concentration(const double* tp, int n, double time, double creation)
+{
+    const double global_time = time + creation;
+    for (int i = 0; i < n; i++) {
+        const double t_in_pulse = global_time - tp[i] - 2.0;
+        if (t_in_pulse >= 14.0) continue;
+        if (t_in_pulse <= 0.0) return 0.0;
+        if (t_in_pulse < 2.0) return t_in_pulse * 0.5;
+        if (t_in_pulse < 10.0) return 1.0;
+        return 1 - (t_in_pulse - 10.0) * 0.25;
+    }
+    return 0.0;
+}
+// FirstDiscontinuity (:44-51): NaN without pulses
+BDF_INL double pulse_first(const double* tp, int n, double creation)
+{
+    return (n > 0) ? tp[0] - creation + 2.0 : __builtin_nan("");
+}
+// NextDiscontinuity (:53-71): the corner after `time` (exact corner times), NaN past the last
+BDF_INL double pulse_next(const double* tp, int n, double time, double creation)
+{
+    for (int i = 0; i < n; i++) {
+        if (time == tp[i] - creation + 2.0) return tp[i] - creation + 4.0;
+        if (time == tp[i] - creation + 4.0) return tp[i] - creation + 10.0;
+        if (time == tp[i] - creation + 10.0) return tp[i] - creation + 14.0;
+        if (time == tp[i] - creation + 14.0) return (i < n - 1) ? tp[i + 1] - creation + 2.0 : __builtin_nan("");
+    }
+    return __builtin_nan("");
+}
+
+#if CP_NTREAT > 0
+// the constant species with the treatment species at their concentration at time t
+// (Cell::SetTreatmentConcentration before every right-hand side, Cell.cpp:414-430); the generated
+// code indexes with literals, so the selects fold at compile time
+struct TreatedConstants {
+    const double* cs;
+    double v[CP_NTREAT];
+    BDF_INL double operator[](int k) const
+    {
+        double r = cs[k];
+#pragma unroll
+        for (int i = 0; i < CP_NTREAT; i++) r = (k == kTreatSpecies[i]) ? v[i] : r;
+        return r;
+    }
+};
+template <class SH>
+BDF_INL TreatedConstants treated(const SH& sh, double t)
+{
+    TreatedConstants c{sh.cs, {}};
+#pragma unroll
+    for (int i = 0; i < CP_NTREAT; i++)
+        c.v[i] = pulse_concentration(sh.treat_times + sh.treat_off[i], sh.treat_off[i + 1] - sh.treat_off[i], t,
+                                     sh.creation);
+    return c;
+}
+#define CP_CONSTANTS(sh, t) treated(sh, t)
+#else
+#define CP_CONSTANTS(sh, t) (sh).cs
+#endif
+
 // ---- the model ---------------------------------------------------------------------------------
 template <int NS, int NP, int NC, class SH>
-BDF_INL double rhs_v(SH& sh, double y)
+BDF_INL double rhs_v(SH& sh, double y, double t)
 {
+    (void)t;
     double o[NS];
     if constexpr (NS <= 16) {
         // the state reaches every lane of the row by DPP broadcasts: no LDS round trip
         RegSpecies<NS> sp;
         cfor<0, NS>([&](auto k) __attribute__((always_inline)) { sp.v[CI(k)] = rbc<CI(k)>(y); });
-        generated_derivative(o, sp, sh.cs, sh.prm, (const double*)nullptr);
+        generated_derivative(o, sp, CP_CONSTANTS(sh, t), sh.prm, (const double*)nullptr);
     } else {
         wave_sync();
         if (lane() < NS) sh.sy[lane()] = y;
         wave_sync();
-        generated_derivative(o, LdsSpecies{sh.sy}, sh.cs, sh.prm, (const double*)nullptr);
+        generated_derivative(o, LdsSpecies{sh.sy}, CP_CONSTANTS(sh, t), sh.prm, (const double*)nullptr);
     }
     double r = o[NS - 1];
 #pragma unroll
@@ -199,8 +273,9 @@ BDF_INL double rhs_v(SH& sh, double y)
 // DifferenceQuotientJacobian (ODESolverCVODE.cpp:496-537) into sh.J: lane j evaluates the
 // perturbed state of column j
 template <int NS, int NP, int NC, class SH, class S>
-BDF_INL void dq_jacobian(SH& sh, const S& s, double y, double fy)
+BDF_INL void dq_jacobian(SH& sh, const S& s, double y, double fy, double t)
 {
+    (void)t;
     const double p = fy * s.ewt;
     const double fnorm = sqrt(lane_sum<NS>(sh, p * p) / NS);
     const double srur = 1.4901161193847656e-08;  // SUNRsqrt(DBL_EPSILON)
@@ -213,7 +288,7 @@ BDF_INL void dq_jacobian(SH& sh, const S& s, double y, double fy)
     }
     wave_sync();
     double o[NS];
-    generated_derivative(o, PertSpecies{sh.sy, y + inc, lane()}, sh.cs, sh.prm, (const double*)nullptr);
+    generated_derivative(o, PertSpecies{sh.sy, y + inc, lane()}, CP_CONSTANTS(sh, t), sh.prm, (const double*)nullptr);
     const double inc_inv = 1.0 / inc;
     if (lane() < NS) {
 #pragma unroll
@@ -637,7 +712,7 @@ BDF_INL bool newton(SH& sh, S& s, double rl1, int convfail, bool callSetup)
         double f;
         {
             CP_PH_BEGIN();
-            f = rhs_v<NS, NP, NC>(sh, y);
+            f = rhs_v<NS, NP, NC>(sh, y, s.tn);
             CP_PH_END(sh, 0);
         }
         double delta = __builtin_fma(rl1, s.zn[1], s.acor);
@@ -650,7 +725,7 @@ BDF_INL bool newton(SH& sh, S& s, double rl1, int convfail, bool callSetup)
             if (jnew) {
                 s.nstlj = s.nst;
                 CP_PH_BEGIN();
-                dq_jacobian<NS, NP, NC>(sh, s, y, f);
+                dq_jacobian<NS, NP, NC>(sh, s, y, f, s.tn);
                 CP_PH_END(sh, 1);
             }
             {
@@ -732,7 +807,7 @@ BDF_INL int hin(SH& sh, S& s, double tout)
     for (int count1 = 1; count1 <= MAX_ITERS; count1++) {
         const double hgs = hg * sign;
         const double yy = __builtin_fma(hgs, s.zn[1], s.zn[0]);
-        double tv = rhs_v<NS, NP, NC>(sh, yy);
+        double tv = rhs_v<NS, NP, NC>(sh, yy, s.tn + hgs);
         const double a = frcp(hgs);
         tv = a * (tv - s.zn[1]);
         const double yddnrm = wrms<NS>(sh, tv, s.ewt);
@@ -756,21 +831,28 @@ BDF_INL int hin(SH& sh, S& s, double tout)
 
 constexpr double ONEPSM = 1.000001;
 
-// CVode(..., CV_ONE_STEP) without tstop (cells have no discontinuities without treatment
-// trajectories); returns tret and the state in s.zn[0]
+// CVode(..., CV_ONE_STEP) (cvode.c:1016-1440); tstop only with treatment trajectories (CVodeSetStopTime
+// of ODESolverCVODE::Solve); returns tret and the output vector's component in yout
 template <int NS, int NP, int NC, class SH, class S>
-BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
+BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret, double& yout)
 {
     if (s.nst == 0) {
         s.tretlast = tret = s.tn;
         ewt_set(s);
         s.nstlj = 0;
         s.nls_jcur = 0;
-        s.zn[1] = rhs_v<NS, NP, NC>(sh, s.zn[0]);
-        const int hflag = hin<NS, NP, NC>(sh, s, tout);
+        s.zn[1] = rhs_v<NS, NP, NC>(sh, s.zn[0], s.tn);
+        double tout_hin = tout;
+        if constexpr (CP_NTREAT > 0) {
+            if (s.tstopset && ((s.tstop - s.tn) * (tout - s.tn) <= 0.0)) return CV_ILL_INPUT;
+            if (s.tstopset && ((tout - s.tn) * (tout - s.tstop) > 0.0)) tout_hin = s.tstop;
+        }
+        const int hflag = hin<NS, NP, NC>(sh, s, tout_hin);
         if (hflag != CV_SUCCESS) return hflag;
         // hmax_inv = 0 (no clamp); |h| < hmin -> hmin (cvode.c:1121-1124)
         if (fabs(s.h) < s.hmin) s.h *= s.hmin / fabs(s.h);
+        if constexpr (CP_NTREAT > 0)
+            if (s.tstopset && ((s.tn + s.h - s.tstop) * s.h > 0.0)) s.h = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
         s.hscale = s.h;
         s.hprime = s.h;
         s.zn[1] *= s.h;
@@ -778,7 +860,20 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         if (fabs(s.tn - s.tretlast) > troundoff) {
             s.tretlast = tret = s.tn;
+            yout = s.zn[0];
             return CV_SUCCESS;
+        }
+        if (CP_NTREAT > 0 && s.tstopset) {
+            if (fabs(s.tn - s.tstop) <= troundoff) {
+                if (get_dky(s, s.tstop, yout) != CV_SUCCESS) return CV_ILL_INPUT;
+                s.tretlast = tret = s.tstop;
+                s.tstopset = 0;
+                return CV_TSTOP_RETURN;
+            }
+            if ((s.tn + s.hprime - s.tstop) * s.h > 0.0) {
+                s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+                s.eta = fdiv(s.hprime, s.h);
+            }
         }
         ewt_set(s);
     }
@@ -798,6 +893,7 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
         }
         if (too_much) {
             s.tretlast = tret = s.tn;
+            yout = s.zn[0];
             return CV_TOO_MUCH_ACC;
         }
     }
@@ -867,7 +963,7 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
         s.h *= s.eta;
         s.hscale = s.h;
         s.qwait = LONG_WAIT;
-        const double tv = rhs_v<NS, NP, NC>(sh, s.zn[0]);
+        const double tv = rhs_v<NS, NP, NC>(sh, s.zn[0], s.tn);
         s.zn[1] = s.h * tv;
         do_rescale = false;
     }
@@ -932,7 +1028,22 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret)
     CP_PH_END(sh, 7);
     s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
     s.acor *= s.tq[2];
+    // tn at or near tstop (cvode.c:1410-1426)
+    if (CP_NTREAT > 0 && s.tstopset) {
+        const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
+        if (fabs(s.tn - s.tstop) <= troundoff) {
+            get_dky(s, s.tstop, yout);
+            s.tretlast = tret = s.tstop;
+            s.tstopset = 0;
+            return CV_TSTOP_RETURN;
+        }
+        if ((s.tn + s.hprime - s.tstop) * s.h > 0.0) {
+            s.hprime = (s.tstop - s.tn) * (1.0 - 4.0 * UROUND);
+            s.eta = fdiv(s.hprime, s.h);
+        }
+    }
     s.tretlast = tret = s.tn;
+    yout = s.zn[0];
     return CV_SUCCESS;
 }
 
@@ -987,6 +1098,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
     for (int k = ln; k < NP; k += ROW) sh.prm[k] = a.params[(size_t)slot * NP + k];
     for (int k = ln; k < NC; k += ROW) sh.cs[k] = a.constant_species[k];
     const double creation = a.creation[slot];
+#if CP_NTREAT > 0
+    sh.treat_times = a.treat_times;
+    for (int k = ln; k <= CP_NTREAT; k += ROW) sh.treat_off[k] = a.treat_offset[k];
+    sh.creation = creation;
+#endif
     const double y0 = (ln < NS) ? a.y0[(size_t)slot * NS + ln] : 0.0;
     const int M = MM;
     double* outv = sh.outl;
@@ -1040,17 +1156,40 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
         s.zn[0] = y0;
         s.nst = 0;
         s.nstlp = 0;
+        s.tstop = 0.0;
+        s.tstopset = 0;
+        // Cell::Simulate: the first treatment discontinuity (Cell.cpp:212-229) becomes the solver's
+        // stop time (ODESolver::SetDiscontinuity ignores times <= 0; ODESolverCVODE::Solve :337-339)
+        double next_disc = __builtin_nan("");
+#if CP_NTREAT > 0
+        {
+            double first = __builtin_nan("");
+            for (int i = 0; i < CP_NTREAT; i++) {
+                const double* tp = a.treat_times + sh.treat_off[i];
+                const int nt = sh.treat_off[i + 1] - sh.treat_off[i];
+                double dd = pulse_first(tp, nt, creation);
+                if (dd == dd)
+                    while (dd < 0.0) dd = pulse_next(tp, nt, dd, creation);
+                if (!(first < dd)) first = dd;
+            }
+            if (first == first && first > 0.0) next_disc = first;
+        }
+        if (next_disc == next_disc) {
+            s.tstop = next_disc;
+            s.tstopset = 1;
+        }
+#endif
         double end_time = a.output_times[M - 1] - creation;
         double t = 0.0;
         int tpi = ti;
         // the next output time in a register: no global load on every step's critical path
         double next_out = a.output_times[tpi] - creation;
         for (;;) {
-            double tret;
+            double tret, y;
             int r;
             {
                 CP_PH_BEGIN();
-                r = cvode_one_step<NS, NP, NC>(sh, s, end_time, tret);
+                r = cvode_one_step<NS, NP, NC>(sh, s, end_time, tret, y);
                 CP_PH_END(sh, 4);
             }
             if (r < 0) {
@@ -1071,8 +1210,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
                 if (tpi < M) next_out = a.output_times[tpi] - creation;
             }
             if (!ok) break;
-            // Cell::integration_step_cb (Cell.cpp:463-538)
-            const double y = s.zn[0];
+            // Cell::integration_step_cb (Cell.cpp:463-538) on CVode's output vector
             bool cont = true;
             if constexpr (CP_EV0 >= 0)
                 if (ev[0] != ev[0] && ev_value<CP_EV0>(y) > 1e-4) ev[0] = crossing_time(t, previous_step_time, 1e-4, true);
@@ -1112,6 +1250,33 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
                 ok = false;
                 break;
             }
+#if CP_NTREAT > 0
+            // a treatment discontinuity: Cell::discontinuity_cb gives the next one, then CVodeReInit at
+            // (t, y) and the new stop time (ODESolverCVODE::Solve :449-460; Cell.cpp:447-461)
+            if (next_disc == next_disc && (r == CV_TSTOP_RETURN || next_disc == t)) {
+                double dn = __builtin_inf();
+                for (int i = 0; i < CP_NTREAT; i++) {
+                    const double dd = pulse_next(a.treat_times + sh.treat_off[i], sh.treat_off[i + 1] - sh.treat_off[i], t,
+                                                 creation);
+                    if (dd < dn) dn = dd;
+                }
+                next_disc = (dn == __builtin_inf()) ? __builtin_nan("") : dn;
+                // CVodeReInit(t, y) (cvode.c:706-760)
+                s.tn = t;
+                s.q = 1;
+                s.L = 2;
+                s.qwait = 2;
+                s.etamax = ETAMX1;
+                s.hu = 0.0;
+                s.zn[0] = y;
+                s.nst = 0;
+                s.nstlp = 0;
+                if (next_disc == next_disc && next_disc < __builtin_inf()) {
+                    s.tstop = next_disc;
+                    s.tstopset = 1;
+                }
+            }
+#endif
         }
         if (ok && !divided && !died) {
             // simulation_end_y = the solution at the last output time

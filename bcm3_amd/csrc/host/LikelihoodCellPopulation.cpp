@@ -161,6 +161,9 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
     trailing = ex.get_double("trailing_simulation_time", 0.0);
     past_cs = ex.get_double("simulate_past_chromatid_separation_time", 0.0);
 
+    treat_names.clear();
+    treat_times.clear();
+    treat_offset.assign(1, 0);
     for (const auto& c : ex.children) {
         if (c->name == "set_parameter") {
             const std::string p = c->get("parameter_name");
@@ -169,10 +172,44 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
                 return false;
             }
             forced[p] = c->get_double("value");
-        } else if (c->name == "set_species" || c->name == "experiment_specific_parameter" ||
-                   c->name == "treatment_trajectory") {
+        } else if (c->name == "set_species" || c->name == "experiment_specific_parameter") {
             LOGERROR("cell_population: <%s> is not supported", c->name.c_str());
             return false;
+        } else if (c->name == "treatment_trajectory") {
+            // Experiment::Load (Experiment.cpp:571-584) + TreatmentTrajectory::Create / Load
+            const std::string type = c->get("type");
+            if (type == "from_data") {
+                // TreatmentTrajectoryFromData::Load fails in the reference (its data read is #if TODO)
+                LOGERROR("Treatment trajectory type \"from_data\" cannot be loaded (the reference's loader returns failure)");
+                return false;
+            }
+            if (type != "pulses") {
+                LOGERROR("Unknown trajectory type \"%s\"", type.c_str());
+                return false;
+            }
+            treat_names.push_back(c->get("species_name"));
+            // TreatmentTrajectoryPulses::Load: comma-separated times, sorted
+            std::vector<double> t;
+            const std::string ts = c->get("times");
+            size_t p0 = 0;
+            while (p0 <= ts.size()) {
+                size_t p1 = ts.find(',', p0);
+                if (p1 == std::string::npos) p1 = ts.size();
+                std::string tok = ts.substr(p0, p1 - p0);
+                tok.erase(0, tok.find_first_not_of(" \t"));
+                tok.erase(tok.find_last_not_of(" \t") + 1);
+                char* end = nullptr;
+                const double v = strtod(tok.c_str(), &end);
+                if (tok.empty() || *end) {
+                    LOGERROR("Treatment trajectory: could not read pulse time \"%s\"", tok.c_str());
+                    return false;
+                }
+                t.push_back(v);
+                p0 = p1 + 1;
+            }
+            std::sort(t.begin(), t.end());
+            treat_times.insert(treat_times.end(), t.begin(), t.end());
+            treat_offset.push_back((int32_t)treat_times.size());
         }
     }
     // cell variabilities (VariabilityDescription::Load, VariabilityDescriptionVariable::Load)
@@ -425,6 +462,27 @@ bool LikelihoodCellPopulation::PostInitialize()
     const int sobol_points = scales.empty() ? 0 : num_cells * 100;
     sobol = SobolPoints(sobol_points, scales.size());
 
+    // treatment trajectories: the species must be a constant species (Experiment.cpp:573-577); every
+    // cell must see its own first discontinuity: the reference's solver keeps the last one across the
+    // cells of its pool when a cell sets none (ODESolver::SetDiscontinuity is skipped, Cell.cpp:226),
+    // which this restatement does not reproduce, so pulses must run past the experiment's end
+    treat_species.clear();
+    for (size_t i = 0; i < treat_names.size(); i++) {
+        const size_t ix = sbml.GetConstantSpeciesByName(treat_names[i]);
+        if (ix == SIZE_MAX) {
+            LOGERROR("Cannot find \"%s\" as a constant species for treatment trajectory (the species needs to be constant).",
+                     treat_names[i].c_str());
+            return false;
+        }
+        treat_species.push_back((int32_t)ix);
+        const int n = treat_offset[i + 1] - treat_offset[i];
+        if (n == 0 || treat_times[treat_offset[i + 1] - 1] + 14.0 <= output_times.back() + trailing) {
+            LOGERROR("Treatment trajectory for \"%s\": the pulses end before the experiment does; cells created after "
+                     "the last pulse would inherit another cell's solver discontinuity in the reference (not supported)",
+                     treat_names[i].c_str());
+            return false;
+        }
+    }
     data_flat.clear();
     for (const auto& d : data)
         data_flat.push_back(bcm3hip_cellpop_data{(int32_t)d.times.size(), d.R, d.observed.data(), d.entry.data(), d.stdev,
@@ -463,6 +521,10 @@ bool LikelihoodCellPopulation::PostInitialize()
     model.actions = actions.data();
     model.n_data = (int32_t)data_flat.size();
     model.data = data_flat.data();
+    model.n_treat = (int32_t)treat_species.size();
+    model.treat_species = treat_species.data();
+    model.treat_offset = treat_offset.data();
+    model.treat_times = treat_times.data();
     if (host_only) return true;
     std::vector<bcm3hip_cellpop_model> models{model};
     for (const auto& e : more_experiments) models.push_back(e->model);

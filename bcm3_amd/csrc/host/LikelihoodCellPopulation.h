@@ -76,6 +76,10 @@ private:
     std::vector<bcm3hip_value_ref> scales;
     std::vector<bcm3hip_variability_action> actions;
     std::vector<bcm3hip_cellpop_data> data_flat;
+    // <treatment_trajectory type="pulses">: constant-species index, pulse start times per trajectory
+    std::vector<int32_t> treat_species, treat_offset{0};
+    std::vector<double> treat_times;
+    std::vector<std::string> treat_names;
     bcm3hip_cellpop_model model{};
     bool host_only = false;
     // the second and later <experiment>s (host-side descriptions; one device context sums them)

@@ -236,6 +236,14 @@ typedef struct {
     const bcm3hip_variability_action* actions;
     int32_t n_data;
     const bcm3hip_cellpop_data* data;
+    /* <treatment_trajectory type="pulses"> (TreatmentTrajectoryPulses, src/cellpop/
+     * TreatmentTrajectoryPulses.cpp): the constant species treat_species[i] follows pulses starting at
+     * treat_times[treat_offset[i] .. treat_offset[i+1]) (sorted), with the solver's discontinuities at
+     * the pulse corners (Cell.cpp:212-229, 447-461); n_treat = 0: none */
+    int32_t n_treat;
+    const int32_t* treat_species;  /* [n_treat] constant-species index */
+    const int32_t* treat_offset;   /* [n_treat + 1] */
+    const double* treat_times;     /* [treat_offset[n_treat]] */
 } bcm3hip_cellpop_model;
 
 /* Per-cell results of the last evaluation (bcm3hip_cellpop_cells), one record per cell slot. */

@@ -47,7 +47,8 @@ class CellIn(C.Structure):
                 ("max_steps", C.c_int), ("divide_cells", C.c_int), ("simulate_past_chromatid_separation_time", C.c_double),
                 ("ev_replicating", C.c_int), ("ev_replicated", C.c_int), ("ev_pcna", C.c_int),
                 ("ev_nuclear_envelope", C.c_int), ("ev_chromatid_separation", C.c_int), ("ev_cytokinesis", C.c_int),
-                ("ev_apoptosis", C.c_int)]
+                ("ev_apoptosis", C.c_int), ("n_constant", C.c_int), ("n_treat", C.c_int), ("treat_cs", C.c_void_p),
+                ("treat_off", C.c_void_p), ("treat_times", C.c_void_p)]
 
 
 class CellOut(C.Structure):
@@ -193,6 +194,15 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant=""):
     for sp in ex.iter("set_parameter"):
         forced[sp.get("parameter_name")] = float(sp.get("value"))
     e["forced"] = forced
+    # treatment trajectories (Experiment.cpp:571-584; TreatmentTrajectoryPulses::Load): in document
+    # order, the constant species index and the sorted pulse start times
+    treats = []
+    for tt in ex.iter("treatment_trajectory"):
+        assert tt.get("type") == "pulses", tt.get("type")
+        ci = model.constant_index(tt.get("species_name"))
+        assert ci is not None, tt.get("species_name")
+        treats.append((ci, sorted(float(x) for x in tt.get("times").split(","))))
+    e["treatments"] = treats
     # variabilities (VariabilityDescription::Load; diagonal_gaussian)
     vds = []
     for cv in ex.iter("cell_variability"):
@@ -329,6 +339,10 @@ def simulate_experiment(e, prob, values):
     lib = ref_lib(prob.get("variant", ""))
     rhs = C.cast(e["deriv_lib"].generated_derivative, C.c_void_p).value
     const = np.ascontiguousarray(e["constant_init"], dtype=float)
+    treats = e.get("treatments", [])
+    t_cs = np.array([t[0] for t in treats] or [0], dtype=np.int32)
+    t_off = np.array([0] + list(np.cumsum([len(t[1]) for t in treats])), dtype=np.int32)
+    t_times = np.array([x for t in treats for x in t[1]] or [0.0], dtype=float)
     cells = []  # dicts
     fail = False
 
@@ -383,6 +397,11 @@ def simulate_experiment(e, prob, values):
         cin.simulate_past_chromatid_separation_time = e["past_cs"]
         (cin.ev_replicating, cin.ev_replicated, cin.ev_pcna, cin.ev_nuclear_envelope, cin.ev_chromatid_separation,
          cin.ev_cytokinesis, cin.ev_apoptosis) = e["events"]
+        cin.n_constant = len(const)
+        cin.n_treat = len(treats)
+        cin.treat_cs = t_cs.ctypes.data
+        cin.treat_off = t_off.ctypes.data
+        cin.treat_times = t_times.ctypes.data
         cout = CellOut()
         vals = np.empty(M)
         end_y = np.empty(N)

@@ -62,6 +62,13 @@ typedef struct {
     // event species: SIMULATED-species indices used on the ODE state (Cell.cpp:44-50); -1 = absent
     int ev_replicating, ev_replicated, ev_pcna, ev_nuclear_envelope, ev_chromatid_separation, ev_cytokinesis,
         ev_apoptosis;
+    // treatment trajectories of type pulses (TreatmentTrajectoryPulses.cpp): constant species
+    // treat_cs[i] follows the pulses treat_times[treat_off[i] .. treat_off[i+1]) (sorted)
+    int n_constant;  // constant species (constant_species[n_constant])
+    int n_treat;
+    const int* treat_cs;
+    const int* treat_off;
+    const double* treat_times;
 } cp_cell_in;
 
 typedef struct {
@@ -132,6 +139,7 @@ struct Cell {
     int N;
     void* mem;
     std::vector<double> y_copy, work;
+    std::vector<double> cs;  // constant_species_y with the treatment concentrations
     // Cell / ODESolver state
     double t;
     double previous_integration_step_time;
@@ -142,10 +150,62 @@ struct Cell {
 
 void silent_err(int, const char*, const char*, char*, void*) {}
 
+// TreatmentTrajectoryPulses::GetConcentration / FirstDiscontinuity / NextDiscontinuity (:22-71)
+double pulse_concentration(const double* tp, int n, double time, double creation_time)
+{
+    const double global_time = time + creation_time;
+    for (int i = 0; i < n; i++) {
+        const double t_in_pulse = global_time - tp[i] - 2.0;
+        if (t_in_pulse >= 14.0) {
+            continue;
+        } else if (t_in_pulse <= 0.0) {
+            return 0.0;
+        } else if (t_in_pulse < 2.0) {
+            return t_in_pulse * 0.5;
+        } else if (t_in_pulse < 10.0) {
+            return 1.0;
+        } else {
+            return 1 - (t_in_pulse - 10.0) * 0.25;
+        }
+    }
+    return 0.0;
+}
+double pulse_first(const double* tp, int n, double creation_time)
+{
+    return n > 0 ? tp[0] - creation_time + 2.0 : std::numeric_limits<double>::quiet_NaN();
+}
+double pulse_next(const double* tp, int n, double time, double creation_time)
+{
+    for (int i = 0; i < n; i++) {
+        if (time == tp[i] - creation_time + 2.0) {
+            return tp[i] - creation_time + 4.0;
+        } else if (time == tp[i] - creation_time + 4.0) {
+            return tp[i] - creation_time + 10.0;
+        } else if (time == tp[i] - creation_time + 10.0) {
+            return tp[i] - creation_time + 14.0;
+        } else if (time == tp[i] - creation_time + 14.0) {
+            if (i < n - 1) return tp[i + 1] - creation_time + 2.0;
+            return std::numeric_limits<double>::quiet_NaN();
+        }
+    }
+    return std::numeric_limits<double>::quiet_NaN();
+}
+
+// Cell::SetTreatmentConcentration (Cell.cpp:414-420)
+const double* constants_at(Cell* c, double t)
+{
+    const cp_cell_in* in = c->in;
+    for (int i = 0; i < in->n_treat; i++)
+        c->cs[in->treat_cs[i]] = pulse_concentration(in->treat_times + in->treat_off[i], in->treat_off[i + 1] - in->treat_off[i],
+                                                     t, in->creation_time);
+    return c->cs.data();
+}
+
+// Cell::solver_rhs_fn (Cell.cpp:422-432)
 int rhs_fn(realtype t, N_Vector y, N_Vector ydot, void* user)
 {
     Cell* c = (Cell*)user;
-    c->in->rhs(NV_DATA_S(ydot), NV_DATA_S(y), c->in->constant_species, c->in->parameters, c->in->non_sampled_parameters);
+    c->in->rhs(NV_DATA_S(ydot), NV_DATA_S(y), constants_at(c, t), c->in->parameters, c->in->non_sampled_parameters);
     return 0;
 }
 
@@ -171,7 +231,7 @@ int jac_fn(realtype t, N_Vector y, N_Vector fy, SUNMatrix J, void* user, N_Vecto
     for (int j = 0; j < N; j++) {
         const double inc = std::max(srur * fabs(yd[j]), minInc / ewt[j]);
         c->y_copy[j] += inc;
-        c->in->rhs(c->work.data(), c->y_copy.data(), c->in->constant_species, c->in->parameters,
+        c->in->rhs(c->work.data(), c->y_copy.data(), constants_at(c, t), c->in->parameters,
                    c->in->non_sampled_parameters);
         c->y_copy[j] = yd[j];
         const double inc_inv = 1.0 / inc;
@@ -257,6 +317,7 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
     c.N = N;
     c.y_copy.assign(N, 0.0);
     c.work.assign(N, 0.0);
+    c.cs.assign(in->constant_species, in->constant_species + in->n_constant);
     c.divided = c.died = false;
     for (int k = 0; k < 5; k++) c.ev[k] = std::numeric_limits<double>::quiet_NaN();
     out->nsteps = 0;
@@ -302,7 +363,24 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
         CVodeSetMaxStep(mem, in->hmax);
         CVodeSetErrHandlerFn(mem, silent_err, nullptr);
         CVodeSVtolerances(mem, in->rtol, atol);
+        // Cell::Simulate: the first discontinuity of the treatment trajectories (Cell.cpp:212-229);
+        // ODESolver::SetDiscontinuity ignores times <= 0 (a fresh solver: NaN)
+        double next_disc = std::numeric_limits<double>::quiet_NaN();
+        {
+            double first = std::numeric_limits<double>::quiet_NaN();
+            for (int i = 0; i < in->n_treat; i++) {
+                const double* tpp = in->treat_times + in->treat_off[i];
+                const int nt = in->treat_off[i + 1] - in->treat_off[i];
+                double d = pulse_first(tpp, nt, in->creation_time);
+                if (!std::isnan(d)) {
+                    while (d < 0.0) d = pulse_next(tpp, nt, d, in->creation_time);
+                }
+                if (!(first < d)) first = d;  // Cell.cpp:222: a NaN replaces
+            }
+            if (!std::isnan(first) && first > 0.0) next_disc = first;
+        }
         CVodeReInit(mem, 0.0, y);
+        if (!std::isnan(next_disc)) CVodeSetStopTime(mem, next_disc);
         // ODESolverCVODE::Solve (:322-463)
         long current_step = 0;
         c.t = 0.0;
@@ -331,6 +409,23 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
             if (current_step == in->max_steps) {
                 result = false;
                 break;
+            }
+            // ODESolverCVODE::Solve :449-460 with Cell::discontinuity_cb (Cell.cpp:447-461)
+            if (!std::isnan(next_disc) && (r == CV_TSTOP_RETURN || next_disc == c.t)) {
+                double disc = std::numeric_limits<double>::infinity();
+                for (int i = 0; i < in->n_treat; i++) {
+                    const double d = pulse_next(in->treat_times + in->treat_off[i], in->treat_off[i + 1] - in->treat_off[i],
+                                                c.t, in->creation_time);
+                    if (d < disc) disc = d;
+                }
+                next_disc = (disc == std::numeric_limits<double>::infinity()) ? std::numeric_limits<double>::quiet_NaN()
+                                                                               : disc;
+                if (!std::isnan(next_disc) && next_disc < std::numeric_limits<double>::infinity()) {
+                    CVodeReInit(mem, c.t, y);
+                    CVodeSetStopTime(mem, next_disc);
+                } else {
+                    CVodeReInit(mem, c.t, y);
+                }
             }
         }
         nst = current_step;

@@ -163,14 +163,15 @@ def prior_text():
 
 
 def likelihood_text(num_cells=500, max_cells=2048, data_file="cellpop_data.json", model_file="cellpop_model.xml",
-                    data_attrs='stdev="stdev"', experiment_attrs=""):
+                    data_attrs='stdev="stdev"', experiment_attrs="", extra=""):
+    """extra: further children of the <experiment> (e.g. a <treatment_trajectory>)"""
     return f"""<bcm_likelihood type="cell_population">
   <experiment name="exp1" model_file="{model_file}" data_file="{data_file}" num_cells="{num_cells}" max_cells="{max_cells}" entry_time="0"{experiment_attrs}>
     <cell_variability distribution="diagonal_gaussian">
       <variable model_parameter="k_D" apply="multiplicative_log" scale="var_kD"/>
       <variable initial_condition_species="CycD" apply="multiplicative_log" scale="var_CycD0"/>
     </cell_variability>
-    <data type="time_course_population_average" data_name="pcna_mean" species_name="PCNA_gfp" {data_attrs}/>
+    <data type="time_course_population_average" data_name="pcna_mean" species_name="PCNA_gfp" {data_attrs}/>{extra}
   </experiment>
 </bcm_likelihood>
 """

@@ -196,3 +196,41 @@ def test_several_experiments_load(tmp_path):
     none.write_text('<bcm_likelihood type="cell_population">\n</bcm_likelihood>\n')
     with pytest.raises(RuntimeError):
         Likelihood(str(none), CH.PRIOR, options="backend=none")
+
+
+def test_treatment_trajectory_options(tmp_path):
+    """<treatment_trajectory> (Experiment.cpp:571-584, TreatmentTrajectory::Create): pulses load, with
+    their times sorted; from_data fails (its loader returns failure in the reference), unknown types
+    and non-constant species fail; pulses that end before the experiment does are refused (the
+    reference would carry a stale discontinuity between the cells of its pool)"""
+    from bcm3_amd.likelihood import Likelihood
+    good = '\n    <treatment_trajectory type="pulses" species_name="mitogen" times="13,-1"/>'
+    path = CH.write_likelihood(tmp_path, 4, 16, name="treat_ok.xml", extra=good)
+    Likelihood(path, CH.PRIOR, options="backend=none").close()
+    e = CP.load_problem(path, CH.PRIOR)["experiments"][0]
+    assert e["treatments"] == [(0, [-1.0, 13.0])]
+    bad = ['\n    <treatment_trajectory type="from_data" species_name="mitogen"/>',
+           '\n    <treatment_trajectory type="steps" species_name="mitogen" times="1"/>',
+           '\n    <treatment_trajectory type="pulses" species_name="CycD" times="1"/>',
+           '\n    <treatment_trajectory type="pulses" species_name="mitogen" times="0,2"/>',
+           '\n    <treatment_trajectory type="pulses" species_name="mitogen" times="1,x"/>']
+    for i, b in enumerate(bad):
+        p = CH.write_likelihood(tmp_path, 4, 16, name=f"treat_bad{i}.xml", extra=b)
+        with pytest.raises(RuntimeError):
+            Likelihood(p, CH.PRIOR, options="backend=none")
+
+
+def test_oracle_runs_treatment_trajectory(tmp_path):
+    """the oracle with a pulse treatment on mitogen (the constant species of CycD synthesis): mitogen is
+    0 outside the pulses, so the treated population divides later than the untreated one (mitogen 1)"""
+    good = '\n    <treatment_trajectory type="pulses" species_name="mitogen" times="13,-1"/>'
+    treated = CP.load_problem(CH.write_likelihood(tmp_path, 4, 32, name="t.xml", extra=good), CH.PRIOR)
+    plain = CP.load_problem(CH.write_likelihood(tmp_path, 4, 32, name="p.xml"), CH.PRIOR)
+    x = CH.draws(2, 5)
+    rt, rp = CP.simulate(treated, x), CP.simulate(plain, x)
+    for i in range(2):
+        ct, cp = rt["detail"][i]["cells"], rp["detail"][i]["cells"]
+        assert all(c["ok"] for c in ct if "ok" in c)
+        first_t = min(c["sim_end"] for c in ct[:4] if c["divided"]) if any(c["divided"] for c in ct[:4]) else 1e9
+        first_p = min(c["sim_end"] for c in cp[:4] if c["divided"]) if any(c["divided"] for c in cp[:4]) else 1e9
+        assert first_t > first_p, (i, first_t, first_p)

@@ -28,6 +28,8 @@ import cellpop as CP
 pytestmark = pytest.mark.gpu
 
 
+TREAT = '\n    <treatment_trajectory type="pulses" species_name="mitogen" times="13,-1"/>'
+
 # (initial cells, max cells, draws, likelihood options): the small case runs many draws; the larger
 # one fills several four-cell wavefronts per generation with cells of different dynamics (rows
 # diverge); the last two take the other error models (DataLikelihoodBase.cpp:51-70) and a
@@ -35,10 +37,17 @@ pytestmark = pytest.mark.gpu
 CASES = [(6, 64, 12, {}), (40, 256, 4, {}),
          (8, 64, 6, dict(data_attrs='stdev="stdev" error_model="additive_proportional_normal" proportional_stdev="0.05"')),
          (6, 32, 6, dict(data_attrs='stdev="stdev" error_model="t4"', experiment_attrs=' divide_cells="false"')),
-         (6, 64, 6, dict(data_attrs='stdev="stdev" relative_to_time_average="true" offset="0.05"'))]
+         (6, 64, 6, dict(data_attrs='stdev="stdev" relative_to_time_average="true" offset="0.05"')),
+         # a treatment trajectory (TreatmentTrajectoryPulses) on the constant species mitogen: the
+         # right-hand side follows the pulses and the solver stops and restarts at every pulse corner
+         (8, 64, 6, dict(extra=TREAT)),
+         # overlapping pulses: the next corner the reference's NextDiscontinuity gives after a pulse
+         # end can lie behind the cell's time; CVode then refuses the stop time and the cell fails
+         (6, 64, 4, dict(extra=TREAT.replace('"13,-1"', '"6,-1,13"')))]
 
 
-@pytest.fixture(scope="module", params=CASES, ids=["6cells", "40cells", "addprop", "t4_nodiv", "reltime"])
+@pytest.fixture(scope="module", params=CASES, ids=["6cells", "40cells", "addprop", "t4_nodiv", "reltime", "pulses",
+                                                           "pulses_overlap"])
 def setup(request, tmp_path_factory):
     from bcm3_amd.likelihood import Likelihood
     nc, mc, nd, attrs = request.param
