@@ -543,10 +543,8 @@ BDF_INL void complete_head_q(S& s)
     BDF_PH(7);
 }
 
-// tq13_held (fast_run): s.tq[1] / s.tq[3] already hold tq_13 of the current coefficients (tc and h
-// unchanged since they were computed), so they are not computed again -- the same bits
 template <int Q, int NS, bool FAST, class S>
-BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc, bool* tq13_held = nullptr)
+BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
 {
     constexpr int q = Q;
     if (BDF_UNLIKELY(!FAST && (s.etamax == 1.0))) {
@@ -560,23 +558,12 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc, bool* tq13_held =
         s.qprime = q;
         if (s.qwait == 0) {
             s.qwait = 2;
-            if (!tq13_held || !*tq13_held) {
-                vec::tq_13<q>(s, tc);  // qwait was 1 in this step's set_bdf_q
-                if (tq13_held) *tq13_held = true;
-            }
+            vec::tq_13<q>(s, tc);  // qwait was 1 in this step's set_bdf_q
             double etaqm1 = 0.0, etaqp1 = 0.0;
             if constexpr (q > 1) etaqm1 = uni::eta_candidate<q>(BIAS1 * vec::wrms<NS>(s.zn[q], s.ewt) * s.tq[1]);
             if constexpr (q != QMAX) {
                 if (s.saved_tq5 != 0.0) {
-                    double cquot;
-#ifdef BCM3_CORRECTLY_ROUNDED
-                    // at an unchanged step size and coefficients both quotients are x / x = 1 exactly
-                    // (correctly rounded division), so cquot = 1 * 1^(q+1) = 1
-                    if ((s.tq[5] == s.saved_tq5) & (s.h == s.tau[2]) & (fabs(s.h) < INFINITY) & (fabs(s.tq[5]) < INFINITY))
-                        cquot = 1.0;
-                    else
-#endif
-                        cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
+                    const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
                     const double tv = __builtin_fma(-cquot, s.zn[QMAX], s.acor);
                     etaqp1 = uni::eta_candidate<q + 2>(BIAS3 * vec::wrms<NS>(tv, s.ewt) * s.tq[3]);
                 }
@@ -605,10 +592,10 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc, bool* tq13_held =
 }
 
 template <int Q, int NS, bool FAST, class S>
-BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc, bool* tq13_held = nullptr)
+BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc)
 {
     vec::complete_head_q<Q>(s);
-    vec::complete_eta_q<Q, NS, FAST>(s, dsm, tc, tq13_held);
+    vec::complete_eta_q<Q, NS, FAST>(s, dsm, tc);
 }
 
 template <int Q, int NS, bool FAST = false, class S, class Model>
@@ -826,7 +813,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
     // setup has changed gammap since. cscale_h is the Newton scale 2 / (1 + gamrat) computed from
     // gamrat_h, the gamrat it was computed with.
     int run = 0;
-    bool have = false, tq13 = false;  // tq13: s.tq[1] / s.tq[3] hold tq_13 of the coefficients in tc
+    bool have = false;
     TqCtx tc;
     double rl1 = 0.0, cscale_h = 1.0, gamrat_h = 0.0;
     for (;;) {
@@ -866,10 +853,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             if (eta_eff != 1.0) vec::rescale_q<Q>(s, eta_eff);
             vec::predict_q<Q>(s);
             BDF_PH(3);
-            if (!reuse) {
-                rl1 = vec::set_bdf_q<Q, true>(s, tc);
-                tq13 = false;
-            }
+            if (!reuse) rl1 = vec::set_bdf_q<Q, true>(s, tc);
             BDF_PH(4);
             setup = (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);
             cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
@@ -903,7 +887,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
                 return NEED_ATTEMPTS;
             }
         }
-        vec::complete_q<Q, NS, true>(s, dsm, tc, &tq13);
+        vec::complete_q<Q, NS, true>(s, dsm, tc);
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         const bool quiet = (fabs(s.tn - s.tstop) > troundoff) & !((s.tn + s.hprime - s.tstop) * s.h > 0.0) &
                            (s.tn < tlim) & (s.qprime == Q) & (current_step + 1 != max_steps);
