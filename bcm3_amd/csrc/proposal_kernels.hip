@@ -914,7 +914,8 @@ __global__ void __launch_bounds__(64 * kKnnWaves) ptmh_spec_predict_kernel(int C
 // wavefronts the device runs at once one per SIMD (first_round): the hardware gives batch
 // positions p and p + R the same SIMD (measured, tools/placement.py), so the M - R shortest go to
 // positions R.., the next M - R shortest to positions 0.. (they share SIMDs with each other), and
-// the 2R - M longest run alone at positions M - R .. R - 1; first_round = 0: plain longest first.
+// the 2R - M longest run alone at positions M - R .. R - 1 (R < M <= 2R); otherwise, or with
+// first_round = 0, plain longest first.
 constexpr int kSpecSortMax = 4096;
 constexpr int kSpecBuckets = 2048;
 __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, const double* __restrict__ prop,
@@ -965,8 +966,10 @@ __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, con
     for (int i = tid; i < kSpecSortMax; i += blockDim.x) pos_of[i] = -1;
     __syncthreads();
     const int R = first_round;
-    const int S2 = (R > 0 && M > R) ? M - R : 0;  // entries of the second round
-    const int L = M - 2 * S2;                      // entries that run alone
+    // entries of the second round; beyond 2R entries every SIMD takes two and more wait for a free
+    // one, so the layout is plain longest first there
+    const int S2 = (R > 0 && M > R && M <= 2 * R) ? M - R : 0;
+    const int L = M - 2 * S2;  // entries that run alone (L >= 0)
     for (int q = 0; q < kPer; q++) {
         if (bk[q] < 0) continue;
         const int r = cnt[bk[q]] + rk[q];

@@ -248,6 +248,27 @@ def test_speculative_pairs_bit_identical(tmp_path, proposal, C, t_dof):
         assert _same(v0, v1)
 
 
+@pytest.mark.parametrize("C", [256, 512])
+def test_speculative_pairs_bit_identical_large_batches(C):
+    """the batch layouts of ptmh_spec_batch_kernel at the chip's size: 256 chains make ~1,300 entries
+    (more than the 1,024 SIMDs: the shortest pair up on shared SIMDs, the longest run alone); 512
+    chains make ~2,600 (more than two per SIMD: plain longest-first order). Either way every entry is
+    evaluated once and the chains match the one-launch-per-iteration loop bit for bit"""
+    res = []
+    for spec in (0, 1):
+        s = _native(*C3, C, 23, 0, speculate=spec)
+        s.iterate(24)
+        s.synchronize()
+        res.append((s.state(), s.counters()))
+        if spec:
+            info = s.spec_batch_info()
+            assert info is not None and len(info[0]) > C  # speculation was used
+            assert len(set(info[0].tolist())) == len(info[0])  # each entry at one position
+        s.close()
+    _compare(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1]
+
+
 def test_speculation_is_used_for_popk():
     """the C3 sampler runs its iterations as speculative pairs: one likelihood launch per two
     iterations (the timing log counts launches)"""

@@ -99,7 +99,7 @@ def main():
     # the batch layout (ptmh_spec_batch_kernel): predicted rank r -> position; invert it with the
     # device's SIMD count R (positions p and p + R share a SIMD)
     R = _hip.lib().bcm3hip_current_device_simds() if hasattr(_hip.lib(), "bcm3hip_current_device_simds") else 0
-    S2 = n - R if 0 < R < n else 0
+    S2 = n - R if 0 < R < n <= 2 * R else 0
     L = n - 2 * S2
     p = np.arange(n)
     pred_rank = np.where(p < S2, L + p, np.where(p < R, p - S2, L + S2 + (p - R))) if S2 else p
