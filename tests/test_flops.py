@@ -46,3 +46,22 @@ def test_counter_counts_only_arithmetic():
     n1 = orc.lib.orc_flops_take()
     orc.lib.orc_log_pdf_tnu4(3.0, 0.5, 2.0)
     assert orc.lib.orc_flops_take() == n1 > 0
+
+
+def test_c4_falg_fixture_matches_the_model():
+    """tests/golden/c4_falg.json (bench.py's C4 FP64 roofline): its right-hand-side operation count
+    is the count of the committed cell model's generated derivative (make_c4_falg.rhs_ops), and the
+    per-cell-step figure is within the model's range (RHS-dominated, N = 15 species)"""
+    import sys
+    if GOLDEN not in sys.path:
+        sys.path.insert(0, GOLDEN)
+    import cellpop as CP
+    import cellpop_helpers as CH
+    import make_c4_falg as F
+    with open(os.path.join(GOLDEN, "c4_falg.json")) as f:
+        fx = json.load(f)
+    prob = CP.load_problem(os.path.join(GOLDEN, "cellpop_likelihood.xml"), CH.PRIOR)
+    e = prob["experiments"][0]
+    assert fx["species"] == len(e["model"].ode) == 15
+    assert fx["f_rhs"] == F.rhs_ops(e["derivative_body"])
+    assert 20 * fx["species"] + 70 < fx["flops_per_cell_step"] < 10 * (fx["species"] * fx["f_rhs"])
