@@ -130,6 +130,9 @@ def lib() -> C.CDLL:
     if hasattr(L, "bcm3hip_placement_log"):  # (absent from libraries built before it: tools/variant_timing.py)
         L.bcm3hip_placement_log.argtypes = [vp, i64, vp]
         L.bcm3hip_placement_log.restype = i64
+    if hasattr(L, "bcm3hip_assign_cells"):
+        L.bcm3hip_assign_cells.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
+        L.bcm3hip_assign_cells.restype = C.c_int
     L.bcm3hip_eval_batch_detail.argtypes = [vp, sz, sz, vp, vp, vp, vp, vp, vp]
     for f in ("bcm3hip_open_popk", "bcm3hip_open_analytic", "bcm3hip_open_expm_pk", "bcm3hip_close", "bcm3hip_set_option",
               "bcm3hip_num_variables", "bcm3hip_eval_batch", "bcm3hip_eval_batch_device",
@@ -143,6 +146,23 @@ def check(code: int, what: str = "bcm3hip"):
     if code != 0:
         msg = lib().bcm3hip_error_string(code).decode()
         raise RuntimeError(f"{what} failed: {msg} ({code})")
+
+
+def assign_cells(lik):
+    """The time-course likelihood's observed-to-simulated cell matching alone, on lik's device
+    (bcm3hip_assign_cells). lik: CUDA float64 tensor [problems, observed cells, simulated cells] of
+    cell log-likelihoods. Returns numpy (match [problems, R], sum [problems], ok [problems])."""
+    import torch
+    lik = lik.contiguous()
+    P, R, S = lik.shape
+    match = torch.empty((P, R), dtype=torch.int32, device=lik.device)
+    total = torch.empty(P, dtype=torch.float64, device=lik.device)
+    ok = torch.empty(P, dtype=torch.int32, device=lik.device)
+    stream = torch.cuda.current_stream(lik.device).cuda_stream
+    check(lib().bcm3hip_assign_cells(P, R, S, lik.data_ptr(), match.data_ptr(), total.data_ptr(), ok.data_ptr(),
+                                     stream), "bcm3hip_assign_cells")
+    torch.cuda.synchronize(lik.device)
+    return match.cpu().numpy(), total.cpu().numpy(), ok.cpu().numpy()
 
 
 def _ptr(a: Optional[np.ndarray]):

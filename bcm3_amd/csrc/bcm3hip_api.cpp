@@ -29,6 +29,10 @@ int cellpop_launch(CellPopDev* c, size_t n, const double* values, double* logp, 
 int cellpop_cells(CellPopDev* c, size_t item, int32_t* count, bcm3hip_cell_record* rec, double* values, double* end_y);
 hipError_t launch_cp_accumulate(int32_t n, double* logp, int32_t* status, const double* x, const int32_t* xstatus,
                                 hipStream_t s);
+hipError_t launch_cp_assign(int32_t n_problems, int32_t R, int32_t nsim, const double* lik, unsigned char* ws_global,
+                            size_t ws_stride, int32_t* match, double* sum, int32_t* ok, hipStream_t s);
+size_t cp_assign_ws_bytes(int n);
+inline bool cp_assign_lds_fits(int n) { return cp_assign_ws_bytes(n) <= 56 * 1024; }
 }  // namespace bcm3hip
 
 struct bcm3hip_ctx {
@@ -511,6 +515,29 @@ int64_t bcm3hip_placement_log(bcm3hip_ctx* c, int64_t n_max, uint64_t* host_out)
     const int64_t m = n_max < c->place_n ? n_max : c->place_n;
     if (m > 0) HIPCHK(hipMemcpy(host_out, c->place, (size_t)m * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost));
     return m;
+}
+
+int bcm3hip_assign_cells(int32_t n_problems, int32_t R, int32_t nsim, const double* lik, int32_t* match, double* sum,
+                         int32_t* ok, void* stream)
+{
+    if (n_problems < 0 || R < 1 || R > 1024 || nsim < 1 || nsim > 65535 || (n_problems > 0 && (!lik || !match || !sum || !ok)))
+        return BCM3HIP_ERR_ARG;
+    if (n_problems == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    const int nw = R > nsim ? R : nsim;
+    unsigned char* ws = nullptr;
+    size_t stride = 0;
+    if (!bcm3hip::cp_assign_lds_fits(nw)) {
+        stride = (bcm3hip::cp_assign_ws_bytes(nw) + 255) / 256 * 256;
+        HIPCHK(hipMalloc((void**)&ws, stride * n_problems));
+    }
+    hipError_t e = bcm3hip::launch_cp_assign(n_problems, R, nsim, lik, ws, stride, match, sum, ok, s);
+    if (ws) {
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        hipFree(ws);
+    }
+    HIPCHK(e);
+    return 0;
 }
 
 static int ensure_traj_scratch(bcm3hip_ctx* c, size_t n)

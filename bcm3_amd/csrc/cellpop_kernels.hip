@@ -8,7 +8,11 @@
 //                     gaussian: QuantileNormal(sobol) * exp(scale); ApplyVariability*);
 //   cp_popavg_kernel  one wavefront per evaluation: CountCellsAtTime + NotifySimulatedValue in cell
 //                     order (Experiment.cpp:298-311, DataLikelihoodTimeCoursePopulationAverage.cpp)
-//                     and DataLikelihoodTimeCoursePopulationAverage::Evaluate.
+//                     and DataLikelihoodTimeCoursePopulationAverage::Evaluate, then the sum over
+//                     the data likelihoods (time courses from cp_timecourse_kernel);
+//   cp_timecourse_kernel  one workgroup per (evaluation, time-course data likelihood): the cell
+//                     likelihood matrix and the observed-to-simulated matching
+//                     (DataLikelihoodTimeCourse::Evaluate).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -104,6 +108,7 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
                                                        const int32_t* ncells, const int32_t* failed,
                                                        const double* out_values, const double* creation,
                                                        const double* sim_end, double* avg /*[n][M]*/,
+                                                       const double* tc_logp, const int32_t* tc_ok,
                                                        double* logp, int32_t* status)
 {
     const int e = blockIdx.x;
@@ -135,12 +140,20 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
         if (status) status[e] = BCM3HIP_STATUS_SOLVER_FAIL;
         return;
     }
+    // Experiment::EvaluateLogProbability (Experiment.cpp:346-355): the data likelihoods in order; one
+    // whose Evaluate fails (a time course with a NaN cell likelihood) ends the sum, which is kept
     double total = 0.0;
     for (int di = 0; di < m.n_data; di++) {
         const bcm3hip_cellpop_data dl = m.data[di];
-        const double stdev = cp_ref(dl.stdev, v, m.transforms, 1.0);
+        if (dl.kind == BCM3HIP_CP_DATA_TIME_COURSE) {
+            if (!tc_ok[(size_t)e * m.n_data + di]) break;
+            total += tc_logp[(size_t)e * m.n_data + di];
+            continue;
+        }
         const double offset = cp_ref(dl.offset, v, m.transforms, 0.0);
         const double scale = cp_ref(dl.scale, v, m.transforms, 1.0);
+        double stdev = cp_ref(dl.stdev, v, m.transforms, 1.0);
+        if (dl.stdev_relative_to_scale) stdev *= scale;  // GetCurrentSTDev (DataLikelihoodBase.cpp:151-153)
         const double pstdev = cp_ref(dl.proportional_stdev, v, m.transforms, 0.0);
         const double minus_log_sigma = -log(stdev);
         const double inv2 = 1.0 / (2.0 * stdev * stdev);
@@ -189,6 +202,437 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
     if (status) status[e] = BCM3HIP_STATUS_OK;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Time-course data likelihood (DataLikelihoodTimeCourse, src/cellpop/DataLikelihoodTimeCourse.cpp):
+// the likelihood of every observed cell against every simulated cell, then the assignment of
+// observed to simulated cells by the reference's vendored matching routine (dependencies/
+// hungarian2/hungarian.cpp, hungarianMinimumWeightPerfectMatching). One workgroup per
+// (evaluation, data likelihood): its threads fill the cost matrix, one lane runs the matching over
+// a workspace in LDS (global memory when the matrix is too large for 64 KB).
+
+// the matching workspace of one problem with n left and n right nodes
+struct HgWs {
+    double* cost;        // [n*n] -cell likelihood, row = observed cell, column = simulated cell
+    uint16_t* adj;       // [n*n] each left node's edge list (right node per position)
+    double *lpot, *rpot, *slack;
+    int32_t *ntight, *slack_from, *slack_edge, *lmatch, *rmatch, *back, *queue;
+    uint8_t* seen;
+};
+
+__host__ __device__ inline size_t hg_ws_bytes(int n)
+{
+    const size_t nn = (size_t)n * n;
+    return nn * 8 + ((nn * 2 + 7) / 8) * 8 + (size_t)n * 3 * 8 + (size_t)n * 7 * 4 + (size_t)n;
+}
+
+__device__ inline HgWs hg_carve(unsigned char* p, int n)
+{
+    const size_t nn = (size_t)n * n;
+    HgWs w;
+    w.cost = (double*)p;
+    p += nn * 8;
+    w.adj = (uint16_t*)p;
+    p += ((nn * 2 + 7) / 8) * 8;
+    w.lpot = (double*)p;
+    w.rpot = w.lpot + n;
+    w.slack = w.rpot + n;
+    p += (size_t)n * 3 * 8;
+    w.ntight = (int32_t*)p;
+    w.slack_from = w.ntight + n;
+    w.slack_edge = w.slack_from + n;
+    w.lmatch = w.slack_edge + n;
+    w.rmatch = w.lmatch + n;
+    w.back = w.rmatch + n;
+    w.queue = w.back + n;
+    p += (size_t)n * 7 * 4;
+    w.seen = (uint8_t*)p;
+    return w;
+}
+
+// (int)r < 1e-12 as compiled for x86-64 (hungarian.cpp:167-169): r stored in an int truncates
+// toward zero, so every reduced cost below 1 is "tight"; NaN and out-of-range values convert to
+// INT_MIN, tight as well
+__device__ inline bool hg_tight0(double r)
+{
+    if (!(r > -2147483649.0 && r < 2147483648.0)) return true;
+    return (double)(int)r < 1e-12;
+}
+
+// hungarianMinimumWeightPerfectMatching(n, n, edges) over the complete bipartite graph of the
+// cost matrix, edges given row by row (the order DataLikelihoodTimeCourse::Evaluate builds them,
+// .cpp:289-315), so every left node's sorted edge list starts as 0..n-1. Statement for statement
+// the vendored routine (see oracle/hungarian.py for the behaviours this keeps); sequential, one
+// lane. Returns false when it finds no perfect matching.
+__device__ bool hg_match(int n, const HgWs& w)
+{
+    constexpr double OO = 1.7976931348623157e308;
+    const double* C = w.cost;
+    for (int i = 0; i < n; i++) {  // left potentials: the smallest incident cost (:122-134)
+        double m = C[(size_t)i * n];
+        for (int j = 1; j < n; j++)
+            if (C[(size_t)i * n + j] < m) m = C[(size_t)i * n + j];
+        w.lpot[i] = m;
+    }
+    for (int j = 0; j < n; j++) w.rpot[j] = OO;
+    for (int i = 0; i < n; i++)  // right potentials over the edges in order (:141-148)
+        for (int j = 0; j < n; j++) {
+            const double red = C[(size_t)i * n + j] - w.lpot[i];
+            if (w.rpot[j] > red) w.rpot[j] = red;
+        }
+    for (int i = 0; i < n; i++) {  // tight prefixes (:162-177)
+        uint16_t* a = w.adj + (size_t)i * n;
+        for (int k = 0; k < n; k++) a[k] = (uint16_t)k;
+        int t = 0;
+        for (int k = 0; k < n; k++) {
+            const int r = a[k];
+            if (hg_tight0(C[(size_t)i * n + r] - w.lpot[i] - w.rpot[r])) {
+                if (k != t) {
+                    const uint16_t x = a[t];
+                    a[t] = a[k];
+                    a[k] = x;
+                }
+                t++;
+            }
+        }
+        w.ntight[i] = t;
+    }
+    int card = 0;
+    for (int i = 0; i < n; i++) {
+        w.lmatch[i] = -1;
+        w.rmatch[i] = -1;
+    }
+    for (int i = 0; i < n; i++) {  // greedy start (:192-203)
+        const uint16_t* a = w.adj + (size_t)i * n;
+        for (int k = 0; k < w.ntight[i]; k++) {
+            const int j = a[k];
+            if (w.rmatch[j] == -1) {
+                card++;
+                w.rmatch[j] = i;
+                w.lmatch[i] = j;
+                break;
+            }
+        }
+    }
+    while (card < n) {
+        for (int j = 0; j < n; j++) {
+            w.slack[j] = OO;
+            w.slack_from[j] = -1;
+            w.back[j] = -1;
+            w.seen[j] = 0;
+        }
+        int start = -1;
+        double fewest = OO;
+        for (int i = 0; i < n; i++)
+            if (w.lmatch[i] == -1 && (double)w.ntight[i] < fewest) {
+                fewest = (double)w.ntight[i];
+                start = i;
+            }
+        int qh = 0, qt = 0;
+        w.queue[qt++] = start;
+        w.seen[start] = 1;
+        int end = -1;
+        while (end == -1) {
+            while (end == -1 && qh < qt) {  // breadth-first over tight edges (:292-329)
+                const int i = w.queue[qh++];
+                uint16_t* a = w.adj + (size_t)i * n;
+                for (int k = 0; k < w.ntight[i];) {
+                    const int j = a[k];
+                    if (C[(size_t)i * n + j] > w.lpot[i] + w.rpot[j]) {  // loose now
+                        const int last = --w.ntight[i];
+                        const uint16_t x = a[k];
+                        a[k] = a[last];
+                        a[last] = x;
+                        continue;
+                    }
+                    if (w.back[j] == -1) {
+                        w.back[j] = i;
+                        const int m = w.rmatch[j];
+                        if (m == -1) {
+                            end = j;  // the scan goes on: the last unmatched node wins
+                        } else if (!w.seen[m]) {
+                            w.seen[m] = 1;
+                            w.queue[qt++] = m;
+                        }
+                    }
+                    k++;
+                }
+                if (end == -1) {  // slack caches (:336-357)
+                    const double p = w.lpot[i];
+                    for (int k = w.ntight[i]; k < n; k++) {
+                        const int j = a[k];
+                        const int m = w.rmatch[j];
+                        if (m == -1 || !w.seen[m]) {
+                            const double red = C[(size_t)i * n + j] - p - w.rpot[j];
+                            if (red < w.slack[j]) {
+                                w.slack[j] = red;
+                                w.slack_from[j] = i;
+                                w.slack_edge[j] = k;
+                            }
+                        }
+                    }
+                }
+            }
+            if (end == -1) {
+                int jmin = -1;
+                double smin = OO;
+                for (int j = 0; j < n; j++) {  // (:372-381)
+                    const int m = w.rmatch[j];
+                    if ((m == -1 || !w.seen[m]) && w.slack[j] < smin) {
+                        smin = w.slack[j];
+                        jmin = j;
+                    }
+                }
+                if (jmin == -1 || w.slack_from[jmin] == -1) return false;
+                for (int i = 0; i < n; i++)  // (:396-403)
+                    if (w.seen[i]) {
+                        w.lpot[i] += smin;
+                        if (w.lmatch[i] != -1) w.rpot[w.lmatch[i]] -= smin;
+                    }
+                for (int j = 0; j < n; j++) {  // (:406-444)
+                    const int m0 = w.rmatch[j];
+                    if (m0 == -1 || !w.seen[m0]) {
+                        w.slack[j] -= smin;
+                        if (w.slack[j] == 0) {
+                            const int i = w.slack_from[j];
+                            const int k = w.slack_edge[j];
+                            uint16_t* a = w.adj + (size_t)i * n;
+                            if (k != w.ntight[i]) {
+                                const uint16_t x = a[k];
+                                a[k] = a[w.ntight[i]];
+                                a[w.ntight[i]] = x;
+                            }
+                            w.ntight[i]++;
+                            if (end == -1) {
+                                w.back[j] = i;
+                                const int m = w.rmatch[j];
+                                if (m == -1) {
+                                    end = j;
+                                } else if (!w.seen[m]) {
+                                    w.seen[m] = 1;
+                                    w.queue[qt++] = m;
+                                }
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        card++;
+        for (int j = end; j != -1;) {  // flip the augmenting path (:457-468)
+            const int i = w.back[j];
+            const int nxt = w.lmatch[i];
+            w.rmatch[j] = i;
+            w.lmatch[i] = j;
+            j = nxt;
+        }
+    }
+    return true;
+}
+
+__device__ inline double cp_log_pdf_normal(double x, double mu, double sigma)
+{
+    // bcm3::LogPdfNormal (src/utils/ProbabilityDistributions.cpp:129-138)
+    const double two_sigma_sq = 2.0 * sigma * sigma;
+    const double dd = x - mu;
+    return -log(sigma) - 0.91893853320467274178032973640562 - dd * dd / two_sigma_sq;
+}
+
+// the likelihood of observed cell i against simulated cell j: CalculateCellLikelihood for one
+// species and no observed lineage (DataLikelihoodTimeCourse.cpp:451-497), the simulated values
+// scaled and shifted first (:236-241), a missing simulated value penalised by the distance to the
+// cell's first / last simulated time point (CalculateMissingValueLikelihood, :566-588)
+__device__ double cp_cell_likelihood(const bcm3hip_cellpop_data& dl, const double* times, const double* obs,
+                                     const double* xv, double scale, double offset, double stdev, double pstd,
+                                     double msd)
+{
+    const int T = dl.T;
+    const double mls = -log(stdev);
+    const double inv2 = 1.0 / (2.0 * stdev * stdev);
+    double lp = 0.0;
+    for (int k = 0; k < T; k++) {
+        const double y = obs[k];
+        if (y != y) continue;
+        double x = xv[dl.entry[k]] * scale;
+        x += offset;
+        if (x != x) {
+            double first = times[dl.entry[T - 1]], last = times[dl.entry[0]];
+            for (int m = 0; m < T; m++) {
+                double z = xv[dl.entry[m]] * scale;
+                z += offset;
+                if (z == z) {
+                    first = times[dl.entry[m]];
+                    break;
+                }
+            }
+            for (int m = T - 1; m >= 0; m--) {
+                double z = xv[dl.entry[m]] * scale;
+                z += offset;
+                if (z == z) {
+                    last = times[dl.entry[m]];
+                    break;
+                }
+            }
+            const double tk = times[dl.entry[k]];
+            const double off = fmin(fabs(tk - first), fabs(tk - last));
+            lp += (dl.error_model == BCM3HIP_CP_ERR_T4) ? log_pdf_tnu4(off, 0.0, msd) : cp_log_pdf_normal(off, 0.0, msd);
+        } else if (dl.error_model == BCM3HIP_CP_ERR_NORMAL) {
+            const double dd = y - x;
+            lp += mls - 0.91893853320467274178032973640562 - dd * dd * inv2;
+        } else if (dl.error_model == BCM3HIP_CP_ERR_T4) {
+            lp += log_pdf_tnu4(y, x, stdev);
+        } else {
+            // (:274-285, 475-483): sigma from the scaled value, -log(sigma), 1 / (2 sigma^2)
+            double sigma = pstd * fmax(x, 0.0);
+            if (dl.error_model == BCM3HIP_CP_ERR_ADDITIVE_PROPORTIONAL) sigma += stdev;
+            const double dd = y - x;
+            lp += -log(sigma) - 0.91893853320467274178032973640562 - dd * dd * (1.0 / (2.0 * (sigma * sigma)));
+        }
+    }
+    return lp;
+}
+
+// the cost matrix rows' checks and the matching, on the workspace; lane 0 of the block. Returns
+// Evaluate's result (false: a NaN cell likelihood, .cpp:299-302) and the data likelihood's logp
+__device__ bool cp_tc_assign(int R, int nsim, const HgWs& w, const uint8_t* row_nan, const int32_t* row_finite,
+                             double weight, double* logp, int32_t* match_out)
+{
+    for (int i = 0; i < R; i++) {  // rows in order: NaN -> failure, then too few finite entries
+        if (row_nan[i]) {
+            *logp = -__builtin_inf();
+            return false;
+        }
+        if (row_finite[i] < R) {
+            *logp = -__builtin_inf();
+            return true;
+        }
+    }
+    // n = max(R, nsim); a node without edges (R != nsim) ends the routine (hungarian.cpp:66-71)
+    if (R != nsim || !hg_match(R, w)) {
+        *logp = -__builtin_inf();
+        return true;
+    }
+    double lp = 0.0;
+    for (int i = 0; i < R; i++) {
+        lp += -w.cost[(size_t)i * R + w.lmatch[i]];
+        if (match_out) match_out[i] = w.lmatch[i];
+    }
+    *logp = lp * weight;
+    return true;
+}
+
+// grid (evaluation, data likelihood); blocks of non-time-course data likelihoods return at once
+__global__ __launch_bounds__(256) void cp_timecourse_kernel(CpStatic m, int32_t n, const double* values,
+                                                             const int32_t* ncells, const int32_t* failed,
+                                                             const double* out_values, unsigned char* ws_global,
+                                                             size_t ws_stride, double* tc_logp, int32_t* tc_ok)
+{
+    extern __shared__ __align__(16) unsigned char cp_lds[];
+    const int e = blockIdx.x, di = blockIdx.y;
+    const bcm3hip_cellpop_data dl = m.data[di];
+    if (dl.kind != BCM3HIP_CP_DATA_TIME_COURSE || e >= n || failed[e]) return;
+    const int R = dl.R, nsim = ncells[e];
+    const int nw = R > nsim ? R : nsim;
+    unsigned char* base = ws_global ? ws_global + ((size_t)e * m.n_data + di) * ws_stride : cp_lds;
+    const HgWs w = hg_carve(base, nw);
+    __shared__ int32_t row_finite[1024];
+    __shared__ uint8_t row_nan[1024];
+    const double* v = values + (size_t)e * m.d;
+    const double offset = cp_ref(dl.offset, v, m.transforms, 0.0);
+    const double scale = cp_ref(dl.scale, v, m.transforms, 1.0);
+    double stdev = cp_ref(dl.stdev, v, m.transforms, 1.0);
+    if (dl.stdev_relative_to_scale) stdev *= scale;
+    const double pstd = cp_ref(dl.proportional_stdev, v, m.transforms, 0.0);
+    const double msd = cp_ref(dl.missing_stdev, v, m.transforms, 300.0);
+    const size_t cbase = (size_t)e * m.max_cells;
+    for (int p = threadIdx.x; p < R * nsim; p += blockDim.x) {
+        const int i = p / nsim, j = p % nsim;
+        // simulated cells with a parent are not matched (.cpp:307-309): the initial cells are the
+        // first n0 slots
+        const double L = (j < m.n0) ? cp_cell_likelihood(dl, m.output_times, dl.observed + (size_t)i * dl.T,
+                                                         out_values + (cbase + j) * m.M, scale, offset, stdev, pstd,
+                                                         msd)
+                                    : -__builtin_inf();
+        w.cost[(size_t)i * nw + j] = -L;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < R; i += blockDim.x) {
+        int fin = 0;
+        uint8_t nan = 0;
+        for (int j = 0; j < nsim; j++) {
+            const double c = w.cost[(size_t)i * nw + j];
+            if (j < m.n0 && c != c) nan = 1;
+            fin += (c < __builtin_inf()) ? 1 : 0;
+        }
+        row_finite[i] = fin;
+        row_nan[i] = nan;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double lp;
+    const bool ok = cp_tc_assign(R, nsim, w, row_nan, row_finite, dl.weight, &lp, nullptr);
+    tc_logp[(size_t)e * m.n_data + di] = lp;
+    tc_ok[(size_t)e * m.n_data + di] = ok ? 1 : 0;
+}
+
+hipError_t launch_cp_timecourse(const CpStatic& m, int32_t n, int32_t max_R, const double* values,
+                                const int32_t* ncells, const int32_t* failed, const double* out_values,
+                                unsigned char* ws_global, size_t ws_stride, double* tc_logp, int32_t* tc_ok,
+                                hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    const size_t lds = ws_global ? 0 : hg_ws_bytes(max_R);
+    hipLaunchKernelGGL(cp_timecourse_kernel, dim3(n, m.n_data), dim3(256), lds, s, m, n, values, ncells, failed,
+                       out_values, ws_global, ws_stride, tc_logp, tc_ok);
+    return hipGetLastError();
+}
+
+size_t cp_assign_ws_bytes(int n) { return hg_ws_bytes(n); }
+
+// the matching alone on given cell likelihoods (bcm3hip_assign_cells): one block per problem
+__global__ __launch_bounds__(64) void cp_assign_kernel(int32_t R, int32_t nsim, const double* lik,
+                                                       unsigned char* ws_global, size_t ws_stride, int32_t* match,
+                                                       double* sum, int32_t* ok)
+{
+    extern __shared__ __align__(16) unsigned char cp_lds[];
+    const int p = blockIdx.x;
+    const int nw = R > nsim ? R : nsim;
+    unsigned char* base = ws_global ? ws_global + (size_t)p * ws_stride : cp_lds;
+    const HgWs w = hg_carve(base, nw);
+    __shared__ int32_t row_finite[1024];
+    __shared__ uint8_t row_nan[1024];
+    const double* L = lik + (size_t)p * R * nsim;
+    for (int q = threadIdx.x; q < R * nsim; q += blockDim.x) w.cost[(size_t)(q / nsim) * nw + q % nsim] = -L[q];
+    __syncthreads();
+    for (int i = threadIdx.x; i < R; i += blockDim.x) {
+        int fin = 0;
+        uint8_t nan = 0;
+        for (int j = 0; j < nsim; j++) {
+            const double c = w.cost[(size_t)i * nw + j];
+            nan |= (c != c) ? 1 : 0;
+            fin += (c < __builtin_inf()) ? 1 : 0;
+        }
+        row_finite[i] = fin;
+        row_nan[i] = nan;
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    for (int i = 0; i < R; i++) match[(size_t)p * R + i] = -1;
+    double lp;
+    ok[p] = cp_tc_assign(R, nsim, w, row_nan, row_finite, 1.0, &lp, match + (size_t)p * R) ? 1 : 0;
+    sum[p] = lp;
+}
+
+hipError_t launch_cp_assign(int32_t n_problems, int32_t R, int32_t nsim, const double* lik, unsigned char* ws_global,
+                            size_t ws_stride, int32_t* match, double* sum, int32_t* ok, hipStream_t s)
+{
+    if (n_problems <= 0) return hipSuccess;
+    const int nw = R > nsim ? R : nsim;
+    const size_t lds = ws_global ? 0 : hg_ws_bytes(nw);
+    hipLaunchKernelGGL(cp_assign_kernel, dim3(n_problems), dim3(64), lds, s, R, nsim, lik, ws_global, ws_stride, match,
+                       sum, ok);
+    return hipGetLastError();
+}
+
 hipError_t launch_cp_init(const CpStatic& m, int32_t n_items, const CpInitItem* items, const double* values,
                           double* params, double* y0, double* creation, const double* end_y, const double* achieved,
                           hipStream_t s)
@@ -201,11 +645,12 @@ hipError_t launch_cp_init(const CpStatic& m, int32_t n_items, const CpInitItem* 
 
 hipError_t launch_cp_popavg(const CpStatic& m, int32_t n, const double* values, const int32_t* ncells,
                             const int32_t* failed, const double* out_values, const double* creation,
-                            const double* sim_end, double* avg, double* logp, int32_t* status, hipStream_t s)
+                            const double* sim_end, double* avg, const double* tc_logp, const int32_t* tc_ok,
+                            double* logp, int32_t* status, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(cp_popavg_kernel, dim3(n), dim3(64), 0, s, m, n, values, ncells, failed, out_values, creation,
-                       sim_end, avg, logp, status);
+                       sim_end, avg, tc_logp, tc_ok, logp, status);
     return hipGetLastError();
 }
 

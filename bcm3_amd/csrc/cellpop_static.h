@@ -37,7 +37,19 @@ hipError_t launch_cp_init(const CpStatic& m, int32_t n_items, const CpInitItem* 
                           hipStream_t s);
 hipError_t launch_cp_popavg(const CpStatic& m, int32_t n, const double* values, const int32_t* ncells,
                             const int32_t* failed, const double* out_values, const double* creation,
-                            const double* sim_end, double* avg, double* logp, int32_t* status, hipStream_t s);
+                            const double* sim_end, double* avg, const double* tc_logp, const int32_t* tc_ok,
+                            double* logp, int32_t* status, hipStream_t s);
+// the time-course data likelihoods: per (evaluation, data likelihood) logp and Evaluate's result;
+// ws_global = nullptr: the matching workspace of max_R cells in LDS (cp_assign_lds_fits)
+hipError_t launch_cp_timecourse(const CpStatic& m, int32_t n, int32_t max_R, const double* values,
+                                const int32_t* ncells, const int32_t* failed, const double* out_values,
+                                unsigned char* ws_global, size_t ws_stride, double* tc_logp, int32_t* tc_ok,
+                                hipStream_t s);
+// the matching alone (bcm3hip_assign_cells)
+hipError_t launch_cp_assign(int32_t n_problems, int32_t R, int32_t nsim, const double* lik, unsigned char* ws_global,
+                            size_t ws_stride, int32_t* match, double* sum, int32_t* ok, hipStream_t s);
+size_t cp_assign_ws_bytes(int n);  // the matching workspace of n x n cells
+inline bool cp_assign_lds_fits(int n) { return cp_assign_ws_bytes(n) <= 56 * 1024; }
 // out[w] = flags[work[w]]
 hipError_t launch_cp_gather(const int32_t* work, int32_t n, const int32_t* flags, int32_t* out, hipStream_t s);
 // the next experiment's (x, xstatus) into the running sum (logp, status) of

@@ -270,12 +270,20 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
         return false;
     }
     for (const XmlNode* dn : ex.children_named("data")) {
+        // DataLikelihoodBase::Create (DataLikelihoodBase.cpp:20-36): time_course by default
         const std::string type = dn->has_attr("type") ? dn->get("type") : std::string("time_course");
-        if (type != "time_course_population_average") {
-            LOGERROR("cell_population: data type \"%s\" is not supported (time_course_population_average only)", type.c_str());
+        DataLikelihood d;
+        if (type == "time_course")
+            d.kind = BCM3HIP_CP_DATA_TIME_COURSE;
+        else if (type == "time_course_population_average")
+            d.kind = BCM3HIP_CP_DATA_POPULATION_AVERAGE;
+        else if (type == "time_points" || type == "duration") {
+            LOGERROR("cell_population: data type \"%s\" is not supported", type.c_str());
+            return false;
+        } else {
+            LOGERROR("Unknown data likelihood type \"%s\"", type.c_str());
             return false;
         }
-        DataLikelihood d;
         d.data_name = dn->get("data_name");
         d.weight = dn->get_double("weight", 1.0);
         const std::string em = dn->has_attr("error_model") ? dn->get("error_model") : std::string("normal");
@@ -292,12 +300,31 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
             LOGERROR("cell_population: error model \"%s\" is not supported", em.c_str());
             return false;
         }
-        d.relative_to_time_average = dn->get_bool("relative_to_time_average", false) ? 1 : 0;
-        if (dn->get_bool("use_log_ratio", false) ||
-            dn->get_bool("optimize_offset_scale", false) || dn->get_bool("include_only_cells_that_went_through_mitosis", false) ||
+        d.relative_to_time_average = (d.kind == BCM3HIP_CP_DATA_POPULATION_AVERAGE &&
+                                      dn->get_bool("relative_to_time_average", false)) ? 1 : 0;
+        d.stdev_relative_to_scale = dn->get_bool("stdev_relative_to_scale", false) ? 1 : 0;
+        // include_only_cells_that_went_through_mitosis is read by DataLikelihoodTimeCourseBase::Load
+        // but used by neither likelihood built here; the population average of this restatement
+        // refuses it as before
+        if (dn->get_bool("use_log_ratio", false) || dn->get_bool("optimize_offset_scale", false) ||
+            (d.kind == BCM3HIP_CP_DATA_POPULATION_AVERAGE && dn->get_bool("include_only_cells_that_went_through_mitosis", false)) ||
             dn->has_attr("saturation_scale")) {
             LOGERROR("cell_population: unsupported option on data \"%s\"", d.data_name.c_str());
             return false;
+        }
+        if (d.kind == BCM3HIP_CP_DATA_TIME_COURSE) {
+            // DataLikelihoodTimeCourse::Load (DataLikelihoodTimeCourse.cpp:27-41)
+            const std::string sync = dn->has_attr("synchronize") ? dn->get("synchronize") : std::string();
+            if (!(sync.empty() || sync == "none")) {
+                LOGERROR("cell_population: synchronized time courses (\"%s\") are not supported", sync.c_str());
+                return false;
+            }
+            // missing_simulation_time_stdev (DataLikelihoodTimeCourseBase.cpp:93-110): a variable
+            // or a number, 300 when absent
+            d.missing_stdev = bcm3hip_value_ref{BCM3HIP_REF_FIXED, -1, 300.0};
+            if (dn->has_attr("missing_simulation_time_stdev") && !dn->get("missing_simulation_time_stdev").empty() &&
+                !ParseRef(dn->get("missing_simulation_time_stdev"), d.missing_stdev))
+                return false;
         }
         if (!ParseRef(dn->get("stdev"), d.stdev)) return false;
         const std::string ps = dn->has_attr("proportional_stdev") ? dn->get("proportional_stdev") : std::string();
@@ -328,11 +355,83 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
         }
         for (const auto& t : tdata->arr) d.times.push_back(t.as_double());
         const size_t T = d.times.size();
-        d.R = dims->arr.size() == 1 ? 1 : (int32_t)values->arr[0].arr.size();
-        d.observed.assign((size_t)d.R * T, NaN);
-        for (size_t i = 0; i < T && i < values->arr.size(); i++)
-            for (int j = 0; j < d.R; j++)
-                d.observed[(size_t)j * T + i] = dims->arr.size() == 1 ? values->arr[i].as_double() : values->arr[i].arr[j].as_double();
+        const size_t nd = dims->arr.size();
+        if (d.kind == BCM3HIP_CP_DATA_POPULATION_AVERAGE) {
+            if (nd > 2) {
+                LOGERROR("Time course population likelihood for data %s; data has %zu dimensions but can only handle 1 or 2 dimensions.",
+                         d.data_name.c_str(), nd);
+                return false;
+            }
+            d.R = nd == 1 ? 1 : (int32_t)values->arr[0].arr.size();
+            d.observed.assign((size_t)d.R * T, NaN);
+            for (size_t i = 0; i < T && i < values->arr.size(); i++)
+                for (int j = 0; j < d.R; j++)
+                    d.observed[(size_t)j * T + i] = nd == 1 ? values->arr[i].as_double() : values->arr[i].arr[j].as_double();
+        } else {
+            // DataLikelihoodTimeCourse::Load (DataLikelihoodTimeCourse.cpp:43-130): time x cells
+            // (x markers, of which one species reads the first); use_only_cell_ix picks cells
+            if (nd < 1 || nd > 3) {
+                LOGERROR("Time course likelihood for data %s; data has %zu dimensions but can only handle 1, 2 or 3 dimensions.",
+                         d.data_name.c_str(), nd);
+                return false;
+            }
+            if (group->find("parent")) {
+                LOGERROR("cell_population: observed cell lineages (variable \"parent\") are not supported");
+                return false;
+            }
+            const std::string only = option_get(vm, "cellpop.use_only_cell_ix", "-1");
+            const size_t ncells_data = nd == 1 ? 1 : values->arr.empty() ? 0 : values->arr[0].arr.size();
+            std::vector<size_t> pick;
+            if (only == "-1") {
+                for (size_t j = 0; j < ncells_data; j++) pick.push_back(j);
+            } else {
+                if (nd == 1) {
+                    LOGERROR("use_only_cell_ix has been specified, but there is only 1 cell in the data.");
+                    return false;
+                }
+                size_t p0 = 0;
+                while (p0 <= only.size()) {
+                    size_t p1 = only.find(',', p0);
+                    if (p1 == std::string::npos) p1 = only.size();
+                    const std::string tok = only.substr(p0, p1 - p0);
+                    char* end = nullptr;
+                    const long ix = strtol(tok.c_str(), &end, 10);
+                    if (tok.empty() || *end || ix < 0) {
+                        LOGERROR("cellpop.use_only_cell_ix: could not read \"%s\"", tok.c_str());
+                        return false;
+                    }
+                    if ((size_t)ix >= ncells_data) {
+                        LOGERROR("Requested to use cell %ld, but data contains only %zu cells", ix, ncells_data);
+                        return false;
+                    }
+                    pick.push_back((size_t)ix);
+                    p0 = p1 + 1;
+                }
+            }
+            d.R = (int32_t)pick.size();
+            d.observed.assign((size_t)d.R * T, NaN);
+            for (size_t i = 0; i < T && i < values->arr.size(); i++)
+                for (int j = 0; j < d.R; j++) {
+                    const Json& row = values->arr[i];
+                    d.observed[(size_t)j * T + i] = nd == 1   ? row.as_double()
+                                                    : nd == 2 ? row.arr[pick[j]].as_double()
+                                                              : row.arr[pick[j]].arr[0].as_double();
+                }
+            if (max_cells < d.R) {
+                LOGERROR("Maximum number of simulated cells (%d) in the experiment is not sufficient for the amount of cells in the data (%d)",
+                         max_cells, d.R);
+                return false;
+            }
+            if (max_cells > d.R) {
+                LOGERROR("Simulating more cells (%d) than there are cells in the data (%d) - currently not supported.", max_cells, d.R);
+                return false;
+            }
+            if (num_cells > max_cells || d.R > 1024) {
+                LOGERROR("cell_population: time course with %d initial cells for %d observed cells (at most max_cells, 1024) is not supported",
+                         num_cells, d.R);
+                return false;
+            }
+        }
         // species reference (RequestSimulationInfo): ODE species, else constant species
         d.species_name = dn->get("species_name");
         size_t six = sbml.GetODEIntegratedSpeciesByName(d.species_name);
@@ -487,7 +586,8 @@ bool LikelihoodCellPopulation::PostInitialize()
     for (const auto& d : data)
         data_flat.push_back(bcm3hip_cellpop_data{(int32_t)d.times.size(), d.R, d.observed.data(), d.entry.data(), d.stdev,
                                                  d.offset, d.scale, d.weight, d.error_model,
-                                                 d.proportional_stdev, d.relative_to_time_average});
+                                                 d.proportional_stdev, d.relative_to_time_average, d.kind,
+                                                 d.stdev_relative_to_scale, d.missing_stdev});
     model = bcm3hip_cellpop_model{};
     model.derivative_body = derivative_body.c_str();
     model.NS = (int32_t)NS;

@@ -9,12 +9,14 @@
 // (netCDF classic, or a JSON sidecar with the netCDF group's variables), num_cells, max_cells,
 // divide_cells, entry_time, trailing_simulation_time, simulate_past_chromatid_separation_time,
 // solver_* settings (solver_type CVODE); <set_parameter>; <cell_variability
-// distribution="diagonal_gaussian">; <data type="time_course_population_average"> with the normal /
-// additive_normal / proportional_normal / additive_proportional_normal / student_t4 error models,
-// stdev / proportional_stdev / offset / scale / weight / relative_to_time_average. Not built:
-// treatment trajectories (time-varying
-// constant species), synchronised data (time_course, time_points, duration likelihoods), the DP5
-// solver, full_gaussian variability, several experiments in one likelihood, non-sampled parameters.
+// distribution="diagonal_gaussian">; <treatment_trajectory type="pulses">; <data> of type
+// "time_course_population_average" or "time_course" (the default type; single cells matched to
+// the simulated cells, no observed lineage, no synchronisation) with the normal / additive_normal /
+// proportional_normal / additive_proportional_normal / student_t4 error models, stdev /
+// proportional_stdev / offset / scale / stdev_relative_to_scale / weight / relative_to_time_average /
+// missing_simulation_time_stdev, and the cellpop.use_only_cell_ix option. Not built: the
+// time_points and duration likelihoods, synchronised time courses, the DP5 solver, full_gaussian
+// variability, non-sampled parameters.
 #pragma once
 #include <memory>
 #include <string>
@@ -48,6 +50,8 @@ private:
         double weight = 1.0;
         int32_t error_model = 0;
         int32_t relative_to_time_average = 0;
+        int32_t kind = BCM3HIP_CP_DATA_POPULATION_AVERAGE, stdev_relative_to_scale = 0;
+        bcm3hip_value_ref missing_stdev{};
         std::vector<int32_t> entry;
     };
     bool LoadExperiment(const XmlNode& ex, const OptionsMap& vm);

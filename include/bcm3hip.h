@@ -191,10 +191,11 @@ typedef struct {
     int32_t only_initial_cells;
 } bcm3hip_variability_action;
 
-/* DataLikelihoodTimeCoursePopulationAverage (one species) */
+/* A data likelihood of one species: DataLikelihoodTimeCoursePopulationAverage (kind 0) or
+ * DataLikelihoodTimeCourse (kind 1, no observed lineage, no synchronisation). */
 typedef struct {
     int32_t T;                /* time points */
-    int32_t R;                /* replicates */
+    int32_t R;                /* population average: replicates; time course: observed cells */
     const double* observed;   /* [R*T], NaN = missing */
     const int32_t* entry;     /* [T] output entry (sorted simulation time point) of each time point */
     bcm3hip_value_ref stdev, offset, scale;
@@ -202,7 +203,11 @@ typedef struct {
     int32_t error_model;      /* BCM3HIP_CP_ERR_*: DataLikelihoodBase::Load's error_model */
     bcm3hip_value_ref proportional_stdev; /* proportional_stdev (BCM3HIP_REF_NONE = 0) */
     int32_t relative_to_time_average;     /* log(x / time mean of x) before the data likelihood */
+    int32_t kind;                         /* BCM3HIP_CP_DATA_* */
+    int32_t stdev_relative_to_scale;      /* stdev_relative_to_scale: stdev *= scale */
+    bcm3hip_value_ref missing_stdev;      /* time course: missing_simulation_time_stdev (NONE = 300) */
 } bcm3hip_cellpop_data;
+enum { BCM3HIP_CP_DATA_POPULATION_AVERAGE = 0, BCM3HIP_CP_DATA_TIME_COURSE = 1 };
 enum { BCM3HIP_CP_ERR_NORMAL = 0, BCM3HIP_CP_ERR_T4 = 1, BCM3HIP_CP_ERR_PROPORTIONAL = 2,
        BCM3HIP_CP_ERR_ADDITIVE_PROPORTIONAL = 3 };
 
@@ -335,6 +340,15 @@ int bcm3hip_last_kernel_ms(bcm3hip_ctx* ctx, float* ms);
  * (100 MHz) when the trajectory started and when it finished. Copies min(n_max, trajectories) rows
  * (synchronises with the launch) and returns that count, or a negative error. */
 int64_t bcm3hip_placement_log(bcm3hip_ctx* ctx, int64_t n_max, uint64_t* host_out);
+/* The observed-to-simulated cell assignment of the time-course data likelihood alone
+ * (DataLikelihoodTimeCourse.cpp:287-360 with dependencies/hungarian2's
+ * hungarianMinimumWeightPerfectMatching), on the current device, for n_problems matrices of cell
+ * log-likelihoods lik[p][i][j] (observed cell i, simulated cell j, -inf = not matchable, R <= 1024).
+ * Device pointers: match[p][R] receives the simulated cell of every observed cell (-1 when none),
+ * sum[p] the matched likelihoods summed in observed-cell order (-inf when the routine finds no
+ * matching), ok[p] Evaluate's result (0: a NaN likelihood). Runs on `stream`, no synchronisation. */
+int bcm3hip_assign_cells(int32_t n_problems, int32_t R, int32_t nsim, const double* lik, int32_t* match, double* sum,
+                         int32_t* ok, void* stream);
 /* With BCM3HIP_OPT_TIMING_LOG on: synchronises on every launch logged since the last call and
  * returns the summed / maximum kernel time (HIP events recorded on each launch's own stream) and
  * the number of launches, then clears the log. Lets a timed loop run without host syncs. */

@@ -154,7 +154,8 @@ def _bool(s, default):
     return s.strip().lower() in ("1", "true")
 
 
-def load_problem(likelihood_xml, prior_xml, num_cells=None, max_cells=None, variant=""):
+def load_problem(likelihood_xml, prior_xml, num_cells=None, max_cells=None, variant="", use_only_cell_ix="-1"):
+    """use_only_cell_ix: the reference's cellpop.use_only_cell_ix option (CellPopulationLikelihood.cpp:116)"""
     root = ET.parse(prior_xml).getroot()
     variables, transforms = [], []
     for v in root.iter("variable"):
@@ -166,7 +167,7 @@ def load_problem(likelihood_xml, prior_xml, num_cells=None, max_cells=None, vari
     assert lik.get("type") == "cell_population"
     exps = []
     for ex in lik.iter("experiment"):
-        exps.append(_load_experiment(ex, base, variables, num_cells, max_cells, variant))
+        exps.append(_load_experiment(ex, base, variables, num_cells, max_cells, variant, use_only_cell_ix))
     return dict(variables=variables, transforms=transforms, experiments=exps, variant=variant)
 
 
@@ -177,7 +178,7 @@ def _ref_value(s, variables):
     return ("fixed", float(s))
 
 
-def _load_experiment(ex, base, variables, num_cells, max_cells, variant=""):
+def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_only_cell_ix="-1"):
     model = SG.SBMLModel(os.path.join(base, ex.get("model_file")))
     e = dict(name=ex.get("name"), model=model)
     e["rtol"] = float(ex.get("solver_relative_tolerance", 4 * FLT_EPS))
@@ -222,28 +223,49 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant=""):
     dls = []
     timepoints = []  # Experiment::simulation_timepoints: (dl index, time, time_ix, species_ix)
     for dl in ex.iter("data"):
-        assert dl.get("type", "time_course") == "time_course_population_average"
+        kind = dl.get("type", "time_course")  # DataLikelihoodBase::Create (DataLikelihoodBase.cpp:22)
+        assert kind in ("time_course_population_average", "time_course"), kind
         var = data[dl.get("data_name")]
         tdim = var["dims"][0]
         times = [float(t) for t in data[tdim]["data"]]
         obs = np.array(var["data"], dtype=float)
-        if obs.ndim == 1:
-            obs = obs[:, None]
-        obs = obs.T  # replicates x timepoints
+        if kind == "time_course":
+            # DataLikelihoodTimeCourse::Load (DataLikelihoodTimeCourse.cpp:43-130): cells x time
+            # points; a third (marker) dimension is read, of which one species uses column 0
+            assert "parent" not in data, "observed lineages"
+            if obs.ndim == 1:
+                assert use_only_cell_ix == "-1"
+                obs = obs[None, :]
+            else:
+                if obs.ndim == 3:
+                    obs = obs[:, :, 0]
+                obs = obs.T
+                if use_only_cell_ix != "-1":
+                    obs = obs[[int(t) for t in use_only_cell_ix.split(",")]]
+            assert e["max_cells"] == obs.shape[0], "max_cells must equal the observed cells (.cpp:174-183)"
+            assert (dl.get("synchronize", "") or "none") == "none"
+        else:
+            if obs.ndim == 1:
+                obs = obs[:, None]
+            obs = obs.T  # replicates x timepoints
         sname = dl.get("species_name").strip()
         six = model.ode_index(sname)
         if six is None:
             six = len(model.ode) + model.constant_index(sname)
         em = dl.get("error_model", "normal")
-        d = dict(times=times, observed=obs, species=six, weight=float(dl.get("weight", 1.0)),
+        msd = dl.get("missing_simulation_time_stdev", "")
+        d = dict(kind=kind, times=times, observed=obs, species=six, weight=float(dl.get("weight", 1.0)),
                  stdev=_ref_value(dl.get("stdev"), variables),
                  offset=_ref_value(dl.get("offset"), variables) if dl.get("offset") else None,
                  scale=_ref_value(dl.get("scale"), variables) if dl.get("scale") else None,
+                 stdev_relative_to_scale=_bool(dl.get("stdev_relative_to_scale"), False),
                  error_model={"normal": "normal", "additive_normal": "normal", "student_t4": "t4", "t4": "t4",
                               "proportional_normal": "proportional",
                               "additive_proportional_normal": "additive_proportional"}[em],
                  proportional_stdev=(_ref_value(dl.get("proportional_stdev"), variables)
                                      if dl.get("proportional_stdev") else None),
+                 # DataLikelihoodTimeCourseBase: missing_simulation_time_stdev, fixed 300 by default
+                 missing_stdev=_ref_value(msd, variables) if msd else ("fixed", 300.0),
                  relative_to_time_average=_bool(dl.get("relative_to_time_average"), False))
         for ti, t in enumerate(times):
             timepoints.append((len(dls), t, ti, six))
@@ -422,8 +444,9 @@ def simulate_experiment(e, prob, values):
         i += 1
     if fail:
         return dict(ok=False, logp=-math.inf, cells=cells)
-    # population averages (Experiment.cpp:298-311 + NotifySimulatedValue)
+    # population averages / cell trajectories (Experiment.cpp:298-311 + NotifySimulatedValue)
     avgs = [np.zeros((len(d["times"]), 1)) for d in e["data"]]
+    trajs = [np.full((e["max_cells"], len(d["times"])), np.nan) for d in e["data"]]
     for k, (dli, t, ti, six) in enumerate(e["timepoints"]):
         alive = [c for c in cells if 0.0 <= t - c["creation"] <= c["sim_end"]]
         pop = len(alive)
@@ -431,17 +454,136 @@ def simulate_experiment(e, prob, values):
             x = c["values"][k]
             if x == x:
                 avgs[dli][ti, 0] += x / pop
+                trajs[dli][c["index"], ti] = x
+    # Experiment::EvaluateLogProbability (Experiment.cpp:346-355): a data likelihood whose Evaluate
+    # returns false ends the sum there, and the experiment keeps what it had (it still succeeds)
     logp = 0.0
+    roots = [c["parent"] < 0 for c in cells]
     for dli, d in enumerate(e["data"]):
-        logp += _popavg_logp(d, avgs[dli], tv)
-    return dict(ok=True, logp=logp, cells=cells, population_average=[a[:, 0] for a in avgs])
+        if d["kind"] == "time_course":
+            ok, lp = _timecourse_logp(d, trajs[dli], roots, tv)
+            if not ok:
+                break
+            logp += lp
+        else:
+            logp += _popavg_logp(d, avgs[dli], tv)
+    return dict(ok=True, logp=logp, cells=cells, population_average=[a[:, 0] for a in avgs],
+                cell_trajectories=trajs)
+
+
+def _data_stdev(d, tv, scale):
+    """DataLikelihoodBase::GetCurrentSTDev (DataLikelihoodBase.cpp:130-156)"""
+    s = _refval(d["stdev"], tv)
+    return s * scale if d.get("stdev_relative_to_scale") else s
+
+
+def _log_pdf_normal(x, mu, sigma):
+    # bcm3::LogPdfNormal (src/utils/ProbabilityDistributions.cpp:129-138)
+    two_sigma_sq = 2.0 * sigma * sigma
+    dd = x - mu
+    return -math.log(sigma) - 0.91893853320467274178032973640562 - dd * dd / two_sigma_sq
+
+
+def _log_pdf_tnu4(x, mu, sigma):
+    # bcm3::LogPdfTnu4 (ProbabilityDistributions.cpp:216-224)
+    xn = (x - mu) / sigma
+    return -0.9808292530117262 - 2.5 * math.log1p(0.25 * xn * xn) - math.log(sigma)
+
+
+def _timecourse_logp(d, traj, roots, tv):
+    """DataLikelihoodTimeCourse::Evaluate (DataLikelihoodTimeCourse.cpp:230-365) for one species and
+    no observed lineage: the likelihood of every observed cell against every simulated initial cell
+    (CalculateCellLikelihood, :431-497; missing simulated values: CalculateMissingValueLikelihood,
+    :566-588), then the observed-to-simulated assignment of the vendored hungarian2 routine
+    (oracle/hungarian.py). Returns (Evaluate's result, logp)."""
+    import hungarian as HG
+    offset = _refval(d["offset"], tv) if d["offset"] else 0.0
+    scale = _refval(d["scale"], tv) if d["scale"] else 1.0
+    stdev = _data_stdev(d, tv, scale)
+    pstd = _refval(d["proportional_stdev"], tv) if d["proportional_stdev"] else 0.0
+    msd = _refval(d["missing_stdev"], tv)
+    em = d["error_model"]
+    times = d["times"]
+    T = len(times)
+    x = traj * scale  # (.cpp:236-241): col *= scale; col += offset
+    x = x + offset
+    obs = d["observed"]
+    R = obs.shape[0]
+    nsim = len(roots)
+    n = max(R, nsim)
+
+    def missing(j, k):
+        first = times[T - 1]
+        for m in range(T):
+            if not math.isnan(x[j, m]):
+                first = times[m]
+                break
+        last = times[0]
+        for m in range(T - 1, -1, -1):
+            if not math.isnan(x[j, m]):
+                last = times[m]
+                break
+        off = min(abs(times[k] - first), abs(times[k] - last))
+        return _log_pdf_tnu4(off, 0.0, msd) if em == "t4" else _log_pdf_normal(off, 0.0, msd)
+
+    def cell(i, j):
+        lp = 0.0
+        mls = -math.log(stdev)
+        inv2 = 1.0 / (2.0 * stdev * stdev)
+        for k in range(T):
+            y = obs[i, k]
+            if math.isnan(y):
+                continue
+            xv = x[j, k]
+            if math.isnan(xv):
+                lp += missing(j, k)
+            elif em == "normal":
+                dd = y - xv
+                lp += mls - 0.91893853320467274178032973640562 - dd * dd * inv2
+            elif em == "t4":
+                lp += _log_pdf_tnu4(y, xv, stdev)
+            else:
+                # (.cpp:274-285): sigma from the scaled trajectory, Eigen's vectorised log and
+                # inverse (the device and this checker use the scalar log: see the test's tolerance)
+                sigma = np.float64(pstd * max(xv, 0.0))
+                if em == "additive_proportional":
+                    sigma += stdev
+                dd = y - xv
+                with np.errstate(all="ignore"):  # IEEE: sigma = 0 gives inf - inf = NaN
+                    lp += float(-np.log(sigma) - 0.91893853320467274178032973640562
+                                - dd * dd * (np.float64(1.0) / (2.0 * (sigma * sigma))))
+        return lp
+
+    L = np.full((n, n), 0.0)
+    edges = []
+    for i in range(R):
+        finite = 0
+        for j in range(nsim):
+            if roots[j]:
+                L[i, j] = cell(i, j)
+                if math.isnan(L[i, j]):
+                    return False, -math.inf
+                if L[i, j] > -math.inf:
+                    finite += 1
+            else:
+                L[i, j] = -math.inf
+            edges.append((i, j, -L[i, j]))
+        if finite < R:
+            return True, -math.inf
+    match = HG.min_weight_perfect_matching(n, nsim, edges)
+    if len(match) != R:
+        return True, -math.inf
+    lp = 0.0
+    for i in range(R):
+        lp += L[i, match[i]]
+    return True, lp * d["weight"]
 
 
 def _popavg_logp(d, avg, tv):
     """DataLikelihoodTimeCoursePopulationAverage::Evaluate (one species)."""
-    stdev = _refval(d["stdev"], tv)
     offset = _refval(d["offset"], tv) if d["offset"] else 0.0
     scale = _refval(d["scale"], tv) if d["scale"] else 1.0
+    stdev = _data_stdev(d, tv, scale)
     a = avg.copy()
     if d["relative_to_time_average"]:
         # DataLikelihoodTimeCoursePopulationAverage.cpp:106-113 (the time mean summed in time order;

@@ -163,15 +163,18 @@ def prior_text():
 
 
 def likelihood_text(num_cells=500, max_cells=2048, data_file="cellpop_data.json", model_file="cellpop_model.xml",
-                    data_attrs='stdev="stdev"', experiment_attrs="", extra=""):
-    """extra: further children of the <experiment> (e.g. a <treatment_trajectory>)"""
+                    data_attrs='stdev="stdev"', experiment_attrs="", extra="", data_xml=None, entry_time="0"):
+    """extra: further children of the <experiment> (e.g. a <treatment_trajectory>); data_xml: the
+    <data> element(s) in place of the population average"""
+    if data_xml is None:
+        data_xml = f'<data type="time_course_population_average" data_name="pcna_mean" species_name="PCNA_gfp" {data_attrs}/>'
     return f"""<bcm_likelihood type="cell_population">
-  <experiment name="exp1" model_file="{model_file}" data_file="{data_file}" num_cells="{num_cells}" max_cells="{max_cells}" entry_time="0"{experiment_attrs}>
+  <experiment name="exp1" model_file="{model_file}" data_file="{data_file}" num_cells="{num_cells}" max_cells="{max_cells}" entry_time="{entry_time}"{experiment_attrs}>
     <cell_variability distribution="diagonal_gaussian">
       <variable model_parameter="k_D" apply="multiplicative_log" scale="var_kD"/>
       <variable initial_condition_species="CycD" apply="multiplicative_log" scale="var_CycD0"/>
     </cell_variability>
-    <data type="time_course_population_average" data_name="pcna_mean" species_name="PCNA_gfp" {data_attrs}/>{extra}
+    {data_xml}{extra}
   </experiment>
 </bcm_likelihood>
 """
@@ -212,7 +215,45 @@ def write_data(d=HERE):
     print("cells", sim["num_cells"], "population average", np.round(avg, 3))
 
 
+TC_CELLS = 16
+
+
+def write_tc_data(d=HERE):
+    """cellpop_tc_data.json: single-cell PCNA_gfp time courses for the time_course likelihood
+    (DataLikelihoodTimeCourse): TC_CELLS non-dividing cells simulated at the true parameters plus
+    noise, a few observations missing (NaN); the population average of cellpop_data.json
+    alongside, a 1-D series (one cell) and a 3-D copy with a second marker"""
+    import numpy as np
+    import tempfile
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "oracle"))
+    import cellpop as CP
+    tmp = tempfile.mkdtemp()
+    path = os.path.join(tmp, "l.xml")
+    with open(path, "w") as f:
+        f.write(likelihood_text(num_cells=TC_CELLS, max_cells=TC_CELLS, data_file=os.path.join(d, "cellpop_data.json"),
+                                model_file=os.path.join(d, "cellpop_model.xml"), experiment_attrs=' divide_cells="false"'))
+    prob = CP.load_problem(path, os.path.join(d, "cellpop_prior.xml"))
+    sim = CP.simulate(prob, np.array(true_values()))
+    cells = sim["detail"][0]["cells"]
+    vals = np.array([c["values"] for c in cells])  # cells x times
+    rng = np.random.default_rng(20261017)
+    sd = 10.0 ** TRUE["stdev"]
+    obs = vals.T + sd * rng.standard_normal((len(TIMES), TC_CELLS))
+    for t, c in ((3, 2), (7, 5), (12, 11), (20, 0)):
+        obs[t, c] = float("nan")
+    with open(os.path.join(d, "cellpop_data.json")) as f:
+        group = json.load(f)["exp1"]
+    group["pcna_cells"] = {"dims": ["time", "cell"], "data": obs.tolist()}
+    group["pcna_cell0"] = {"dims": ["time"], "data": obs[:, 1].tolist()}
+    m2 = np.stack([obs, rng.standard_normal(obs.shape)], axis=2)
+    group["pcna_cells_markers"] = {"dims": ["time", "cell", "marker"], "data": m2.tolist()}
+    with open(os.path.join(d, "cellpop_tc_data.json"), "w") as f:
+        json.dump({"exp1": group}, f, indent=1)
+
+
 if __name__ == "__main__":
     write_model_files()
     if "--data" in sys.argv:
         write_data()
+    if "--tc-data" in sys.argv:
+        write_tc_data()
