@@ -12,7 +12,10 @@
 //                     the data likelihoods (time courses from cp_timecourse_kernel);
 //   cp_timecourse_kernel  one workgroup per (evaluation, time-course data likelihood): the cell
 //                     likelihood matrix and the observed-to-simulated matching
-//                     (DataLikelihoodTimeCourse::Evaluate).
+//                     (DataLikelihoodTimeCourse::Evaluate);
+//   cp_timepoints_kernel  one workgroup per (evaluation, time-points data likelihood): per data
+//                     time point the cells alive, their likelihood matrix and the matching
+//                     (DataLikelihoodTimePoints::Evaluate).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
     double total = 0.0;
     for (int di = 0; di < m.n_data; di++) {
         const bcm3hip_cellpop_data dl = m.data[di];
-        if (dl.kind == BCM3HIP_CP_DATA_TIME_COURSE) {
+        if (dl.kind == BCM3HIP_CP_DATA_TIME_COURSE || dl.kind == BCM3HIP_CP_DATA_TIME_POINTS) {
             if (!tc_ok[(size_t)e * m.n_data + di]) break;
             total += tc_logp[(size_t)e * m.n_data + di];
             continue;
@@ -587,6 +590,159 @@ hipError_t launch_cp_timecourse(const CpStatic& m, int32_t n, int32_t max_R, con
 }
 
 size_t cp_assign_ws_bytes(int n) { return hg_ws_bytes(n); }
+
+// ---------------------------------------------------------------------------------------------
+// Time-points data likelihood (DataLikelihoodTimePoints, src/cellpop/DataLikelihoodTimePoints.cpp):
+// at every data time point, the observed cells with a finite marker are matched to the simulated
+// cells alive then by the same vendored routine; logp = the matched cell likelihoods summed over
+// the time points in order, times the weight.
+
+// cell_trajectories[j](ti, l) (NotifySimulatedValue, .cpp:345-370): the column's species values
+// summed in notification order, NaN when none was notified (a value is notified when it is not NaN)
+__device__ inline double cp_tp_value(const bcm3hip_cellpop_data& dl, const double* xv, int ti, int l)
+{
+    double v = __builtin_nan("");
+    for (int k = dl.term_offset[l]; k < dl.term_offset[l + 1]; k++) {
+        const double x = xv[dl.term_entry[(size_t)k * dl.T + ti]];
+        if (x == x) v = (v != v) ? x : v + x;
+    }
+    return v;
+}
+
+// the simulated cell j takes part at ti (.cpp:234-239, 351-353)
+__device__ inline bool cp_tp_sim(const CpStatic& m, const bcm3hip_cellpop_data& dl, const double* xv, int j, int ti)
+{
+    if (dl.only_nondivided && j >= m.n0) return false;  // is_newborn: i >= initial_number_of_cells
+    if (cp_tp_value(dl, xv, ti, 0) != cp_tp_value(dl, xv, ti, 0)) return false;
+    return dl.relative_ix < 0 || cp_tp_value(dl, xv, dl.relative_ix, 0) == cp_tp_value(dl, xv, dl.relative_ix, 0);
+}
+
+// observed cell i has a finite marker at ti (observed_data[ti].row(i).isFinite().any())
+__device__ inline bool cp_tp_data(const bcm3hip_cellpop_data& dl, int i, int ti)
+{
+    const double* o = dl.observed + ((size_t)i * dl.T + ti) * dl.MK;
+    for (int k = 0; k < dl.MK; k++)
+        if (fabs(o[k]) < __builtin_inf()) return true;
+    return false;
+}
+
+// wavefront 0 lists, in order, the indices i < count with pred(i), at most cap of them; returns how
+// many satisfy pred (all of them, also beyond cap)
+template <typename F>
+__device__ inline int cp_compact(int count, int cap, F pred, int32_t* out)
+{
+    const int lane = threadIdx.x & 63;
+    int total = 0;
+    for (int b = 0; b < count; b += 64) {
+        const int i = b + lane;
+        const bool c = i < count && pred(i);
+        const unsigned long long mask = __ballot(c);
+        const int pos = total + __popcll(mask & ((1ull << lane) - 1ull));
+        if (c && pos < cap) out[pos] = i;
+        total += __popcll(mask);
+    }
+    return total;
+}
+
+__global__ __launch_bounds__(256) void cp_timepoints_kernel(CpStatic m, int32_t n, const double* values,
+                                                             const int32_t* ncells, const int32_t* failed,
+                                                             const double* out_values, unsigned char* ws_global,
+                                                             size_t ws_stride, double* tc_logp, int32_t* tc_ok)
+{
+    extern __shared__ __align__(16) unsigned char cp_lds[];
+    const int e = blockIdx.x, di = blockIdx.y;
+    const bcm3hip_cellpop_data dl = m.data[di];
+    if (dl.kind != BCM3HIP_CP_DATA_TIME_POINTS || e >= n || failed[e]) return;
+    __shared__ int32_t rows[1024], sims[1024];
+    __shared__ double stdevs[8], offsets[8], scales[8];
+    __shared__ int32_t counts[2];
+    __shared__ int32_t stop;
+    const int nc = ncells[e];
+    const double* v = values + (size_t)e * m.d;
+    const double* xcells = out_values + (size_t)e * m.max_cells * m.M;
+    unsigned char* base = ws_global ? ws_global + ((size_t)e * m.n_data + di) * ws_stride : cp_lds;
+    if (threadIdx.x < dl.L) {  // GetCurrentSTDev / DataOffset / DataScale per column (.cpp:212-219)
+        const int l = threadIdx.x;
+        const double sc = cp_ref(dl.col_ref[3 * l + 2], v, m.transforms, 1.0);
+        double sd = cp_ref(dl.col_ref[3 * l], v, m.transforms, 0.0);
+        if (dl.stdev_relative_to_scale) sd *= sc;
+        stdevs[l] = sd;
+        offsets[l] = cp_ref(dl.col_ref[3 * l + 1], v, m.transforms, 0.0);
+        scales[l] = sc;
+    }
+    if (threadIdx.x == 0) stop = 0;
+    double lp = 0.0;     // thread 0's running sum
+    bool early = false;  // thread 0: Evaluate returned -inf before the weight
+    for (int ti = 0; ti < dl.T; ti++) {
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int fd = cp_compact(dl.R, dl.R, [&](int i) { return cp_tp_data(dl, i, ti); }, rows);
+            const int fs = cp_compact(nc, fd, [&](int j) { return cp_tp_sim(m, dl, xcells + (size_t)j * m.M, j, ti); }, sims);
+            if (threadIdx.x == 0) {
+                counts[0] = fd;
+                counts[1] = fs;
+            }
+        }
+        __syncthreads();
+        const int fd = counts[0], fs = counts[1];
+        if (fd == 0) continue;
+        if (fs < fd) {  // too few simulated cells at this time point: -inf, no weight (.cpp:241-245)
+            early = true;
+            break;
+        }
+        // the routine keeps the edges to right nodes < fd only (hungarian.cpp:52-84): the first fd
+        // simulated cells of the list
+        const HgWs w = hg_carve(base, fd);
+        for (int p = threadIdx.x; p < fd * fd; p += blockDim.x) {
+            const int i = p / fd, j = p % fd;
+            const double* o = dl.observed + ((size_t)rows[i] * dl.T + ti) * dl.MK;
+            const double* xv = xcells + (size_t)sims[j] * m.M;
+            double cl = 0.0;
+            for (int l = 0; l < dl.L; l++) {
+                double x = cp_tp_value(dl, xv, ti, l);
+                if (dl.relative_ix >= 0) {
+                    x += offsets[l];
+                    x /= cp_tp_value(dl, xv, dl.relative_ix, l);
+                    x *= scales[l];
+                } else {
+                    x *= scales[l];
+                    x += offsets[l];
+                }
+                const double y = o[l];
+                if (y != y) continue;
+                cl += (dl.error_model == BCM3HIP_CP_ERR_T4) ? log_pdf_tnu4(y, x, stdevs[l]) : cp_log_pdf_normal(y, x, stdevs[l]);
+            }
+            w.cost[(size_t)i * fd + j] = -cl;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (!hg_match(fd, w)) {  // no perfect matching (.cpp:308-311)
+                early = true;
+                stop = 1;
+            } else {
+                for (int i = 0; i < fd; i++) lp += -w.cost[(size_t)i * fd + w.lmatch[i]];
+            }
+        }
+        __syncthreads();
+        if (stop) break;
+    }
+    if (threadIdx.x != 0) return;
+    // Evaluate returns true in every case; the weight applies when the loop ran through
+    tc_logp[(size_t)e * m.n_data + di] = early ? -__builtin_inf() : lp * dl.weight;
+    tc_ok[(size_t)e * m.n_data + di] = 1;
+}
+
+hipError_t launch_cp_timepoints(const CpStatic& m, int32_t n, int32_t max_R, const double* values,
+                                const int32_t* ncells, const int32_t* failed, const double* out_values,
+                                unsigned char* ws_global, size_t ws_stride, double* tc_logp, int32_t* tc_ok,
+                                hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    const size_t lds = ws_global ? 0 : hg_ws_bytes(max_R);
+    hipLaunchKernelGGL(cp_timepoints_kernel, dim3(n, m.n_data), dim3(256), lds, s, m, n, values, ncells, failed,
+                       out_values, ws_global, ws_stride, tc_logp, tc_ok);
+    return hipGetLastError();
+}
 
 // the matching alone on given cell likelihoods (bcm3hip_assign_cells): one block per problem
 __global__ __launch_bounds__(64) void cp_assign_kernel(int32_t R, int32_t nsim, const double* lik,

@@ -45,6 +45,11 @@ hipError_t launch_cp_timecourse(const CpStatic& m, int32_t n, int32_t max_R, con
                                 const int32_t* ncells, const int32_t* failed, const double* out_values,
                                 unsigned char* ws_global, size_t ws_stride, double* tc_logp, int32_t* tc_ok,
                                 hipStream_t s);
+// the time-points data likelihoods, same outputs and workspace as the time courses
+hipError_t launch_cp_timepoints(const CpStatic& m, int32_t n, int32_t max_R, const double* values,
+                                const int32_t* ncells, const int32_t* failed, const double* out_values,
+                                unsigned char* ws_global, size_t ws_stride, double* tc_logp, int32_t* tc_ok,
+                                hipStream_t s);
 // the matching alone (bcm3hip_assign_cells)
 hipError_t launch_cp_assign(int32_t n_problems, int32_t R, int32_t nsim, const double* lik, unsigned char* ws_global,
                             size_t ws_stride, int32_t* match, double* sum, int32_t* ok, hipStream_t s);

@@ -39,6 +39,31 @@ bool parse_double(const std::string& s, double& v)
     return *end == '\0';
 }
 
+// bcm3::tokenize (src/utils/Utils.cpp:7-25): boost char_separator with keep_empty_tokens, a trailing
+// newline dropped, nothing for an empty string
+std::vector<std::string> tokenize(std::string s, char delim)
+{
+    std::vector<std::string> out;
+    if (s.empty()) return out;
+    if (s.back() == '\n') s.pop_back();
+    size_t p0 = 0;
+    for (;;) {
+        const size_t p1 = s.find(delim, p0);
+        out.push_back(s.substr(p0, p1 == std::string::npos ? std::string::npos : p1 - p0));
+        if (p1 == std::string::npos) break;
+        p0 = p1 + 1;
+    }
+    return out;
+}
+
+std::string trim(const std::string& s)
+{
+    size_t a = 0, b = s.size();
+    while (a < b && std::isspace((unsigned char)s[a])) a++;
+    while (b > a && std::isspace((unsigned char)s[b - 1])) b--;
+    return s.substr(a, b - a);
+}
+
 // Joe & Kuo (2008) new-joe-kuo-6.21201, dimensions 2..13: (s, a, m_1..m_s)
 struct JK {
     int s, a;
@@ -277,8 +302,15 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
             d.kind = BCM3HIP_CP_DATA_TIME_COURSE;
         else if (type == "time_course_population_average")
             d.kind = BCM3HIP_CP_DATA_POPULATION_AVERAGE;
-        else if (type == "time_points" || type == "duration") {
-            LOGERROR("cell_population: data type \"%s\" is not supported", type.c_str());
+        else if (type == "time_points") {
+            d.kind = BCM3HIP_CP_DATA_TIME_POINTS;
+            if (!LoadTimePoints(*dn, d, *group, vm)) return false;
+            data.push_back(d);
+            continue;
+        } else if (type == "duration") {
+            // DataLikelihoodDuration::Evaluate fills likelihoods(i, count) but reads likelihoods(i, j)
+            // with the simulated-cell index j (DataLikelihoodDuration.cpp:95-110): past its matrix
+            LOGERROR("cell_population: data type \"duration\" is not supported (the reference reads past its likelihood matrix)");
             return false;
         } else {
             LOGERROR("Unknown data likelihood type \"%s\"", type.c_str());
@@ -446,6 +478,212 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
     return true;
 }
 
+// DataLikelihoodBase::Load + DataLikelihoodTimePoints::Load (DataLikelihoodBase.cpp:38-75,
+// DataLikelihoodTimePoints.cpp:19-201) and the per-column references of PostInitialize (:77-127)
+bool LikelihoodCellPopulation::LoadTimePoints(const XmlNode& dn, DataLikelihood& d, const Json& group,
+                                              const OptionsMap& vm) const
+{
+    d.data_name = dn.get("data_name");
+    d.weight = dn.get_double("weight", 1.0);
+    const std::string em = dn.has_attr("error_model") ? dn.get("error_model") : std::string("normal");
+    if (em == "normal" || em == "additive_normal")
+        d.error_model = BCM3HIP_CP_ERR_NORMAL;
+    else if (em == "student_t4" || em == "t4")
+        d.error_model = BCM3HIP_CP_ERR_T4;
+    else if (em == "proportional_normal" || em == "additive_proportional_normal") {
+        // Evaluate handles normal and t4 only; the other models give a NaN cell likelihood
+        // (DataLikelihoodTimePoints.cpp:283-290, assert compiled out)
+        LOGERROR("cell_population: time points data \"%s\": error model \"%s\" gives NaN cell likelihoods in the reference (not supported)",
+                 d.data_name.c_str(), em.c_str());
+        return false;
+    } else {
+        LOGERROR("Unknown error model \"%s\"", em.c_str());
+        return false;
+    }
+    d.stdev_relative_to_scale = dn.get_bool("stdev_relative_to_scale", false) ? 1 : 0;
+    d.only_nondivided = dn.get_bool("use_only_nondivided", false) ? 1 : 0;
+    const std::string sync = dn.has_attr("synchronize") ? dn.get("synchronize") : std::string();
+    if (!(sync.empty() || sync == "none")) {
+        if (sync == "DNA_replication_start" || sync == "PCNA_gfp_increase" || sync == "mitosis" ||
+            sync == "nuclear_envelope_breakdown" || sync == "anaphase" || sync == "anaphase_onset")
+            LOGERROR("cell_population: synchronized time points (\"%s\") are not supported", sync.c_str());
+        else
+            LOGERROR("Synchronization is specified as \"%s\" which is not a recognized synchronization point", sync.c_str());
+        return false;
+    }
+    // data: time x cells (x markers)
+    const Json* var = group.find(d.data_name);
+    const Json* dims = var ? var->find("dims") : nullptr;
+    const Json* values = var ? var->find("data") : nullptr;
+    if (!dims || !values || dims->arr.empty()) {
+        LOGERROR("Data \"%s\" not found in group \"%s\"", d.data_name.c_str(), name.c_str());
+        return false;
+    }
+    const size_t nd = dims->arr.size();
+    if (nd != 2 && nd != 3) {
+        LOGERROR("Need 2 or 3 dimensional data");
+        return false;
+    }
+    const Json* tvar = group.find(dims->arr[0].str);
+    const Json* tdata = tvar ? tvar->find("data") : nullptr;
+    if (!tdata) {
+        LOGERROR("Time dimension \"%s\" not found", dims->arr[0].str.c_str());
+        return false;
+    }
+    d.times.clear();
+    for (const auto& t : tdata->arr) d.times.push_back(t.as_double());
+    const size_t T = d.times.size();
+    if (T == 0 || values->arr.size() < T) {
+        LOGERROR("Data \"%s\": fewer rows than time points", d.data_name.c_str());
+        return false;
+    }
+    const size_t ncells_data = values->arr[0].arr.size();
+    const std::string only = option_get(vm, "cellpop.use_only_cell_ix", "-1");
+    std::vector<size_t> pick;
+    if (only == "-1") {
+        for (size_t j = 0; j < ncells_data; j++) pick.push_back(j);
+    } else if (nd == 3) {
+        LOGERROR("Not implemented yet");  // use_only_cell_ix on 3-D data (.cpp:112-114)
+        return false;
+    } else {
+        for (const std::string& tok : tokenize(only, ',')) {
+            char* end = nullptr;
+            const long ix = strtol(tok.c_str(), &end, 10);
+            if (tok.empty() || *end || ix < 0) {
+                LOGERROR("cellpop.use_only_cell_ix: could not read \"%s\"", tok.c_str());
+                return false;
+            }
+            if ((size_t)ix >= ncells_data) {
+                LOGERROR("Requested to use cell %ld, but data contains only %zu cells", ix, ncells_data);
+                return false;
+            }
+            pick.push_back((size_t)ix);
+        }
+    }
+    d.R = (int32_t)pick.size();
+    d.MK = nd == 3 ? (int32_t)(ncells_data ? values->arr[0].arr[0].arr.size() : 0) : 1;
+    if (d.R < 1 || d.MK < 1) {
+        LOGERROR("Data \"%s\" holds no cells", d.data_name.c_str());
+        return false;
+    }
+    d.observed.assign((size_t)d.R * T * d.MK, NaN);
+    for (size_t i = 0; i < T; i++)
+        for (int j = 0; j < d.R; j++)
+            for (int m = 0; m < d.MK; m++) {
+                const Json& c = values->arr[i].arr[pick[j]];
+                d.observed[((size_t)j * T + i) * d.MK + m] = nd == 2 ? c.as_double() : c.arr[m].as_double();
+            }
+    // species columns: "a;b" -> columns, "a+b" -> sums; a species is registered for simulation once,
+    // at its first use (species_map, .cpp:139-188)
+    d.species_name = dn.get("species_name");
+    std::vector<std::string> cols;
+    if (d.species_name.find(';') != std::string::npos) {
+        for (const std::string& c : tokenize(d.species_name, ';')) cols.push_back(trim(c));
+    } else {
+        cols.push_back(d.species_name);
+    }
+    d.L = (int32_t)cols.size();
+    d.term_offset.assign(1, 0);
+    d.term_species.clear();
+    d.species_order.clear();
+    for (const std::string& col : cols) {
+        std::vector<std::string> terms;
+        if (col.find('+') != std::string::npos) {
+            for (const std::string& t : tokenize(col, '+')) terms.push_back(trim(t));
+        } else if (col.find('/') != std::string::npos) {
+            LOGERROR("Division currently not supported for time points data");
+            return false;
+        } else {
+            terms.push_back(col);
+        }
+        for (const std::string& t : terms) {
+            const size_t six = sbml.GetODEIntegratedSpeciesByName(t);
+            if (six == SIZE_MAX) {
+                if (sbml.GetConstantSpeciesByName(t) == SIZE_MAX)
+                    LOGERROR("Could not find species \"%s\" as either an dynamic or constant species", t.c_str());
+                else
+                    LOGERROR("cell_population: time points of the constant species \"%s\" are not supported", t.c_str());
+                return false;
+            }
+            d.term_species.push_back((int32_t)six);
+            if (std::find(d.species_order.begin(), d.species_order.end(), (int32_t)six) == d.species_order.end())
+                d.species_order.push_back((int32_t)six);
+        }
+        d.term_offset.push_back((int32_t)d.term_species.size());
+    }
+    // Evaluate reads observed(i, l) for l < L: the data need that many markers
+    if (d.L > 8) {
+        LOGERROR("cell_population: time points data \"%s\" with %d species columns (at most 8) are not supported",
+                 d.data_name.c_str(), d.L);
+        return false;
+    }
+    if (d.L > d.MK) {
+        LOGERROR("cell_population: time points data \"%s\" has %d marker(s) for %d species columns", d.data_name.c_str(),
+                 d.MK, d.L);
+        return false;
+    }
+    if (max_cells < d.R) {
+        LOGERROR("Maximum number of simulated cells (%d) in the experiment is not sufficient for the amount of cells in the data (%d)",
+                 max_cells, d.R);
+        return false;
+    }
+    if (d.R > 1024) {
+        LOGERROR("cell_population: time points with %d observed cells (at most 1024) are not supported", d.R);
+        return false;
+    }
+    // value_relative_to_timepoint_ix (DataLikelihoodBase.cpp:49): a time point index of these data
+    d.relative_ix = -1;
+    if (dn.has_attr("value_relative_to_timepoint_ix")) {
+        const std::string s = dn.get("value_relative_to_timepoint_ix");
+        char* end = nullptr;
+        const long ix = strtol(s.c_str(), &end, 10);
+        if (s.empty() || *end || ix < 0 || (size_t)ix >= T) {
+            LOGERROR("cell_population: value_relative_to_timepoint_ix \"%s\" is not a time point of data \"%s\"", s.c_str(),
+                     d.data_name.c_str());
+            return false;
+        }
+        d.relative_ix = (int32_t)ix;
+    }
+    // stdev / offset / scale: one value for every column or one per column (GetCurrentSTDev & co.,
+    // DataLikelihoodBase.cpp:130-215: an index past a longer list gives NaN)
+    auto refs = [&](const std::string& attr, bcm3hip_value_ref none, int slot) {
+        const std::string s = dn.has_attr(attr) ? dn.get(attr) : std::string();
+        const std::vector<std::string> toks = tokenize(s, ';');
+        for (int l = 0; l < d.L; l++) {
+            bcm3hip_value_ref r = none;
+            if (toks.size() == 1) {
+                if (!ParseRef(toks[0], r)) return false;
+            } else if ((size_t)l < toks.size()) {
+                if (!ParseRef(toks[l], r)) return false;
+            } else if (!toks.empty()) {
+                r = bcm3hip_value_ref{BCM3HIP_REF_FIXED, -1, NaN};
+            }
+            d.col_ref[(size_t)l * 3 + slot] = r;
+        }
+        for (size_t k = (size_t)d.L; k < toks.size(); k++) {  // parsed by PostInitialize all the same
+            bcm3hip_value_ref r;
+            if (!ParseRef(toks[k], r)) return false;
+        }
+        return true;
+    };
+    d.col_ref.assign((size_t)d.L * 3, bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0});
+    if (!dn.has_attr("stdev")) {
+        LOGERROR("cell_population: data \"%s\" needs a stdev", d.data_name.c_str());
+        return false;
+    }
+    if (!refs("stdev", bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0}, 0) ||
+        !refs("offset", bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0}, 1) ||
+        !refs("scale", bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 1.0}, 2))
+        return false;
+    d.stdev = d.col_ref[0];
+    d.offset = d.col_ref[1];
+    d.scale = d.col_ref[2];
+    d.proportional_stdev = bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0};
+    d.missing_stdev = bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0};
+    d.species_ix = d.term_species[0];
+    return true;
+}
+
 // Experiment::PostInitialize (Experiment.cpp:145-237) + the flat device model
 std::vector<const bcm3hip_cellpop_model*> LikelihoodCellPopulation::GetDeviceModels() const
 {
@@ -469,15 +707,24 @@ bool LikelihoodCellPopulation::PostInitialize()
         return false;
     }
     // simulation time points: (data likelihood, time, time index, species), sorted stably by time
+    // (time points data: one run per species in first-use order, DataLikelihoodTimePoints.cpp:139-188)
     struct TP {
         int dl;
         double t;
         int ti;
         int species;
+        int order;
     };
     std::vector<TP> tps;
-    for (size_t k = 0; k < data.size(); k++)
-        for (size_t i = 0; i < data[k].times.size(); i++) tps.push_back(TP{(int)k, data[k].times[i], (int)i, data[k].species_ix});
+    for (size_t k = 0; k < data.size(); k++) {
+        if (data[k].kind == BCM3HIP_CP_DATA_TIME_POINTS) {
+            for (size_t o = 0; o < data[k].species_order.size(); o++)
+                for (size_t i = 0; i < data[k].times.size(); i++)
+                    tps.push_back(TP{(int)k, data[k].times[i], (int)i, data[k].species_order[o], (int)o});
+            continue;
+        }
+        for (size_t i = 0; i < data[k].times.size(); i++) tps.push_back(TP{(int)k, data[k].times[i], (int)i, data[k].species_ix, 0});
+    }
     std::stable_sort(tps.begin(), tps.end(), [](const TP& a, const TP& b) { return a.t < b.t; });
     if (tps.empty()) {
         LOGERROR("cell_population: no data time points");
@@ -485,11 +732,38 @@ bool LikelihoodCellPopulation::PostInitialize()
     }
     output_times.clear();
     output_species.clear();
-    for (auto& d : data) d.entry.assign(d.times.size(), -1);
+    std::vector<std::vector<int32_t>> order_entry(data.size());  // time points: [order][T]
+    for (size_t k = 0; k < data.size(); k++) {
+        data[k].entry.assign(data[k].times.size(), -1);
+        order_entry[k].assign(std::max<size_t>(1, data[k].species_order.size()) * data[k].times.size(), -1);
+    }
     for (size_t k = 0; k < tps.size(); k++) {
         output_times.push_back(tps[k].t);
         output_species.push_back(tps[k].species);
-        data[tps[k].dl].entry[tps[k].ti] = (int32_t)k;
+        DataLikelihood& d = data[tps[k].dl];
+        if (d.kind == BCM3HIP_CP_DATA_TIME_POINTS)
+            order_entry[tps[k].dl][(size_t)tps[k].order * d.times.size() + tps[k].ti] = (int32_t)k;
+        else
+            d.entry[tps[k].ti] = (int32_t)k;
+    }
+    // a column's terms are summed in the order their values are notified: the order of the entries
+    // (DataLikelihoodTimePoints::NotifySimulatedValue, .cpp:345-370, over the sorted time points)
+    for (size_t k = 0; k < data.size(); k++) {
+        DataLikelihood& d = data[k];
+        if (d.kind != BCM3HIP_CP_DATA_TIME_POINTS) continue;
+        const size_t T = d.times.size();
+        d.term_entry.assign(d.term_species.size() * T, -1);
+        for (int l = 0; l < d.L; l++) {
+            std::vector<int32_t> ord;
+            for (int q = d.term_offset[l]; q < d.term_offset[l + 1]; q++)
+                ord.push_back((int32_t)(std::find(d.species_order.begin(), d.species_order.end(), d.term_species[q]) -
+                                        d.species_order.begin()));
+            std::stable_sort(ord.begin(), ord.end());  // entries at one time follow the species order
+            for (size_t q = 0; q < ord.size(); q++)
+                for (size_t i = 0; i < T; i++)
+                    d.term_entry[(d.term_offset[l] + q) * T + i] = order_entry[k][(size_t)ord[q] * T + i];
+        }
+        for (size_t i = 0; i < T; i++) d.entry[i] = d.term_entry[i];
     }
     transforms.clear();
     for (size_t i = 0; i < varset->GetNumVariables(); i++) transforms.push_back((int32_t)varset->GetVariableTransform(i));
@@ -583,11 +857,16 @@ bool LikelihoodCellPopulation::PostInitialize()
         }
     }
     data_flat.clear();
-    for (const auto& d : data)
+    for (const auto& d : data) {
+        const bool tp = d.kind == BCM3HIP_CP_DATA_TIME_POINTS;
         data_flat.push_back(bcm3hip_cellpop_data{(int32_t)d.times.size(), d.R, d.observed.data(), d.entry.data(), d.stdev,
                                                  d.offset, d.scale, d.weight, d.error_model,
                                                  d.proportional_stdev, d.relative_to_time_average, d.kind,
-                                                 d.stdev_relative_to_scale, d.missing_stdev});
+                                                 d.stdev_relative_to_scale, d.missing_stdev, tp ? d.L : 0,
+                                                 tp ? d.MK : 0, tp ? d.term_offset.data() : nullptr,
+                                                 tp ? d.term_entry.data() : nullptr, tp ? d.col_ref.data() : nullptr,
+                                                 tp ? d.relative_ix : -1, tp ? d.only_nondivided : 0});
+    }
     model = bcm3hip_cellpop_model{};
     model.derivative_body = derivative_body.c_str();
     model.NS = (int32_t)NS;

@@ -14,9 +14,11 @@
 // the simulated cells, no observed lineage, no synchronisation) with the normal / additive_normal /
 // proportional_normal / additive_proportional_normal / student_t4 error models, stdev /
 // proportional_stdev / offset / scale / stdev_relative_to_scale / weight / relative_to_time_average /
-// missing_simulation_time_stdev, and the cellpop.use_only_cell_ix option. Not built: the
-// time_points and duration likelihoods, synchronised time courses, the DP5 solver, full_gaussian
-// variability, non-sampled parameters.
+// missing_simulation_time_stdev, and the cellpop.use_only_cell_ix option; <data type="time_points">
+// (DataLikelihoodTimePoints: cells matched at every time point, ";"-separated species columns, "+"
+// sums, 2-D or 3-D data, value_relative_to_timepoint_ix, use_only_nondivided; normal / student_t4).
+// Not built: the duration likelihood (the reference's reads past its matrix), synchronised time
+// courses / time points, the DP5 solver, full_gaussian variability, non-sampled parameters.
 #pragma once
 #include <memory>
 #include <string>
@@ -26,6 +28,8 @@
 #include "SBMLModel.h"
 
 namespace bcm3 {
+
+struct Json;
 
 class LikelihoodCellPopulation : public LikelihoodGPUBase {
 public:
@@ -53,8 +57,15 @@ private:
         int32_t kind = BCM3HIP_CP_DATA_POPULATION_AVERAGE, stdev_relative_to_scale = 0;
         bcm3hip_value_ref missing_stdev{};
         std::vector<int32_t> entry;
+        // time points (DataLikelihoodTimePoints): observed [R][T][MK]; column l sums the species
+        // term_species[term_offset[l] .. term_offset[l+1]); the species registered for simulation in
+        // first-use order (species_order), their entries per time point (term_entry[k][T])
+        int32_t L = 0, MK = 0, relative_ix = -1, only_nondivided = 0;
+        std::vector<int32_t> term_offset, term_species, species_order, term_entry;
+        std::vector<bcm3hip_value_ref> col_ref;  // [3L] stdev, offset, scale
     };
     bool LoadExperiment(const XmlNode& ex, const OptionsMap& vm);
+    bool LoadTimePoints(const XmlNode& dn, DataLikelihood& d, const Json& group, const OptionsMap& vm) const;
     bool ParseRef(const std::string& s, bcm3hip_value_ref& r) const;
 
     SBMLModel sbml;

@@ -191,13 +191,16 @@ typedef struct {
     int32_t only_initial_cells;
 } bcm3hip_variability_action;
 
-/* A data likelihood of one species: DataLikelihoodTimeCoursePopulationAverage (kind 0) or
- * DataLikelihoodTimeCourse (kind 1, no observed lineage, no synchronisation). */
+/* A data likelihood: DataLikelihoodTimeCoursePopulationAverage (kind 0) or DataLikelihoodTimeCourse
+ * (kind 1, one species, no observed lineage, no synchronisation), or DataLikelihoodTimePoints (kind 2,
+ * src/cellpop/DataLikelihoodTimePoints.cpp: L species columns, each a sum of species, matched cell by
+ * cell at every time point, no synchronisation). */
 typedef struct {
     int32_t T;                /* time points */
-    int32_t R;                /* population average: replicates; time course: observed cells */
-    const double* observed;   /* [R*T], NaN = missing */
-    const int32_t* entry;     /* [T] output entry (sorted simulation time point) of each time point */
+    int32_t R;                /* population average: replicates; time course / time points: observed cells */
+    const double* observed;   /* [R*T] (time points: [R*T*MK]), NaN = missing */
+    const int32_t* entry;     /* [T] output entry (sorted simulation time point) of each time point
+                                 (time points: of column 0's first term) */
     bcm3hip_value_ref stdev, offset, scale;
     double weight;
     int32_t error_model;      /* BCM3HIP_CP_ERR_*: DataLikelihoodBase::Load's error_model */
@@ -206,8 +209,16 @@ typedef struct {
     int32_t kind;                         /* BCM3HIP_CP_DATA_* */
     int32_t stdev_relative_to_scale;      /* stdev_relative_to_scale: stdev *= scale */
     bcm3hip_value_ref missing_stdev;      /* time course: missing_simulation_time_stdev (NONE = 300) */
+    /* time points only (zero otherwise) */
+    int32_t L;                            /* species columns ("a;b+c" -> 2) */
+    int32_t MK;                           /* markers per observed cell (1 for 2-D data); columns read 0..L-1 */
+    const int32_t* term_offset;           /* [L+1] terms of each column */
+    const int32_t* term_entry;            /* [terms*T] output entry of term k at time point i */
+    const bcm3hip_value_ref* col_ref;     /* [3L] stdev, offset, scale of each column */
+    int32_t relative_ix;                  /* value_relative_to_timepoint_ix, -1 = none */
+    int32_t only_nondivided;              /* use_only_nondivided: daughters are not simulated cells */
 } bcm3hip_cellpop_data;
-enum { BCM3HIP_CP_DATA_POPULATION_AVERAGE = 0, BCM3HIP_CP_DATA_TIME_COURSE = 1 };
+enum { BCM3HIP_CP_DATA_POPULATION_AVERAGE = 0, BCM3HIP_CP_DATA_TIME_COURSE = 1, BCM3HIP_CP_DATA_TIME_POINTS = 2 };
 enum { BCM3HIP_CP_ERR_NORMAL = 0, BCM3HIP_CP_ERR_T4 = 1, BCM3HIP_CP_ERR_PROPORTIONAL = 2,
        BCM3HIP_CP_ERR_ADDITIVE_PROPORTIONAL = 3 };
 

@@ -224,8 +224,16 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
     timepoints = []  # Experiment::simulation_timepoints: (dl index, time, time_ix, species_ix)
     for dl in ex.iter("data"):
         kind = dl.get("type", "time_course")  # DataLikelihoodBase::Create (DataLikelihoodBase.cpp:22)
-        assert kind in ("time_course_population_average", "time_course"), kind
+        assert kind in ("time_course_population_average", "time_course", "time_points"), kind
         var = data[dl.get("data_name")]
+        if kind == "time_points":
+            d = _load_time_points(dl, data, var, model, variables, e["max_cells"], use_only_cell_ix)
+            # AddSimulationTimepoints once per species, at its first use (.cpp:139-188)
+            for six in d["species_order"]:
+                for ti, t in enumerate(d["times"]):
+                    timepoints.append((len(dls), t, ti, six))
+            dls.append(d)
+            continue
         tdim = var["dims"][0]
         times = [float(t) for t in data[tdim]["data"]]
         obs = np.array(var["data"], dtype=float)
@@ -295,6 +303,131 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
     e["y_init"] = np.array([model.species[s]["initial"] for s in model.ode])
     e["constant_init"] = np.array([model.species[s]["initial"] for s in model.constant])
     return e
+
+
+def _load_time_points(dl, data, var, model, variables, max_cells, use_only_cell_ix):
+    """DataLikelihoodTimePoints::Load (DataLikelihoodTimePoints.cpp:19-201) and the per-column
+    references of DataLikelihoodBase::PostInitialize (DataLikelihoodBase.cpp:77-127)"""
+    times = [float(t) for t in data[var["dims"][0]]["data"]]
+    obs = np.array(var["data"], dtype=float)
+    assert obs.ndim in (2, 3), "Need 2 or 3 dimensional data"
+    if obs.ndim == 2:
+        if use_only_cell_ix != "-1":
+            obs = obs[:, [int(t) for t in use_only_cell_ix.split(",")]]
+        obs = obs[:, :, None]
+    else:
+        assert use_only_cell_ix == "-1", "Not implemented yet"
+    obs = obs.transpose(1, 0, 2)  # cells x time points x markers
+    assert max_cells >= obs.shape[0]
+    sname = dl.get("species_name")
+    cols = [c.strip() for c in sname.split(";")] if ";" in sname else [sname]
+    species_map = {}  # species index -> columns it adds to, in order
+    order = []
+    for l, col in enumerate(cols):
+        assert "/" not in col, "Division currently not supported for time points data"
+        for t in ([x.strip() for x in col.split("+")] if "+" in col else [col]):
+            six = model.ode_index(t)
+            assert six is not None, t
+            if six not in species_map:
+                species_map[six] = []
+                order.append(six)
+            species_map[six].append(l)
+    assert len(cols) <= obs.shape[2]
+
+    def refs(attr, none):
+        s = dl.get(attr, "")
+        toks = s.split(";") if s else []
+        out = []
+        for l in range(len(cols)):
+            if len(toks) == 1:
+                out.append(_ref_value(toks[0], variables))
+            elif l < len(toks):
+                out.append(_ref_value(toks[l], variables))
+            elif toks:
+                out.append(("fixed", math.nan))  # GetCurrent*: "Out of bounds" -> NaN
+            else:
+                out.append(("fixed", none))
+        return out
+
+    em = dl.get("error_model", "normal")
+    rel = dl.get("value_relative_to_timepoint_ix")
+    return dict(kind="time_points", times=times, observed=obs, columns=len(cols), species_map=species_map,
+                species_order=order, species=order[0], weight=float(dl.get("weight", 1.0)),
+                stdevs=refs("stdev", 1.0), offsets=refs("offset", 0.0), scales=refs("scale", 1.0),
+                stdev_relative_to_scale=_bool(dl.get("stdev_relative_to_scale"), False),
+                error_model={"normal": "normal", "additive_normal": "normal", "student_t4": "t4", "t4": "t4"}[em],
+                relative_ix=int(rel) if rel is not None else None,
+                only_nondivided=_bool(dl.get("use_only_nondivided"), False))
+
+
+def notify_time_points(e, dli, values):
+    """cell_trajectories of time-points data likelihood dli from the cells' values at the sorted
+    simulation time points (values[cell][entry]): Experiment.cpp:298-311 calls NotifySimulatedValue
+    for every time point in order and every cell with a non-NaN value; DataLikelihoodTimePoints::
+    NotifySimulatedValue (.cpp:345-370) skips daughters under use_only_nondivided and adds the value
+    to every column the species belongs to. Returns traj[max_cells][T][columns]."""
+    d = e["data"][dli]
+    traj = np.full((e["max_cells"], len(d["times"]), d["columns"]), np.nan)
+    for k, (tdl, t, ti, six) in enumerate(e["timepoints"]):
+        if tdl != dli:
+            continue
+        for c in range(len(values)):
+            x = values[c][k]
+            if x != x or (d["only_nondivided"] and c >= e["num_cells"]):
+                continue
+            for l in d["species_map"][six]:
+                v = traj[c, ti, l]
+                traj[c, ti, l] = x if math.isnan(v) else v + x
+    return traj
+
+
+def _timepoints_logp(d, traj, tv):
+    """DataLikelihoodTimePoints::Evaluate (DataLikelihoodTimePoints.cpp:210-343): at every time point
+    the observed cells with a finite marker against the simulated cells with a value, matched by the
+    vendored hungarian2 routine (oracle/hungarian.py) over (observed, simulated) edges in row order;
+    traj[cell][ti][column]."""
+    import hungarian as HG
+    L = d["columns"]
+    scales = [_refval(r, tv) for r in d["scales"]]
+    offsets = [_refval(r, tv) for r in d["offsets"]]
+    stdevs = [_refval(r, tv) * (scales[l] if d["stdev_relative_to_scale"] else 1.0) for l, r in enumerate(d["stdevs"])]
+    rel = d["relative_ix"]
+    obs = d["observed"]
+    logp = 0.0
+    for ti in range(len(d["times"])):
+        rows = [i for i in range(obs.shape[0]) if np.isfinite(obs[i, ti]).any()]
+        if not rows:
+            continue
+        sims = [j for j in range(traj.shape[0])
+                if not math.isnan(traj[j, ti, 0]) and (rel is None or not math.isnan(traj[j, rel, 0]))]
+        if len(sims) < len(rows):
+            return -math.inf
+        lik = np.full((len(rows), len(sims)), -math.inf)
+        edges = []
+        for a, i in enumerate(rows):
+            for b, j in enumerate(sims):
+                cl = 0.0
+                for l in range(L):
+                    x = traj[j, ti, l]
+                    if rel is not None:
+                        x += offsets[l]
+                        x /= traj[j, rel, l]
+                        x *= scales[l]
+                    else:
+                        x *= scales[l]
+                        x += offsets[l]
+                    y = obs[i, ti, l]
+                    if math.isnan(y):
+                        continue
+                    cl += _log_pdf_tnu4(y, x, stdevs[l]) if d["error_model"] == "t4" else _log_pdf_normal(y, x, stdevs[l])
+                lik[a, b] = cl
+                edges.append((a, b, -cl))
+        match = HG.min_weight_perfect_matching(len(rows), len(sims), edges)
+        if len(match) != len(rows):
+            return -math.inf
+        for a in range(len(rows)):
+            logp += lik[a, match[a]]
+    return logp * d["weight"]
 
 
 def _apply(kind, x, value):
@@ -446,15 +579,22 @@ def simulate_experiment(e, prob, values):
         return dict(ok=False, logp=-math.inf, cells=cells)
     # population averages / cell trajectories (Experiment.cpp:298-311 + NotifySimulatedValue)
     avgs = [np.zeros((len(d["times"]), 1)) for d in e["data"]]
-    trajs = [np.full((e["max_cells"], len(d["times"])), np.nan) for d in e["data"]]
+    trajs = [np.full((e["max_cells"], len(d["times"])) + ((d["columns"],) if d["kind"] == "time_points" else ()), np.nan)
+             for d in e["data"]]
     for k, (dli, t, ti, six) in enumerate(e["timepoints"]):
         alive = [c for c in cells if 0.0 <= t - c["creation"] <= c["sim_end"]]
         pop = len(alive)
+        d = e["data"][dli]
         for c in cells:
             x = c["values"][k]
             if x == x:
+                if d["kind"] == "time_points":
+                    continue
                 avgs[dli][ti, 0] += x / pop
                 trajs[dli][c["index"], ti] = x
+    for dli, d in enumerate(e["data"]):
+        if d["kind"] == "time_points" and cells:
+            trajs[dli] = notify_time_points(e, dli, np.array([c["values"] for c in cells]))
     # Experiment::EvaluateLogProbability (Experiment.cpp:346-355): a data likelihood whose Evaluate
     # returns false ends the sum there, and the experiment keeps what it had (it still succeeds)
     logp = 0.0
@@ -465,6 +605,8 @@ def simulate_experiment(e, prob, values):
             if not ok:
                 break
             logp += lp
+        elif d["kind"] == "time_points":
+            logp += _timepoints_logp(d, trajs[dli], tv)
         else:
             logp += _popavg_logp(d, avgs[dli], tv)
     return dict(ok=True, logp=logp, cells=cells, population_average=[a[:, 0] for a in avgs],

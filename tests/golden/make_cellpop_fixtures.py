@@ -251,9 +251,28 @@ def write_tc_data(d=HERE):
         json.dump({"exp1": group}, f, indent=1)
 
 
+def write_tp_data(d=HERE):
+    """adds to cellpop_tc_data.json the variants the time-points tests read (DataLikelihoodTimePoints
+    takes 2-D or 3-D data only): pcna_cell0_2d (time x 1 cell, the data of pcna_cell0) and
+    pcna_cells_late (pcna_cells without the observations of the first two time points)"""
+    import math
+    fn = os.path.join(d, "cellpop_tc_data.json")
+    with open(fn) as f:
+        doc = json.load(f)
+    g = doc["exp1"]
+    cells = g["pcna_cells"]["data"]
+    g["pcna_cell0_2d"] = {"dims": ["time", "cell1"], "data": [[row[1]] for row in cells]}
+    g["pcna_cells_late"] = {"dims": ["time", "cell"],
+                            "data": [[math.nan] * len(row) if t < 2 else list(row) for t, row in enumerate(cells)]}
+    with open(fn, "w") as f:
+        json.dump(doc, f, indent=1)
+
+
 if __name__ == "__main__":
     write_model_files()
     if "--data" in sys.argv:
         write_data()
     if "--tc-data" in sys.argv:
         write_tc_data()
+    if "--tc-data" in sys.argv or "--tp-data" in sys.argv:
+        write_tp_data()

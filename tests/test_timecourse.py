@@ -170,7 +170,6 @@ def test_loader_accepts_time_course(tmp_path):
     (TC.replace("/>", ' saturation_scale="2"/>'), {}, None),
     (TC.replace("pcna_cells", "pcna_cell0"), dict(num_cells=1, max_cells=1), "backend=none;cellpop.use_only_cell_ix=0"),
     (TC, dict(num_cells=2, max_cells=2), "backend=none;cellpop.use_only_cell_ix=0,16"),  # out of range
-    (TC.replace('data_name=', 'type="time_points" data_name='), {}, None),
     (TC.replace('data_name=', 'type="duration" data_name='), {}, None),
     (TC.replace('data_name=', 'type="nonsense" data_name='), {}, None),
 ])
