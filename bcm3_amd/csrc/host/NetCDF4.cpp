@@ -1,0 +1,243 @@
+// NetCDF4.cpp -- netCDF-4 (HDF5-backed) data files through the system's libnetcdf, loaded at run
+// time when present (the reference links libnetcdf and reads its data through NetCDFDataFile,
+// src/utils/NetCDFDataFile.cpp). Neither libnetcdf nor HDF5 is in this image, so the library is
+// dlopen()ed: $BCM3_LIBNETCDF if set, else libnetcdf.so / .so.22 / .so.19 / .so.18 / .so.15 on the
+// loader's search path. Without it a netCDF-4 file is refused with the conversion command
+// (tools/nc_convert.py), as before. The result has the layout NcClassicRead gives a classic file:
+// doc[group][variable] = {"dims": [dimension names], "data": nested values}, nested groups named
+// "a.b", the root group "", fill values -> NaN, char arrays -> strings.
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "NetCDFClassic.h"
+
+namespace bcm3 {
+
+namespace {
+
+// the subset of the netCDF C API (netcdf.h) this reader calls
+struct NcApi {
+    int (*open)(const char*, int, int*) = nullptr;
+    int (*close)(int) = nullptr;
+    int (*inq_grps)(int, int*, int*) = nullptr;
+    int (*inq_grpname)(int, char*) = nullptr;
+    int (*inq_varids)(int, int*, int*) = nullptr;
+    int (*inq_var)(int, int, char*, int*, int*, int*, int*) = nullptr;
+    int (*inq_dim)(int, int, char*, size_t*) = nullptr;
+    int (*get_var_double)(int, int, double*) = nullptr;
+    int (*get_var_text)(int, int, char*) = nullptr;
+    int (*get_var_string)(int, int, char**) = nullptr;
+    int (*free_string)(size_t, char**) = nullptr;
+    int (*inq_att)(int, int, const char*, int*, size_t*) = nullptr;
+    int (*get_att_double)(int, int, const char*, double*) = nullptr;
+    const char* (*strerror)(int) = nullptr;
+    void* handle = nullptr;
+    std::string error;
+};
+
+constexpr int kNcNoWrite = 0, kNcMaxName = 256, kNcMaxDims = 1024;
+constexpr int kNcByte = 1, kNcChar = 2, kNcShort = 3, kNcInt = 4, kNcFloat = 5, kNcDouble = 6, kNcString = 12;
+constexpr double kFillDouble = 9.9692099683868690e+36, kFillFloat = 9.9692099683868690e+36f;
+
+// loads libnetcdf on first success; a failed attempt is retried on the next call (a later
+// $BCM3_LIBNETCDF or install is seen)
+const NcApi& api()
+{
+    static NcApi a;
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
+    if (a.handle) return a;
+    std::vector<std::string> names;
+    if (const char* e = std::getenv("BCM3_LIBNETCDF")) names.push_back(e);
+    for (const char* n : {"libnetcdf.so", "libnetcdf.so.22", "libnetcdf.so.19", "libnetcdf.so.18", "libnetcdf.so.15"})
+        names.push_back(n);
+    void* h = nullptr;
+    for (const auto& n : names)
+        if ((h = dlopen(n.c_str(), RTLD_NOW | RTLD_LOCAL))) break;
+    if (!h) {
+        a.error = "libnetcdf was not found";
+        return a;
+    }
+    NcApi t;
+    bool ok = true;
+    auto sym = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        ok &= fn != nullptr;
+    };
+    sym(t.open, "nc_open");
+    sym(t.close, "nc_close");
+    sym(t.inq_grps, "nc_inq_grps");
+    sym(t.inq_grpname, "nc_inq_grpname");
+    sym(t.inq_varids, "nc_inq_varids");
+    sym(t.inq_var, "nc_inq_var");
+    sym(t.inq_dim, "nc_inq_dim");
+    sym(t.get_var_double, "nc_get_var_double");
+    sym(t.get_var_text, "nc_get_var_text");
+    sym(t.get_var_string, "nc_get_var_string");
+    sym(t.free_string, "nc_free_string");
+    sym(t.inq_att, "nc_inq_att");
+    sym(t.get_att_double, "nc_get_att_double");
+    sym(t.strerror, "nc_strerror");
+    if (!ok) {
+        dlclose(h);
+        a.error = "the libnetcdf found lacks the netCDF-4 group API";
+        return a;
+    }
+    t.handle = h;
+    a = t;
+    return a;
+}
+
+void check(const NcApi& a, int rc, const std::string& what)
+{
+    if (rc != 0) throw JsonError{"netCDF-4: " + what + ": " + (a.strerror ? a.strerror(rc) : std::to_string(rc))};
+}
+
+// nest a flat row-major vector along `shape`
+Json nest(std::vector<Json> flat, const std::vector<size_t>& shape)
+{
+    if (shape.empty()) return flat.empty() ? Json() : flat[0];
+    for (size_t k = shape.size(); k-- > 1;) {
+        std::vector<Json> up;
+        const size_t m = shape[k];
+        for (size_t i = 0; i + m <= flat.size() && m > 0; i += m) {
+            Json a;
+            a.type = Json::Array;
+            a.arr.assign(std::make_move_iterator(flat.begin() + i), std::make_move_iterator(flat.begin() + i + m));
+            up.push_back(std::move(a));
+        }
+        flat = std::move(up);
+    }
+    Json data;
+    data.type = Json::Array;
+    data.arr = std::move(flat);
+    return data;
+}
+
+void read_group(const NcApi& a, int grp, const std::string& path, Json& doc)
+{
+    int nvars = 0;
+    check(a, a.inq_varids(grp, &nvars, nullptr), "nc_inq_varids");
+    std::vector<int> ids((size_t)nvars);
+    if (nvars) check(a, a.inq_varids(grp, &nvars, ids.data()), "nc_inq_varids");
+    for (int vid : ids) {
+        char name[kNcMaxName + 1] = {0};
+        int type = 0, ndims = 0, natts = 0;
+        std::vector<int> dimids(kNcMaxDims);
+        check(a, a.inq_var(grp, vid, name, &type, &ndims, dimids.data(), &natts), "nc_inq_var");
+        std::vector<size_t> shape;
+        Json dims;
+        dims.type = Json::Array;
+        size_t total = 1;
+        for (int k = 0; k < ndims; k++) {
+            char dn[kNcMaxName + 1] = {0};
+            size_t len = 0;
+            check(a, a.inq_dim(grp, dimids[k], dn, &len), std::string("nc_inq_dim of ") + name);
+            shape.push_back(len);
+            total *= len;
+            Json d;
+            d.type = Json::String;
+            d.str = dn;
+            dims.arr.push_back(d);
+        }
+        std::vector<Json> flat;
+        if (type == kNcChar && !shape.empty()) {  // the last dimension holds the characters
+            std::vector<char> buf(total);
+            if (total) check(a, a.get_var_text(grp, vid, buf.data()), std::string("nc_get_var_text of ") + name);
+            const size_t inner = std::max<size_t>(shape.back(), 1);
+            for (size_t i = 0; i + inner <= buf.size(); i += inner) {
+                Json s;
+                s.type = Json::String;
+                s.str.assign(&buf[i], strnlen(&buf[i], inner));
+                flat.push_back(std::move(s));
+            }
+            shape.pop_back();
+            dims.arr.pop_back();
+        } else if (type == kNcString) {
+            std::vector<char*> buf(total, nullptr);
+            if (total) check(a, a.get_var_string(grp, vid, buf.data()), std::string("nc_get_var_string of ") + name);
+            for (char* p : buf) {
+                Json s;
+                s.type = Json::String;
+                if (p) s.str = p;
+                flat.push_back(std::move(s));
+            }
+            if (total) a.free_string(total, buf.data());
+        } else if (type >= kNcByte && type <= 11) {  // numeric types, converted by the library
+            std::vector<double> buf(total);
+            if (total) check(a, a.get_var_double(grp, vid, buf.data()), std::string("nc_get_var_double of ") + name);
+            // fill values -> NaN: the variable's _FillValue, else the type's default fill
+            int at = 0;
+            size_t alen = 0;
+            double fill = std::numeric_limits<double>::quiet_NaN();
+            bool has_fill = a.inq_att(grp, vid, "_FillValue", &at, &alen) == 0 && alen == 1 &&
+                            a.get_att_double(grp, vid, "_FillValue", &fill) == 0;
+            for (double x : buf) {
+                bool is_fill = has_fill ? x == fill
+                                        : (type == kNcDouble && (x == kFillDouble || x == (double)kFillFloat)) ||
+                                              (type == kNcFloat && x == (double)kFillFloat) ||
+                                              (type == kNcInt && x == -2147483647.0) || (type == kNcShort && x == -32767.0) ||
+                                              (type == kNcByte && x == -127.0);
+                Json e;
+                e.type = Json::Number;
+                e.num = is_fill ? std::numeric_limits<double>::quiet_NaN() : x;
+                flat.push_back(std::move(e));
+            }
+        } else {
+            continue;  // compound / opaque / enum / vlen: not data BCM3 reads
+        }
+        Json var;
+        var.type = Json::Object;
+        var.obj["dims"] = dims;
+        var.obj["data"] = nest(std::move(flat), shape);
+        Json& g = doc.obj[path];
+        g.type = Json::Object;
+        g.obj[name] = std::move(var);
+    }
+    int ngrps = 0;
+    check(a, a.inq_grps(grp, &ngrps, nullptr), "nc_inq_grps");
+    std::vector<int> sub((size_t)ngrps);
+    if (ngrps) check(a, a.inq_grps(grp, &ngrps, sub.data()), "nc_inq_grps");
+    for (int s : sub) {
+        char gn[kNcMaxName + 1] = {0};
+        check(a, a.inq_grpname(s, gn), "nc_inq_grpname");
+        read_group(a, s, path.empty() ? std::string(gn) : path + "." + gn, doc);
+    }
+}
+
+}  // namespace
+
+bool NcNetCDF4Available(std::string* why)
+{
+    const NcApi& a = api();
+    if (why) *why = a.error;
+    return a.handle != nullptr;
+}
+
+Json NcNetCDF4Read(const std::string& filename)
+{
+    const NcApi& a = api();
+    if (!a.handle) throw JsonError{a.error};
+    int nc = -1;
+    check(a, a.open(filename.c_str(), kNcNoWrite, &nc), "nc_open " + filename);
+    Json doc;
+    doc.type = Json::Object;
+    try {
+        read_group(a, nc, "", doc);
+    } catch (...) {
+        a.close(nc);
+        throw;
+    }
+    a.close(nc);
+    return doc;
+}
+
+}  // namespace bcm3

@@ -421,9 +421,13 @@ Json LoadDataFile(const std::string& filename)
     unsigned char m[4] = {0, 0, 0, 0};
     f.read((char*)m, 4);
     if (m[0] == 'C' && m[1] == 'D' && m[2] == 'F') return NcClassicRead(filename);
-    if (m[0] == 0x89 && m[1] == 'H' && m[2] == 'D' && m[3] == 'F')
-        throw JsonError{filename + " is netCDF-4 (HDF5), which this build reads after conversion: "
+    if (m[0] == 0x89 && m[1] == 'H' && m[2] == 'D' && m[3] == 'F') {
+        // netCDF-4: through the system's libnetcdf when it can be loaded (NetCDF4.cpp)
+        std::string why;
+        if (NcNetCDF4Available(&why)) return NcNetCDF4Read(filename);
+        throw JsonError{filename + " is netCDF-4 (HDF5) and " + why + " ($BCM3_LIBNETCDF names it); convert it: "
                                    "python tools/nc_convert.py to-classic " + filename + " <out.nc>"};
+    }
     return json_load(filename);
 }
 

@@ -71,9 +71,12 @@ Json NcClassicRead(const std::string& filename);
 bool NcIsClassic(const std::string& filename);
 
 // A likelihood data file (NetCDFDataFile::Open): netCDF classic (NcClassicRead) or the JSON
-// sidecar, chosen by the file's magic bytes; a netCDF-4 (HDF5) file is refused with the
-// conversion command. Throws JsonError.
+// sidecar, chosen by the file's magic bytes; a netCDF-4 (HDF5) file goes through libnetcdf when
+// it can be loaded at run time, else it is refused with the conversion command. Throws JsonError.
 Json LoadDataFile(const std::string& filename);
+// netCDF-4 through a run-time loaded libnetcdf (NetCDF4.cpp): same layout as NcClassicRead
+bool NcNetCDF4Available(std::string* why);
+Json NcNetCDF4Read(const std::string& filename);
 // {"dims", "data"} variable records -> their data arrays, for the loaders that index arrays
 void UnwrapDataVariables(Json& doc);
 

@@ -1,8 +1,8 @@
 """The reference's zero-change route to the GPU: single-vector EvaluateLogProbability calls from
 many sampling threads at once (TaskManager, README.md:77 re-entrancy) -- through libbcm3.so and
 through the LikelihoodDLL plugin libbcm3_dll.so -- are combined into batched launches, with each
-result equal to the batched evaluation of its own vector (which the PopPK tests check against
-the oracle)."""
+result equal to the batched evaluation of its own vector and inside the parity envelope of the
+oracle (the reference's CVODE restated bit for bit, tests/parity.py)."""
 import ctypes as C
 import os
 import threading
@@ -25,6 +25,19 @@ def _draws(n, seed):
     lo = np.array([v.lower for v in prob.variables])
     hi = np.array([v.upper for v in prob.variables])
     return H.draws(lo, hi, n, seed)
+
+
+def _assert_matches_oracle(x, got):
+    import oracle as O
+    import parity
+    prob = H.c3_problem(1)
+    r = O.Oracle("restated").popk_eval(prob, x, nthreads=8, want_traj=False)
+    ref = r["logp"]
+    mism = np.isfinite(got) != np.isfinite(ref)
+    assert np.all(r["stats"][mism, 0, 0] >= 0.99 * prob.max_steps)
+    err = parity.llh_err(got[~mism], ref[~mism])
+    parity.log_summary({"llh_t1": float(np.mean(err <= parity.LLH_T1)), "llh_max": float(err.max())}, n=int(err.size))
+    assert np.mean(err <= parity.LLH_T1) >= parity.llh_min_fraction(err.size) and np.all(err <= parity.LLH_T2)
 
 
 def _threads(fn, nt, x):
@@ -59,6 +72,7 @@ def test_concurrent_single_evaluations_are_combined():
     ll.set_option(_hip.OPT_TIMING_LOG, 0)
     assert np.array_equal(got, want)  # per-item results do not depend on the batch
     assert launches < len(x) // 2, launches  # requests were combined into batched launches
+    _assert_matches_oracle(x, got)
 
 
 def test_dll_plugin_route_many_threads():
@@ -88,3 +102,4 @@ def test_dll_plugin_route_many_threads():
 
     got = _threads(one, 48, x)
     assert np.array_equal(got, want)
+    _assert_matches_oracle(x, got)

@@ -3,8 +3,11 @@ likelihood's data file (NetCDFDataFile::Open / GetValues, src/utils/NetCDFDataFi
 classic-format output.nc writer (SampleHandlerNetCDF.cpp:24-110), checked against an independent
 implementation of the format (scipy.io.netcdf_file) in both directions.
 
-Parity unpinned: the reference ships no netCDF fixture and its netCDF-4 files need HDF5, which is
-absent here; the files below are the committed JSON sidecars converted by tools/nc_convert.py."""
+netCDF-4 data go through the system's libnetcdf when it loads at run time (csrc/host/NetCDF4.cpp);
+neither box has it, so that path is tested against a test double of its C API
+(tests/plugins/fake_netcdf.c). Parity unpinned: the reference ships no netCDF fixture and its
+netCDF-4 files need HDF5, which is absent here; the files below are the committed JSON sidecars
+converted by tools/nc_convert.py."""
 import ctypes as C
 import math
 import os
@@ -245,3 +248,75 @@ def test_corrupt_dimension_length_is_an_error(tmp_path):
     open(bad, "wb").write(bytes(data))
     with pytest.raises(RuntimeError):
         _lik(_xml_with(tmp_path, "c3", "c3_pkdata.json", bad), "c3")
+
+
+def _fake_netcdf(tmp_path):
+    """tests/plugins/fake_netcdf.c: a test double of libnetcdf's C API (no libnetcdf here)"""
+    so = str(tmp_path / "libfake_netcdf.so")
+    subprocess.run(["gcc", "-O1", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tests", "plugins", "fake_netcdf.c")],
+                   check=True)
+    return so
+
+
+def _netcdf4_stand_in(classic, out):
+    """the groups of a classic file ("g.n" names) as nested netCDF-4 groups in the test double's
+    manifest, behind the HDF5 signature"""
+    groups, dims, lines = {"": 0}, {}, []
+    with netcdf_file(classic, "r", mmap=False) as f:
+        for dn, ln in f.dimensions.items():
+            dims[dn] = len(dims)
+            lines.append(f"D {dn.rpartition('.')[2]} {ln if ln is not None else f.variables[[k for k, v in f.variables.items() if v.dimensions and v.dimensions[0] == dn][0]].shape[0]}")
+        for name, v in f.variables.items():
+            path, _, leaf = name.rpartition(".")
+            parent = ""
+            for part in path.split(".") if path else []:
+                key = f"{parent}.{part}" if parent else part
+                if key not in groups:
+                    groups[key] = len(groups)
+                    lines.append(f"G {groups[parent]} {part}")
+                parent = key
+            data = np.array(v[:])
+            fill = getattr(v, "_FillValue", None)
+            ids = " ".join(str(dims[d]) for d in v.dimensions)
+            if data.dtype.kind == "S":
+                strs = [b"".join(r).decode() or "-" for r in data.reshape(-1, data.shape[-1])]
+                lines.append(f"V {groups[path]} {leaf} 2 {len(v.dimensions)} {ids} 0 0 {len(strs)} " + " ".join(strs))
+            else:
+                flat = data.astype(float).reshape(-1)
+                lines.append(f"V {groups[path]} {leaf} 6 {len(v.dimensions)} {ids} {0 if fill is None else 1} "
+                             f"{0.0 if fill is None else float(fill)} {flat.size} " + " ".join(repr(float(x)) for x in flat))
+    with open(out, "wb") as f:
+        f.write(b"\x89HDF\r\n\x1a\n fake netCDF-4 (tests/plugins/fake_netcdf.c manifest)\n")
+        f.write("\n".join(lines).encode() + b"\n")
+
+
+@pytest.mark.parametrize("name", ["c3", "p64"])
+def test_netcdf4_through_libnetcdf_when_present(tmp_path, monkeypatch, name):
+    """a netCDF-4 data file goes through the system's libnetcdf when it can be loaded at run time
+    (csrc/host/NetCDF4.cpp, dlopen; $BCM3_LIBNETCDF names it): the test double of libnetcdf serves
+    the C3 / P64 data as nested groups, and the likelihood reads the arrays of the JSON sidecar"""
+    classic = str(tmp_path / "classic.nc")
+    _convert("to-classic", os.path.join(GOLDEN, f"{name}_pkdata.json"), classic)
+    nc4 = str(tmp_path / f"{name}_pkdata4.nc")
+    _netcdf4_stand_in(classic, nc4)
+    monkeypatch.setenv("BCM3_LIBNETCDF", _fake_netcdf(tmp_path))
+    ref, ref_s = _popk_arrays(_lik(os.path.join(GOLDEN, f"{name}_likelihood.xml"), name))
+    got, got_s = _popk_arrays(_lik(_xml_with(tmp_path, name, f"{name}_pkdata.json", nc4), name))
+    assert got_s == ref_s
+    for k in ref:
+        assert np.array_equal(got[k], ref[k], equal_nan=True), k
+
+
+def test_netcdf4_cellpop_through_libnetcdf(tmp_path, monkeypatch):
+    classic = str(tmp_path / "cellpop_data.nc")
+    _convert("to-classic", os.path.join(GOLDEN, "cellpop_tc_data.json"), classic)
+    nc4 = str(tmp_path / "cellpop_data4.nc")
+    _netcdf4_stand_in(classic, nc4)
+    monkeypatch.setenv("BCM3_LIBNETCDF", _fake_netcdf(tmp_path))
+    sys.path.insert(0, GOLDEN)
+    import make_cellpop_fixtures as F
+    data = '<data type="time_points" data_name="pcna_cells_markers" species_name="PCNA_gfp;CycB" stdev="stdev;0.5"/>'
+    p = tmp_path / "l.xml"
+    p.write_text(F.likelihood_text(num_cells=16, max_cells=16, data_file=nc4, data_xml=data,
+                                   model_file=os.path.join(GOLDEN, "cellpop_model.xml"), experiment_attrs=' divide_cells="false"'))
+    _lik(str(p), "cellpop")

@@ -64,6 +64,21 @@ def test_native_matches_python_loop_c3():
     for k in ("accepted_mutate", "attempted_mutate", "accepted_exchange", "attempted_exchange"):
         assert c[k] == cnt[k], k
     assert c["samples_done"] == 50 and c["rounds"] == 50
+    # not only self-consistent: every chain's llh is the oracle's value of its parameter vector
+    # (the reference's CVODE restated bit for bit) inside the parity envelope (tests/parity.py)
+    _assert_llh_matches_oracle(s.state())
+
+
+def _assert_llh_matches_oracle(st):
+    import oracle as O
+    import parity
+    r = O.Oracle("restated").popk_eval(H.c3_problem(1), st["values"], nthreads=8, want_traj=False)
+    got, ref = st["llh"], r["logp"]
+    mism = np.isfinite(got) != np.isfinite(ref)
+    assert np.all(r["stats"][mism, 0, 0] >= 0.99 * H.c3_problem(1).max_steps)
+    err = parity.llh_err(got[~mism], ref[~mism])
+    parity.log_summary({"llh_t1": float(np.mean(err <= parity.LLH_T1)), "llh_max": float(err.max())}, n=int(err.size))
+    assert np.mean(err <= parity.LLH_T1) >= parity.llh_min_fraction(err.size) and np.all(err <= parity.LLH_T2)
 
 
 @pytest.mark.parametrize("proposal,scheme", [("gaussian_mixture", "deterministic_even_odd"),
