@@ -16,7 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("BCM3HIP_LIB") or os.path.join(_HERE, "lib", "libbcm3hip.so")
 
 PK_TYPES = {"one": 0, "two": 1, "one_biphasic": 2, "two_biphasic": 3, "one_transit": 4, "two_transit": 5}
-ANALYTIC_BANANA, ANALYTIC_CIRCULAR = 1, 2
+ANALYTIC_BANANA, ANALYTIC_CIRCULAR, ANALYTIC_DUMMY = 1, 2, 3
+MIXTURE_NORMAL, MIXTURE_T = 1, 2
 OPT_LANES_PER_WAVE, OPT_BLOCK_WAVES, OPT_TIMING_LOG, OPT_UNI_SOLVER, OPT_BLOCK_LDS = 1, 2, 3, 4, 5
 OPT_PLACEMENT_LOG = 6
 PRIOR_UNIFORM, PRIOR_NORMAL = 0, 1
@@ -64,6 +65,12 @@ class AnalyticModel(C.Structure):
                 ("p2", C.c_double)]
 
 
+class MixtureModel(C.Structure):
+    """bcm3hip_mixture_model"""
+    _fields_ = [("kind", C.c_int32), ("d", C.c_int32), ("K", C.c_int32), ("log_weights", C.c_void_p),
+                ("means", C.c_void_p), ("covariances", C.c_void_p), ("nus", C.c_void_p)]
+
+
 class TrajStats(C.Structure):
     """bcm3hip_traj_stats"""
     _fields_ = [(k, C.c_int32) for k in ("nst", "nfe", "nni", "nsetups", "nje", "netf", "ncfn", "nreinit")]
@@ -106,6 +113,7 @@ def lib() -> C.CDLL:
     L.bcm3hip_open_popk.argtypes = [C.c_int, C.POINTER(PopPKModel), C.POINTER(vp)]
     L.bcm3hip_open_analytic.argtypes = [C.c_int, C.POINTER(AnalyticModel), C.POINTER(vp)]
     L.bcm3hip_open_expm_pk.argtypes = [C.c_int, C.POINTER(ExpmPKModel), C.POINTER(vp)]
+    L.bcm3hip_open_mixture.argtypes = [C.c_int, C.POINTER(MixtureModel), C.POINTER(vp)]
     L.bcm3hip_close.argtypes = [vp]
     L.bcm3hip_set_option.argtypes = [vp, C.c_int, i64]
     L.bcm3hip_num_variables.argtypes = [vp]
@@ -134,7 +142,7 @@ def lib() -> C.CDLL:
         L.bcm3hip_assign_cells.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp]
         L.bcm3hip_assign_cells.restype = C.c_int
     L.bcm3hip_eval_batch_detail.argtypes = [vp, sz, sz, vp, vp, vp, vp, vp, vp]
-    for f in ("bcm3hip_open_popk", "bcm3hip_open_analytic", "bcm3hip_open_expm_pk", "bcm3hip_close", "bcm3hip_set_option",
+    for f in ("bcm3hip_open_popk", "bcm3hip_open_analytic", "bcm3hip_open_mixture", "bcm3hip_open_expm_pk", "bcm3hip_close", "bcm3hip_set_option",
               "bcm3hip_num_variables", "bcm3hip_eval_batch", "bcm3hip_eval_batch_device",
               "bcm3hip_last_kernel_ms", "bcm3hip_eval_batch_detail"):
         getattr(L, f).restype = C.c_int
@@ -211,6 +219,21 @@ class Context:
         m = AnalyticModel(kind, d, p0, p1, p2)
         h = C.c_void_p()
         check(lib().bcm3hip_open_analytic(device, C.byref(m), C.byref(h)), "bcm3hip_open_analytic")
+        return cls(h, d)
+
+    @classmethod
+    def mixture(cls, kind: int, log_weights, means, covariances, nus=None, device: int = 0) -> "Context":
+        """bcm3hip_open_mixture: means [K][d], covariances [K][d][d] (lower triangles used)."""
+        lw = np.ascontiguousarray(log_weights, np.float64)
+        mu = np.ascontiguousarray(means, np.float64)
+        cov = np.ascontiguousarray(covariances, np.float64)
+        K, d = mu.shape
+        assert lw.shape == (K,) and cov.shape == (K, d, d)
+        nu = None if nus is None else np.ascontiguousarray(nus, np.float64)
+        m = MixtureModel(kind, d, K, lw.ctypes.data, mu.ctypes.data, cov.ctypes.data,
+                         None if nu is None else nu.ctypes.data)
+        h = C.c_void_p()
+        check(lib().bcm3hip_open_mixture(device, C.byref(m), C.byref(h)), "bcm3hip_open_mixture")
         return cls(h, d)
 
     @classmethod

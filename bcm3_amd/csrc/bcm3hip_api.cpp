@@ -250,7 +250,8 @@ int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* m, bcm3hip_c
 {
     if (!m || !out) return BCM3HIP_ERR_ARG;
     *out = nullptr;
-    if (m->kind != BCM3HIP_ANALYTIC_BANANA && m->kind != BCM3HIP_ANALYTIC_CIRCULAR) return BCM3HIP_ERR_MODEL;
+    if (m->kind != BCM3HIP_ANALYTIC_BANANA && m->kind != BCM3HIP_ANALYTIC_CIRCULAR && m->kind != BCM3HIP_ANALYTIC_DUMMY)
+        return BCM3HIP_ERR_MODEL;
     if (m->d < (m->kind == BCM3HIP_ANALYTIC_BANANA ? 2 : 1)) return BCM3HIP_ERR_MODEL;
     bcm3hip_ctx* c = new (std::nothrow) bcm3hip_ctx();
     if (!c) return BCM3HIP_ERR_ALLOC;
@@ -266,6 +267,84 @@ int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* m, bcm3hip_c
     c->am.p0 = m->p0;
     c->am.p1 = m->p1;
     c->am.p2 = m->p2;
+    *out = c;
+    return 0;
+}
+
+// Eigen::LLT<MatrixXd>::compute for small matrices (llt_inplace<double, Lower>::unblocked, LLT.h): the
+// lower triangle of A (row-major, n x n) is factorised in place column by column,
+//   L(k,k) = sqrt(A(k,k) - sum_j<k L(k,j)^2),  L(i,k) = (A(i,k) - sum_j<k L(i,j) L(k,j)) / L(k,k);
+// false (Eigen's info() != Success) when a pivot is not > 0. The strict upper triangle is zeroed.
+static bool llt_lower(int n, double* A)
+{
+    for (int k = 0; k < n; k++) {
+        double x = A[k * n + k];
+        for (int j = 0; j < k; j++) x -= A[k * n + j] * A[k * n + j];
+        if (!(x > 0.0)) return false;
+        x = std::sqrt(x);
+        A[k * n + k] = x;
+        for (int i = k + 1; i < n; i++) {
+            double s = A[i * n + k];
+            for (int j = 0; j < k; j++) s -= A[i * n + j] * A[k * n + j];
+            A[i * n + k] = s / x;
+        }
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = i + 1; j < n; j++) A[i * n + j] = 0.0;
+    return true;
+}
+
+int bcm3hip_open_mixture(int device, const bcm3hip_mixture_model* m, bcm3hip_ctx** out)
+{
+    if (!m || !out) return BCM3HIP_ERR_ARG;
+    *out = nullptr;
+    if (m->kind != BCM3HIP_MIXTURE_NORMAL && m->kind != BCM3HIP_MIXTURE_T) return BCM3HIP_ERR_MODEL;
+    if (m->d < 1 || m->d > BCM3HIP_MIXTURE_DMAX || m->K < 1 || m->K > BCM3HIP_MIXTURE_KMAX) return BCM3HIP_ERR_MODEL;
+    if (!m->log_weights || !m->means || !m->covariances || (m->kind == BCM3HIP_MIXTURE_T && !m->nus))
+        return BCM3HIP_ERR_ARG;
+    const int d = m->d, K = m->K;
+    std::vector<double> chol((size_t)K * d * d), cst((size_t)K * 3);
+    for (int k = 0; k < K; k++) {
+        double* L = &chol[(size_t)k * d * d];
+        std::copy(m->covariances + (size_t)k * d * d, m->covariances + (size_t)(k + 1) * d * d, L);
+        const double nu = (m->kind == BCM3HIP_MIXTURE_T) ? m->nus[k] : 0.0;
+        double logc;
+        if (m->kind == BCM3HIP_MIXTURE_T && !(nu > 0.0)) return BCM3HIP_ERR_MODEL;
+        if (m->kind == BCM3HIP_MIXTURE_T && d == 1) {
+            // dmvt with p = 1 is LogPdfT(x, mu, sigma(0,0), nu) (mvt.cpp:129-134), whose constant is
+            // -log(sigma sqrt(nu) B(nu/2, 1/2)) (ProbabilityDistributions.cpp:176; boost::math::beta
+            // there, its lgamma form here -- parity of this constant unpinned, Boost absent)
+            const double sigma = L[0];
+            const double beta = std::exp(std::lgamma(0.5 * nu) + std::lgamma(0.5) - std::lgamma(0.5 * nu + 0.5));
+            logc = -std::log(sigma * std::sqrt(nu) * beta);
+        } else {
+            if (!llt_lower(d, L)) return BCM3HIP_ERR_MODEL;
+            double det = 0.0;
+            for (int i = 0; i < d; i++) det += std::log(L[i * d + i]);
+            if (m->kind == BCM3HIP_MIXTURE_NORMAL)
+                logc = -det - 0.5 * d * std::log(2.0 * M_PI);  // mvn.cpp:22
+            else
+                logc = std::lgamma(0.5 * (d + nu)) - (std::lgamma(0.5 * nu) + det + 0.5 * d * std::log(M_PI * nu));  // mvt.cpp:145
+        }
+        cst[3 * k] = m->log_weights[k];
+        cst[3 * k + 1] = logc;
+        cst[3 * k + 2] = nu;
+    }
+    bcm3hip_ctx* c = new (std::nothrow) bcm3hip_ctx();
+    if (!c) return BCM3HIP_ERR_ALLOC;
+    int r = ctx_common_init(c, device);
+    if (r == 0) r = upload(c, m->means, (size_t)K * d, &c->am.mean);
+    if (r == 0) r = upload(c, (const double*)chol.data(), chol.size(), &c->am.chol);
+    if (r == 0) r = upload(c, (const double*)cst.data(), cst.size(), &c->am.cst);
+    if (r) {
+        bcm3hip_close(c);
+        return r;
+    }
+    c->kind = 2;
+    c->d = d;
+    c->am.kind = bcm3hip::kAnalyticMixtureBase + m->kind;
+    c->am.d = d;
+    c->am.K = K;
     *out = c;
     return 0;
 }

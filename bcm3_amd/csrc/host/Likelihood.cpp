@@ -58,7 +58,7 @@ std::string option_get(const OptionsMap& vm, const std::string& key, const std::
 std::vector<std::string> LikelihoodFactory::SupportedTypes()
 {
     return {"pop_pk_trajectory", "pharmacokinetic_trajectory", "pharmaco_single", "pharmaco_population", "banana", "circular",
-            "cell_population", "dll"};
+            "multimodal_gaussians", "truncated_t", "dummy", "cell_population", "dll"};
 }
 
 std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::string& fn,
@@ -103,12 +103,18 @@ std::shared_ptr<Likelihood> LikelihoodFactory::CreateLikelihood(const std::strin
         ll = std::make_shared<TestLikelihoodBanana>(sampling_threads, evaluation_threads);
     } else if (type == "circular") {
         ll = std::make_shared<TestLikelihoodCircular>(sampling_threads, evaluation_threads);
+    } else if (type == "multimodal_gaussians") {
+        ll = std::make_shared<TestLikelihoodMultimodalGaussians>(sampling_threads, evaluation_threads);
+    } else if (type == "truncated_t") {
+        ll = std::make_shared<TestLikelihoodTruncatedT>(sampling_threads, evaluation_threads);
+    } else if (type == "dummy") {
+        ll = std::make_shared<LikelihoodDummy>(sampling_threads, evaluation_threads);
     } else if (type == "cell_population") {
         ll = std::make_shared<LikelihoodCellPopulation>(sampling_threads, evaluation_threads);
     } else if (type == "dll") {
         ll = std::make_shared<LikelihoodDLL>(sampling_threads, evaluation_threads);
     } else {
-        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, pharmaco_single, pharmaco_population, banana, circular, cell_population, dll)",
+        LOGERROR("Unknown likelihood type \"%s\" (supported on this backend: pop_pk_trajectory, pharmacokinetic_trajectory, pharmaco_single, pharmaco_population, banana, circular, multimodal_gaussians, truncated_t, dummy, cell_population, dll)",
                  type.c_str());
         return ll;
     }

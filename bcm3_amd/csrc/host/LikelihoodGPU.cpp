@@ -1,6 +1,7 @@
 // LikelihoodGPU.cpp -- see LikelihoodGPU.h
 #include "LikelihoodGPU.h"
 
+#include <cctype>
 #include <cmath>
 #include <cstdlib>
 #include <exception>
@@ -1068,6 +1069,193 @@ bool TestLikelihoodCircular::Initialize(std::shared_ptr<const VariableSet> vs, c
     int rr = bcm3hip_open_analytic(device, &m, &ctx);
     if (rr != 0) {
         LOGERROR("Opening the circular GPU context failed: %s", bcm3hip_error_string(rr));
+        return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// bcm3::tokenize (src/utils/Utils.cpp:7-25): boost::char_separator with keep_empty_tokens, one
+// trailing newline dropped; an empty string gives no tokens
+static std::vector<std::string> tokenize_keep_empty(std::string str, char delim)
+{
+    std::vector<std::string> t;
+    if (str.empty()) return t;
+    if (str.back() == '\n') str.pop_back();
+    size_t b = 0;
+    for (;;) {
+        size_t e = str.find(delim, b);
+        t.push_back(str.substr(b, e == std::string::npos ? std::string::npos : e - b));
+        if (e == std::string::npos) break;
+        b = e + 1;
+    }
+    return t;
+}
+
+// boost::lexical_cast<double>: the whole token, no surrounding whitespace, no hexadecimal form
+static bool lexical_cast_real(const std::string& s, Real& v)
+{
+    if (s.empty() || std::isspace((unsigned char)s.front()) || std::isspace((unsigned char)s.back())) return false;
+    if (s.find_first_of("xX") != std::string::npos) return false;
+    char* e = nullptr;
+    v = std::strtod(s.c_str(), &e);
+    return e && *e == 0;
+}
+
+bool ParseVectorFromString(const std::string& str, std::vector<Real>& v)
+{
+    const std::vector<std::string> tok = tokenize_keep_empty(str, ';');
+    v.assign(tok.size(), 0.0);
+    for (size_t i = 0; i < tok.size(); i++) {
+        if (!lexical_cast_real(tok[i], v[i])) {
+            LOGERROR("Could not cast value \"%s\" to a constant real value: bad lexical cast", tok[i].c_str());
+            return false;
+        }
+    }
+    return true;
+}
+
+bool ParseMatrixFromString(const std::string& str, std::vector<std::vector<Real>>& m)
+{
+    const std::vector<std::string> rows = tokenize_keep_empty(str, ';');
+    m.clear();
+    if (rows.empty()) return false;  // the reference reads rows[0] of an empty list
+    const size_t cols = tokenize_keep_empty(rows[0], ',').size();
+    for (const std::string& r : rows) {
+        const std::vector<std::string> row = tokenize_keep_empty(r, ',');
+        if (row.size() != cols) {
+            LOGERROR("Inconsistent matrix");
+            return false;
+        }
+        std::vector<Real> vals(cols);
+        for (size_t j = 0; j < cols; j++) {
+            if (!lexical_cast_real(row[j], vals[j])) {
+                LOGERROR("Could not cast string to a Real value: bad lexical cast");
+                return false;
+            }
+        }
+        m.push_back(vals);
+    }
+    return true;
+}
+
+static bool open_mixture_ctx(int device, int kind, size_t d, const std::vector<Real>& log_w,
+                             const std::vector<std::vector<Real>>& mus, const std::vector<std::vector<std::vector<Real>>>& sigmas,
+                             const std::vector<Real>& nus, bcm3hip_ctx** ctx, const char* what)
+{
+    const size_t K = log_w.size();
+    std::vector<double> mean, cov;
+    for (size_t k = 0; k < K; k++) {
+        mean.insert(mean.end(), mus[k].begin(), mus[k].end());
+        for (size_t i = 0; i < d; i++) cov.insert(cov.end(), sigmas[k][i].begin(), sigmas[k][i].end());
+    }
+    bcm3hip_mixture_model m{kind, (int32_t)d, (int32_t)K, log_w.data(), mean.data(), cov.data(),
+                            nus.empty() ? nullptr : nus.data()};
+    const int r = bcm3hip_open_mixture(device, &m, ctx);
+    if (r != 0) {
+        LOGERROR("Opening the %s GPU context failed: %s%s", what, bcm3hip_error_string(r),
+                 r == BCM3HIP_ERR_MODEL ? " (a covariance that is not positive definite, a nu <= 0, or more than "
+                                          "16 dimensions / 64 clusters)"
+                                        : "");
+        return false;
+    }
+    return true;
+}
+
+// TestLikelihoodMultimodalGaussians::Initialize (TestLikelihoodMultimodalGaussians.cpp:15-34): two
+// fixed 2-D components, weights 1/2: means (-5,-5), (5,5), covariances [1 -0.9; -0.9 1], [2 -0.5; -0.5 1]
+bool TestLikelihoodMultimodalGaussians::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& node,
+                                                   const OptionsMap& vm)
+{
+    varset = vs;
+    if (varset->GetNumVariables() != 2) {
+        LOGERROR("Inconsistent prior and likelihood (%zu variables and %zu dimensions)", varset->GetNumVariables(),
+                 (size_t)2);
+        return false;
+    }
+    if (!OpenDevice(vm)) return false;
+    if (option_get(vm, "backend", "") == "none") return true;
+    const std::vector<Real> lw = {std::log(0.5), std::log(0.5)};
+    const std::vector<std::vector<Real>> mus = {{-5, -5}, {5, 5}};
+    const std::vector<std::vector<std::vector<Real>>> sig = {{{1, -0.9}, {-0.9, 1}}, {{2, -0.5}, {-0.5, 1}}};
+    return open_mixture_ctx(device, BCM3HIP_MIXTURE_NORMAL, 2, lw, mus, sig, {}, &ctx, "multimodal_gaussians");
+}
+
+// TestLikelihoodTruncatedT::Initialize (TestLikelihoodTruncatedT.cpp:20-79): num_clusters components
+// mu<i> / sigma<i> (1-based), nus, weights normalised to sum 1 (log taken per evaluation there, once here)
+bool TestLikelihoodTruncatedT::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& node,
+                                          const OptionsMap& vm)
+{
+    varset = vs;
+    std::vector<std::vector<Real>> mus;
+    std::vector<std::vector<std::vector<Real>>> sigmas;
+    std::vector<Real> nus, weights;
+    try {
+        if (!node.has_attr("dimensions")) throw XmlError{"No such node (<xmlattr>.dimensions)"};
+        if (!node.has_attr("num_clusters")) throw XmlError{"No such node (<xmlattr>.num_clusters)"};
+        const long dl = node.get_long("dimensions", -1), kl = node.get_long("num_clusters", -1);
+        if (dl < 0 || kl < 0) throw XmlError{"conversion of data to type \"size_t\" failed"};
+        dimensions = (size_t)dl;
+        num_clusters = (size_t)kl;
+        if (varset->GetNumVariables() != dimensions) {
+            LOGERROR("Incorrect number of variables in prior for samples a %zu-dimensional space", dimensions);
+            return false;
+        }
+        mus.resize(num_clusters);
+        sigmas.resize(num_clusters);
+        for (size_t i = 0; i < num_clusters; i++) {
+            if (!ParseVectorFromString(node.get("mu" + std::to_string(i + 1)), mus[i])) return false;
+            if (mus[i].size() != dimensions) {
+                LOGERROR("Inconsistent dimension for mu%zu", i);
+                return false;
+            }
+            if (!ParseMatrixFromString(node.get("sigma" + std::to_string(i + 1)), sigmas[i])) return false;
+            if (sigmas[i].size() != dimensions || sigmas[i][0].size() != dimensions) {
+                LOGERROR("Inconsistent dimension for sigma%zu", i);
+                return false;
+            }
+        }
+        if (!ParseVectorFromString(node.get("nus"), nus)) return false;
+        if (nus.size() != num_clusters) {
+            LOGERROR("Inconsistent number of nus");
+            return false;
+        }
+        if (!ParseVectorFromString(node.get("weights"), weights)) return false;
+        if (weights.size() != num_clusters) {
+            LOGERROR("Inconsistent number of weights");
+            return false;
+        }
+    } catch (XmlError& e) {
+        LOGERROR("Error parsing likelihood file: %s", e.what.c_str());
+        return false;
+    }
+    if (num_clusters == 0) {
+        LOGERROR("truncated_t needs at least one cluster (the reference's logp is -inf for every sample)");
+        return false;
+    }
+    Real wsum = 0.0;
+    for (Real w : weights) wsum += w;
+    std::vector<Real> lw(num_clusters);
+    for (size_t i = 0; i < num_clusters; i++) lw[i] = std::log(weights[i] / wsum);
+    if (!OpenDevice(vm)) return false;
+    if (option_get(vm, "backend", "") == "none") return true;
+    return open_mixture_ctx(device, BCM3HIP_MIXTURE_T, dimensions, lw, mus, sigmas, nus, &ctx, "truncated_t");
+}
+
+// LikelihoodDummy::Initialize / EvaluateLogProbability (LikelihoodDummy.cpp:13-32): LogPdfTnu4(values[0], 0, 1)
+bool LikelihoodDummy::Initialize(std::shared_ptr<const VariableSet> vs, const XmlNode& node, const OptionsMap& vm)
+{
+    varset = vs;
+    if (varset->GetNumVariables() < 1) {
+        LOGERROR("The dummy likelihood reads the first variable; the prior has none");
+        return false;
+    }
+    if (!OpenDevice(vm)) return false;
+    if (option_get(vm, "backend", "") == "none") return true;
+    bcm3hip_analytic_model m{BCM3HIP_ANALYTIC_DUMMY, (int32_t)varset->GetNumVariables(), 0.0, 0.0, 0.0};
+    const int r = bcm3hip_open_analytic(device, &m, &ctx);
+    if (r != 0) {
+        LOGERROR("Opening the dummy GPU context failed: %s", bcm3hip_error_string(r));
         return false;
     }
     return true;

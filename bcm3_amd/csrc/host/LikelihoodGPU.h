@@ -6,6 +6,9 @@
 //   pharmaco_single    PharmacoLikelihoodSingle  (src/pharmaco/PharmacoLikelihoodSingle.h; matrix-exponential PK)
 //   banana             TestLikelihoodBanana      (src/likelihoods/TestLikelihoodBanana.cpp)
 //   circular           TestLikelihoodCircular    (src/likelihoods/TestLikelihoodCircular.cpp)
+//   multimodal_gaussians TestLikelihoodMultimodalGaussians (src/likelihoods/TestLikelihoodMultimodalGaussians.cpp)
+//   truncated_t        TestLikelihoodTruncatedT  (src/likelihoods/TestLikelihoodTruncatedT.cpp)
+//   dummy              LikelihoodDummy           (src/likelihoods/LikelihoodDummy.cpp)
 // Each owns one libbcm3hip context (include/bcm3hip.h) on the configured device. There is no
 // CPU fallback: without a GPU, Initialize fails.
 #pragma once
@@ -201,5 +204,35 @@ private:
     size_t dimension = 0;
     Real r = 2.0, offset = 3.5, w = 0.1;
 };
+
+class TestLikelihoodMultimodalGaussians : public LikelihoodGPUBase {
+public:
+    TestLikelihoodMultimodalGaussians(size_t sampling_threads, size_t evaluation_threads) {}
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+};
+
+class TestLikelihoodTruncatedT : public LikelihoodGPUBase {
+public:
+    TestLikelihoodTruncatedT(size_t sampling_threads, size_t evaluation_threads) {}
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+
+private:
+    size_t dimensions = 0, num_clusters = 0;
+};
+
+class LikelihoodDummy : public LikelihoodGPUBase {
+public:
+    LikelihoodDummy(size_t sampling_threads, size_t evaluation_threads) {}
+    bool Initialize(std::shared_ptr<const VariableSet> varset, const XmlNode& likelihood_node,
+                    const OptionsMap& vm) override;
+};
+
+// bcm3::ParseVectorFromString (src/utils/VectorUtils.cpp:204-219: ';'-separated, empty tokens kept,
+// each converted by boost::lexical_cast<Real>) and ParseMatrixFromString (VectorUtils.h:39-67: rows
+// separated by ';', columns by ','; every row as long as the first). Errors are logged.
+bool ParseVectorFromString(const std::string& str, std::vector<Real>& v);
+bool ParseMatrixFromString(const std::string& str, std::vector<std::vector<Real>>& m);
 
 }  // namespace bcm3

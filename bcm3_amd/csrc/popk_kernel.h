@@ -35,7 +35,14 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
 struct AnalyticDevModel {
     int32_t kind, d;
     double p0, p1, p2;
+    // mixtures (kind = 16 + BCM3HIP_MIXTURE_*): K components; mean [K][d], chol [K][d][d] (lower
+    // factor, row-major), cst [K][3] = (log weight, log normalising constant, nu)
+    int32_t K;
+    const double* mean;
+    const double* chol;
+    const double* cst;
 };
+constexpr int32_t kAnalyticMixtureBase = 16;
 
 hipError_t launch_analytic(const AnalyticDevModel& m, int64_t n, const double* values, double* logp,
                            int32_t* status, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);

@@ -104,7 +104,9 @@ typedef struct {
     const int32_t* simulate_until;        /* [P] number of time points simulated */
 } bcm3hip_popk_model;
 
-enum { BCM3HIP_ANALYTIC_BANANA = 1, BCM3HIP_ANALYTIC_CIRCULAR = 2 };
+/* BANANA TestLikelihoodBanana, CIRCULAR TestLikelihoodCircular, DUMMY LikelihoodDummy
+ * (src/likelihoods/LikelihoodDummy.cpp:18-32: LogPdfTnu4(values[0], 0, 1)) */
+enum { BCM3HIP_ANALYTIC_BANANA = 1, BCM3HIP_ANALYTIC_CIRCULAR = 2, BCM3HIP_ANALYTIC_DUMMY = 3 };
 typedef struct {
     int32_t kind; /* BCM3HIP_ANALYTIC_* */
     int32_t d;    /* dimension */
@@ -112,6 +114,28 @@ typedef struct {
     double p1;    /* banana: sd2 ; circular: offset */
     double p2;    /* circular: width */
 } bcm3hip_analytic_model;
+
+/* Mixture test likelihoods: logp = logsum_k (log w_k + log density_k(values)), summed with
+ * bcm3::logsum in component order from -inf.
+ *   NORMAL  TestLikelihoodMultimodalGaussians (TestLikelihoodMultimodalGaussians.cpp:36-42), each
+ *           component bcm3::dmvnormal (src/stats/mvn.cpp:9-33)
+ *   T       TestLikelihoodTruncatedT (TestLikelihoodTruncatedT.cpp:81-90), each component
+ *           bcm3::dmvt (src/stats/mvt.cpp:119-157; d = 1 goes through LogPdfT with the 1x1
+ *           "covariance" as the scale, ProbabilityDistributions.cpp:159-180, as the reference does)
+ * The Cholesky factors and log normalising constants are computed once at open time
+ * (Eigen::LLT reads the lower triangle of each covariance). */
+enum { BCM3HIP_MIXTURE_NORMAL = 1, BCM3HIP_MIXTURE_T = 2 };
+#define BCM3HIP_MIXTURE_DMAX 16
+#define BCM3HIP_MIXTURE_KMAX 64
+typedef struct {
+    int32_t kind;               /* BCM3HIP_MIXTURE_* */
+    int32_t d;                  /* dimension, 1..BCM3HIP_MIXTURE_DMAX */
+    int32_t K;                  /* components, 1..BCM3HIP_MIXTURE_KMAX */
+    const double* log_weights;  /* [K] log of each component's weight, added as given */
+    const double* means;        /* [K][d] */
+    const double* covariances;  /* [K][d][d] row-major; the lower triangle is used */
+    const double* nus;          /* [K] degrees of freedom (T), > 0; NULL for NORMAL */
+} bcm3hip_mixture_model;
 
 /* Linear-compartment PK model solved by matrix exponentials: the pharmaco_single likelihood
  * (src/pharmaco/PharmacoLikelihoodSingle.cpp:149-218) over PharmacokineticModel::Solve /
@@ -300,6 +324,9 @@ const char* bcm3hip_error_string(int code);
 
 int bcm3hip_open_popk(int device, const bcm3hip_popk_model* model, bcm3hip_ctx** out);
 int bcm3hip_open_analytic(int device, const bcm3hip_analytic_model* model, bcm3hip_ctx** out);
+/* multimodal_gaussians / truncated_t; BCM3HIP_ERR_MODEL when a covariance is not positive
+ * definite (the reference's LLT fails and its ASSERT is compiled out) or a nu is not > 0 */
+int bcm3hip_open_mixture(int device, const bcm3hip_mixture_model* model, bcm3hip_ctx** out);
 /* pharmaco_single (PharmacoLikelihoodSingle::EvaluateLogProbability); per-item status 1 when
  * PharmacokineticModel::Solve fails (NaN state): logp = -inf */
 int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* model, bcm3hip_ctx** out);
