@@ -8,8 +8,9 @@
 // Cross-lane work is the two small contractions of the linear PK systems and the norms:
 //   * matrix-vector products (RHS  A y, solve  A^-1 b): the column j of the matrix lives in
 //     the lanes (lane i: a(i, j)) and y_j is broadcast to every lane with one DPP row_newbcast
-//     move, f = a(:,0) y0 -> fma(a(:,1), y1, f) -> fma(a(:,2), y2, f): the same products and
-//     fma order as the scalar model (PKLane::rhs / lin_solve), so the bits agree;
+//     move; the RHS as f = a(:,0) y0 -> fma(a(:,1), y1, f) -> fma(a(:,2), y2, f) (matvec), the
+//     solve as the reference's unfused p0 + (p1 + p2) (solvevec): the same products and order
+//     as the scalar model (PKLane::rhs / lin_solve), so the bits agree;
 //   * weighted RMS norms: squares in lanes, the sum ((p0^2 + p1^2) + p2^2) from broadcasts in
 //     component order, made wave-uniform with readfirstlane (wrms of bdf_lane.h sums the same
 //     rounded squares in the same order).
@@ -86,6 +87,17 @@ BDF_INL double matvec(const double (&col)[NS], double x)
     double r = col[0] * bc<0>(x);
     cfor<1, NS>([&](auto j) __attribute__((always_inline)) { r = __builtin_fma(col[CI(j)], bc<CI(j)>(x), r); });
     return r;
+}
+
+// x = A^-1 b for the inverse held as lane columns, in PKLane::lin_solve's order: unfused
+// p0 + p1 (N = 2) or Eigen's p0 + (p1 + p2) (N = 3)
+template <int NS>
+BDF_INL double solvevec(const double (&col)[NS], double x)
+{
+    if constexpr (NS == 3)
+        return col[0] * bc<0>(x) + (col[1] * bc<1>(x) + col[2] * bc<2>(x));
+    else
+        return col[0] * bc<0>(x) + col[1] * bc<1>(x);
 }
 
 // per-trajectory solver statistics only when the caller asked for them: without, the counters
@@ -437,7 +449,7 @@ BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& csc
         s.nstlp = s.nst;
     }
     s.cnt.nni++;
-    double x = vec::matvec<NS>(s.icol, -delta);
+    double x = vec::solvevec<NS>(s.icol, -delta);
     x *= cscale;
     s.acor += x;
     return vec::wrms<NS>(x, s.ewt);

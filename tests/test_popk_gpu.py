@@ -30,14 +30,15 @@ def c3():
     ctx.close()
 
 
-def _check(prob, g, o, near_cap=None):
+def _check(prob, g, o, near_cap=None, ref_self=None):
     T = prob.T
     y1 = parity.y1_rel_err(g["traj"][:, :, 1, :].reshape(-1, T), o["traj"][:, :, 1, :].reshape(-1, T), prob.atol)
     pg = g["patient_llh"].reshape(-1)
     po = o["patient_llh"].reshape(-1)
     le = parity.llh_err(pg, po)
     return parity.assert_parity(y1, le, g["stats"]["nst"].reshape(-1), o["stats"][:, :, 0].reshape(-1),
-                                (~np.isneginf(pg)).astype(int), (~np.isneginf(po)).astype(int), near_cap)
+                                (~np.isneginf(pg)).astype(int), (~np.isneginf(po)).astype(int), near_cap,
+                                ref_self=ref_self)
 
 
 def test_c3_golden_fixture(c3, golden_dir):
@@ -48,7 +49,7 @@ def test_c3_golden_fixture(c3, golden_dir):
     le = parity.llh_err(g["logp"], gold["logp"])
     near = gold["stats"][:, 0, 0] >= 0.99 * prob.max_steps
     parity.assert_parity(y1, le, g["stats"]["nst"][:, 0], gold["stats"][:, 0, 0], (g["status"] == 0).astype(int),
-                         gold["ok"][:, 0], near)
+                         gold["ok"][:, 0], near, ref_self=parity.reference_self_spread(prob, gold["values"]))
 
 
 def test_c3_golden_llh_8192(c3):
@@ -81,7 +82,7 @@ def test_c3_prior_draws_vs_oracle(c3, orc):
     g = ctx.eval(vals, detail=True)
     o = orc.popk_eval(prob, vals, nthreads=8)
     near = o["stats"][:, 0, 0] >= 0.99 * prob.max_steps
-    _check(prob, g, o, near)
+    _check(prob, g, o, near, ref_self=parity.reference_self_spread(prob, vals))
     # logp of an evaluation with P = 1 is 0 + patient term
     assert np.array_equal(g["logp"], 0.0 + g["patient_llh"][:, 0])
 
