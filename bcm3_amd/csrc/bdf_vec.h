@@ -9,8 +9,8 @@
 //   * matrix-vector products (RHS  A y, solve  A^-1 b): the column j of the matrix lives in
 //     the lanes (lane i: a(i, j)) and y_j is broadcast to every lane with one DPP row_newbcast
 //     move; the RHS as f = a(:,0) y0 -> fma(a(:,1), y1, f) -> fma(a(:,2), y2, f) (matvec), the
-//     solve as the reference's unfused p0 + (p1 + p2) (solvevec): the same products and order
-//     as the scalar model (PKLane::rhs / lin_solve), so the bits agree;
+//     solve as the reference build's contraction of Eigen's p0 + (p1 + p2) (solvevec): the same
+//     products and order as the scalar model (PKLane::rhs / lin_solve), so the bits agree;
 //   * weighted RMS norms: squares in lanes, the sum ((p0^2 + p1^2) + p2^2) from broadcasts in
 //     component order, made wave-uniform with readfirstlane (wrms of bdf_lane.h sums the same
 //     rounded squares in the same order).
@@ -89,15 +89,15 @@ BDF_INL double matvec(const double (&col)[NS], double x)
     return r;
 }
 
-// x = A^-1 b for the inverse held as lane columns, in PKLane::lin_solve's order: unfused
-// p0 + p1 (N = 2) or Eigen's p0 + (p1 + p2) (N = 3)
+// x = A^-1 b for the inverse held as lane columns, in PKLane::lin_solve's order: the reference
+// build's fma(c0 b0, c1 b1) (N = 2) and fma(c0 b0, fma(c2 b2, c1 b1)) (N = 3, Eigen's p0 + (p1 + p2))
 template <int NS>
 BDF_INL double solvevec(const double (&col)[NS], double x)
 {
     if constexpr (NS == 3)
-        return col[0] * bc<0>(x) + (col[1] * bc<1>(x) + col[2] * bc<2>(x));
+        return __builtin_fma(col[0], bc<0>(x), __builtin_fma(col[2], bc<2>(x), col[1] * bc<1>(x)));
     else
-        return col[0] * bc<0>(x) + col[1] * bc<1>(x);
+        return __builtin_fma(col[0], bc<0>(x), col[1] * bc<1>(x));
 }
 
 // per-trajectory solver statistics only when the caller asked for them: without, the counters

@@ -146,16 +146,18 @@ struct PKLane {
     }
     // SUNLinSolSolve_Dense_Eigen2x2 (sunlinsol_dense_eigen.cpp:157-167): inv(i,0) b0 + inv(i,1) b1;
     // _Eigen3x3 (:169-176): Eigen's Matrix3d * VectorXd, whose row sum is its unrolled reduction
-    // p0 + (p1 + p2). Products and sums unfused: the arithmetic of the reference's solve without FMA
-    // contraction, bit for bit the oracle's (checked against the vendored Eigen, oracle/eigen_ls.cpp)
+    // p0 + (p1 + p2). Both as the reference's own build (-O3 -march=native) contracts them:
+    // fma(i0, b0, i1 b1) and fma(i0, b0, fma(i2, b2, i1 b1)) -- checked against the vendored Eigen
+    // compiled with FMA (oracle/eigen_ls.cpp)
     BDF_INL void lin_solve(const Inv& r, const double (&b)[NS], double (&x)[NS]) const
     {
         cfor<0, NS>([&](auto I) __attribute__((always_inline)) {
             constexpr int i = CI(I);
             if constexpr (NS == 3)
-                x[i] = inv_at(r, i, 0) * b[0] + (inv_at(r, i, 1) * b[1] + inv_at(r, i, 2) * b[2]);
+                x[i] = __builtin_fma(inv_at(r, i, 0), b[0],
+                                     __builtin_fma(inv_at(r, i, 2), b[2], inv_at(r, i, 1) * b[1]));
             else
-                x[i] = inv_at(r, i, 0) * b[0] + inv_at(r, i, 1) * b[1];
+                x[i] = __builtin_fma(inv_at(r, i, 0), b[0], inv_at(r, i, 1) * b[1]);
         });
     }
 
