@@ -95,6 +95,34 @@ __global__ void cp_init_kernel(CpStatic m, int32_t n_items, const CpInitItem* it
     const double* sob = m.sobol + (size_t)it.sobol_ix * m.sobol_dims;
     for (int k = 0; k < m.sobol_dims && k < DMAX; k++)
         pr[k] = quantile_normal(sob[k], 0.0, 1.0) * exp(cp_ref(m.scales[k], v, m.transforms, 0.0));
+    // full gaussian groups (VariabilityDescription.cpp:69-128): z = QuantileNormal(sobol) and
+    // L(i, j) = exp(scale_i) * prod_{k < i, k <= j} (k == j ? cos : sin)(cov(k, i) * pi), j <= i; the
+    // vector is L z (Eigen's MatrixXd * VectorXd, summed over j in order)
+    const bcm3hip_value_ref* cov = m.covariance;
+    for (int g = 0; g < m.n_full; g++) {
+        const int g0 = m.full_groups[2 * g], D = m.full_groups[2 * g + 1];
+        double z[DMAX];
+        for (int i = 0; i < D; i++) z[i] = quantile_normal(sob[g0 + i], 0.0, 1.0);
+        for (int i = 0; i < D; i++) {
+            const double exp_scale = exp(cp_ref(m.scales[g0 + i], v, m.transforms, 0.0));
+            double acc = 0.0;
+            for (int j = 0; j < D; j++) {
+                double lij = 0.0;
+                if (j <= i) {
+                    lij = exp_scale;
+                    for (int k = 0; k < i; k++) {
+                        if (k <= j) {
+                            const double cv = cp_ref(cov[(i - 1) * i / 2 + k], v, m.transforms, 0.0) * M_PI;
+                            lij *= (k == j) ? cos(cv) : sin(cv);
+                        }
+                    }
+                }
+                acc = (j == 0) ? lij * z[0] : acc + lij * z[j];
+            }
+            pr[g0 + i] = acc;
+        }
+        cov += D * (D - 1) / 2;
+    }
     for (int a = 0; a < m.n_actions; a++) {
         const bcm3hip_variability_action act = m.actions[a];
         if (act.only_initial_cells && !it.is_initial) continue;

@@ -22,6 +22,9 @@ struct CpStatic {
     const bcm3hip_value_ref* scales;
     int32_t n_actions;
     const bcm3hip_variability_action* actions;
+    int32_t n_full;
+    const int32_t* full_groups;          // [n_full][2] first dimension, D
+    const bcm3hip_value_ref* covariance;  // D(D-1)/2 per full group
     const double* output_times;
     int32_t n_data;
     const bcm3hip_cellpop_data* data;  // device copy; observed / entry point to device arrays

@@ -239,8 +239,9 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
     }
     // cell variabilities (VariabilityDescription::Load, VariabilityDescriptionVariable::Load)
     for (const XmlNode* cv : ex.children_named("cell_variability")) {
-        if (cv->get("distribution") != "diagonal_gaussian") {
-            LOGERROR("cell_population: only diagonal_gaussian cell variability is supported");
+        const std::string dist = cv->get("distribution");
+        if (dist != "diagonal_gaussian" && dist != "full_gaussian") {
+            LOGERROR("Unknown distribution \"%s\" in variability description", dist.c_str());
             return false;
         }
         std::vector<VarVariable> vv;
@@ -272,6 +273,23 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
             vv.push_back(x);
         }
         variabilities.push_back(vv);
+        std::vector<bcm3hip_value_ref> cov;
+        if (dist == "full_gaussian") {
+            // the covariance references covar_base_name + (j + 1) + "_" + (i + 1), j < i, resolved in
+            // PostInitialize as a sampled variable or a number (ValueReference::Load)
+            const std::string base_name = cv->get("covar_base_name");
+            for (size_t i = 0; i < vv.size(); i++)
+                for (size_t j = 0; j < i; j++) {
+                    bcm3hip_value_ref r{};
+                    if (!ParseRef(base_name + std::to_string(j + 1) + "_" + std::to_string(i + 1), r)) {
+                        LOGERROR("Missing parameter for covariance");
+                        return false;
+                    }
+                    cov.push_back(r);
+                }
+        }
+        variability_full.push_back(dist == "full_gaussian" ? 1 : 0);
+        variability_cov.push_back(cov);
     }
     if (!ParseRef(ex.get("entry_time"), entry_time)) return false;
 
@@ -800,8 +818,16 @@ bool LikelihoodCellPopulation::PostInitialize()
     // variabilities: Sobol table, per-dimension scales, application list in Cell::Initialize order
     scales.clear();
     actions.clear();
+    full_groups.clear();
+    covariance.clear();
     int dim0 = 0;
-    for (const auto& vv : variabilities) {
+    for (size_t g = 0; g < variabilities.size(); g++) {
+        const auto& vv = variabilities[g];
+        if (variability_full[g]) {
+            full_groups.push_back(dim0);
+            full_groups.push_back((int32_t)vv.size());
+            covariance.insert(covariance.end(), variability_cov[g].begin(), variability_cov[g].end());
+        }
         for (size_t k = 0; k < vv.size(); k++) {
             if (vv[k].entry_time) {
                 LOGERROR("cell_population: entry_time variability is not supported");
@@ -898,6 +924,9 @@ bool LikelihoodCellPopulation::PostInitialize()
     model.scales = scales.data();
     model.n_actions = (int32_t)actions.size();
     model.actions = actions.data();
+    model.n_full = (int32_t)(full_groups.size() / 2);
+    model.full_groups = full_groups.data();
+    model.covariance = covariance.data();
     model.n_data = (int32_t)data_flat.size();
     model.data = data_flat.data();
     model.n_treat = (int32_t)treat_species.size();

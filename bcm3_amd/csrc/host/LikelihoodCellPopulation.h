@@ -83,6 +83,12 @@ private:
         bcm3hip_value_ref scale{};
     };
     std::vector<std::vector<VarVariable>> variabilities;
+    // per variability: full_gaussian (VariabilityDescription.cpp:184-212) and its covariance references
+    // b<j+1>_<i+1>, j < i, in the reference's order
+    std::vector<int> variability_full;
+    std::vector<std::vector<bcm3hip_value_ref>> variability_cov;
+    std::vector<int32_t> full_groups;
+    std::vector<bcm3hip_value_ref> covariance;
     std::vector<DataLikelihood> data;
 
     // flat device model and its arrays

@@ -284,6 +284,14 @@ typedef struct {
     const int32_t* treat_species;  /* [n_treat] constant-species index */
     const int32_t* treat_offset;   /* [n_treat + 1] */
     const double* treat_times;     /* [treat_offset[n_treat]] */
+    /* <cell_variability distribution="full_gaussian" covar_base_name="b"> (VariabilityDescription.cpp:
+     * 69-128, 184-212): the group's pseudorandom vector is L z, z_i = QuantileNormal(sobol_i) and L the
+     * spherical (Pinheiro & Bates) Cholesky factor from exp(scale_i) and the references b<j+1>_<i+1>
+     * (j < i) times pi; diagonal_gaussian groups (the rest) use z_i exp(scale_i). n_full = 0: none. */
+    int32_t n_full;
+    const int32_t* full_groups;          /* [n_full][2]: first sobol dimension, D */
+    const bcm3hip_value_ref* covariance; /* the full groups' D(D-1)/2 references each, in order, entry
+                                            (i-1)i/2 + k of a group for the pair (k, i), k < i */
 } bcm3hip_cellpop_model;
 
 /* Per-cell results of the last evaluation (bcm3hip_cellpop_cells), one record per cell slot. */

@@ -204,10 +204,10 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
         assert ci is not None, tt.get("species_name")
         treats.append((ci, sorted(float(x) for x in tt.get("times").split(","))))
     e["treatments"] = treats
-    # variabilities (VariabilityDescription::Load; diagonal_gaussian)
-    vds = []
+    # variabilities (VariabilityDescription::Load, VariabilityDescription.cpp:170-212)
+    vds, vfull = [], []
     for cv in ex.iter("cell_variability"):
-        assert cv.get("distribution") == "diagonal_gaussian"
+        assert cv.get("distribution") in ("diagonal_gaussian", "full_gaussian"), cv.get("distribution")
         vv = []
         for v in cv.iter("variable"):
             entry_time = v.get("entry_time", "") != ""
@@ -216,7 +216,13 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
                            negate=_bool(v.get("negate"), False),
                            only_initial=_bool(v.get("only_initial_cells"), entry_time)))
         vds.append(vv)
+        cov = None
+        if cv.get("distribution") == "full_gaussian":
+            b = cv.get("covar_base_name")
+            cov = [_ref_value(f"{b}{j + 1}_{i + 1}", variables) for i in range(len(vv)) for j in range(i)]
+        vfull.append(cov)
     e["variabilities"] = vds
+    e["variability_cov"] = vfull
     # data file (JSON sidecar with the netCDF group's variables)
     with open(os.path.join(base, ex.get("data_file"))) as f:
         data = json.load(f)[e["name"]]
@@ -458,13 +464,37 @@ def _cell_init(e, prob, tv, y, sobol_ix, is_initial):
     params = np.array(tv, dtype=float)
     y = np.array(y, dtype=float)
     k = 0
-    for vv in e["variabilities"]:
-        # VariabilityDescription::GetPseudorandomVector (diagonal)
-        pr = []
-        for v in vv:
-            scale = _refval(v["scale"], tv)
-            pr.append(quantile_normal(e["sobol"][sobol_ix, k]) * math.exp(scale))
-            k += 1
+    for g, vv in enumerate(e["variabilities"]):
+        cov = e.get("variability_cov", [None] * len(e["variabilities"]))[g]
+        if cov is None:
+            # VariabilityDescription::GetPseudorandomVector (diagonal, VariabilityDescription.cpp:58-67)
+            pr = []
+            for v in vv:
+                scale = _refval(v["scale"], tv)
+                pr.append(quantile_normal(e["sobol"][sobol_ix, k]) * math.exp(scale))
+                k += 1
+        else:
+            # full gaussian (:69-128): spherical Cholesky factor L from exp(scale_i) and cov(k, i) * pi,
+            # then L z with z = QuantileNormal(sobol), summed over j in order
+            D = len(vv)
+            L = [[0.0] * D for _ in range(D)]
+            for i in range(D):
+                exp_scale = math.exp(_refval(vv[i]["scale"], tv))
+                for j in range(i + 1):
+                    x = exp_scale
+                    for kk in range(i):
+                        if kk <= j:
+                            cvv = _refval(cov[(i - 1) * i // 2 + kk], tv) * math.pi
+                            x *= math.cos(cvv) if kk == j else math.sin(cvv)
+                    L[i][j] = x
+            z = [quantile_normal(e["sobol"][sobol_ix, k + i]) for i in range(D)]
+            pr = []
+            for i in range(D):
+                acc = L[i][0] * z[0]
+                for j in range(1, D):
+                    acc = acc + L[i][j] * z[j]
+                pr.append(acc)
+            k += D
         for i, name in enumerate(prob["variables"]):
             for v, r in zip(vv, pr):
                 if v["parameter"] and v["parameter"] == name and (not v["only_initial"] or is_initial):

@@ -35,3 +35,35 @@ def draws(n, seed):
     x = lo + rng.random((n, len(F.PRIOR))) * (hi - lo)
     x[0] = F.true_values()
     return x
+
+
+# full_gaussian cell variability (VariabilityDescription.cpp:69-128, 184-212): the two variability
+# dimensions correlated through the sampled variable rho1_2 (covar_base_name="rho")
+FULL_GAUSSIAN = ('<cell_variability distribution="diagonal_gaussian">',
+                 '<cell_variability distribution="full_gaussian" covar_base_name="rho">')
+RHO = ("rho1_2", -0.45, 0.45)
+
+
+def write_full_gaussian(directory, num_cells, max_cells, covar_base_name="rho"):
+    """(likelihood, prior) paths: the C4 model with a full_gaussian variability and rho1_2 appended
+    to the prior"""
+    path = write_likelihood(directory, num_cells, max_cells, name="cellpop_full_likelihood.xml")
+    text = open(path).read().replace(FULL_GAUSSIAN[0], FULL_GAUSSIAN[1].replace('"rho"', f'"{covar_base_name}"'))
+    with open(path, "w") as f:
+        f.write(text)
+    prior = os.path.join(str(directory), "cellpop_full_prior.xml")
+    rows = open(PRIOR).read().replace("</variableset>",
+                                      f'  <variable name="{RHO[0]}" distribution="uniform" lower="{RHO[1]}" '
+                                      f'upper="{RHO[2]}"/>\n</variableset>')
+    with open(prior, "w") as f:
+        f.write(rows)
+    return path, prior
+
+
+def draws_full(n, seed):
+    """draws() with rho1_2 appended (the first draw: the true parameters and rho = 0.3)"""
+    x = draws(n, seed)
+    rng = np.random.default_rng(seed + 1)
+    rho = RHO[1] + rng.random(n) * (RHO[2] - RHO[1])
+    rho[0] = 0.3
+    return np.concatenate([x, rho[:, None]], axis=1)

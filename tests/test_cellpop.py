@@ -97,12 +97,48 @@ def test_sobol_sequence_matches_restatement():
         assert np.array_equal(np.sort(np.concatenate([[0.0], p[:, d]])), np.arange(256) / 256.0)
 
 
-def test_unsupported_options_fail_loudly(tmp_path):
+def test_unsupported_options_fail_loudly(tmp_path, capfd):
     path = CH.write_likelihood(tmp_path, 4, 64)
-    text = open(path).read().replace('distribution="diagonal_gaussian"', 'distribution="full_gaussian"')
-    (tmp_path / "bad.xml").write_text(text)
+    text = open(path).read()
+    # VariabilityDescription::Load (VariabilityDescription.cpp:184-212): an unknown distribution, and
+    # full_gaussian without covar_base_name, fail to load
+    for bad, msg in ((text.replace('"diagonal_gaussian"', '"lognormal"'), 'Unknown distribution "lognormal"'),
+                     (text.replace('"diagonal_gaussian"', '"full_gaussian"'), "covar_base_name")):
+        (tmp_path / "bad.xml").write_text(bad)
+        with pytest.raises(RuntimeError):
+            _lik(str(tmp_path / "bad.xml"))
+        assert msg in capfd.readouterr().err
+
+
+def test_full_gaussian_variability_loads(tmp_path, capfd):
+    lik, prior = CH.write_full_gaussian(tmp_path, 4, 64)
+    _lik(lik, prior).close()
+    e = CP.load_problem(lik, prior)["experiments"][0]
+    assert e["variability_cov"] == [[("var", 7)]]
+    # the covariance references must be sampled variables or numbers (ValueReference::Load;
+    # "Missing parameter for covariance", VariabilityDescription.cpp:40-44)
+    lik2, _ = CH.write_full_gaussian(tmp_path, 4, 64, covar_base_name="corr")
     with pytest.raises(RuntimeError):
-        _lik(str(tmp_path / "bad.xml"))
+        _lik(lik2, prior)
+    assert "Missing parameter for covariance" in capfd.readouterr().err
+
+
+def test_oracle_full_gaussian_factor():
+    """the oracle's spherical Cholesky factor (VariabilityDescription.cpp:99-118) for D = 2 applied
+    additively to two parameters: L = [[e^s0, 0], [e^s1 cos(pi rho), e^s1 sin(pi rho)]], vector L z"""
+    import math
+
+    class Model:
+        ode, species = [], []
+    vv = [dict(scale=("fixed", 0.1), parameter="a", species="", apply="additive", negate=False, only_initial=False),
+          dict(scale=("fixed", -0.2), parameter="b", species="", apply="additive", negate=False, only_initial=False)]
+    e = {"variabilities": [vv], "variability_cov": [[("fixed", 0.25)]], "sobol": np.array([[0.8, 0.3]]),
+         "model": Model}
+    params, _ = CP._cell_init(e, {"variables": ["a", "b"]}, [0.0, 0.0], [], 0, True)
+    z0, z1 = CP.quantile_normal(0.8), CP.quantile_normal(0.3)
+    c, sn = math.cos(0.25 * math.pi), math.sin(0.25 * math.pi)
+    want = [math.exp(0.1) * z0, math.exp(-0.2) * c * z0 + math.exp(-0.2) * sn * z1]
+    assert np.allclose(params, want, rtol=1e-14)
 
 
 @pytest.fixture(scope="module")

@@ -24,6 +24,7 @@ import pytest
 
 import cellpop_helpers as CH
 import cellpop as CP
+import parity
 
 pytestmark = pytest.mark.gpu
 
@@ -173,6 +174,53 @@ def test_bench_size_batch_matches_oracle(tmp_path):
     for i in (17, 40, 63):
         one, _ = ll.evaluate_batch(x[i:i + 1])
         assert one[0] == lp[i] or (math.isnan(one[0]) and math.isnan(lp[i]))
+    ll.close()
+
+
+def test_full_gaussian_variability_matches_oracle(tmp_path):
+    """<cell_variability distribution="full_gaussian" covar_base_name="rho">: the two variability
+    dimensions correlated through the sampled rho1_2 (VariabilityDescription.cpp:69-128); the cells'
+    parameters / initial conditions and the logp against the reference-CVODE oracle with the same
+    envelope as the diagonal cases"""
+    from bcm3_amd.likelihood import Likelihood
+    lik, prior = CH.write_full_gaussian(tmp_path, 8, 64)
+    x = CH.draws_full(8, 17)
+    ll = Likelihood(lik, prior, device=0)
+    ref = CP.simulate(CP.load_problem(lik, prior), x)
+    ref_nofma = CP.simulate(CP.load_problem(lik, prior, variant="nofma"), x)
+    lp, status = ll.evaluate_batch(x)
+    # the correlation changes the cells: the same draws with rho = 0 give other logp
+    x0 = x.copy()
+    x0[:, -1] = 0.0
+    lp0, _ = ll.evaluate_batch(x0)
+    fin = np.isfinite(lp) & np.isfinite(lp0)
+    assert fin.any() and np.any(lp[fin] != lp0[fin])
+    dev, spread = [], []
+    for i in range(len(x)):
+        r = ref["logp"][i]
+        if r == -math.inf:
+            assert lp[i] == -math.inf and status[i] == 1, i
+            continue
+        tol = max(2e-4 * (1.0 + abs(r)), 3.0 * abs(ref_nofma["logp"][i] - r))
+        assert abs(lp[i] - r) <= tol, (i, lp[i], r, ref_nofma["logp"][i])
+        dev.append(abs(lp[i] - r) / (1.0 + abs(r)))
+        spread.append(abs(ref_nofma["logp"][i] - r) / (1.0 + abs(r)))
+    assert dev and np.median(dev) <= 10.0 * np.median(spread) + 1e-12, (np.median(dev), np.median(spread))
+    # every cell's creation time and division decision as the oracle's
+    e = CP.load_problem(lik, prior)["experiments"][0]
+    M, NS = len(e["output_times"]), len(e["model"].ode)
+    ll.evaluate_batch(x)
+    for i in range(len(x)):
+        if not ref["detail"][i]["ok"]:
+            continue
+        rec, _, _ = ll.cellpop_cells(i, M, NS)
+        cells = ref["detail"][i]["cells"]
+        assert len(rec) == len(cells), i
+        for k, c in enumerate(cells):
+            assert bool(rec["flags"][k] & 2) == c["divided"], (i, k)
+            assert abs(rec["creation"][k] - c["creation"]) <= 0.1, (i, k)
+    parity.log_summary({"logp_dev_median": float(np.median(dev)), "ref_fma_spread_median": float(np.median(spread))},
+                       n=len(dev))
     ll.close()
 
 
