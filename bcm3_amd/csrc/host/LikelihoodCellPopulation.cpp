@@ -828,13 +828,11 @@ bool LikelihoodCellPopulation::PostInitialize()
             full_groups.push_back((int32_t)vv.size());
             covariance.insert(covariance.end(), variability_cov[g].begin(), variability_cov[g].end());
         }
-        for (size_t k = 0; k < vv.size(); k++) {
-            if (vv[k].entry_time) {
-                LOGERROR("cell_population: entry_time variability is not supported");
-                return false;
-            }
-            scales.push_back(vv[k].scale);
-        }
+        // an entry_time variable takes its dimension of the pseudorandom vector (GetPseudorandomVector
+        // covers every variable) but changes nothing: the reference never calls
+        // ApplyVariabilityEntryTime (VariabilityDescriptionVariable.cpp:66-78; Cell::Initialize,
+        // Cell.cpp:150-176, applies parameters and initial conditions only), so it gets no action
+        for (size_t k = 0; k < vv.size(); k++) scales.push_back(vv[k].scale);
         for (size_t i = 0; i < varset->GetNumVariables(); i++)
             for (size_t k = 0; k < vv.size(); k++)
                 if (!vv[k].parameter.empty() && vv[k].parameter == varset->GetVariableName(i))

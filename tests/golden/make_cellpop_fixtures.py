@@ -163,7 +163,8 @@ def prior_text():
 
 
 def likelihood_text(num_cells=500, max_cells=2048, data_file="cellpop_data.json", model_file="cellpop_model.xml",
-                    data_attrs='stdev="stdev"', experiment_attrs="", extra="", data_xml=None, entry_time="0"):
+                    data_attrs='stdev="stdev"', experiment_attrs="", extra="", data_xml=None, entry_time="0",
+                    variability_extra=""):
     """extra: further children of the <experiment> (e.g. a <treatment_trajectory>); data_xml: the
     <data> element(s) in place of the population average"""
     if data_xml is None:
@@ -172,7 +173,7 @@ def likelihood_text(num_cells=500, max_cells=2048, data_file="cellpop_data.json"
   <experiment name="exp1" model_file="{model_file}" data_file="{data_file}" num_cells="{num_cells}" max_cells="{max_cells}" entry_time="{entry_time}"{experiment_attrs}>
     <cell_variability distribution="diagonal_gaussian">
       <variable model_parameter="k_D" apply="multiplicative_log" scale="var_kD"/>
-      <variable initial_condition_species="CycD" apply="multiplicative_log" scale="var_CycD0"/>
+      <variable initial_condition_species="CycD" apply="multiplicative_log" scale="var_CycD0"/>{variability_extra}
     </cell_variability>
     {data_xml}{extra}
   </experiment>

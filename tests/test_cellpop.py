@@ -270,3 +270,16 @@ def test_oracle_runs_treatment_trajectory(tmp_path):
         first_t = min(c["sim_end"] for c in ct[:4] if c["divided"]) if any(c["divided"] for c in ct[:4]) else 1e9
         first_p = min(c["sim_end"] for c in cp[:4] if c["divided"]) if any(c["divided"] for c in cp[:4]) else 1e9
         assert first_t > first_p, (i, first_t, first_p)
+
+
+def test_entry_time_variability_takes_a_dimension(tmp_path):
+    """<variable entry_time="true" ...> loads, gets a column of the Sobol table and no target
+    (VariabilityDescriptionVariable.cpp:66-78 is never called by the reference)"""
+    import make_cellpop_fixtures as F
+    path = tmp_path / "lik.xml"
+    path.write_text(F.likelihood_text(num_cells=4, max_cells=64, data_file=os.path.join(CH.GOLDEN, "cellpop_data.json"),
+                                      model_file=os.path.join(CH.GOLDEN, "cellpop_model.xml"),
+                                      variability_extra='<variable entry_time="true" apply="additive" scale="var_kD"/>'))
+    _lik(str(path)).close()
+    e = CP.load_problem(str(path), CH.PRIOR)["experiments"][0]
+    assert e["sobol"].shape[1] == 3 and e["variabilities"][0][2]["entry_time"]

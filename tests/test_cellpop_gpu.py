@@ -44,11 +44,14 @@ CASES = [(6, 64, 12, {}), (40, 256, 4, {}),
          (8, 64, 6, dict(extra=TREAT)),
          # overlapping pulses: the next corner the reference's NextDiscontinuity gives after a pulse
          # end can lie behind the cell's time; CVode then refuses the stop time and the cell fails
-         (6, 64, 4, dict(extra=TREAT.replace('"13,-1"', '"6,-1,13"')))]
+         (6, 64, 4, dict(extra=TREAT.replace('"13,-1"', '"6,-1,13"'))),
+         # an entry_time variability variable: it takes a sobol dimension of the group (the table gets
+         # three) and is never applied (the reference has no ApplyVariabilityEntryTime call)
+         (6, 64, 6, dict(variability_extra='\n      <variable entry_time="true" apply="additive" scale="var_kD"/>'))]
 
 
 @pytest.fixture(scope="module", params=CASES, ids=["6cells", "40cells", "addprop", "t4_nodiv", "reltime", "pulses",
-                                                           "pulses_overlap"])
+                                                           "pulses_overlap", "entry_time_var"])
 def setup(request, tmp_path_factory):
     from bcm3_amd.likelihood import Likelihood
     nc, mc, nd, attrs = request.param
