@@ -1119,7 +1119,10 @@ bool ParseMatrixFromString(const std::string& str, std::vector<std::vector<Real>
 {
     const std::vector<std::string> rows = tokenize_keep_empty(str, ';');
     m.clear();
-    if (rows.empty()) return false;  // the reference reads rows[0] of an empty list
+    if (rows.empty()) {  // the reference reads rows[0] of an empty list
+        LOGERROR("Empty matrix");
+        return false;
+    }
     const size_t cols = tokenize_keep_empty(rows[0], ',').size();
     for (const std::string& r : rows) {
         const std::vector<std::string> row = tokenize_keep_empty(r, ',');
