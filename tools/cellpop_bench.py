@@ -37,4 +37,6 @@ cells = sum(len(ll.cellpop_cells(i, 21, 15)[0]) for i in range(n))
 steps = sum(int(ll.cellpop_cells(i, 21, 15)[0]["nsteps"].sum()) for i in range(n))
 print(f"n={n}: {dt * 1e3:.2f} ms per batch, {n / dt:.1f} evals/s, {cells / n:.0f} cells/eval, "
       f"{steps / cells:.0f} steps/cell, finite logp {int(torch.isfinite(out).sum())}/{n}", flush=True)
+fin = torch.isfinite(out)
+print(f"logp checksum {float(out[fin].sum()):.17g}", flush=True)
 ll.close()
