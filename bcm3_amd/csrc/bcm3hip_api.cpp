@@ -32,7 +32,9 @@ hipError_t launch_cp_accumulate(int32_t n, double* logp, int32_t* status, const 
 hipError_t launch_cp_assign(int32_t n_problems, int32_t R, int32_t nsim, const double* lik, unsigned char* ws_global,
                             size_t ws_stride, int32_t* match, double* sum, int32_t* ok, hipStream_t s);
 size_t cp_assign_ws_bytes(int n);
-inline bool cp_assign_lds_fits(int n) { return cp_assign_ws_bytes(n) <= 56 * 1024; }
+// the dynamic workspace plus the larger kernel's static LDS (cp_timepoints_kernel, ~8.4 KB) stay within
+// 64 KB, the workgroup limit of parts smaller than gfx950's 160 KB
+inline bool cp_assign_lds_fits(int n) { return cp_assign_ws_bytes(n) <= 52 * 1024; }
 }  // namespace bcm3hip
 
 struct bcm3hip_ctx {

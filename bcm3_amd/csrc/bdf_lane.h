@@ -29,6 +29,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "libm_exact.h"
+
 namespace bcm3hip {
 
 constexpr int QMAX = 5;
@@ -253,6 +255,34 @@ BDF_INL double eta_from(double bx, int k)
     return fdiv(z, __builtin_fma(ADDON, z, 1.0));
 }
 
+// The PopPK solvers (bdf_lane.h cvode_one_step, bdf_uni.h, bdf_vec.h) compute every quantity
+// of the step with the reference's own operations: the products and sums of its C statements
+// in their order (no contraction: the reference is compared against its build without FMA
+// contraction, oracle/_ref/libbcm3ref_nofma.so, which the C restatement matches bit for bit),
+// IEEE quotients and square roots (frcp / fdiv / fsqrt above, correctly rounded), and libm's
+// pow through xm::pow_inv_k (libm_exact.h). The cell-population solver keeps eta_from.
+
+// eta = ONE / (SUNRpowerR(bx, ONE / k) + ADDON) (cvode.c:2986, 3105, 3163, 3187): the rounded
+// exponent fl(1/k) as the reference passes it, the correctly rounded pow, the IEEE quotient
+BDF_INL double eta_exact(double bx, int k)
+{
+    double p;
+    if (bx > 1e-30 && bx < 1e30)
+        p = xm::pow_inv_k(bx, k);
+    else
+        p = (bx > 0.0) ? pow(bx, xm::inv_k(k)) : 0.0;
+    return frcp(p + ADDON);
+}
+
+// cvNlsConvTest (cvode_nls.c:262-263): dcon = del * min(1, crate) / tol, converged when dcon <= 1,
+// tol = tq[4] = CORTES / tq[2]. RN(a / b) <= 1 iff a <= b (1 + 2^-53) (the midpoint 1 + 2^-53
+// rounds to even, i.e. to 1), decided without the division: for b < a <= 2b the difference a - b
+// is exact (Sterbenz). a >= 0 or NaN (false), b > 0.
+BDF_INL bool div_le_one(double a, double b)
+{
+    return (a <= b) | ((a <= 2.0 * b) & ((a - b) <= b * 0x1p-53));
+}
+
 // SUNRpowerI for exponent 1..7 (repeated multiplication, sundials_math.c:28-38)
 BDF_INL double powI(double base, int e)
 {
@@ -356,7 +386,7 @@ BDF_INL double wrms(const double (&x)[NS], const double (&w)[NS])
 template <int NS, class S>
 BDF_INL void ewt_set(const S& s, const double (&ycur)[NS], double (&w)[NS])
 {
-    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { w[CI(i)] = frcp(__builtin_fma(s.rtol, fabs(ycur[CI(i)]), s.atol)); });
+    cfor<0, NS>([&](auto i) __attribute__((always_inline)) { w[CI(i)] = frcp(s.rtol * fabs(ycur[CI(i)]) + s.atol); });
 }
 
 // cvRescale (cvode.c:2393-2406): zn[j] *= eta^j, j = 1..q
@@ -423,7 +453,7 @@ BDF_INL double set_bdf(S& s)
                 hsum += s.tau[CI(j) - 1];
                 xi_inv = fdiv(s.h, hsum);
                 alpha0 -= 1.0 / CI(j);
-                cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xi_inv, s.l[CI(i)]); });
+                cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = s.l[CI(i)] + s.l[CI(i) - 1] * xi_inv; });
             }
         });
         alpha0 -= recip_int(q);
@@ -432,12 +462,12 @@ BDF_INL double set_bdf(S& s)
         xi_inv = fdiv(s.h, hsum);
         alpha0_hat = -s.l[1] - xi_inv;
         cfor_down<QMAX, 1>([&](auto i) __attribute__((always_inline)) {
-            if (CI(i) <= q) s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xistar_inv, s.l[CI(i)]);
+            if (CI(i) <= q) s.l[CI(i)] = s.l[CI(i)] + s.l[CI(i) - 1] * xistar_inv;
         });
     }
     // cvSetTqBDF
     const double A1 = 1.0 - alpha0_hat + alpha0;
-    const double A2 = __builtin_fma((double)q, A1, 1.0);
+    const double A2 = 1.0 + (double)q * A1;
     const double lq = sel(s.l, q);
     s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
     s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
@@ -458,7 +488,7 @@ BDF_INL double set_bdf(S& s)
         const double Cppinv = fdiv(1.0 - A6 + A5, A2);
         s.tq[3] = fabs(fdiv(Cppinv, xi_inv * (double)(q + 2) * A5));
     }
-    // tq[4] = CORTES / tq[2] is used only as the Newton tolerance, folded into the test there
+    s.tq[4] = fdiv(CORTES, s.tq[2]);
     // cvSet
     const double rl1 = frcp(s.l[1]);
     s.gamma = s.h * rl1;
@@ -485,7 +515,7 @@ BDF_INL void increase_bdf(S& s)
             prod *= xi;
             alpha0 -= 1.0 / (CI(j) + 1);
             alpha1 += frcp(xi);
-            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xiold, l[CI(i) - 1]); });
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = l[CI(i)] * xiold + l[CI(i) - 1]; });
             xiold = xi;
         }
     });
@@ -497,7 +527,7 @@ BDF_INL void increase_bdf(S& s)
         if (CI(j) == s.q + 1) {
             cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = znL[CI(i)]; });
         } else if (CI(j) <= s.q) {
-            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = __builtin_fma(l[CI(j)], znL[CI(i)], s.zn[CI(j)][CI(i)]); });
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = s.zn[CI(j)][CI(i)] + l[CI(j)] * znL[CI(i)]; });
         }
     });
     cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
@@ -515,14 +545,14 @@ BDF_INL void decrease_bdf(S& s)
         if (CI(j) <= s.q - 2) {
             hsum += s.tau[CI(j)];
             const double xi = fdiv(hsum, s.hscale);
-            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xi, l[CI(i) - 1]); });
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = l[CI(i)] * xi + l[CI(i) - 1]; });
         }
     });
     double znq[NS];
     sel_row<NS>(s.zn, s.q, znq);
     cfor<2, QMAX>([&](auto j) __attribute__((always_inline)) {
         if (CI(j) < s.q) {
-            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = __builtin_fma(-l[CI(j)], znq[CI(i)], s.zn[CI(j)][CI(i)]); });
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = s.zn[CI(j)][CI(i)] + (-l[CI(j)]) * znq[CI(i)]; });
         }
     });
     cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
@@ -539,7 +569,8 @@ BDF_INL void adjust_order(S& s, int deltaq)
         decrease_bdf<NS>(s);
 }
 
-// CVodeGetDky(t, k = 0) (cvode.c:1467-1533): z = sum_{j=q..0} s^j zn[j]
+// CVodeGetDky(t, k = 0) (cvode.c:1467-1533): z = sum_{j=q..0} s^j zn[j], the first term a product
+// (N_VLinearCombination / N_VLinearSum of the Eigen N_Vector, nvector_serial_eigen.cpp)
 template <int NS, class S>
 BDF_INL int get_dky(const S& s, double t, double (&dky)[NS])
 {
@@ -554,8 +585,10 @@ BDF_INL int get_dky(const S& s, double t, double (&dky)[NS])
     cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { c[CI(j)] = c[CI(j) - 1] * sv; });
     cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] = 0.0; });
     cfor_down<QMAX, 0>([&](auto j) __attribute__((always_inline)) {
-        if (CI(j) <= s.q) {
-            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] = __builtin_fma(c[CI(j)], s.zn[CI(j)][CI(i)], dky[CI(i)]); });
+        if (CI(j) == s.q) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] = c[CI(j)] * s.zn[CI(j)][CI(i)]; });
+        } else if (CI(j) < s.q) {
+            cfor<0, NS>([&](auto i) __attribute__((always_inline)) { dky[CI(i)] = dky[CI(i)] + c[CI(j)] * s.zn[CI(j)][CI(i)]; });
         }
     });
     return CV_SUCCESS;
@@ -601,8 +634,8 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
         s.cnt.nfe++;
         cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
             constexpr int i = CI(I_);
-            delta[i] = __builtin_fma(rl1, s.zn[1][i], s.acor[i]);
-            delta[i] = __builtin_fma(-s.gamma, f[i], delta[i]);
+            delta[i] = rl1 * s.zn[1][i] + s.acor[i];
+            delta[i] = delta[i] + (-s.gamma) * f[i];
         });
         if (callSetup) {
             // cvNlsLSetup -> cvLsSetup (cvode_ls.c:1415-1500)
@@ -647,8 +680,8 @@ BDF_INL bool newton(S& s, const Model& mdl, double rl1, int convfail, bool callS
         // cvNlsConvTest (cvode_nls.c:236-280)
         const double del = wrms<NS>(x, s.ewt);
         if (curiter > 0) s.crate = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
-        // cvNlsConvTest: dcon = del min(1, crate) / tol <= 1 with tol = CORTES / tq[2]
-        if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
+        // cvNlsConvTest: dcon = del min(1, crate) / tq[4] <= 1
+        if (div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4])) {
             s.acnrm = (curiter == 0) ? del : wrms<NS>(s.acor, s.ewt);
             s.nls_jcur = 0;
             return true;
@@ -689,7 +722,7 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
     cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
         constexpr int i = CI(I_);
         double t1 = frcp(s.ewt[i]);  // N_VInv of the error weights
-        t1 = __builtin_fma(HUB_FACTOR, fabs(s.zn[0][i]), t1);
+        t1 = t1 + HUB_FACTOR * fabs(s.zn[0][i]);
         const double r = fdiv(fabs(s.zn[1][i]), t1);
         hub_inv = (i == 0) ? r : ((r > hub_inv) ? r : hub_inv);  // maxCoeff
     });
@@ -708,7 +741,7 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
         double yy[NS], tv[NS];
         cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
             constexpr int i = CI(I_);
-            yy[i] = __builtin_fma(hgs, s.zn[1][i], s.zn[0][i]);
+            yy[i] = hgs * s.zn[1][i] + s.zn[0][i];
         });
         mdl.rhs(s.tn + hgs, yy, tv);
         s.cnt.nfe++;
@@ -862,7 +895,7 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         nflag = PREV_ERR_FAIL;
         if (nef == MXNEF) return CV_ERR_FAILURE;
         if (nef <= MXNEF1) {
-            double eta = eta_from(BIAS2 * dsm, s.L);
+            double eta = eta_exact(BIAS2 * dsm, s.L);
             eta = SUNMAX(ETAMIN, eta);
             if (nef >= SMALL_NEF) eta = SUNMIN(eta, ETAMXF);
             s.eta = eta;
@@ -905,7 +938,7 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         if (j <= s.q) {
             cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
                 constexpr int i = CI(I_);
-                s.zn[j][i] = __builtin_fma(s.l[j], s.acor[i], s.zn[j][i]);
+                s.zn[j][i] = s.zn[j][i] + s.l[j] * s.acor[i];
             });
         }
     });
@@ -926,7 +959,7 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
         s.hprime = s.h;
         s.eta = 1.0;
     } else {
-        const double etaq = eta_from(BIAS2 * dsm, s.L);
+        const double etaq = eta_exact(BIAS2 * dsm, s.L);
         double eta = etaq;
         s.qprime = s.q;
         if (s.qwait == 0) {
@@ -936,7 +969,7 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
             if (s.q > 1) {
                 double znq[NS];
                 sel_row<NS>(s.zn, s.q, znq);
-                xm = BIAS1 * wrms<NS>(znq, s.ewt) * s.tq[1];
+                xm = BIAS1 * (wrms<NS>(znq, s.ewt) * s.tq[1]);
             }
             const bool do_p = (s.q != QMAX) && (s.saved_tq5 != 0.0);
             if (do_p) {
@@ -944,16 +977,16 @@ BDF_INL int cvode_one_step(S& s, const Model& mdl, double tout, double (&yout)[N
                 double tv[NS];
                 cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
                     constexpr int i = CI(I_);
-                    tv[i] = __builtin_fma(-cquot, s.zn[QMAX][i], s.acor[i]);
+                    tv[i] = (-cquot) * s.zn[QMAX][i] + s.acor[i];
                 });
-                xp = BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3];
+                xp = BIAS3 * (wrms<NS>(tv, s.ewt) * s.tq[3]);
             }
             // the two candidate ratios share one root call site
 #pragma unroll 1
             for (int c = 0; c < 2; c++) {
                 const bool act = (c == 0) ? (s.q > 1) : do_p;
                 if (act) {
-                    const double e = eta_from((c == 0) ? xm : xp, (c == 0) ? s.q : s.L + 1);
+                    const double e = eta_exact((c == 0) ? xm : xp, (c == 0) ? s.q : s.L + 1);
                     if (c == 0)
                         etaqm1 = e;
                     else

@@ -76,17 +76,17 @@ BDF_INL double set_bdf_q(S& s)
             hsum += s.tau[CI(j) - 1];
             xi_inv = fdiv(s.h, hsum);
             alpha0 -= 1.0 / CI(j);
-            cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xi_inv, s.l[CI(i)]); });
+            cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = s.l[CI(i)] + s.l[CI(i) - 1] * xi_inv; });
         });
         alpha0 -= 1.0 / q;
         xistar_inv = -s.l[1] - alpha0;
         hsum += s.tau[q - 1];
         xi_inv = fdiv(s.h, hsum);
         alpha0_hat = -s.l[1] - xi_inv;
-        cfor_down<Q, 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xistar_inv, s.l[CI(i)]); });
+        cfor_down<Q, 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = s.l[CI(i)] + s.l[CI(i) - 1] * xistar_inv; });
     }
     const double A1 = 1.0 - alpha0_hat + alpha0;
-    const double A2 = __builtin_fma((double)q, A1, 1.0);
+    const double A2 = 1.0 + (double)q * A1;
     const double lq = s.l[q];
     s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
     // tq[5] unconditionally as cvSetTqBDF does (qwait <= 2, when it is read, holds in almost every
@@ -113,7 +113,7 @@ BDF_INL double set_bdf_q(S& s)
             s.tq[3] = tq3;
         }
     }
-    // tq[4] = CORTES / tq[2] only serves as the Newton tolerance (folded into the test there)
+    s.tq[4] = fdiv(CORTES, s.tq[2]);
     // at q = 2, l[1] = 1.5 is a compile-time constant here but not in the lane solver (runtime q):
     // the compiler would fold v_rcp_f64(1.5) to the correctly rounded value while the hardware
     // estimate (one Newton step, frcp) differs, so the operand is passed through a runtime 1.0
@@ -125,28 +125,17 @@ BDF_INL double set_bdf_q(S& s)
     return rl1;
 }
 
-// eta_from of bdf_lane.h (same operations) with the range check as one scalar branch
+// eta_exact of bdf_lane.h with the range check as one scalar branch
 BDF_INL double eta_from_u(double bx, int k)
 {
-    if (!((bx > 1e-30) & (bx < 1e30))) return frcp((bx > 0.0 ? pow(bx, recip_int(k)) : 0.0) + ADDON);
-    const double rk = recip_int(k);
-    const float lf = __builtin_amdgcn_logf((float)bx);
-    double z = (double)__builtin_amdgcn_exp2f(-lf * (float)rk);
-    cfor<0, 2>([&](auto) __attribute__((always_inline)) {
-        double zk = z;
-        cfor<2, 8>([&](auto I) __attribute__((always_inline)) {
-            if (CI(I) <= k) zk *= z;
-        });
-        const double t = __builtin_fma(-bx, zk, 1.0);
-        z = __builtin_fma(z * t, rk, z);
-    });
-    return fdiv(z, __builtin_fma(ADDON, z, 1.0));
+    if (!((bx > 1e-30) & (bx < 1e30))) return frcp((bx > 0.0 ? pow(bx, xm::inv_k(k)) : 0.0) + ADDON);
+    return frcp(xm::pow_inv_k(bx, k) + ADDON);
 }
 
 // Step-size ratios below THRESH are discarded (cvSetEta: eta = 1), so an eta candidate only has
 // to be computed exactly when it can reach THRESH. eta = 1 / (bx^(1/k) + ADDON) >= THRESH needs
 // bx <= (1/THRESH - ADDON)^k; above that bound (with a 1e-9 relative margin, far wider than the
-// few-ulp error of eta_from) the candidate is replaced by 0, which every later use (the
+// few-ulp error of the seed) the candidate is replaced by 0, which every later use (the
 // THRESH test, the max over candidates and the equality tests of cvChooseEta) treats exactly
 // like the true value < THRESH.
 constexpr double eta_cut(int k)
@@ -178,8 +167,8 @@ BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& csc
     s.cnt.nfe++;
     cfor<0, NS>([&](auto I_) __attribute__((always_inline)) {
         constexpr int i = CI(I_);
-        delta[i] = __builtin_fma(rl1, s.zn[1][i], s.acor[i]);
-        delta[i] = __builtin_fma(-s.gamma, f[i], delta[i]);
+        delta[i] = rl1 * s.zn[1][i] + s.acor[i];
+        delta[i] = delta[i] + (-s.gamma) * f[i];
     });
     if (BDF_UNLIKELY(setup)) {
         // cvNlsLSetup -> cvLsSetup (cvode_ls.c:1415-1500)
@@ -225,8 +214,8 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
     for (;;) {
         // iteration 0 (crate as left by the previous step)
         double del = newton_correction<NS>(s, mdl, rl1, cscale, callSetup, jbad, convfail);
-        // cvNlsConvTest: dcon = del min(1, crate) / tol <= 1 with tol = CORTES / tq[2]
-        if (BDF_LIKELY(del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES)) {
+        // cvNlsConvTest: dcon = del min(1, crate) / tq[4] <= 1
+        if (BDF_LIKELY(div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4]))) {
             s.acnrm = del;
             s.nls_jcur = 0;
             return true;
@@ -236,7 +225,7 @@ BDF_INL bool newton_u(S& s, const Model& mdl, double rl1, int convfail, bool cal
         for (int it = 1; it < NLS_MAXCOR; it++) {
             del = newton_correction<NS>(s, mdl, rl1, cscale, false, false, convfail);
             s.crate = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
-            if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
+            if (div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4])) {
                 s.acnrm = wrms<NS>(s.acor, s.ewt);
                 s.nls_jcur = 0;
                 return true;
@@ -292,7 +281,7 @@ BDF_INL void complete_q(S& s, double dsm)
     if constexpr (q == 1) s.tau[2] = (s.nst > 1) ? s.tau[1] : s.tau[2];
     s.tau[1] = s.h;
     cfor<0, Q + 1>([&](auto j) __attribute__((always_inline)) {
-        cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = __builtin_fma(s.l[CI(j)], s.acor[CI(i)], s.zn[CI(j)][CI(i)]); });
+        cfor<0, NS>([&](auto i) __attribute__((always_inline)) { s.zn[CI(j)][CI(i)] = s.zn[CI(j)][CI(i)] + s.l[CI(j)] * s.acor[CI(i)]; });
     });
     s.qwait--;
     if constexpr (q != QMAX) {
@@ -317,15 +306,15 @@ BDF_INL void complete_q(S& s, double dsm)
             // cvComputeEtaqm1 / cvComputeEtaqp1 / cvChooseEta, every q+1 steps
             s.qwait = 2;
             double etaqm1 = 0.0, etaqp1 = 0.0;
-            if constexpr (q > 1) etaqm1 = eta_candidate<q>(BIAS1 * wrms<NS>(s.zn[q], s.ewt) * s.tq[1]);
+            if constexpr (q > 1) etaqm1 = eta_candidate<q>(BIAS1 * (wrms<NS>(s.zn[q], s.ewt) * s.tq[1]));
             if constexpr (q != QMAX) {
                 if (s.saved_tq5 != 0.0) {
                     const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
                     double tv[NS];
                     cfor<0, NS>([&](auto i) __attribute__((always_inline)) {
-                        tv[CI(i)] = __builtin_fma(-cquot, s.zn[QMAX][CI(i)], s.acor[CI(i)]);
+                        tv[CI(i)] = (-cquot) * s.zn[QMAX][CI(i)] + s.acor[CI(i)];
                     });
-                    etaqp1 = eta_candidate<q + 2>(BIAS3 * wrms<NS>(tv, s.ewt) * s.tq[3]);
+                    etaqp1 = eta_candidate<q + 2>(BIAS3 * (wrms<NS>(tv, s.ewt) * s.tq[3]));
                 }
             }
             const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
@@ -482,7 +471,7 @@ BDF_INL int cvode_one_step_u(S& s, const Model& mdl, double tout, double (&yout)
         nflag = PREV_ERR_FAIL;
         if (nef == MXNEF) return CV_ERR_FAILURE;
         if (nef <= MXNEF1) {
-            double eta = eta_from(BIAS2 * dsm, s.L);
+            double eta = eta_exact(BIAS2 * dsm, s.L);
             eta = SUNMAX(ETAMIN, eta);
             if (nef >= SMALL_NEF) eta = SUNMIN(eta, ETAMXF);
             s.eta = eta;

@@ -5,11 +5,11 @@
 // instruction instead of NS; the scalars of the step (tn, h, l, tq, gamma, eta, counters) stay
 // wave-uniform exactly as in bdf_uni.h and share its code (set_bdf_q, eta_candidate).
 //
-// Cross-lane work is the two small contractions of the linear PK systems and the norms:
-//   * matrix-vector products (RHS  A y, solve  A^-1 b): the column j of the matrix lives in
-//     the lanes (lane i: a(i, j)) and y_j is broadcast to every lane with one DPP row_newbcast
-//     move; the RHS as f = a(:,0) y0 -> fma(a(:,1), y1, f) -> fma(a(:,2), y2, f) (matvec), the
-//     solve as the reference build's contraction of Eigen's p0 + (p1 + p2) (solvevec): the same
+// Cross-lane work is the right-hand side and the solve of the linear PK systems and the norms:
+//   * the right-hand side is the model's (PKLane::rhs_v: each lane evaluates its component's
+//     own expression of the reference, the operands moved in by DPP); the solve A^-1 b has
+//     column j of the inverse in the lanes (lane i: inv(i, j)) and b_j broadcast to every lane
+//     with one DPP row_newbcast move, summed as Eigen's p0 + (p1 + p2) (solvevec): the same
 //     products and order as the scalar model (PKLane::rhs / lin_solve), so the bits agree;
 //   * weighted RMS norms: squares in lanes, the sum ((p0^2 + p1^2) + p2^2) from broadcasts in
 //     component order, made wave-uniform with readfirstlane (wrms of bdf_lane.h sums the same
@@ -80,24 +80,16 @@ BDF_INL double wrms(double x, double w)
     return wave_uniform(fsqrt(fdiv_c(vec::lane_sum_v<NS>(p * p), (double)NS, 1.0 / NS)));
 }
 
-// y = M x for M held as lane columns (lane i of col[j] = m(i, j))
-template <int NS>
-BDF_INL double matvec(const double (&col)[NS], double x)
-{
-    double r = col[0] * bc<0>(x);
-    cfor<1, NS>([&](auto j) __attribute__((always_inline)) { r = __builtin_fma(col[CI(j)], bc<CI(j)>(x), r); });
-    return r;
-}
-
-// x = A^-1 b for the inverse held as lane columns, in PKLane::lin_solve's order: the reference
-// build's fma(c0 b0, c1 b1) (N = 2) and fma(c0 b0, fma(c2 b2, c1 b1)) (N = 3, Eigen's p0 + (p1 + p2))
+// x = A^-1 b for the inverse held as lane columns, in PKLane::lin_solve's order: c0 b0 + c1 b1
+// (N = 2, sunlinsol_dense_eigen.cpp:157-167) and c0 b0 + (c1 b1 + c2 b2) (N = 3, Eigen's unrolled
+// p0 + (p1 + p2), :169-176)
 template <int NS>
 BDF_INL double solvevec(const double (&col)[NS], double x)
 {
     if constexpr (NS == 3)
-        return __builtin_fma(col[0], bc<0>(x), __builtin_fma(col[2], bc<2>(x), col[1] * bc<1>(x)));
+        return col[0] * bc<0>(x) + (col[1] * bc<1>(x) + col[2] * bc<2>(x));
     else
-        return __builtin_fma(col[0], bc<0>(x), col[1] * bc<1>(x));
+        return col[0] * bc<0>(x) + col[1] * bc<1>(x);
 }
 
 // per-trajectory solver statistics only when the caller asked for them: without, the counters
@@ -117,7 +109,8 @@ struct VecState {
     double unity;  // 1.0 the compiler cannot see (see set_bdf_q)
     double zn[QMAX + 1];  // lane i: component i
     double ewt, acor;
-    double acol[NS];  // columns of the RHS matrix A(ka) (constant between ReInits)
+    double acol[4];   // per-lane coefficients of the right-hand side (PKLane::rhs_columns;
+                      // constant between ReInits)
     double icol[NS];  // columns of (I - gamma J)^-1 (lin_setup)
     double tau[QMAX + 2], tq[6], l[QMAX + 1];
     double tn, h, hprime, eta, hscale, hu, tretlast;
@@ -139,7 +132,7 @@ struct VecState {
 template <class S>
 BDF_INL void ewt_set(S& s)
 {
-    s.ewt = frcp(__builtin_fma(s.rtol, fabs(s.zn[0]), s.atol));
+    s.ewt = frcp(s.rtol * fabs(s.zn[0]) + s.atol);
 }
 
 template <int Q, class S>
@@ -191,7 +184,7 @@ BDF_INL void increase_bdf(S& s)
             prod *= xi;
             alpha0 -= 1.0 / (CI(j) + 1);
             alpha1 += frcp(xi);
-            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xiold, l[CI(i) - 1]); });
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = l[CI(i)] * xiold + l[CI(i) - 1]; });
             xiold = xi;
         }
     });
@@ -201,7 +194,7 @@ BDF_INL void increase_bdf(S& s)
         if (CI(j) == s.q + 1)
             s.zn[CI(j)] = znL;
         else if (CI(j) <= s.q)
-            s.zn[CI(j)] = __builtin_fma(l[CI(j)], znL, s.zn[CI(j)]);
+            s.zn[CI(j)] = s.zn[CI(j)] + l[CI(j)] * znL;
     });
     cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
 }
@@ -217,14 +210,14 @@ BDF_INL void decrease_bdf(S& s)
         if (CI(j) <= s.q - 2) {
             hsum += s.tau[CI(j)];
             const double xi = fdiv(hsum, s.hscale);
-            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = __builtin_fma(l[CI(i)], xi, l[CI(i) - 1]); });
+            cfor_down<CI(j) + 2, 2>([&](auto i) __attribute__((always_inline)) { l[CI(i)] = l[CI(i)] * xi + l[CI(i) - 1]; });
         }
     });
     // zn[q] by a select chain starting from a constant (see sel in bdf_lane.h)
     double znq = 0.0;
     cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { znq = (s.q == CI(j)) ? s.zn[CI(j)] : znq; });
     cfor<2, QMAX>([&](auto j) __attribute__((always_inline)) {
-        if (CI(j) < s.q) s.zn[CI(j)] = __builtin_fma(-l[CI(j)], znq, s.zn[CI(j)]);
+        if (CI(j) < s.q) s.zn[CI(j)] = s.zn[CI(j)] + (-l[CI(j)]) * znq;
     });
     cfor<0, QMAX + 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = l[CI(i)]; });
 }
@@ -254,7 +247,10 @@ BDF_INL int get_dky(const S& s, double t, double& dky)
     cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { c[CI(j)] = c[CI(j) - 1] * sv; });
     dky = 0.0;
     cfor_down<QMAX, 0>([&](auto j) __attribute__((always_inline)) {
-        if (CI(j) <= s.q) dky = __builtin_fma(c[CI(j)], s.zn[CI(j)], dky);
+        if (CI(j) == s.q)
+            dky = c[CI(j)] * s.zn[CI(j)];
+        else if (CI(j) < s.q)
+            dky = dky + c[CI(j)] * s.zn[CI(j)];
     });
     return CV_SUCCESS;
 }
@@ -298,7 +294,7 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
     const double hlb = HLB_FACTOR * tround;
     // cvUpperBoundH0: max over components in component order
     double t1 = frcp(s.ewt);
-    t1 = __builtin_fma(HUB_FACTOR, fabs(s.zn[0]), t1);
+    t1 = t1 + HUB_FACTOR * fabs(s.zn[0]);
     const double r = fdiv(fabs(s.zn[1]), t1);
     double hub_inv = bc<0>(r);
     cfor<1, NS>([&](auto i) __attribute__((always_inline)) {
@@ -317,7 +313,7 @@ BDF_INL int hin(S& s, const Model& mdl, double tout)
 #pragma unroll 1
     for (int count1 = 1; count1 <= MAX_ITERS; count1++) {
         const double hgs = hg * sign;
-        const double yy = __builtin_fma(hgs, s.zn[1], s.zn[0]);
+        const double yy = hgs * s.zn[1] + s.zn[0];
         double tv = mdl.rhs_v(s.tn + hgs, yy, s.acol);
         s.cnt.nfe++;
         const double a = frcp(hgs);
@@ -363,20 +359,21 @@ BDF_INL double set_bdf_q(S& s, TqCtx& c)
             hsum += s.tau[CI(j) - 1];
             xi_inv = fdiv(s.h, hsum);
             alpha0 -= 1.0 / CI(j);
-            cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xi_inv, s.l[CI(i)]); });
+            cfor_down<CI(j), 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = s.l[CI(i)] + s.l[CI(i) - 1] * xi_inv; });
         });
         alpha0 -= 1.0 / q;
         xistar_inv = -s.l[1] - alpha0;
         hsum += s.tau[q - 1];
         xi_inv = fdiv(s.h, hsum);
         alpha0_hat = -s.l[1] - xi_inv;
-        cfor_down<Q, 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = __builtin_fma(s.l[CI(i) - 1], xistar_inv, s.l[CI(i)]); });
+        cfor_down<Q, 1>([&](auto i) __attribute__((always_inline)) { s.l[CI(i)] = s.l[CI(i)] + s.l[CI(i) - 1] * xistar_inv; });
     }
     const double A1 = 1.0 - alpha0_hat + alpha0;
-    const double A2 = __builtin_fma((double)q, A1, 1.0);
+    const double A2 = 1.0 + (double)q * A1;
     const double lq = s.l[q];
     s.tq[2] = fabs(fdiv(A1, alpha0 * A2));
     s.tq[5] = fabs(fdiv(A2 * xistar_inv, lq * xi_inv));
+    s.tq[4] = fdiv(CORTES, s.tq[2]);
     c.alpha0 = alpha0;
     c.alpha0_hat = alpha0_hat;
     c.xi_inv = xi_inv;
@@ -430,8 +427,8 @@ BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& csc
     const double y = s.zn[0] + s.acor;
     const double f = mdl.rhs_v(s.tn, y, s.acol);
     s.cnt.nfe++;
-    double delta = __builtin_fma(rl1, s.zn[1], s.acor);
-    delta = __builtin_fma(-s.gamma, f, delta);
+    double delta = rl1 * s.zn[1] + s.acor;
+    delta = delta + (-s.gamma) * f;
     if (BDF_UNLIKELY(setup)) {
         if (jbad) convfail = CONV_BAD_J;
         const double dgamma = fabs(fdiv(s.gamma, s.gammap) - 1.0);
@@ -462,7 +459,7 @@ BDF_INL bool newton_rest(S& s, const Model& mdl, double rl1, int convfail, bool 
     bool jbad = false;
     for (bool first = true;; first = false) {
         if (!first) del = vec::newton_correction<NS>(s, mdl, rl1, cscale, callSetup, jbad, convfail);
-        if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
+        if (div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4])) {
             s.acnrm = del;
             s.nls_jcur = 0;
             return true;
@@ -471,7 +468,7 @@ BDF_INL bool newton_rest(S& s, const Model& mdl, double rl1, int convfail, bool 
         for (int it = 1; it < NLS_MAXCOR; it++) {
             del = vec::newton_correction<NS>(s, mdl, rl1, cscale, false, false, convfail);
             s.crate = SUNMAX(CRDOWN * s.crate, fdiv(del, s.delp));
-            if (del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) {
+            if (div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4])) {
                 s.acnrm = vec::wrms<NS>(s.acor, s.ewt);
                 s.nls_jcur = 0;
                 return true;
@@ -509,7 +506,7 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
     double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
     const double del = vec::newton_correction<NS>(s, mdl, rl1, cscale, callSetup, false, convfail);
     const double dsm1 = del * s.tq[2];
-    if (BDF_LIKELY((del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) & (dsm1 <= 1.0))) {
+    if (BDF_LIKELY(div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4]) & (dsm1 <= 1.0))) {
         s.acnrm = del;
         s.nls_jcur = 0;
         dsm = dsm1;
@@ -543,7 +540,7 @@ BDF_INL void complete_head_q(S& s)
     cfor_down<Q, 2>([&](auto i) __attribute__((always_inline)) { s.tau[CI(i)] = s.tau[CI(i) - 1]; });
     if constexpr (q == 1) s.tau[2] = (s.nst > 1) ? s.tau[1] : s.tau[2];
     s.tau[1] = s.h;
-    cfor<0, Q + 1>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j)] = __builtin_fma(s.l[CI(j)], s.acor, s.zn[CI(j)]); });
+    cfor<0, Q + 1>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j)] = s.zn[CI(j)] + s.l[CI(j)] * s.acor; });
     s.qwait--;
     if constexpr (q != QMAX) {
         // qwait is a scalar counter: a scalar branch instead of four VALU selects every step
@@ -572,12 +569,12 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
             s.qwait = 2;
             vec::tq_13<q>(s, tc);  // qwait was 1 in this step's set_bdf_q
             double etaqm1 = 0.0, etaqp1 = 0.0;
-            if constexpr (q > 1) etaqm1 = uni::eta_candidate<q>(BIAS1 * vec::wrms<NS>(s.zn[q], s.ewt) * s.tq[1]);
+            if constexpr (q > 1) etaqm1 = uni::eta_candidate<q>(BIAS1 * (vec::wrms<NS>(s.zn[q], s.ewt) * s.tq[1]));
             if constexpr (q != QMAX) {
                 if (s.saved_tq5 != 0.0) {
                     const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), q + 1);
-                    const double tv = __builtin_fma(-cquot, s.zn[QMAX], s.acor);
-                    etaqp1 = uni::eta_candidate<q + 2>(BIAS3 * vec::wrms<NS>(tv, s.ewt) * s.tq[3]);
+                    const double tv = (-cquot) * s.zn[QMAX] + s.acor;
+                    etaqp1 = uni::eta_candidate<q + 2>(BIAS3 * (vec::wrms<NS>(tv, s.ewt) * s.tq[3]));
                 }
             }
             const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
@@ -686,7 +683,7 @@ BDF_INL int attempt_loop(S& s, const Model& mdl, double (&yout)[NS], double& tre
         nflag = PREV_ERR_FAIL;
         if (nef == MXNEF) return CV_ERR_FAILURE;
         if (nef <= MXNEF1) {
-            double eta = eta_from(BIAS2 * dsm, s.L);
+            double eta = eta_exact(BIAS2 * dsm, s.L);
             eta = SUNMAX(ETAMIN, eta);
             if (nef >= SMALL_NEF) eta = SUNMIN(eta, ETAMXF);
             s.eta = eta;
@@ -880,7 +877,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         // (a first-iteration convergence has local error dsm = acnrm tq[2] = del tq[2]) -- is ONE
         // branch; anything else goes on through newton_rest, which repeats the convergence test
         double dsm = del * s.tq[2];
-        if (BDF_LIKELY((del * SUNMIN(1.0, s.crate) * s.tq[2] <= CORTES) & (dsm <= 1.0))) {
+        if (BDF_LIKELY(div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4]) & (dsm <= 1.0))) {
             s.acnrm = del;
             s.nls_jcur = 0;
             BDF_PH(5);

@@ -57,7 +57,9 @@ hipError_t launch_cp_timepoints(const CpStatic& m, int32_t n, int32_t max_R, con
 hipError_t launch_cp_assign(int32_t n_problems, int32_t R, int32_t nsim, const double* lik, unsigned char* ws_global,
                             size_t ws_stride, int32_t* match, double* sum, int32_t* ok, hipStream_t s);
 size_t cp_assign_ws_bytes(int n);  // the matching workspace of n x n cells
-inline bool cp_assign_lds_fits(int n) { return cp_assign_ws_bytes(n) <= 56 * 1024; }
+// the dynamic workspace plus the larger kernel's static LDS (cp_timepoints_kernel, ~8.4 KB) stay within
+// 64 KB, the workgroup limit of parts smaller than gfx950's 160 KB
+inline bool cp_assign_lds_fits(int n) { return cp_assign_ws_bytes(n) <= 52 * 1024; }
 // out[w] = flags[work[w]]
 hipError_t launch_cp_gather(const int32_t* work, int32_t n, const int32_t* flags, int32_t* out, hipStream_t s);
 // the next experiment's (x, xstatus) into the running sum (logp, status) of

@@ -152,16 +152,17 @@ bool LoadPriorMarginals(const XmlNode& root, std::vector<Marginal>& out)
                     return false;
                 }
                 const long vix = (long)out.size();
-                if (id > (long)groups.size()) {
-                    groups.resize(id);
-                    // only dirichlet (PriorIndependence.cpp:47-51)
+                if (id > (long)groups.size()) groups.resize(id);
+                Group& g = groups[id - 1];
+                if (g.first < 0) {
+                    // the group's first member names its distribution; only dirichlet
+                    // (PriorIndependence.cpp:47-51), checked whatever order the ids come in
                     if (var->get("distribution") != "dirichlet") {
                         LOGERROR("Multivariate distribution of unknown type (only dirichlet supported).");
                         return false;
                     }
+                    g.first = vix;
                 }
-                Group& g = groups[id - 1];
-                if (g.first < 0) g.first = vix;
                 g.alpha.push_back(var->get_double("alpha"));
                 if (vix != g.first + (long)g.alpha.size() - 1) {
                     LOGERROR("All variables in a multivariate distribution should follow each other directly");

@@ -8,19 +8,20 @@
 
 namespace bcm3hip {
 
-BDF_INL double fastpow10(double x) { return exp(x * 2.3025850929940459); }
+// libm's exp / log / log1p / erf / erfc through libm_exact.h (the glibc results of the oracle)
+BDF_INL double fastpow10(double x) { return xm::exp(x * 2.3025850929940459); }
 
 BDF_INL double transform_var(int tf, double x)
 {
     switch (tf) {
-    case 1: return exp(x);
+    case 1: return xm::exp(x);
     case 2: return fastpow10(x);
     case 3:
         if (x > 0) {
-            double z = exp(-x);
+            double z = xm::exp(-x);
             return 1.0 / (1.0 + z);
         } else {
-            double z = exp(x);
+            double z = xm::exp(x);
             return z / (1.0 + z);
         }
     default: return x;
@@ -34,7 +35,7 @@ __device__ double ndtri_lower(double p)
 {
     double x;
     if (p < 0.02425) {
-        double q = sqrt(-2.0 * log(p));
+        double q = sqrt(-2.0 * xm::log(p));
         x = (((((-7.784894002430293e-03 * q - 3.223964580411365e-01) * q - 2.400758277161838e+00) * q -
                2.549732539343734e+00) * q + 4.374664141464968e+00) * q + 2.938163982698783e+00) /
             ((((7.784695709041462e-03 * q + 3.224671290700398e-01) * q + 2.445134137142996e+00) * q +
@@ -48,9 +49,9 @@ __device__ double ndtri_lower(double p)
     }
     const bool central = (p > 0.25);  // residual via erf near p = 0.5 (p - 0.5 exact)
     for (int it = 0; it < 3; it++) {
-        double e = central ? 0.5 * erf(x / 1.4142135623730951) - (p - 0.5)
-                           : 0.5 * erfc(-x / 1.4142135623730951) - p;
-        double u = e * 2.5066282746310002 * exp(0.5 * x * x);
+        double e = central ? 0.5 * xm::erf(x / 1.4142135623730951) - (p - 0.5)
+                           : 0.5 * xm::erfc(-x / 1.4142135623730951) - p;
+        double u = e * 2.5066282746310002 * xm::exp(0.5 * x * x);
         x = x - u / (1.0 + 0.5 * x * u);
     }
     return x;
@@ -77,7 +78,7 @@ __device__ double quantile_normal(double p, double mu, double sigma)
 BDF_INL double log_pdf_tnu4(double x, double mu, double sigma)
 {
     double xn = (x - mu) / sigma;
-    return -0.9808292530117262 - 2.5 * log1p(0.25 * xn * xn) - log(sigma);
+    return -0.9808292530117262 - 2.5 * xm::log1p(0.25 * xn * xn) - xm::log(sigma);
 }
 
 }  // namespace bcm3hip

@@ -58,31 +58,22 @@ struct PKLane {
         return ka;
     }
 
-    // The PK systems are linear, dy/dt = A(ka) y + u(t) e0 (RHS_*, .cpp:446-560): A's entries
-    // (a(i, j)) and the transit input u are evaluated once per call; every product of the
-    // matrix-vector sum is an fma in the fixed order j = 0, 1, 2 -- including the structural
-    // zeros -- so the one-trajectory-per-wavefront solver, which forms the same sums across
-    // lanes, produces identical bits.
-    BDF_INL double a(int i, int j) const
-    {
-        const double k = cur_ka();
-        if constexpr (TR::two) {
-            const double m[3][3] = {{-(k + ke), 0.0, 0.0}, {k, -(kel + kf), kb}, {0.0, kf, -kb}};
-            return m[i][j];
-        } else {
-            const double m[2][2] = {{-(k + ke), 0.0}, {k, -kel}};
-            return m[i][j];
-        }
-    }
+    // CalculateDerivative_* (.cpp:446-627): every component in the reference's own expression,
+    //   dydt0 = [transit -] (ka + ke) y0
+    //   dydt1 = ka y0 - kel y1 [- kf y1 + kb y2]
+    //   dydt2 = kf y1 - kb y2
+    // (left to right, no contraction), so the one-trajectory-per-wavefront solver, which forms the
+    // same expressions lane by lane, and the reference produce identical bits.
+    BDF_INL double a00() const { return -(cur_ka() + ke); }
 
-    // transit absorption input (.cpp:568-592), 0 for the other models
+    // transit absorption input (.cpp:568-592), 0 for the other models; libm's exp / log
     BDF_INL double input(double t) const
     {
         if constexpr (TR::transit) {
             double d = dose;
             if (t >= dose_change_time) d = dose_after;
             const double tst = t - last_treatment;
-            const double transit = exp((ntr * log(ktr * tst) - ktr * tst) - lnf);
+            const double transit = xm::exp((ntr * xm::log(ktr * tst) - ktr * tst) - lnf);
             return ktr * transit * d;
         }
         return 0.0;
@@ -90,20 +81,26 @@ struct PKLane {
 
     BDF_INL void rhs(double t, const double (&y)[NS], double (&dydt)[NS]) const
     {
-        cfor<0, NS>([&](auto I) __attribute__((always_inline)) {
-            constexpr int i = CI(I);
-            double f = a(i, 0) * y[0];
-            cfor<1, NS>([&](auto J) __attribute__((always_inline)) { f = __builtin_fma(a(i, CI(J)), y[CI(J)], f); });
-            dydt[i] = f;
-        });
-        if constexpr (TR::transit) dydt[0] = dydt[0] + input(t);
+        const double k = cur_ka();
+        const double m0 = a00() * y[0];  // = -((ka + ke) y0), exactly
+        if constexpr (TR::transit)
+            dydt[0] = input(t) + m0;
+        else
+            dydt[0] = m0;
+        if constexpr (TR::two) {
+            dydt[1] = k * y[0] - kel * y[1] - kf * y[1] + kb * y[2];
+            dydt[2] = kf * y[1] - kb * y[2];
+        } else {
+            dydt[1] = k * y[0] - kel * y[1];
+        }
     }
 
     // Jacobian (CalculateJacobian_*, .cpp:457-642) is constant within a dosing segment, so the
-    // saved Jacobian of cvLsLinSys is re-derived here. Structural zeros of J (and hence of
-    // A = I - gamma J, sunmatrix_dense_eigen.cpp:128-133) are exploited in the closed-form inverse
-    // of sunlinsol_dense_eigen.cpp:111-178 / Eigen compute_inverse<3>: every cofactor term with a
-    // structural-zero factor is an exact zero there too.
+    // saved Jacobian of cvLsLinSys is re-derived here: A = J (-gamma), then 1 added to the diagonal
+    // (SUNMatScaleAddI, sunmatrix_dense_eigen.cpp:128-133). Structural zeros of J make every
+    // cofactor term with a zero factor an exact (signed) zero in the closed-form inverse of
+    // sunlinsol_dense_eigen.cpp:111-178 / Eigen compute_inverse<3>, so only the other terms are
+    // formed; the remaining products and differences are the reference's.
     struct Inv {
         double i00, i10, i11, i12, i20, i21, i22;
     };
@@ -112,15 +109,15 @@ struct PKLane {
     {
         const double a = cur_ka();
         const double ng = -gamma;
-        const double a00 = __builtin_fma(-(a + ke), ng, 1.0);
+        const double a00 = (-(a + ke)) * ng + 1.0;
         const double a10 = a * ng;
         if constexpr (TR::two) {
-            const double a11 = __builtin_fma(-(kel + kf), ng, 1.0);
+            const double a11 = (-(kel + kf)) * ng + 1.0;
             const double a12 = kb * ng;
             const double a21 = kf * ng;
-            const double a22 = __builtin_fma(-kb, ng, 1.0);
-            const double c0 = __builtin_fma(a11, a22, -(a12 * a21));  // cofactor(0,0)
-            const double invdet = frcp(c0 * a00);    // det = c0*a00 + 0*a10 + 0*a20
+            const double a22 = (-kb) * ng + 1.0;
+            const double c0 = a11 * a22 - a12 * a21;  // cofactor(0,0)
+            const double invdet = frcp(c0 * a00);     // det = c0*a00 + (+-0) + (+-0)
             r.i00 = c0 * invdet;
             r.i10 = (-(a10 * a22)) * invdet;
             r.i11 = (a22 * a00) * invdet;
@@ -129,8 +126,8 @@ struct PKLane {
             r.i21 = (-(a21 * a00)) * invdet;
             r.i22 = (a00 * a11) * invdet;
         } else {
-            const double a11 = __builtin_fma(-kel, ng, 1.0);
-            const double invdet = frcp(a00 * a11);  // a00*a11 - a01*a10, a01 = 0
+            const double a11 = (-kel) * ng + 1.0;
+            const double invdet = frcp(a00 * a11);  // a00*a11 - a01*a10, a01 = -0
             r.i00 = a11 * invdet;
             r.i10 = -a10 * invdet;
             r.i11 = a00 * invdet;
@@ -146,38 +143,59 @@ struct PKLane {
     }
     // SUNLinSolSolve_Dense_Eigen2x2 (sunlinsol_dense_eigen.cpp:157-167): inv(i,0) b0 + inv(i,1) b1;
     // _Eigen3x3 (:169-176): Eigen's Matrix3d * VectorXd, whose row sum is its unrolled reduction
-    // p0 + (p1 + p2). Both as the reference's own build (-O3 -march=native) contracts them:
-    // fma(i0, b0, i1 b1) and fma(i0, b0, fma(i2, b2, i1 b1)) -- checked against the vendored Eigen
-    // compiled with FMA (oracle/eigen_ls.cpp)
+    // p0 + (p1 + p2) (checked against the vendored Eigen, oracle/eigen_ls.cpp)
     BDF_INL void lin_solve(const Inv& r, const double (&b)[NS], double (&x)[NS]) const
     {
         cfor<0, NS>([&](auto I) __attribute__((always_inline)) {
             constexpr int i = CI(I);
             if constexpr (NS == 3)
-                x[i] = __builtin_fma(inv_at(r, i, 0), b[0],
-                                     __builtin_fma(inv_at(r, i, 2), b[2], inv_at(r, i, 1) * b[1]));
+                x[i] = inv_at(r, i, 0) * b[0] + (inv_at(r, i, 1) * b[1] + inv_at(r, i, 2) * b[2]);
             else
-                x[i] = __builtin_fma(inv_at(r, i, 0), b[0], inv_at(r, i, 1) * b[1]);
+                x[i] = inv_at(r, i, 0) * b[0] + inv_at(r, i, 1) * b[1];
         });
     }
 
-    // ---- lane-vector forms for bdf_vec.h (lane i = component i; same products, same order)
-    // columns of A: lane i of c[j] = a(i, j)
-    BDF_INL void rhs_columns(double (&c)[NS]) const
+    // ---- lane-vector forms for bdf_vec.h (lane i = component i; same expressions)
+    // Lane i evaluates ((c0 u - c1 y) - c2 y) + c3 y2 and keeps the prefix its component's
+    // expression has: lane 0 c0 u = a00 y0; lane 1 the whole chain with (ka, kel, kf, kb), u = y0;
+    // lane 2 c0 u - c1 y = kf y1 - kb y2, u = y1. u comes from one DPP quad permutation
+    // (lanes 0, 1 <- lane 0, lane 2 <- lane 1), y2 from a row broadcast.
+    BDF_INL void rhs_columns(double (&c)[4]) const
     {
-        cfor<0, NS>([&](auto J) __attribute__((always_inline)) {
-            constexpr int j = CI(J);
-            double col[NS];
-            cfor<0, NS>([&](auto I) __attribute__((always_inline)) { col[CI(I)] = a(CI(I), j); });
-            c[j] = vec::from_array<NS>(col);
-        });
+        const double k = cur_ka();
+        if constexpr (TR::two) {
+            const double p[3] = {a00(), k, kf}, qv[3] = {0.0, kel, kb}, rv[3] = {0.0, kf, 0.0}, sv[3] = {0.0, kb, 0.0};
+            c[0] = vec::from_array<3>(p);
+            c[1] = vec::from_array<3>(qv);
+            c[2] = vec::from_array<3>(rv);
+            c[3] = vec::from_array<3>(sv);
+        } else {
+            const double p[2] = {a00(), k}, qv[2] = {0.0, kel};
+            c[0] = vec::from_array<2>(p);
+            c[1] = vec::from_array<2>(qv);
+            c[2] = c[3] = 0.0;
+        }
     }
-    BDF_INL double rhs_v(double t, double y, const double (&acol)[NS]) const
+    BDF_INL double rhs_v(double t, double y, const double (&c)[4]) const
     {
-        double f = vec::matvec<NS>(acol, y);
+        const int ln = vec::lane_id();
+        // quad_perm [0, 0, 1, 3]
+        const double u = __builtin_amdgcn_mov_dpp(y, 0xD0, 0xf, 0xf, false);
+        const double t1 = c[0] * u;
+        const double t2 = t1 - c[1] * y;
+        double f;
+        if constexpr (TR::two) {
+            const double t3 = t2 - c[2] * y;
+            const double t4 = t3 + c[3] * vec::bc<2>(y);
+            f = (ln == 1) ? t4 : t2;
+        } else {
+            f = t2;
+        }
         if constexpr (TR::transit) {
-            const double u = input(t);
-            f = (vec::lane_id() == 0) ? f + u : f;
+            const double uin = input(t);
+            f = (ln == 0) ? uin + t1 : f;
+        } else {
+            f = (ln == 0) ? t1 : f;
         }
         return f;
     }
@@ -299,7 +317,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         mdl.ntr = transform_var(m.transforms[ni], v[ni]);
         mdl.ktr = (mdl.ntr + 1) / transform_var(m.transforms[ti], v[ti]);
         const double n = mdl.ntr;
-        mdl.lnf = 0.9189385332046727 + (n + 0.5) * log(n) - n + log(1 + 1 / (12.0 * n));
+        mdl.lnf = 0.9189385332046727 + (n + 0.5) * xm::log(n) - n + xm::log(1 + 1 / (12.0 * n));
     }
     const double interval = m.dosing_interval[j];
     double tsw = 0.0;

@@ -1044,7 +1044,10 @@ __global__ void ptmh_spec_select_kernel(int C, int d, const double* __restrict__
     }
     const int sl = c * BCM3HIP_SPEC_SLOTS + k;
     if (!S.cand_active[sl]) {
+        // internal error: poison the row, so the accept step's fatal-NaN path stops the sampler at
+        // its next check instead of letting this chain reuse iteration r's proposal
         if (error) *error = 1;
+        llh_prop[c] = __builtin_nan("");
         return;
     }
     for (int i = 0; i < d; i++) prop[(int64_t)c * d + i] = S.cand_x[(int64_t)sl * d + i];

@@ -9,7 +9,9 @@ Outputs (all data; no reference source text):
                                      simulated by the reference-built CVODE at TRUE_* + t4 noise
   c3_prior.xml, c3_likelihood.xml    inputs in the reference's own XML formats
   c3_golden.npz                      512 prior draws (seed 20251016) with the reference-built
-                                     oracle's logp, per-patient llh, trajectories, step counters
+                                     oracle's logp, per-patient llh, trajectories, step counters,
+                                     from the build with FMA contraction (as the reference's CMake
+                                     builds it) and without (`*_nofma`, the arithmetic the GPU follows)
   analytic_golden.npz                banana / circular draws with reference-formula outputs
   c3_golden_llh.npz                  8,192 prior draws (seed 20251021, regenerated from the seed by
                                      synthetic.prior_draws) with the reference-built oracle's logp,
@@ -88,8 +90,11 @@ def make_c3_golden():
     prob = O.build_problem(pk, S.TRIAL, S.DRUG, S.PK_TYPE, variables(1))
     draws = S.prior_draws(1, 512, 20251016)
     ref = O.Oracle("ref").popk_eval(prob, draws)
+    nof = O.Oracle("ref_nofma").popk_eval(prob, draws)
     np.savez_compressed(os.path.join(HERE, "c3_golden.npz"), values=draws, logp=ref["logp"],
-                        patient_llh=ref["patient_llh"], traj=ref["traj"], stats=ref["stats"], ok=ref["ok"])
+                        patient_llh=ref["patient_llh"], traj=ref["traj"], stats=ref["stats"], ok=ref["ok"],
+                        logp_nofma=nof["logp"], patient_llh_nofma=nof["patient_llh"], traj_nofma=nof["traj"],
+                        stats_nofma=nof["stats"], ok_nofma=nof["ok"])
 
 
 def main():

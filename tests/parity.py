@@ -8,13 +8,15 @@ without FMA contraction (oracle/_ref/libbcm3ref.so vs libbcm3ref_nofma.so) diffe
     BDF step counts equal:    99.3%;  ok/fail status identical for 100%.
 (Round 3: with the 3x3 solve of both builds run by the vendored Eigen itself, 8192 draws give 92.8 %,
 98.97 %, 99.67 %; llh 99.13 %; steps 99.29 %.)
-The contract asserts the GPU is inside that envelope, at the reference's own FMA on/off spread
-minus a small margin (VERDICT r02 "Next round" 1): y1 >=92% at 1e-9, >=98.5% at 1e-6, >=99.5% at
-2e-5; llh >=99% at 1e-8. Where a test passes the reference's own spread measured on the same draws
-(reference_self_spread), a tier the reference's two builds themselves miss on that sample is held
-to their fraction minus two binomial standard deviations instead -- e.g. on the 4,096 draws of
-test_c3_prior_draws_vs_oracle the two builds agree to 1e-8 on 99.05 % of llh. Every assert_parity call appends its measured fractions to the JSON-lines
-file named by $BCM3_PARITY_LOG (committed under profiles/ per round).
+The device follows the no-FMA build's arithmetic operation for operation (round 4), so
+against that build and the C restatement (bit-exact to it) the tiers are absolute: y1 >=92% at 1e-9,
+>=98.5% at 1e-6, >=99.5% at 2e-5; llh >=99% at 1e-8 (measured round 4: 99.2 % / 99.95 % / 100 %, llh
+99.93 % on 4,096 draws), plus a floor on the fraction of bit-identical llh (BITEXACT_MIN).
+Against the FMA build, which no other build reproduces, a test may pass the reference's own
+spread measured on the same draws (reference_self_spread): a tier the reference's two builds
+themselves miss on that sample is held to their fraction minus two binomial standard deviations.
+Every assert_parity call appends its measured fractions to the JSON-lines file named by
+$BCM3_PARITY_LOG (committed under profiles/ per round).
 """
 from __future__ import annotations
 
@@ -41,6 +43,16 @@ def llh_min_fraction(n: int) -> float:
     allowed = int(np.floor(n * p + 2.0 * np.sqrt(n * p * (1.0 - p))))
     return 1.0 - allowed / max(1, n)
 STEPS_FRACTION = 0.98
+# The device computes the reference's operations in the reference's order with glibc's libm results
+# (DESIGN.md §3): against the reference built without FMA contraction it is bit-identical wherever
+# glibc's exp / pow happen to be correctly rounded along the whole solve (measured 88 % of C3 draws,
+# profiles/r04b_bitexact_probe.txt). Large C3 samples must keep at least this fraction.
+BITEXACT_MIN = 0.80
+
+
+def bitexact_fraction(a, b) -> float:
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.mean((a == b) | (np.isnan(a) & np.isnan(b))))
 
 
 def y1_rel_err(a: np.ndarray, b: np.ndarray, floor: float) -> np.ndarray:
@@ -106,18 +118,24 @@ def _bar(frac: float, ref_frac: float | None, n: int) -> float:
     """The tier's fraction, or -- when the reference's own two builds fall short of it on these
     draws -- their fraction minus two binomial standard deviations (the GPU must sit inside the
     reference's own envelope measured on the same sample)."""
-    if ref_frac is None:
+    if ref_frac is None or ref_frac >= frac:
         return frac
     sd = np.sqrt(max(ref_frac * (1.0 - ref_frac), 1e-6) / max(n, 1))
     return min(frac, ref_frac - 2.0 * sd)
 
 
-def assert_parity(y1_err, llh_e, steps_a, steps_b, ok_a, ok_b, near_cap=None, ref_self=None):
-    """Assert the GPU-vs-oracle differences are inside the reference's self-parity envelope.
-    ref_self (reference_self_spread on the same draws) lowers a tier's bar only where the
-    reference's own FMA / no-FMA builds miss that tier on this sample."""
+def assert_parity(y1_err, llh_e, steps_a, steps_b, ok_a, ok_b, near_cap=None, ref_self=None, bitexact=None):
+    """Assert the GPU-vs-oracle differences are inside the contract's tiers. ref_self
+    (reference_self_spread on the same draws) lowers a tier's bar only where the reference's own
+    FMA / no-FMA builds miss that tier on this sample (used only against the FMA build, which the
+    device does not follow). bitexact (fraction of identical log-likelihoods) is asserted >=
+    BITEXACT_MIN when given."""
     s = summarize(y1_err, llh_e, steps_a, steps_b)
+    if bitexact is not None:
+        s["bitexact"] = bitexact
     log_summary(s, n=int(np.asarray(llh_e).size), **({"ref_self": ref_self} if ref_self else {}))
+    if bitexact is not None:
+        assert bitexact >= BITEXACT_MIN, s
     rs = ref_self or {}
     ok_a, ok_b = np.asarray(ok_a), np.asarray(ok_b)
     differ = ok_a != ok_b

@@ -159,6 +159,9 @@ def test_dirichlet_prior_host_parse(tmp_path):
     ('<variable name="w0" multivariate="true" id="1" distribution="wishart" alpha="2"/>', "only dirichlet"),
     ('<variable name="w0" multivariate="true" id="0" distribution="dirichlet" alpha="2"/>', "start at 1"),
     ('<variable name="w0" multivariate="true" id="1" repeat="2" distribution="dirichlet" alpha="2"/>', "repeat"),
+    # ids out of order: group 1's first member still names its distribution
+    ('<variable name="v0" multivariate="true" id="2" distribution="dirichlet" alpha="2"/>'
+     '<variable name="w0" multivariate="true" id="1" distribution="wishart" alpha="2"/>', "only dirichlet"),
 ])
 def test_dirichlet_prior_errors(tmp_path, body, msg):
     from bcm3_amd.likelihood import lib

@@ -1,9 +1,10 @@
 """GPU parity tests for the PopPK likelihood (through the C-ABI, libbcm3hip.so).
 
-Each test compares the HIP kernel with the oracle on the same inputs (restated CVODE, which is
-bit-exact to the reference's own CVODE build; golden fixtures from the reference-flags build)
-inside the parity envelope of tests/parity.py, and checks the reference's -inf / failure and
-summation semantics exactly.
+Each test compares the HIP kernel with the oracle on the same inputs (the restated CVODE, which is
+bit-exact to the reference's own CVODE built without FMA contraction; golden fixtures from both
+reference builds) inside the parity tiers of tests/parity.py, the C3 tests also with a floor on the
+fraction of bit-identical log-likelihoods, and checks the reference's -inf / failure and summation
+semantics exactly.
 """
 import os
 
@@ -30,7 +31,7 @@ def c3():
     ctx.close()
 
 
-def _check(prob, g, o, near_cap=None, ref_self=None):
+def _check(prob, g, o, near_cap=None, ref_self=None, bitexact=None):
     T = prob.T
     y1 = parity.y1_rel_err(g["traj"][:, :, 1, :].reshape(-1, T), o["traj"][:, :, 1, :].reshape(-1, T), prob.atol)
     pg = g["patient_llh"].reshape(-1)
@@ -38,24 +39,35 @@ def _check(prob, g, o, near_cap=None, ref_self=None):
     le = parity.llh_err(pg, po)
     return parity.assert_parity(y1, le, g["stats"]["nst"].reshape(-1), o["stats"][:, :, 0].reshape(-1),
                                 (~np.isneginf(pg)).astype(int), (~np.isneginf(po)).astype(int), near_cap,
-                                ref_self=ref_self)
+                                ref_self=ref_self, bitexact=bitexact)
 
 
 def test_c3_golden_fixture(c3, golden_dir):
+    """512 golden draws: the GPU against the reference's CVODE built without FMA contraction (the
+    arithmetic the device follows) with the contract's absolute tiers and a bit-exact
+    floor; against the reference's own -O3 FMA build inside that build's spread to the first."""
     prob, ctx = c3
     gold = np.load(os.path.join(golden_dir, "c3_golden.npz"))
     g = ctx.eval(gold["values"], detail=True)
+    ok_g = (g["status"] == 0).astype(int)
+    near = gold["stats_nofma"][:, 0, 0] >= 0.99 * prob.max_steps
+    y1 = parity.y1_rel_err(g["traj"][:, 0, 1], gold["traj_nofma"][:, 0, 1], prob.atol)
+    le = parity.llh_err(g["logp"], gold["logp_nofma"])
+    parity.assert_parity(y1, le, g["stats"]["nst"][:, 0], gold["stats_nofma"][:, 0, 0], ok_g, gold["ok_nofma"][:, 0],
+                         near, bitexact=parity.bitexact_fraction(g["logp"], gold["logp_nofma"]))
+    # the FMA build (as the reference's CMake compiles it): inside its own distance to the build above
     y1 = parity.y1_rel_err(g["traj"][:, 0, 1], gold["traj"][:, 0, 1], prob.atol)
     le = parity.llh_err(g["logp"], gold["logp"])
     near = gold["stats"][:, 0, 0] >= 0.99 * prob.max_steps
-    parity.assert_parity(y1, le, g["stats"]["nst"][:, 0], gold["stats"][:, 0, 0], (g["status"] == 0).astype(int),
-                         gold["ok"][:, 0], near, ref_self=parity.reference_self_spread(prob, gold["values"]))
+    parity.assert_parity(y1, le, g["stats"]["nst"][:, 0], gold["stats"][:, 0, 0], ok_g, gold["ok"][:, 0], near,
+                         ref_self=parity.reference_self_spread(prob, gold["values"]))
 
 
 def test_c3_golden_llh_8192(c3):
     """8,192 prior draws against the reference-built CVODE (tests/golden/c3_golden_llh.npz): identical
-    ok / fail status, llh within 1e-8 (1 + |llh|) for >= 99 % of the draws (the reference's own FMA /
-    no-FMA builds: 99.21 % on the same draws), within 1e-3 for all, step counts equal for >= 98 %"""
+    ok / fail status; against the build without FMA contraction llh within 1e-8 (1 + |llh|) for
+    >= 99 % of the draws and a bit-exact floor (parity.BITEXACT_MIN); against the FMA build >= 99 %
+    too (the two builds agree on 99.13 % of these draws); within 1e-3 for all, steps equal >= 98 %"""
     prob, ctx = c3
     z = np.load(os.path.join(H.GOLDEN, "c3_golden_llh.npz"))
     vals = H.S.prior_draws(1, int(z["n"]), int(z["seed"]))
@@ -65,24 +77,31 @@ def test_c3_golden_llh_8192(c3):
     ok_r = z["ok"].astype(bool)
     near = z["nst"] >= 0.99 * prob.max_steps
     assert np.all((ok_g == ok_r) | near)
-    e = parity.llh_err(g["logp"], z["logp"])
+    e = parity.llh_err(g["logp"], z["logp_nofma"])
+    e_fma = parity.llh_err(g["logp"], z["logp"])
     self_spread = parity.llh_err(z["logp_nofma"], z["logp"])
     s = {"llh_t1": float(np.mean(e <= parity.LLH_T1)), "llh_max": float(e[ok_g & ok_r].max()),
+         "llh_t1_vs_fma_build": float(np.mean(e_fma <= parity.LLH_T1)),
          "ref_self_llh_t1": float(np.mean(self_spread <= parity.LLH_T1)),
-         "steps_equal": float(np.mean(g["stats"]["nst"][:, 0] == z["nst"]))}
+         "bitexact": parity.bitexact_fraction(g["logp"], z["logp_nofma"]),
+         "steps_equal": float(np.mean(g["stats"]["nst"][:, 0] == z["nst_nofma"]))}
     parity.log_summary(s, n=len(vals))
     assert s["llh_t1"] >= parity.LLH_T1_FRAC, s
-    assert np.all(e[ok_g & ok_r] <= parity.LLH_T2), s
+    assert s["llh_t1_vs_fma_build"] >= parity.LLH_T1_FRAC, s
+    assert s["bitexact"] >= parity.BITEXACT_MIN, s
+    assert np.all(e[ok_g & ok_r] <= parity.LLH_T2) and np.all(e_fma[ok_g & ok_r] <= parity.LLH_T2), s
     assert s["steps_equal"] >= parity.STEPS_FRACTION, s
 
 
 def test_c3_prior_draws_vs_oracle(c3, orc):
+    """4,096 prior draws against the C restatement (bit-exact to the reference's no-FMA build):
+    the contract's absolute tiers, no relaxation, and the bit-exact floor"""
     prob, ctx = c3
     vals = H.S.prior_draws(1, 4096, 20251019)
     g = ctx.eval(vals, detail=True)
     o = orc.popk_eval(prob, vals, nthreads=8)
     near = o["stats"][:, 0, 0] >= 0.99 * prob.max_steps
-    _check(prob, g, o, near, ref_self=parity.reference_self_spread(prob, vals))
+    _check(prob, g, o, near, bitexact=parity.bitexact_fraction(g["logp"], o["logp"]))
     # logp of an evaluation with P = 1 is 0 + patient term
     assert np.array_equal(g["logp"], 0.0 + g["patient_llh"][:, 0])
 
