@@ -269,6 +269,7 @@ struct SamplerPTDevice::Impl {
     DevBuf<double> sp_cand_x, sp_cand_lp, sp_cand_lmh, sp_cand_llh, sp_cand_sc, sp_batch_x, sp_batch_llh;
     DevBuf<int32_t> sp_cand_sel, sp_cand_upd, sp_cand_steps, sp_steps_hint, sp_steps_prop, sp_batch_status,
         sp_batch_steps, sp_batch_src, sp_batch_n, sp_err;
+    DevBuf<int64_t> sp_total;  // entries of all speculative batches (bcm3hip_spec::batch_total)
     DevBuf<uint8_t> sp_cand_active, acc_mut, acc_exc;
     DevBuf<int32_t> partner[2], pair_first[2];
     DevBuf<double> sp_send_last, sp_send_first, sp_remote;  // boundary rows [state | proposal] of a sharded ladder
@@ -337,6 +338,8 @@ struct SamplerPTDevice::Impl {
 
     bool Eval(double* x, double* out)
     {
+        cnt.likelihood_launches++;
+        cnt.evaluated_entries += C;
         if (!ll->EvaluateLogProbabilityBatchDevice((size_t)C, x, out, status.p, stream)) {
             LOGERROR("EvaluateLogProbabilityBatchDevice failed");
             return false;
@@ -396,6 +399,8 @@ struct SamplerPTDevice::Impl {
             if (spec_on) {
                 // the same evaluation through the counted entry point, for the solves' step counts
                 const std::vector<int32_t> nC(1, (int32_t)C);
+                cnt.likelihood_launches++;
+                cnt.evaluated_entries += C;
                 if (!Upload(sp_batch_n, nC, stream) ||
                     !ll->EvaluateLogProbabilityBatchDeviceCounted((size_t)C, sp_batch_n.p, prop.p, llh_prop.p,
                                                                   status.p, sp_steps_prop.p, stream) ||
@@ -664,6 +669,7 @@ struct SamplerPTDevice::Impl {
                                             stream),
                     "ptmh_spec_batch"))
             return false;
+        cnt.likelihood_launches++;  // its entries are summed on the device (sp_total)
         if (!ll->EvaluateLogProbabilityBatchDeviceCounted((size_t)C * (1 + BCM3HIP_SPEC_SLOTS), S.batch_n, S.batch_x,
                                                           S.batch_llh, S.batch_status, S.batch_steps, stream)) {
             LOGERROR("EvaluateLogProbabilityBatchDeviceCounted failed");
@@ -742,7 +748,8 @@ struct SamplerPTDevice::Impl {
                   sp_batch_llh.alloc(N) && sp_batch_status.alloc(N) && sp_batch_steps.alloc(N) &&
                   sp_batch_src.alloc(N) && sp_batch_n.alloc(1) && sp_err.alloc(1) && acc_mut.alloc(C) &&
                   acc_exc.alloc(C) && sp_send_last.alloc(2 * d) && sp_send_first.alloc(2 * d) &&
-                  sp_remote.alloc(4 * d) && cross_acc.alloc(2) && sp_pred.alloc(N) && sp_inv_scale.alloc(d);
+                  sp_remote.alloc(4 * d) && cross_acc.alloc(2) && sp_pred.alloc(N) && sp_inv_scale.alloc(d) &&
+                  sp_total.alloc(1);
         for (int st = 0; st < 2 && ok; st++) ok = partner[st].alloc(C) && pair_first[st].alloc(C);
         if (!ok) {
             LOGERROR("SamplerPTDevice: speculative buffers could not be allocated");
@@ -780,7 +787,8 @@ struct SamplerPTDevice::Impl {
             bcm3hip_memset_async(sp_steps_hint.p, 0, C * sizeof(int32_t), stream) != 0 ||
             bcm3hip_memset_async(sp_batch_steps.p, 0, N * sizeof(int32_t), stream) != 0 ||
             bcm3hip_memset_async(sp_cand_steps.p, 0, C * K * sizeof(int32_t), stream) != 0 ||
-            bcm3hip_memset_async(sp_err.p, 0, sizeof(int32_t), stream) != 0)
+            bcm3hip_memset_async(sp_err.p, 0, sizeof(int32_t), stream) != 0 ||
+            bcm3hip_memset_async(sp_total.p, 0, sizeof(int64_t), stream) != 0)
             return false;
         S.cand_x = sp_cand_x.p;
         S.cand_lp = sp_cand_lp.p;
@@ -800,6 +808,7 @@ struct SamplerPTDevice::Impl {
         S.batch_src = sp_batch_src.p;
         S.batch_n = sp_batch_n.p;
         S.pred_steps = sp_pred.p;
+        S.batch_total = sp_total.p;
         return true;
     }
 
@@ -1173,6 +1182,12 @@ PTMHCounters SamplerPTDevice::GetCounters()
         c.accepted_exchange = (int64_t)b;
     }
     c.rounds = s.round;
+    if (s.spec_on) {
+        int64_t t = 0;
+        if (bcm3hip_memcpy_async(&t, s.sp_total.p, sizeof(t), BCM3HIP_D2H, s.stream) == 0 &&
+            bcm3hip_stream_synchronize(s.stream) == 0)
+            c.evaluated_entries += t;
+    }
     return c;
 }
 

@@ -30,6 +30,10 @@ public:
 
 std::unique_ptr<Transport> MakeRcclTransport(const void* nccl_id, int rank, int world);
 
+// between OS processes on one host (e.g. several ranks sharing one GPU, which RCCL refuses):
+// host-staged records over Unix domain sockets under `dir` (SocketTransport.cpp)
+std::unique_ptr<Transport> MakeSocketTransport(const std::string& dir, int rank, int world);
+
 // in-process transport between the ranks of one process (one host thread per rank): host-staged
 // mailboxes, for tests of the sharded exchange on one GPU
 class LocalGroup;
@@ -63,6 +67,9 @@ struct PTMHConfig {
 struct PTMHCounters {
     int64_t attempted_mutate = 0, accepted_mutate = 0, attempted_exchange = 0, accepted_exchange = 0;
     int64_t samples_done = 0, adaptations_done = 0, iterations = 0, rounds = 0;
+    // likelihood launches and the trajectories they evaluated, speculative candidates included
+    // (committed evaluations = attempted_mutate)
+    int64_t likelihood_launches = 0, evaluated_entries = 0;
 };
 
 class SamplerPTDevice {

@@ -159,6 +159,9 @@ int bcm3_ptmh_create(bcm3_likelihood* ll, const char* prior_xml, const bcm3_ptmh
             tr = bcm3::MakeRcclTransport(c->nccl_id, c->rank, c->world);
         } else if (c->transport == BCM3_PTMH_TRANSPORT_LOCAL && c->group) {
             tr = bcm3::MakeLocalTransport(c->group->g, c->rank);
+        } else if (c->transport == BCM3_PTMH_TRANSPORT_SOCKET) {
+            tr = bcm3::MakeSocketTransport(std::string(c->socket_dir, strnlen(c->socket_dir, sizeof(c->socket_dir))),
+                                           c->rank, c->world);
         }
         if (!tr) {
             LOGERROR("bcm3_ptmh_create: %d ranks need a transport", c->world);
@@ -216,7 +219,8 @@ int bcm3_ptmh_get_counters(bcm3_ptmh* h, int64_t* out)
     const bcm3::PTMHCounters c = h->s.GetCounters();
     const int64_t v[BCM3_PTMH_NUM_COUNTERS] = {c.attempted_mutate,   c.accepted_mutate, c.attempted_exchange,
                                                c.accepted_exchange,  c.samples_done,    c.adaptations_done,
-                                               c.iterations,         c.rounds};
+                                               c.iterations,         c.rounds,
+                                               c.likelihood_launches, c.evaluated_entries};
     std::memcpy(out, v, sizeof(v));
     return 0;
 }

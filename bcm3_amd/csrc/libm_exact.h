@@ -77,7 +77,7 @@ XM_FN dd dd_mul(dd a, dd b)
 XM_FN double as_double(long long b) { return __builtin_bit_cast(double, b); }
 XM_FN long long as_bits(double x) { return __builtin_bit_cast(long long, x); }
 // 2^k for -1022 <= k <= 1023
-XM_FN double pow2i(int k) { return as_double((long long)(k + 1023) << 52); }
+XM_FN double pow2i(int k) { return as_double((long long)((unsigned long long)(k + 1023) << 52)); }
 
 // ln 2 = LN2_1 + LN2_2 + LN2_3, LN2_1 and LN2_2 with 42 significant bits (k * LN2_i exact for
 // |k| < 2^11)
@@ -238,7 +238,7 @@ XM_FN double pow_inv_k(double x, int k)
 XM_FN int hi_word(double x) { return (int)(as_bits(x) >> 32); }
 XM_FN double with_hi_word(double x, int h)
 {
-    return as_double((as_bits(x) & 0xffffffffLL) | ((long long)(unsigned)h << 32));
+    return as_double((long long)(((unsigned long long)as_bits(x) & 0xffffffffULL) | ((unsigned long long)(unsigned)h << 32)));
 }
 XM_FN double with_lo_zero(double x) { return as_double(as_bits(x) & ~0xffffffffLL); }
 

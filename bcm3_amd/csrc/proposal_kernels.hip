@@ -977,7 +977,10 @@ __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, con
         if (S2 > 0) p = (r < L) ? S2 + r : (r < L + S2) ? r - L : R + (r - L - S2);
         pos_of[tid + q * 1024] = p;
     }
-    if (tid == 0) S.batch_n[0] = M;
+    if (tid == 0) {
+        S.batch_n[0] = M;
+        if (S.batch_total) S.batch_total[0] += M;
+    }
     __syncthreads();
     for (int i = tid; i < n_all; i += blockDim.x)
         if (pos_of[i] >= 0) S.batch_src[pos_of[i]] = i;

@@ -19,9 +19,9 @@ from .likelihood import Likelihood, lib as host_lib
 
 PROPOSALS = {"global_covariance": 0, "gaussian_mixture": 1, "gaussian_mixture_adjustedAIC": 2, "random_walk": 3}
 SCHEMES = {"deterministic_even_odd": 0, "stochastic_even_odd": 1, "stochastic_random": 2}
-TRANSPORT_NONE, TRANSPORT_RCCL, TRANSPORT_LOCAL = 0, 1, 2
+TRANSPORT_NONE, TRANSPORT_RCCL, TRANSPORT_LOCAL, TRANSPORT_SOCKET = 0, 1, 2, 3
 COUNTERS = ("attempted_mutate", "accepted_mutate", "attempted_exchange", "accepted_exchange", "samples_done",
-            "adaptations_done", "iterations", "rounds")
+            "adaptations_done", "iterations", "rounds", "likelihood_launches", "evaluated_entries")
 
 
 class PTMHConfig(C.Structure):
@@ -36,6 +36,7 @@ class PTMHConfig(C.Structure):
         ("initial_position_tries", C.c_int32), ("nan_check_every", C.c_int32), ("host_threads", C.c_int32),
         ("speculate", C.c_int32),
         ("transport", C.c_int32), ("nccl_id", C.c_uint8 * 128), ("group", C.c_void_p),
+        ("socket_dir", C.c_char * 256),
     ]
 
 
@@ -105,7 +106,7 @@ def load_config(path: str) -> dict:
     would reject."""
     rc = RunConfig()
     _check(_lib().bcm3_run_config_from_file(path.encode(), C.byref(rc)), "bcm3_run_config_from_file")
-    ptmh = {k: getattr(rc.ptmh, k) for k, _ in PTMHConfig._fields_ if k not in ("nccl_id", "group")}
+    ptmh = {k: getattr(rc.ptmh, k) for k, _ in PTMHConfig._fields_ if k not in ("nccl_id", "group", "socket_dir")}
     out = {"ptmh": ptmh}
     for k, _ in RunConfig._fields_:
         if k in ("ptmh", "pad_"):
@@ -141,7 +142,7 @@ class PTMHNative:
     def __init__(self, likelihood: Likelihood, prior_xml: str, num_chains: int, rank: int = 0, world: int = 1,
                  seed: int = 0, proposal: str = "gaussian_mixture", swapping_scheme: str = "deterministic_even_odd",
                  stream: Optional[int] = None, transport: int = TRANSPORT_NONE, nccl_id: Optional[bytes] = None,
-                 group: Optional[LocalGroup] = None, **options):
+                 group: Optional[LocalGroup] = None, socket_dir: Optional[str] = None, **options):
         _hip.lib()
         L = _lib()
         cfg = PTMHConfig()
@@ -156,6 +157,8 @@ class PTMHNative:
         self.group = group
         if group is not None:
             cfg.group = group.h
+        if socket_dir is not None:
+            cfg.socket_dir = socket_dir.encode()
         for k, v in options.items():
             if k not in dict(PTMHConfig._fields_):
                 raise ValueError(f"unknown sampler option {k}")

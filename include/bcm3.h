@@ -123,7 +123,8 @@ int bcm3_gmm_eval(int K, int d, const double* weights, const double* means, cons
 enum { BCM3_PTMH_GLOBAL_COVARIANCE = 0, BCM3_PTMH_GAUSSIAN_MIXTURE = 1, BCM3_PTMH_GAUSSIAN_MIXTURE_ADJUSTED_AIC = 2,
        BCM3_PTMH_RANDOM_WALK = 3 };
 enum { BCM3_PTMH_DETERMINISTIC_EVEN_ODD = 0, BCM3_PTMH_STOCHASTIC_EVEN_ODD = 1, BCM3_PTMH_STOCHASTIC_RANDOM = 2 };
-enum { BCM3_PTMH_TRANSPORT_NONE = 0, BCM3_PTMH_TRANSPORT_RCCL = 1, BCM3_PTMH_TRANSPORT_LOCAL = 2 };
+enum { BCM3_PTMH_TRANSPORT_NONE = 0, BCM3_PTMH_TRANSPORT_RCCL = 1, BCM3_PTMH_TRANSPORT_LOCAL = 2,
+       BCM3_PTMH_TRANSPORT_SOCKET = 3 };
 typedef struct bcm3_ptmh bcm3_ptmh;
 typedef struct bcm3_ptmh_group bcm3_ptmh_group; /* in-process ranks (tests): host-staged transport */
 typedef struct {
@@ -150,9 +151,14 @@ typedef struct {
     int32_t transport;           /* BCM3_PTMH_TRANSPORT_*, world > 1 */
     uint8_t nccl_id[128];        /* BCM3_PTMH_TRANSPORT_RCCL: bcm3_ptmh_nccl_unique_id of rank 0 */
     bcm3_ptmh_group* group;      /* BCM3_PTMH_TRANSPORT_LOCAL */
+    char socket_dir[256];        /* BCM3_PTMH_TRANSPORT_SOCKET: a directory every rank's process can
+                                    reach; rank r listens on <socket_dir>/bcm3_rank<r>.sock (ranks in
+                                    separate processes on one host, e.g. sharing one GPU) */
 } bcm3_ptmh_config;
-enum { BCM3_PTMH_NUM_COUNTERS = 8 }; /* attempted / accepted mutate, attempted / accepted exchange,
-                                        samples done, adaptations done, iterations, exchange rounds */
+enum { BCM3_PTMH_NUM_COUNTERS = 10 }; /* attempted / accepted mutate, attempted / accepted exchange,
+                                         samples done, adaptations done, iterations, exchange rounds,
+                                         likelihood launches, trajectories they evaluated (speculative
+                                         candidates included) */
 void bcm3_ptmh_config_default(bcm3_ptmh_config* cfg);
 int bcm3_ptmh_nccl_unique_id(void* id /* 128 bytes */);
 int bcm3_ptmh_group_create(int world, bcm3_ptmh_group** out);
