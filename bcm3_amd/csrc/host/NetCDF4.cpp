@@ -6,6 +6,9 @@
 // (tools/nc_convert.py), as before. The result has the layout NcClassicRead gives a classic file:
 // doc[group][variable] = {"dims": [dimension names], "data": nested values}, nested groups named
 // "a.b", the root group "", fill values -> NaN, char arrays -> strings.
+// The same library writes the sampler's output.nc and sampler_adaptation.nc as netCDF-4 with real
+// groups (NcNetCDF4Writer: nc_create(NC_CLOBBER | NC_NETCDF4) as NetCDFDataFile::Create,
+// src/utils/NetCDFDataFile.cpp:117-260) when it is present and has the writing API.
 #include <dlfcn.h>
 
 #include <algorithm>
@@ -18,6 +21,7 @@
 #include <vector>
 
 #include "NetCDFClassic.h"
+#include "log.h"
 
 namespace bcm3 {
 
@@ -41,22 +45,29 @@ struct NcApi {
     const char* (*strerror)(int) = nullptr;
     void* handle = nullptr;
     std::string error;
+    std::string env;  // $BCM3_LIBNETCDF when the library was loaded
 };
 
-constexpr int kNcNoWrite = 0, kNcMaxName = 256, kNcMaxDims = 1024;
+constexpr int kNcNoWrite = 0, kNcMaxName = 256, kNcMaxDims = 1024, kNcClobber = 0, kNcNetCDF4 = 0x1000;
 constexpr int kNcByte = 1, kNcChar = 2, kNcShort = 3, kNcInt = 4, kNcFloat = 5, kNcDouble = 6, kNcString = 12;
 constexpr double kFillDouble = 9.9692099683868690e+36, kFillFloat = 9.9692099683868690e+36f;
 
 // loads libnetcdf on first success; a failed attempt is retried on the next call (a later
-// $BCM3_LIBNETCDF or install is seen)
+// $BCM3_LIBNETCDF or install is seen), and a change of $BCM3_LIBNETCDF switches libraries
 const NcApi& api()
 {
     static NcApi a;
     static std::mutex mu;
     std::lock_guard<std::mutex> lock(mu);
-    if (a.handle) return a;
+    const char* env_now = std::getenv("BCM3_LIBNETCDF");
+    const std::string env = env_now ? env_now : "";
+    if (a.handle && a.env == env) return a;
+    if (a.handle) {
+        dlclose(a.handle);
+        a = NcApi();
+    }
     std::vector<std::string> names;
-    if (const char* e = std::getenv("BCM3_LIBNETCDF")) names.push_back(e);
+    if (!env.empty()) names.push_back(env);
     for (const char* n : {"libnetcdf.so", "libnetcdf.so.22", "libnetcdf.so.19", "libnetcdf.so.18", "libnetcdf.so.15"})
         names.push_back(n);
     void* h = nullptr;
@@ -92,6 +103,7 @@ const NcApi& api()
         return a;
     }
     t.handle = h;
+    t.env = env;
     a = t;
     return a;
 }
@@ -213,7 +225,148 @@ void read_group(const NcApi& a, int grp, const std::string& path, Json& doc)
     }
 }
 
+// the writing subset (nc_create ... nc_close), loaded separately: a reader-only test double or an
+// old library still serves the data files
+struct NcWriteApi {
+    int (*create)(const char*, int, int*) = nullptr;
+    int (*def_grp)(int, const char*, int*) = nullptr;
+    int (*def_dim)(int, const char*, size_t, int*) = nullptr;
+    int (*def_var)(int, const char*, int, int, const int*, int*) = nullptr;
+    int (*put_vara_double)(int, int, const size_t*, const size_t*, const double*) = nullptr;
+    int (*put_vara_uint)(int, int, const size_t*, const size_t*, const unsigned int*) = nullptr;
+    int (*put_vara_string)(int, int, const size_t*, const size_t*, const char**) = nullptr;
+    int (*sync)(int) = nullptr;
+    int (*close)(int) = nullptr;
+    const char* (*strerror)(int) = nullptr;
+    bool ok = false;
+    void* handle = nullptr;  // the NcApi library these symbols come from
+};
+
+const NcWriteApi& wapi()
+{
+    static NcWriteApi w;
+    static std::mutex mu;
+    const NcApi& a = api();
+    std::lock_guard<std::mutex> lock(mu);
+    if (w.ok && w.handle == a.handle) return w;
+    w = NcWriteApi();
+    if (!a.handle) return w;
+    NcWriteApi t;
+    bool ok = true;
+    auto sym = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(a.handle, name));
+        ok &= fn != nullptr;
+    };
+    sym(t.create, "nc_create");
+    sym(t.def_grp, "nc_def_grp");
+    sym(t.def_dim, "nc_def_dim");
+    sym(t.def_var, "nc_def_var");
+    sym(t.put_vara_double, "nc_put_vara_double");
+    sym(t.put_vara_uint, "nc_put_vara_uint");
+    sym(t.put_vara_string, "nc_put_vara_string");
+    sym(t.sync, "nc_sync");
+    sym(t.close, "nc_close");
+    t.strerror = a.strerror;
+    t.ok = ok;
+    t.handle = a.handle;
+    if (ok) w = t;
+    return w;
+}
+
+bool wcheck(int rc, const std::string& what)
+{
+    if (rc == 0) return true;
+    const NcWriteApi& w = wapi();
+    LOGERROR("netCDF-4 output: %s: %s", what.c_str(), w.strerror ? w.strerror(rc) : std::to_string(rc).c_str());
+    return false;
+}
+
 }  // namespace
+
+bool NcNetCDF4WriteAvailable(std::string* why)
+{
+    std::string r;
+    const bool have = NcNetCDF4Available(&r) && wapi().ok;
+    if (why) *why = have ? "" : (r.empty() ? "the libnetcdf found cannot write (nc_create / nc_def_*)" : r);
+    if (have) {
+        // BCM3_OUTPUT_FORMAT=classic keeps the netCDF classic output even with libnetcdf present
+        const char* f = std::getenv("BCM3_OUTPUT_FORMAT");
+        if (f && std::string(f) == "classic") {
+            if (why) *why = "BCM3_OUTPUT_FORMAT=classic";
+            return false;
+        }
+    }
+    return have;
+}
+
+// NetCDFDataFile::Create / CreateGroup / CreateDimension / CreateVariable / PutValue(s)
+// (src/utils/NetCDFDataFile.cpp:117-260) over the run-time loaded library
+bool NcNetCDF4Writer::Create(const std::string& filename)
+{
+    Close();
+    const NcWriteApi& w = wapi();
+    if (!w.ok) return false;
+    filename_ = filename;
+    return wcheck(w.create(filename.c_str(), kNcClobber | kNcNetCDF4, &nc_), "nc_create " + filename);
+}
+
+int NcNetCDF4Writer::Group(const std::string& path)
+{
+    if (nc_ < 0) return -1;
+    if (path.empty()) return nc_;
+    auto it = groups_.find(path);
+    if (it != groups_.end()) return it->second;
+    const size_t slash = path.rfind('/');
+    const int parent = (slash == std::string::npos) ? nc_ : Group(path.substr(0, slash));
+    if (parent < 0) return -1;
+    int g = -1;
+    const std::string name = (slash == std::string::npos) ? path : path.substr(slash + 1);
+    if (!wcheck(wapi().def_grp(parent, name.c_str(), &g), "nc_def_grp " + path)) return -1;
+    groups_[path] = g;
+    return g;
+}
+
+int NcNetCDF4Writer::Dim(int grp, const std::string& name, size_t len)
+{
+    int d = -1;
+    return wcheck(wapi().def_dim(grp, name.c_str(), len, &d), "nc_def_dim " + name) ? d : -1;
+}
+
+int NcNetCDF4Writer::Var(int grp, const std::string& name, int type, const std::vector<int>& dims)
+{
+    int v = -1;
+    return wcheck(wapi().def_var(grp, name.c_str(), type, (int)dims.size(), dims.data(), &v), "nc_def_var " + name) ? v
+                                                                                                                       : -1;
+}
+
+bool NcNetCDF4Writer::PutDouble(int grp, int var, const std::vector<size_t>& start, const std::vector<size_t>& count,
+                                const double* data)
+{
+    return wcheck(wapi().put_vara_double(grp, var, start.data(), count.data(), data), "nc_put_vara_double");
+}
+
+bool NcNetCDF4Writer::PutUInt(int grp, int var, const std::vector<size_t>& start, const std::vector<size_t>& count,
+                              const uint32_t* data)
+{
+    return wcheck(wapi().put_vara_uint(grp, var, start.data(), count.data(), data), "nc_put_vara_uint");
+}
+
+bool NcNetCDF4Writer::PutStrings(int grp, int var, const std::vector<std::string>& s)
+{
+    std::vector<const char*> p;
+    for (auto& x : s) p.push_back(x.c_str());
+    const size_t start = 0, count = s.size();
+    return wcheck(wapi().put_vara_string(grp, var, &start, &count, p.data()), "nc_put_vara_string");
+}
+
+bool NcNetCDF4Writer::Sync() { return nc_ < 0 || wcheck(wapi().sync(nc_), "nc_sync"); }
+
+void NcNetCDF4Writer::Close()
+{
+    if (nc_ >= 0) wcheck(wapi().close(nc_), "nc_close " + filename_);
+    nc_ = -1;
+    groups_.clear();
+}
 
 bool NcNetCDF4Available(std::string* why)
 {

@@ -651,6 +651,9 @@ bool SampleFileWriter::Initialize(const std::string& filename, size_t num_sample
         LOGERROR("SampleFileWriter: inconsistent output geometry");
         return false;
     }
+    w4_.reset();
+    if (first_ == 0 && own_ == T && NcNetCDF4WriteAvailable(nullptr))
+        return InitializeNetCDF4(filename, names, transforms, temperatures);
     size_t strlen_max = 1;
     for (auto& s : names) strlen_max = std::max(strlen_max, s.size());
     NcHeader& h = w_.h;
@@ -698,10 +701,57 @@ bool SampleFileWriter::Initialize(const std::string& filename, size_t num_sample
     return true;
 }
 
+// SampleHandlerNetCDF::Initialize (SampleHandlerNetCDF.cpp:24-63) in the reference's own netCDF-4
+// layout: group samples; coordinate variables sample_ix (NC_UINT, 1..n), variable (NC_STRING, the
+// names), temperature (NC_DOUBLE); variable_transform (NC_UINT); variable_values [sample_ix]
+// [temperature][variable], log_prior / log_likelihood / weights [sample_ix][temperature] (NC_DOUBLE,
+// the library's default fill where nothing is written)
+bool SampleFileWriter::InitializeNetCDF4(const std::string& filename, const std::vector<std::string>& names,
+                                         const std::vector<int32_t>& transforms, const std::vector<double>& temperatures)
+{
+    auto w = std::make_unique<NcNetCDF4Writer>();
+    if (!w->Create(filename)) return false;
+    const int g = w->Group("samples");
+    if (g < 0) return false;
+    const size_t T = temperatures.size();
+    const int ds = w->Dim(g, "sample_ix", n_), dv = w->Dim(g, "variable", d_), dt = w->Dim(g, "temperature", T);
+    if (ds < 0 || dv < 0 || dt < 0) return false;
+    const int v_ix = w->Var(g, "sample_ix", Nc4UInt, {ds}), v_names = w->Var(g, "variable", Nc4String, {dv});
+    const int v_temp = w->Var(g, "temperature", Nc4Double, {dt});
+    const int v_tr = w->Var(g, "variable_transform", Nc4UInt, {dv});
+    v_vals_ = w->Var(g, "variable_values", Nc4Double, {ds, dt, dv});
+    v_lp_ = w->Var(g, "log_prior", Nc4Double, {ds, dt});
+    v_llh_ = w->Var(g, "log_likelihood", Nc4Double, {ds, dt});
+    v_w_ = w->Var(g, "weights", Nc4Double, {ds, dt});
+    if (v_ix < 0 || v_names < 0 || v_temp < 0 || v_tr < 0 || v_vals_ < 0 || v_lp_ < 0 || v_llh_ < 0 || v_w_ < 0)
+        return false;
+    std::vector<uint32_t> ix(n_), tr(d_);
+    for (size_t i = 0; i < n_; i++) ix[i] = (uint32_t)(i + 1);
+    for (size_t i = 0; i < d_; i++) tr[i] = (uint32_t)transforms[i];
+    if (!w->PutUInt(g, v_ix, {0}, {n_}, ix.data()) || !w->PutStrings(g, v_names, names) ||
+        !w->PutDouble(g, v_temp, {0}, {T}, temperatures.data()) || !w->PutUInt(g, v_tr, {0}, {d_}, tr.data()))
+        return false;
+    v_six_ = v_ix;
+    g4_ = g;
+    w4_ = std::move(w);
+    return true;
+}
+
 bool SampleFileWriter::Write(size_t sample_ix, size_t t0, size_t nt, const double* values, const double* lprior,
                              const double* llh, const double* weight)
 {
     if (sample_ix >= n_ || t0 + nt > own_) return false;
+    if (w4_) {
+        // SampleHandlerNetCDF::ReceiveSample (:75-110): sample_ix[si] = si (the reference's 0-based
+        // write over the 1-based coordinate), then the rows of these temperatures
+        const uint32_t si = (uint32_t)sample_ix;
+        const size_t t = t0;
+        return w4_->PutUInt(g4_, v_six_, {sample_ix}, {1}, &si) &&
+               w4_->PutDouble(g4_, v_vals_, {sample_ix, t, 0}, {1, nt, d_}, values) &&
+               w4_->PutDouble(g4_, v_lp_, {sample_ix, t}, {1, nt}, lprior) &&
+               w4_->PutDouble(g4_, v_llh_, {sample_ix, t}, {1, nt}, llh) &&
+               w4_->PutDouble(g4_, v_w_, {sample_ix, t}, {1, nt}, weight);
+    }
     const size_t t = first_ + t0;
     const int32_t si = (int32_t)sample_ix;
     return (first_ != 0 || w_.PutInt(v_six_, {sample_ix}, {1}, &si)) &&
@@ -746,8 +796,46 @@ void BundleFile::AddMatrix(const std::string& group, const std::string& name, si
     items_.push_back(std::move(it));
 }
 
+// NetCDFBundler::AddVector / AddMatrix (NetCDFBundler.cpp:34-80) on netCDF-4: per item the
+// dimension(s) <name>_dim or <name>_dim1 / _dim2 with NC_UINT coordinate variables 1..n
+// (NetCDFDataFile::CreateDimension) and an NC_DOUBLE variable (CreateVariable), in nested groups
+bool BundleFile::WriteNetCDF4(const std::string& filename) const
+{
+    NcNetCDF4Writer w;
+    if (!w.Create(filename)) return false;
+    auto coord = [&](int g, const std::string& name, size_t n) {
+        const int d = w.Dim(g, name, n);
+        if (d < 0) return -1;
+        const int v = w.Var(g, name, Nc4UInt, {d});
+        std::vector<uint32_t> c(n);
+        for (size_t k = 0; k < n; k++) c[k] = (uint32_t)(k + 1);
+        if (v < 0 || (n && !w.PutUInt(g, v, {0}, {n}, c.data()))) return -1;
+        return d;
+    };
+    for (const Item& it : items_) {
+        const int g = w.Group(it.group);
+        if (g < 0) return false;
+        if (it.cols == 0) {
+            const int d = coord(g, it.name + "_dim", it.rows);
+            const int v = (d < 0) ? -1 : w.Var(g, it.name, Nc4Double, {d});
+            if (v < 0) return false;
+            std::vector<double> x = it.d;
+            if (it.is_int) x.assign(it.i.begin(), it.i.end());
+            if (it.rows && !w.PutDouble(g, v, {0}, {it.rows}, x.data())) return false;
+        } else {
+            const int d1 = coord(g, it.name + "_dim1", it.rows), d2 = coord(g, it.name + "_dim2", it.cols);
+            const int v = (d1 < 0 || d2 < 0) ? -1 : w.Var(g, it.name, Nc4Double, {d1, d2});
+            if (v < 0) return false;
+            if (it.rows && it.cols && !w.PutDouble(g, v, {0, 0}, {it.rows, it.cols}, it.d.data())) return false;
+        }
+    }
+    w.Close();
+    return true;
+}
+
 bool BundleFile::Write(const std::string& filename) const
 {
+    if (NcNetCDF4WriteAvailable(nullptr)) return WriteNetCDF4(filename);
     NcClassicWriter w;
     std::vector<std::string> groups;
     for (auto& it : items_)

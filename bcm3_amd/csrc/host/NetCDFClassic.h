@@ -14,6 +14,8 @@
 #pragma once
 #include <cstdint>
 #include <cstdio>
+#include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -80,6 +82,33 @@ Json NcNetCDF4Read(const std::string& filename);
 // {"dims", "data"} variable records -> their data arrays, for the loaders that index arrays
 void UnwrapDataVariables(Json& doc);
 
+// netCDF-4 output through the run-time loaded libnetcdf (NetCDF4.cpp), as the reference writes
+// output.nc / sampler_adaptation.nc (NetCDFDataFile::Create, NC_CLOBBER | NC_NETCDF4). Unavailable
+// without a libnetcdf that has the writing API, or with BCM3_OUTPUT_FORMAT=classic.
+enum { Nc4Double = 6, Nc4UInt = 9, Nc4String = 12 };
+bool NcNetCDF4WriteAvailable(std::string* why);
+class NcNetCDF4Writer {
+public:
+    bool Create(const std::string& filename);
+    int Group(const std::string& path);  // nested groups by '/', created on first use; -1 on error
+    int Dim(int grp, const std::string& name, size_t len);
+    int Var(int grp, const std::string& name, int type, const std::vector<int>& dims);
+    bool PutDouble(int grp, int var, const std::vector<size_t>& start, const std::vector<size_t>& count,
+                   const double* data);
+    bool PutUInt(int grp, int var, const std::vector<size_t>& start, const std::vector<size_t>& count,
+                 const uint32_t* data);
+    bool PutStrings(int grp, int var, const std::vector<std::string>& s);
+    bool Sync();
+    void Close();
+    bool IsOpen() const { return nc_ >= 0; }
+    ~NcNetCDF4Writer() { Close(); }
+
+private:
+    int nc_ = -1;
+    std::string filename_;
+    std::map<std::string, int> groups_;
+};
+
 // Write: a fixed-size (non-record) CDF-2 file. Layout() assigns offsets; Create() writes the
 // header and, for the variables of `fill_vars` (all when empty), their fill values; Put()
 // writes a hyperslab [start, start+count) in row-major order, converting from double / int32 /
@@ -113,7 +142,9 @@ private:
 // it); values, log prior, log likelihood and weight per (sample, temperature), NC_FILL_DOUBLE
 // where nothing was received. `first_temperature` / `own` select the temperature columns this
 // process writes (a rank's ladder slice): each rank writes only its own columns of the shared
-// file.
+// file. A process that writes every temperature writes netCDF-4 with the group "samples" instead
+// (the reference's own format) when libnetcdf can be loaded (NcNetCDF4WriteAvailable); the shared
+// file of a sharded ladder stays classic (HDF5 files take one writer).
 class SampleFileWriter {
 public:
     bool Initialize(const std::string& filename, size_t num_samples, const std::vector<std::string>& names,
@@ -122,11 +153,21 @@ public:
     // rows of this process's temperatures (t0 relative to first_temperature): values [own][d]
     bool Write(size_t sample_ix, size_t t0, size_t nt, const double* values, const double* lprior,
                const double* llh, const double* weight);
-    bool Sync() { return w_.Sync(); }
-    void Close() { w_.Close(); }
+    bool Sync() { return w4_ ? w4_->Sync() : w_.Sync(); }
+    void Close()
+    {
+        if (w4_) w4_->Close();
+        w_.Close();
+    }
+    bool IsNetCDF4() const { return w4_ != nullptr; }
 
 private:
+    // one process writing every temperature: netCDF-4 when libnetcdf can be loaded
+    bool InitializeNetCDF4(const std::string& filename, const std::vector<std::string>& names,
+                           const std::vector<int32_t>& transforms, const std::vector<double>& temperatures);
     NcClassicWriter w_;
+    std::unique_ptr<NcNetCDF4Writer> w4_;
+    int g4_ = -1;
     int v_six_ = -1, v_vals_ = -1, v_lp_ = -1, v_llh_ = -1, v_w_ = -1;
     size_t first_ = 0, own_ = 0, d_ = 0, n_ = 0;
 };
@@ -141,9 +182,11 @@ public:
     void AddVector(const std::string& group, const std::string& name, const std::vector<int32_t>& v);
     void AddMatrix(const std::string& group, const std::string& name, size_t rows, size_t cols,
                    const std::vector<double>& row_major);
+    // netCDF-4 with nested groups (adapt<k>/block1) when libnetcdf can be loaded, classic otherwise
     bool Write(const std::string& filename) const;
 
 private:
+    bool WriteNetCDF4(const std::string& filename) const;
     struct Item {
         std::string group, name;
         bool is_int = false;

@@ -7,6 +7,7 @@
 #include "../../../include/bcm3hip.h"
 #include "Likelihood.h"
 #include "LikelihoodGPU.h"
+#include "NetCDFClassic.h"
 #include "Prior.h"
 #include "log.h"
 
@@ -218,5 +219,24 @@ int bcm3_likelihood_set_option(bcm3_likelihood* h, int option, int64_t value)
 }
 
 const char* bcm3_last_error(void) { return bcm3::log_last_error(); }
+
+int64_t bcm3_data_file_json(const char* filename, char* out, int64_t cap)
+{
+    if (!filename) return -1;
+    std::string text;
+    try {
+        bcm3::Json doc = bcm3::NcIsClassic(filename) ? bcm3::NcClassicRead(filename) : bcm3::LoadDataFile(filename);
+        text = bcm3::json_dump(doc);
+    } catch (bcm3::JsonError& e) {
+        LOGERROR("%s: %s", filename, e.what.c_str());
+        return -2;
+    }
+    if (out && cap > 0) {
+        const size_t n = std::min<size_t>((size_t)cap - 1, text.size());
+        std::memcpy(out, text.data(), n);
+        out[n] = '\0';
+    }
+    return (int64_t)text.size();
+}
 
 }  // extern "C"

@@ -2,6 +2,7 @@
 #include "json.h"
 
 #include <cctype>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <fstream>
@@ -201,6 +202,72 @@ Json json_load(const std::string& filename)
     std::stringstream ss;
     ss << f.rdbuf();
     return json_parse(ss.str());
+}
+
+namespace {
+void dump_to(const Json& j, std::string& o)
+{
+    switch (j.type) {
+    case Json::Null: o += "null"; break;
+    case Json::Bool: o += j.b ? "true" : "false"; break;
+    case Json::Number:
+        if (!std::isfinite(j.num)) {
+            o += "null";
+        } else {
+            char buf[32];
+            snprintf(buf, sizeof buf, "%.17g", j.num);
+            o += buf;
+        }
+        break;
+    case Json::String:
+        o += '"';
+        for (char c : j.str) {
+            if (c == '"' || c == '\\') {
+                o += '\\';
+                o += c;
+            } else if ((unsigned char)c < 0x20) {
+                char buf[8];
+                snprintf(buf, sizeof buf, "\\u%04x", (unsigned char)c);
+                o += buf;
+            } else {
+                o += c;
+            }
+        }
+        o += '"';
+        break;
+    case Json::Array:
+        o += '[';
+        for (size_t i = 0; i < j.arr.size(); i++) {
+            if (i) o += ',';
+            dump_to(j.arr[i], o);
+        }
+        o += ']';
+        break;
+    case Json::Object: {
+        o += '{';
+        bool first = true;
+        for (auto& kv : j.obj) {
+            if (!first) o += ',';
+            first = false;
+            Json k;
+            k.type = Json::String;
+            k.str = kv.first;
+            dump_to(k, o);
+            o += ':';
+            dump_to(kv.second, o);
+        }
+        o += '}';
+        break;
+    }
+    }
+}
+}  // namespace
+
+std::string json_dump(const Json& j)
+{
+    std::string o;
+    dump_to(j, o);
+    return o;
 }
 
 }  // namespace bcm3

@@ -28,5 +28,7 @@ struct JsonError {
 
 Json json_parse(const std::string& text);
 Json json_load(const std::string& filename);
+// compact text, numbers round-trip (%.17g), NaN / inf as null
+std::string json_dump(const Json& j);
 
 }  // namespace bcm3

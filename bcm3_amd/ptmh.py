@@ -236,6 +236,22 @@ class PTMHNative:
             pass
 
 
+def read_data_file(path: str) -> dict:
+    """A data or output file as libbcm3's loaders read it (bcm3_data_file_json): netCDF classic,
+    netCDF-4 through a run-time loaded libnetcdf, or the JSON sidecar -> {group: {variable:
+    {"dims": [...], "data": nested lists}}}, fill values as None."""
+    import json
+    L = _lib()
+    L.bcm3_data_file_json.argtypes = [C.c_char_p, C.c_char_p, C.c_int64]
+    L.bcm3_data_file_json.restype = C.c_int64
+    n = L.bcm3_data_file_json(path.encode(), None, 0)
+    if n < 0:
+        raise RuntimeError(f"bcm3_data_file_json failed ({n}): {host_lib().bcm3_last_error().decode()}")
+    buf = C.create_string_buffer(n + 1)
+    L.bcm3_data_file_json(path.encode(), buf, n + 1)
+    return json.loads(buf.value.decode())
+
+
 class SampleFile:
     """bcm3_samples_*: the reference's output.nc (SampleHandlerNetCDF.cpp:24-110) as a netCDF
     classic file written by libbcm3 (group members "samples.<name>"); a process writes the

@@ -84,6 +84,11 @@ int bcm3_likelihood_kernel_time_log(bcm3_likelihood* ll, double* total_ms, int64
 int bcm3_likelihood_set_option(bcm3_likelihood* ll, int option, int64_t value);
 
 const char* bcm3_last_error(void);
+/* A data or output file as the likelihoods' loaders see it (NetCDFDataFile::Open's role): netCDF
+ * classic, netCDF-4 through a run-time loaded libnetcdf, or the JSON sidecar, as JSON text
+ * {"<group>": {"<variable>": {"dims": [...], "data": nested arrays}}} (fill values -> null).
+ * Writes at most cap bytes (NUL-terminated) and returns the full length, < 0 on error. */
+int64_t bcm3_data_file_json(const char* filename, char* out, int64_t cap);
 
 /* ---- proposal adaptation (host C++, GMM.cpp) ----
  * SamplerPTChain::AdaptProposal (src/sampler/SamplerPTChain.cpp:120-178) for the C chains of a rank:

@@ -6,8 +6,12 @@
  *   G <parent group> <name>                          group (root = 0, then 1, 2, ... in order)
  *   D <name> <length>                                dimension (ids 0, 1, ... in order)
  *   V <group> <name> <type> <ndims> <dimids...> <has_fill> <fill> <count> <values...>
- * type 6 = double (values as numbers), 12 = string, 2 = char (values are strings, space-free).
- * Only the calls the reader makes are implemented; anything else returns an error code. */
+ * type 6 = double, 9 = unsigned int (values as numbers), 12 = string, 2 = char (values are strings,
+ * space-free). The writing calls NetCDF4.cpp makes for the sampler's output files (nc_create,
+ * nc_def_grp / _dim / _var, nc_put_vara_double / _uint / _string, nc_sync, nc_close) build the same
+ * model in memory and write it back as such a manifest; a value never written is the type's default
+ * fill (NC_FILL_DOUBLE 9.969209968386869e36, NC_FILL_UINT 4294967295). Anything else returns an
+ * error code. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -66,7 +70,7 @@ int nc_open(const char* path, int mode, int* ncidp)
             for (int k = 0; k < v->ndims; k++)
                 if (fscanf(f, "%d", &v->dims[k]) != 1) break;
             if (fscanf(f, "%d %lf %zu", &v->has_fill, &v->fill, &v->count) != 3) break;
-            if (v->type == 6) {
+            if (v->type == 6 || v->type == 9) {
                 v->num = calloc(v->count + 1, sizeof(double));
                 for (size_t i = 0; i < v->count; i++) {
                     char tok[64];
@@ -88,7 +92,16 @@ int nc_open(const char* path, int mode, int* ncidp)
     return 0;
 }
 
-int nc_close(int ncid) { (void)ncid; return 0; }
+static int write_manifest(void);
+static int writing;
+
+int nc_close(int ncid)
+{
+    (void)ncid;
+    if (!writing) return 0;
+    writing = 0;
+    return write_manifest();
+}
 
 int nc_inq_grps(int ncid, int* numgrps, int* ncids)
 {
@@ -156,7 +169,7 @@ int nc_inq_dim(int ncid, int dimid, char* name, size_t* lenp)
 int nc_get_var_double(int ncid, int varid, double* ip)
 {
     Var* v = var_of(ncid, varid);
-    if (!v || v->type != 6) return -56;
+    if (!v || (v->type != 6 && v->type != 9)) return -56;
     memcpy(ip, v->num, v->count * sizeof(double));
     return 0;
 }
@@ -209,4 +222,172 @@ const char* nc_strerror(int ncerr)
     static char buf[64];
     snprintf(buf, sizeof buf, "fake netCDF error %d", ncerr);
     return buf;
+}
+
+/* ---- writing ---- */
+static char wpath[4096];
+
+static size_t var_count(const Var* v)
+{
+    size_t n = 1;
+    for (int k = 0; k < v->ndims; k++) n *= dlen[v->dims[k]];
+    return n;
+}
+
+int nc_create(const char* path, int cmode, int* ncidp)
+{
+    if (!(cmode & 0x1000)) return -128; /* only NC_NETCDF4 */
+    for (int i = 0; i < nv; i++) {
+        free(vars[i].num);
+        if (vars[i].str)
+            for (size_t k = 0; k < vars[i].count; k++) free(vars[i].str[k]);
+        free(vars[i].str);
+    }
+    ng = 1;
+    nd = nv = 0;
+    gparent[0] = -1;
+    strcpy(gname[0], "/");
+    snprintf(wpath, sizeof wpath, "%s", path);
+    writing = 1;
+    *ncidp = 65536;
+    return 0;
+}
+
+int nc_def_grp(int parent_ncid, const char* name, int* new_ncid)
+{
+    if (ng >= MAXG) return -1;
+    gparent[ng] = gid(parent_ncid);
+    snprintf(gname[ng], sizeof gname[ng], "%s", name);
+    *new_ncid = (ng + 1) * 65536;
+    ng++;
+    return 0;
+}
+
+int nc_def_dim(int ncid, const char* name, size_t len, int* idp)
+{
+    (void)ncid;
+    if (nd >= MAXD) return -1;
+    snprintf(dname[nd], sizeof dname[nd], "%s", name);
+    dlen[nd] = len;
+    *idp = nd++;
+    return 0;
+}
+
+int nc_def_var(int ncid, const char* name, int xtype, int ndims, const int* dimidsp, int* varidp)
+{
+    if (nv >= MAXV || ndims > 8 || (xtype != 6 && xtype != 9 && xtype != 12)) return -1;
+    int g = gid(ncid), k = 0;
+    for (int i = 0; i < nv; i++)
+        if (vars[i].group == g) k++;
+    Var* v = &vars[nv++];
+    memset(v, 0, sizeof(*v));
+    v->group = g;
+    v->type = xtype;
+    v->ndims = ndims;
+    for (int d = 0; d < ndims; d++) v->dims[d] = dimidsp[d];
+    snprintf(v->name, sizeof v->name, "%s", name);
+    v->count = var_count(v);
+    if (xtype == 12) {
+        v->str = calloc(v->count + 1, sizeof(char*));
+        for (size_t i = 0; i < v->count; i++) v->str[i] = strdup("");
+    } else {
+        v->num = calloc(v->count + 1, sizeof(double));
+        for (size_t i = 0; i < v->count; i++) v->num[i] = (xtype == 6) ? 9.9692099683868690e+36 : 4294967295.0;
+    }
+    *varidp = k;
+    return 0;
+}
+
+/* row-major offset of each element of the hyperslab, in order */
+static int slab(const Var* v, const size_t* start, const size_t* count, size_t* n, size_t** offs)
+{
+    size_t total = 1;
+    for (int k = 0; k < v->ndims; k++) {
+        if (start[k] + count[k] > dlen[v->dims[k]]) return -40; /* NC_EEDGE */
+        total *= count[k];
+    }
+    size_t* o = malloc((total + 1) * sizeof(size_t));
+    size_t idx[8] = {0};
+    for (size_t e = 0; e < total; e++) {
+        size_t off = 0;
+        for (int k = 0; k < v->ndims; k++) off = off * dlen[v->dims[k]] + start[k] + idx[k];
+        o[e] = off;
+        for (int k = v->ndims - 1; k >= 0; k--) {
+            if (++idx[k] < count[k]) break;
+            idx[k] = 0;
+        }
+    }
+    *n = total;
+    *offs = o;
+    return 0;
+}
+
+int nc_put_vara_double(int ncid, int varid, const size_t* startp, const size_t* countp, const double* op)
+{
+    Var* v = var_of(ncid, varid);
+    size_t n, *o;
+    if (!v || v->type != 6) return -56;
+    int r = slab(v, startp, countp, &n, &o);
+    if (r) return r;
+    for (size_t e = 0; e < n; e++) v->num[o[e]] = op[e];
+    free(o);
+    return 0;
+}
+
+int nc_put_vara_uint(int ncid, int varid, const size_t* startp, const size_t* countp, const unsigned int* op)
+{
+    Var* v = var_of(ncid, varid);
+    size_t n, *o;
+    if (!v || v->type != 9) return -56;
+    int r = slab(v, startp, countp, &n, &o);
+    if (r) return r;
+    for (size_t e = 0; e < n; e++) v->num[o[e]] = (double)op[e];
+    free(o);
+    return 0;
+}
+
+int nc_put_vara_string(int ncid, int varid, const size_t* startp, const size_t* countp, const char** op)
+{
+    Var* v = var_of(ncid, varid);
+    size_t n, *o;
+    if (!v || v->type != 12) return -56;
+    int r = slab(v, startp, countp, &n, &o);
+    if (r) return r;
+    for (size_t e = 0; e < n; e++) {
+        free(v->str[o[e]]);
+        v->str[o[e]] = strdup(op[e]);
+    }
+    free(o);
+    return 0;
+}
+
+static int write_manifest(void)
+{
+    FILE* f = fopen(wpath, "wb");
+    if (!f) return -31;
+    static const char sig[] = "\x89HDF\r\n\x1a\n fake netCDF-4 written by tests/plugins/fake_netcdf.c\n";
+    fwrite(sig, 1, sizeof sig - 1, f);
+    for (int i = 1; i < ng; i++) fprintf(f, "G %d %s\n", gparent[i], gname[i]);
+    for (int i = 0; i < nd; i++) fprintf(f, "D %s %zu\n", dname[i], dlen[i]);
+    for (int i = 0; i < nv; i++) {
+        const Var* v = &vars[i];
+        fprintf(f, "V %d %s %d %d", v->group, v->name, v->type, v->ndims);
+        for (int k = 0; k < v->ndims; k++) fprintf(f, " %d", v->dims[k]);
+        fprintf(f, " 0 0 %zu", v->count);
+        for (size_t e = 0; e < v->count; e++) {
+            if (v->type == 12)
+                fprintf(f, " %s", v->str[e][0] ? v->str[e] : "-");
+            else
+                fprintf(f, " %.17g", v->num[e]);
+        }
+        fprintf(f, "\n");
+    }
+    fclose(f);
+    return 0;
+}
+
+int nc_sync(int ncid)
+{
+    (void)ncid;
+    return writing ? write_manifest() : 0;
 }

@@ -320,3 +320,66 @@ def test_netcdf4_cellpop_through_libnetcdf(tmp_path, monkeypatch):
     p.write_text(F.likelihood_text(num_cells=16, max_cells=16, data_file=nc4, data_xml=data,
                                    model_file=os.path.join(GOLDEN, "cellpop_model.xml"), experiment_attrs=' divide_cells="false"'))
     _lik(str(p), "cellpop")
+
+
+def _manifest_types(path):
+    """{group path: {variable: type}} of a file the test double wrote (its manifest lines)"""
+    lines = open(path, "rb").read()[8:].split(b"\n", 1)[1].decode().split("\n")  # past the HDF5 signature line
+    gname, gparent, out = {0: ""}, {}, {}
+    gi = 1
+    for ln in lines:
+        t = ln.split()
+        if not t:
+            continue
+        if t[0] == "G":
+            par = int(t[1])
+            gname[gi] = (gname[par] + "/" if gname[par] else "") + t[2]
+            gi += 1
+        elif t[0] == "V":
+            out.setdefault(gname[int(t[1])], {})[t[2]] = int(t[3])
+    return out
+
+
+def test_sample_file_netcdf4_through_libnetcdf(tmp_path, monkeypatch):
+    """with libnetcdf loadable, a process writing every temperature writes output.nc as netCDF-4 as
+    the reference does (NetCDFDataFile::Create, NC_CLOBBER | NC_NETCDF4; SampleHandlerNetCDF.cpp:24-110):
+    group samples, NC_UINT sample_ix / variable_transform, NC_STRING variable, NC_DOUBLE data; the
+    same content as the classic file written without it (BCM3_OUTPUT_FORMAT=classic)"""
+    from bcm3_amd.ptmh import SampleFile, read_data_file
+    names = ["ka", "CL", "long_variable_name"]
+    temps = [0.0, 0.1, 0.4, 0.7, 1.0]
+    rng = np.random.default_rng(5)
+    N = 6
+    vals = rng.normal(size=(N, 5, 3))
+    lp, llh = rng.normal(size=(N, 5)), rng.normal(size=(N, 5))
+
+    def write(path):
+        f = SampleFile(path, N, names, [1, 2, 0], temps)
+        for s in range(5):
+            f.write(s, 0, vals[s], lp[s], llh[s], weight=np.full(5, 0.25))
+        f.close()
+
+    monkeypatch.setenv("BCM3_LIBNETCDF", _fake_netcdf(tmp_path))
+    nc4 = str(tmp_path / "output4.nc")
+    write(nc4)
+    assert open(nc4, "rb").read(8) == b"\x89HDF\r\n\x1a\n"
+    types = _manifest_types(nc4)["samples"]
+    assert types == {"sample_ix": 9, "variable": 12, "temperature": 6, "variable_transform": 9,
+                     "variable_values": 6, "log_prior": 6, "log_likelihood": 6, "weights": 6}
+    d4 = read_data_file(nc4)["samples"]
+    monkeypatch.setenv("BCM3_OUTPUT_FORMAT", "classic")
+    nc3 = str(tmp_path / "output3.nc")
+    write(nc3)
+    d3 = read_data_file(nc3)["samples"]
+    assert set(d4) == set(d3) - {"variable_strlen"}
+    for k in d4:
+        assert d4[k]["dims"] == d3[k]["dims"], k
+        assert d4[k]["data"] == d3[k]["data"], k
+    assert d4["variable"]["data"] == names and d4["sample_ix"]["data"] == [0, 1, 2, 3, 4, 6]
+    assert d4["variable_values"]["data"][5][0][0] is None  # never written: the library's fill
+    assert np.array_equal(np.array(d4["variable_values"]["data"][:5], dtype=float), vals[:5])
+    # libnetcdf gone ($BCM3_LIBNETCDF unset, none installed): classic output again
+    monkeypatch.delenv("BCM3_OUTPUT_FORMAT")
+    monkeypatch.delenv("BCM3_LIBNETCDF")
+    write(nc3)
+    assert open(nc3, "rb").read(3) == b"CDF"

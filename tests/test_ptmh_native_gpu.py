@@ -234,6 +234,47 @@ def test_adaptation_output_file(tmp_path):
     assert "adapt3.block1.gmm_weights" not in v
 
 
+def test_netcdf4_outputs_through_libnetcdf(tmp_path, monkeypatch):
+    """with libnetcdf loadable (the test double tests/plugins/fake_netcdf.c here) the sampler writes
+    output.nc and sampler_adaptation.nc as netCDF-4, as the reference does (NetCDFDataFile::Create,
+    NC_CLOBBER | NC_NETCDF4): real groups samples and adapt<k>/block1, the same content as the
+    classic files of the same run"""
+    import subprocess
+    from bcm3_amd.ptmh import read_data_file
+    so = str(tmp_path / "libfake_netcdf.so")
+    subprocess.run(["gcc", "-O1", "-shared", "-fPIC", "-o", so, os.path.join(os.path.dirname(H.GOLDEN), "plugins", "fake_netcdf.c")],
+                   check=True)
+
+    def run(tag):
+        s = _native(*C2, 16, 6, 0, adapt_proposal_samples=40, adapt_proposal_times=2)
+        out, ad = str(tmp_path / f"output_{tag}.nc"), str(tmp_path / f"adapt_{tag}.nc")
+        s.set_output(out, 130, flush_every=16)
+        s.set_adaptation_output(ad)
+        s.iterate(130)
+        s.synchronize()
+        s.flush_output()
+        s.close()
+        return out, ad
+
+    monkeypatch.setenv("BCM3_LIBNETCDF", so)
+    out4, ad4 = run("4")
+    monkeypatch.setenv("BCM3_OUTPUT_FORMAT", "classic")
+    out3, ad3 = run("3")
+    monkeypatch.setenv("BCM3_OUTPUT_FORMAT", "auto")
+    for p in (out4, ad4):
+        assert open(p, "rb").read(8) == b"\x89HDF\r\n\x1a\n", p
+    a4, a3 = read_data_file(out4), read_data_file(out3)
+    assert a4["samples"]["variable_values"] == {k: v for k, v in a3["samples"]["variable_values"].items()}
+    for k in ("log_prior", "log_likelihood", "weights", "sample_ix", "variable", "temperature"):
+        assert a4["samples"][k]["data"] == a3["samples"][k]["data"], k
+    b4, b3 = read_data_file(ad4), read_data_file(ad3)
+    groups = sorted(g for g in b4 if g)
+    assert groups == ["adapt0.block1", "adapt1.block1", "adapt2.block1"] and groups == sorted(g for g in b3 if g)
+    for g in groups:
+        for k, v in b4[g].items():
+            assert v["dims"] == b3[g][k]["dims"] and v["data"] == b3[g][k]["data"], (g, k)
+
+
 @pytest.mark.parametrize("proposal,C,t_dof", [("gaussian_mixture", 64, 0.0), ("global_covariance", 64, 0.0),
                                               ("gaussian_mixture_adjustedAIC", 63, 0.0), ("gaussian_mixture", 32, 5.0)])
 def test_speculative_pairs_bit_identical(tmp_path, proposal, C, t_dof):
