@@ -270,7 +270,7 @@ struct SamplerPTDevice::Impl {
     DevBuf<int32_t> sp_cand_sel, sp_cand_upd, sp_cand_steps, sp_steps_hint, sp_steps_prop, sp_batch_status,
         sp_batch_steps, sp_batch_src, sp_batch_n, sp_err;
     DevBuf<int64_t> sp_total;  // entries of all speculative batches (bcm3hip_spec::batch_total)
-    DevBuf<uint8_t> sp_cand_active, acc_mut, acc_exc;
+    DevBuf<uint8_t> sp_cand_active, acc_mut, acc_mut2, acc_exc;
     DevBuf<int32_t> partner[2], pair_first[2];
     DevBuf<double> sp_send_last, sp_send_first, sp_remote;  // boundary rows [state | proposal] of a sharded ladder
     DevBuf<uint8_t> cross_acc;
@@ -631,13 +631,34 @@ struct SamplerPTDevice::Impl {
     // exchange r+1 can leave in each slot), one launch over r's proposals and the candidates, accept
     // r; exchange r+1, select the candidate that happened, accept r+1. The same kernels' arithmetic
     // on the same counter-based random numbers as two IterationOnce calls.
+    // an exchange round of a pair and its dispatch-order tracking: on one rank whose pairs cover every
+    // chain once, the exchange, the tracking and the history adds in one launch (spec_exchange)
+    bool PairExchange()
+    {
+        const int st = (int)(round % 2);
+        if (cfg.world == 1 && mask_all[st] && Ctot >= 2) {
+            const bool wrap_local = (Ctot - 1 - st) % 2 == 0;
+            int64_t attempted = wrap_local ? 1 : 0;
+            for (int64_t i = 0; i + 1 < C; i++)
+                if (((g0 + i - st) % 2 + 2) % 2 == 0) attempted++;
+            if (!Launch(bcm3hip_ptmh_spec_exchange((int)C, d, g0, st, wrap_local ? 1 : 0, temps.p, values.p, llh.p,
+                                                   lprior.p, lpp.p, acc_exc.p, acc_exchange.p, cfg.seed,
+                                                   (uint64_t)round, partner[st].p, pair_first[st].p, &S, H, sub,
+                                                   adaptive ? hist.p : nullptr, hcount.p, stream),
+                        "ptmh_spec_exchange"))
+                return false;
+            cnt.attempted_exchange += attempted;
+            round++;
+            return true;
+        }
+        return Exchange(acc_exc.p, cross_acc.p) &&
+               Launch(bcm3hip_ptmh_spec_track((int)C, nullptr, partner[st].p, pair_first[st].p, acc_exc.p, &S, stream),
+                      "ptmh_spec_track");
+    }
+
     bool IterationPair(bool last)
     {
-        const int cur = (int)(round % 2);  // start parity of exchange round r
-        if (!Exchange(acc_exc.p, cross_acc.p) ||
-            !Launch(bcm3hip_ptmh_spec_track((int)C, nullptr, partner[cur].p, pair_first[cur].p, acc_exc.p, &S, stream),
-                    "ptmh_spec_track"))
-            return false;
+        if (!PairExchange()) return false;
         const int nxt = (int)(round % 2);  // start parity of exchange round r + 1
         if (!Launch(bcm3hip_ptmh_propose_adaptive((int)C, d, pkind.p, p0.p, p1.p, p2.p, temps.p, values.p, prop.p,
                                                   lprior_prop.p, log_mh.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
@@ -675,34 +696,27 @@ struct SamplerPTDevice::Impl {
             LOGERROR("EvaluateLogProbabilityBatchDeviceCounted failed");
             return false;
         }
+        // accept r, its dispatch-order tracking and the history add in one launch (spec_commit)
         if (!Launch(bcm3hip_ptmh_spec_scatter((int)C, &S, llh_prop.p, stream), "ptmh_spec_scatter") ||
-            !Launch(bcm3hip_ptmh_accept_adaptive((int)C, d, temps.p, prop.p, lprior_prop.p, llh_prop.p, log_mh.p,
-                                                 cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, acc_mut.p,
-                                                 acc_mutate.p, nan_flag.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
-                    "ptmh_accept_adaptive") ||
-            !Launch(bcm3hip_ptmh_spec_track((int)C, acc_mut.p, nullptr, nullptr, nullptr, &S, stream),
-                    "ptmh_spec_track") ||
-            !HistoryAdd(nullptr))
+            !Launch(bcm3hip_ptmh_spec_commit((int)C, d, 0, temps.p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                             &S, prop.p, lprior_prop.p, log_mh.p, llh_prop.p, cfg.learning_rate,
+                                             values.p, lprior.p, llh.p, lpp.p, acc_mut.p, acc_mutate.p, nan_flag.p, &P,
+                                             g0, cfg.seed, (uint64_t)iter, H, sub, hist.p, hcount.p, sp_err.p, stream),
+                    "ptmh_spec_commit"))
             return false;
         cnt.attempted_mutate += C;
         iter++;
         if (!PostIteration(false)) return false;
         // iteration r + 1
-        if (!Exchange(acc_exc.p, cross_acc.p) ||
-            !Launch(bcm3hip_ptmh_spec_track((int)C, nullptr, partner[nxt].p, pair_first[nxt].p, acc_exc.p, &S, stream),
-                    "ptmh_spec_track"))
-            return false;
-        if (!Launch(bcm3hip_ptmh_spec_select((int)C, d, temps.p, partner[nxt].p, pair_first[nxt].p, acc_mut.p,
-                                             acc_exc.p, cross_acc.p, sp_remote.p, values.p, &S, prop.p, lprior_prop.p,
-                                             log_mh.p, llh_prop.p, &P, sp_err.p, stream),
-                    "ptmh_spec_select") ||
-            !Launch(bcm3hip_ptmh_accept_adaptive((int)C, d, temps.p, prop.p, lprior_prop.p, llh_prop.p, log_mh.p,
-                                                 cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, acc_mut.p,
-                                                 acc_mutate.p, nan_flag.p, &P, g0, cfg.seed, (uint64_t)iter, stream),
-                    "ptmh_accept_adaptive") ||
-            !Launch(bcm3hip_ptmh_spec_track((int)C, acc_mut.p, nullptr, nullptr, nullptr, &S, stream),
-                    "ptmh_spec_track") ||
-            !HistoryAdd(nullptr))
+        if (!PairExchange()) return false;
+        // select the candidate that happened, accept r + 1, tracking, history: one launch (the accept
+        // flags of r + 1 go to acc_mut2, select reads r's from acc_mut)
+        if (!Launch(bcm3hip_ptmh_spec_commit((int)C, d, 1, temps.p, partner[nxt].p, pair_first[nxt].p, acc_mut.p,
+                                             acc_exc.p, cross_acc.p, sp_remote.p, &S, prop.p, lprior_prop.p, log_mh.p,
+                                             llh_prop.p, cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p, acc_mut2.p,
+                                             acc_mutate.p, nan_flag.p, &P, g0, cfg.seed, (uint64_t)iter, H, sub, hist.p,
+                                             hcount.p, sp_err.p, stream),
+                    "ptmh_spec_commit"))
             return false;
         cnt.attempted_mutate += C;
         iter++;
@@ -747,6 +761,7 @@ struct SamplerPTDevice::Impl {
                   sp_steps_hint.alloc(C) && sp_steps_prop.alloc(C) && sp_batch_x.alloc(N * d) &&
                   sp_batch_llh.alloc(N) && sp_batch_status.alloc(N) && sp_batch_steps.alloc(N) &&
                   sp_batch_src.alloc(N) && sp_batch_n.alloc(1) && sp_err.alloc(1) && acc_mut.alloc(C) &&
+                  acc_mut2.alloc(C) &&
                   acc_exc.alloc(C) && sp_send_last.alloc(2 * d) && sp_send_first.alloc(2 * d) &&
                   sp_remote.alloc(4 * d) && cross_acc.alloc(2) && sp_pred.alloc(N) && sp_inv_scale.alloc(d) &&
                   sp_total.alloc(1);

@@ -29,6 +29,7 @@
 #include "../../include/bcm3hip.h"
 #include "ctr_rng.h"
 #include "prior_marginal.h"
+#include "pt_exchange.h"
 
 namespace bcm3hip {
 namespace {
@@ -662,18 +663,15 @@ __global__ void __launch_bounds__(64) ptmh_propose_adaptive_kernel(
                   iter, work + 2 * Km, work + 2 * Km + d, work, work + Km);
 }
 
-__global__ void ptmh_accept_adaptive_kernel(int C, int d, const double* __restrict__ temps,
-                                            const double* __restrict__ prop, const double* __restrict__ lprior_prop,
-                                            const double* __restrict__ llh_prop, const double* __restrict__ log_mh,
-                                            double learning_rate, double* __restrict__ values,
-                                            double* __restrict__ lprior, double* __restrict__ llh,
-                                            double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
-                                            unsigned long long* __restrict__ accepted,
-                                            int32_t* __restrict__ nan_llh, bcm3hip_proposal P, int64_t chain0,
-                                            uint64_t seed, uint64_t iter)
+// Sampler::TestSample / MutateMove's accept of chain c (one thread per chain); returns the flag
+__device__ bool accept_one(int c, int d, const double* __restrict__ temps, const double* __restrict__ prop,
+                           const double* __restrict__ lprior_prop, const double* __restrict__ llh_prop,
+                           const double* __restrict__ log_mh, double learning_rate, double* __restrict__ values,
+                           double* __restrict__ lprior, double* __restrict__ llh, double* __restrict__ lpp,
+                           uint8_t* __restrict__ acc_out, unsigned long long* __restrict__ accepted,
+                           int32_t* __restrict__ nan_llh, const bcm3hip_proposal& P, int64_t chain0, uint64_t seed,
+                           uint64_t iter)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
     const double T = temps[c];
     const double nl = llh_prop[c] * learning_rate;  // Sampler::EvaluateLikelihood
     const double nq = lprior_prop[c];
@@ -711,16 +709,31 @@ __global__ void ptmh_accept_adaptive_kernel(int C, int d, const double* __restri
     }
     if (acc_out) acc_out[c] = acc ? 1 : 0;
     if (accepted && acc) atomicAdd(accepted, 1ull);
+    return acc;
+}
+
+__global__ void ptmh_accept_adaptive_kernel(int C, int d, const double* __restrict__ temps,
+                                            const double* __restrict__ prop, const double* __restrict__ lprior_prop,
+                                            const double* __restrict__ llh_prop, const double* __restrict__ log_mh,
+                                            double learning_rate, double* __restrict__ values,
+                                            double* __restrict__ lprior, double* __restrict__ llh,
+                                            double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
+                                            unsigned long long* __restrict__ accepted,
+                                            int32_t* __restrict__ nan_llh, bcm3hip_proposal P, int64_t chain0,
+                                            uint64_t seed, uint64_t iter)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    accept_one(c, d, temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values, lprior, llh, lpp, acc_out,
+               accepted, nan_llh, P, chain0, seed, iter);
 }
 
 // SampleHistory::AddSample for the chains with T != 0 (and mask[c] != 0 when a mask is given):
 // every `subsampling`-th call stores the values as float in slot n % H of the chain's ring
-__global__ void history_add_kernel(int C, int d, int H, int subsampling, const double* __restrict__ temps,
-                                   const double* __restrict__ values, const uint8_t* __restrict__ mask,
-                                   float* __restrict__ hist, int64_t* __restrict__ counters)
+__device__ void history_one(int c, int d, int H, int subsampling, const double* __restrict__ temps,
+                            const double* __restrict__ values, const uint8_t* __restrict__ mask,
+                            float* __restrict__ hist, int64_t* __restrict__ counters)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
     if (temps[c] == 0.0 || (mask && !mask[c])) return;
     int64_t* n = counters + 2 * (int64_t)c;
     n[1]++;
@@ -730,6 +743,15 @@ __global__ void history_add_kernel(int C, int d, int H, int subsampling, const d
         n[0]++;
         n[1] = 0;
     }
+}
+
+__global__ void history_add_kernel(int C, int d, int H, int subsampling, const double* __restrict__ temps,
+                                   const double* __restrict__ values, const uint8_t* __restrict__ mask,
+                                   float* __restrict__ hist, int64_t* __restrict__ counters)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    history_one(c, d, H, subsampling, temps, values, mask, hist, counters);
 }
 
 // ---- speculative iteration pairs (include/bcm3hip.h "speculative iteration pairs") ----
@@ -1008,16 +1030,13 @@ __global__ void ptmh_spec_scatter_kernel(int C, bcm3hip_spec S, double* __restri
 }
 
 // one thread per chain: the candidate that the accept of r and the exchange of r + 1 made real
-__global__ void ptmh_spec_select_kernel(int C, int d, const double* __restrict__ temps,
-                                        const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first,
-                                        const uint8_t* __restrict__ acc_mut, const uint8_t* __restrict__ acc_exc,
-                                        const uint8_t* __restrict__ cross_acc, const double* __restrict__ remote,
-                                        const double* __restrict__ values, bcm3hip_spec S, double* __restrict__ prop,
-                                        double* __restrict__ lprior_prop, double* __restrict__ log_mh,
-                                        double* __restrict__ llh_prop, bcm3hip_proposal P, int32_t* __restrict__ error)
+__device__ void select_one(int c, int d, const double* __restrict__ temps, const int32_t* __restrict__ partner,
+                           const int32_t* __restrict__ pair_first, const uint8_t* __restrict__ acc_mut,
+                           const uint8_t* __restrict__ acc_exc, const uint8_t* __restrict__ cross_acc,
+                           const double* __restrict__ remote, const double* __restrict__ values, const bcm3hip_spec& S,
+                           double* __restrict__ prop, double* __restrict__ lprior_prop, double* __restrict__ log_mh,
+                           double* __restrict__ llh_prop, const bcm3hip_proposal& P, int32_t* __restrict__ error)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
     int k = 0;
     const bool hot = temps[c] != 0.0;
     if (hot) {
@@ -1065,6 +1084,49 @@ __global__ void ptmh_spec_select_kernel(int C, int d, const double* __restrict__
     }
 }
 
+__global__ void ptmh_spec_select_kernel(int C, int d, const double* __restrict__ temps,
+                                        const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first,
+                                        const uint8_t* __restrict__ acc_mut, const uint8_t* __restrict__ acc_exc,
+                                        const uint8_t* __restrict__ cross_acc, const double* __restrict__ remote,
+                                        const double* __restrict__ values, bcm3hip_spec S, double* __restrict__ prop,
+                                        double* __restrict__ lprior_prop, double* __restrict__ log_mh,
+                                        double* __restrict__ llh_prop, bcm3hip_proposal P, int32_t* __restrict__ error)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    select_one(c, d, temps, partner, pair_first, acc_mut, acc_exc, cross_acc, remote, values, S, prop, lprior_prop,
+               log_mh, llh_prop, P, error);
+}
+
+// The end of one iteration of a speculative pair in ONE launch, one thread per chain: [select
+// (iteration r + 1)], accept, the dispatch-order tracking of the accept, SampleHistory::AddSample --
+// per chain the operations of ptmh_spec_select / ptmh_accept_adaptive / ptmh_spec_track_accept /
+// history_add in that order. Every write is to the thread's own chain; the one cross-chain read, the
+// partner's accept flag of iteration r in select, comes from acc_prev, never from acc_out.
+__global__ void ptmh_spec_commit_kernel(int C, int d, int select, const double* __restrict__ temps,
+                                        const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first,
+                                        const uint8_t* __restrict__ acc_prev, const uint8_t* __restrict__ acc_exc,
+                                        const uint8_t* __restrict__ cross_acc, const double* __restrict__ remote,
+                                        bcm3hip_spec S, double* __restrict__ prop, double* __restrict__ lprior_prop,
+                                        double* __restrict__ log_mh, double* __restrict__ llh_prop,
+                                        double learning_rate, double* __restrict__ values, double* __restrict__ lprior,
+                                        double* __restrict__ llh, double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
+                                        unsigned long long* __restrict__ accepted, int32_t* __restrict__ nan_llh,
+                                        bcm3hip_proposal P, int64_t chain0, uint64_t seed, uint64_t iter, int H,
+                                        int subsampling, float* __restrict__ hist, int64_t* __restrict__ counters,
+                                        int32_t* __restrict__ error)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    if (select)
+        select_one(c, d, temps, partner, pair_first, acc_prev, acc_exc, cross_acc, remote, values, S, prop, lprior_prop,
+                   log_mh, llh_prop, P, error);
+    const bool acc = accept_one(c, d, temps, prop, lprior_prop, llh_prop, log_mh, learning_rate, values, lprior, llh,
+                                lpp, acc_out, accepted, nan_llh, P, chain0, seed, iter);
+    if (acc) S.steps_hint[c] = S.steps_prop[c];
+    if (hist) history_one(c, d, H, subsampling, temps, values, nullptr, hist, counters);
+}
+
 // dispatch-order bookkeeping of the pairs: steps_hint[c] = BDF steps of the solve of the state now in
 // slot c; after an accept (acc[c]: the proposal, whose steps are steps_prop[c], became the state) ...
 __global__ void ptmh_spec_track_accept_kernel(int C, const uint8_t* __restrict__ acc, bcm3hip_spec S)
@@ -1089,6 +1151,41 @@ __global__ void __launch_bounds__(1024) ptmh_spec_track_exchange_kernel(int C, c
     __syncthreads();
     n = 0;
     for (int c = threadIdx.x; c < C && n < 4; c += blockDim.x, n++) S.steps_hint[c] = v[n];
+}
+
+// One exchange round of a single-rank ladder whose pairs cover every chain exactly once, with what
+// follows it in a speculative pair, in ONE workgroup: the local pairs (pt_exchange_kernel), the wrap
+// pair after them, the dispatch-order tracking of the round (ptmh_spec_track_exchange_kernel) and
+// SampleHistory::AddSample of every chain (ExchangeMove adds both chains of each pair,
+// SamplerPTChain.cpp:374-379; history_add_kernel) -- the same per-chain operations in the same order.
+__global__ void __launch_bounds__(1024) ptmh_spec_exchange_kernel(
+    int C, int d, int64_t g0, int start, int wrap_local, const double* temps, double* values, double* llh,
+    double* lprior, double* lpp, uint8_t* acc_mask, unsigned long long* accepted, uint64_t seed, uint64_t round,
+    const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first, bcm3hip_spec S, int H,
+    int subsampling, float* __restrict__ hist, int64_t* __restrict__ counters)
+{
+    const int par = (int)(((g0 - start) % 2 + 2) % 2);
+    for (int p = threadIdx.x;; p += blockDim.x) {
+        const int i = par + 2 * p;
+        if (i + 1 >= C) break;
+        exchange_pair(d, i, i + 1, g0 + i, temps, values, llh, lprior, lpp, acc_mask, accepted, seed, round);
+    }
+    __syncthreads();
+    if (wrap_local && threadIdx.x == 0)
+        exchange_pair(d, C - 1, 0, g0 + C - 1, temps, values, llh, lprior, lpp, acc_mask, accepted, seed, round);
+    __syncthreads();
+    int v[4];
+    int n = 0;
+    for (int c = threadIdx.x; c < C && n < 4; c += blockDim.x, n++) {
+        const int p = partner[c];
+        v[n] = (p >= 0 && acc_mask[pair_first[c]]) ? S.steps_hint[p] : S.steps_hint[c];
+    }
+    __syncthreads();
+    n = 0;
+    for (int c = threadIdx.x; c < C && n < 4; c += blockDim.x, n++) {
+        S.steps_hint[c] = v[n];
+        if (hist) history_one(c, d, H, subsampling, temps, values, nullptr, hist, counters);
+    }
 }
 
 bool proposal_ok(const bcm3hip_proposal* P, int C, int d)
@@ -1206,6 +1303,43 @@ int bcm3hip_ptmh_spec_select(int C, int d, const double* temps, const int32_t* p
     hipLaunchKernelGGL(ptmh_spec_select_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d, temps,
                        partner, pair_first, acc_mutate, acc_exchange, cross_acc, remote, values, *spec, prop,
                        lprior_prop, log_mh, llh_prop, *proposal, error);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_spec_commit(int C, int d, int select, const double* temps, const int32_t* partner,
+                             const int32_t* pair_first, const uint8_t* acc_prev, const uint8_t* acc_exchange,
+                             const uint8_t* cross_acc, const double* remote, const bcm3hip_spec* spec, double* prop,
+                             double* lprior_prop, double* log_mh, double* llh_prop, double learning_rate, double* values,
+                             double* lprior, double* llh, double* lpp, uint8_t* accept_out, uint64_t* accepted,
+                             int32_t* nan_llh, const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed,
+                             uint64_t iter, int H, int subsampling, float* history, int64_t* counters, int32_t* error,
+                             void* stream)
+{
+    if (C <= 0 || d <= 0 || !spec_ok(spec) || !proposal_ok(proposal, C, d) || !temps || !prop || !lprior_prop ||
+        !log_mh || !llh_prop || !values || !lprior || !llh || !lpp || !accept_out ||
+        (select && (!partner || !pair_first || !acc_prev || !acc_exchange || acc_prev == accept_out)) ||
+        (history && (H <= 0 || subsampling <= 0 || !counters)))
+        return BCM3HIP_ERR_ARG;
+    hipLaunchKernelGGL(ptmh_spec_commit_kernel, dim3((C + 63) / 64), dim3(64), 0, (hipStream_t)stream, C, d, select,
+                       temps, partner, pair_first, acc_prev, acc_exchange, cross_acc, remote, *spec, prop, lprior_prop,
+                       log_mh, llh_prop, learning_rate, values, lprior, llh, lpp, accept_out,
+                       (unsigned long long*)accepted, nan_llh, *proposal, chain0, seed, iter, H, subsampling, history,
+                       counters, error);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_spec_exchange(int C, int d, int64_t g0, int start, int wrap_local, const double* temps,
+                               double* values, double* llh, double* lprior, double* lpp, uint8_t* acc_exchange,
+                               uint64_t* accepted, uint64_t seed, uint64_t round, const int32_t* partner,
+                               const int32_t* pair_first, const bcm3hip_spec* spec, int H, int subsampling,
+                               float* history, int64_t* counters, void* stream)
+{
+    if (C < 2 || C > 4096 || d <= 0 || !temps || !values || !llh || !lprior || !lpp || !acc_exchange || !partner ||
+        !pair_first || !spec_ok(spec) || (history && (H <= 0 || subsampling <= 0 || !counters)))
+        return BCM3HIP_ERR_ARG;
+    hipLaunchKernelGGL(ptmh_spec_exchange_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, g0, start,
+                       wrap_local, temps, values, llh, lprior, lpp, acc_exchange, (unsigned long long*)accepted, seed,
+                       round, partner, pair_first, *spec, H, subsampling, history, counters);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -555,6 +555,28 @@ int bcm3hip_ptmh_spec_select(int C, int d, const double* temps, const int32_t* p
                              const double* remote, const double* values, const bcm3hip_spec* spec, double* prop,
                              double* lprior_prop, double* log_mh, double* llh_prop, const bcm3hip_proposal* proposal,
                              int32_t* error, void* stream);
+/* The end of one iteration of a pair in ONE launch, one thread per chain: with select != 0 first
+ * bcm3hip_ptmh_spec_select (iteration r + 1; acc_prev = the accept flags of iteration r, a different
+ * buffer than accept_out), then bcm3hip_ptmh_accept_adaptive (flags to accept_out), the accept's
+ * bcm3hip_ptmh_spec_track and bcm3hip_history_add (mask NULL; skipped when history is NULL) -- per
+ * chain the same operations in the same order as those launches. */
+int bcm3hip_ptmh_spec_commit(int C, int d, int select, const double* temps, const int32_t* partner,
+                             const int32_t* pair_first, const uint8_t* acc_prev, const uint8_t* acc_exchange,
+                             const uint8_t* cross_acc, const double* remote, const bcm3hip_spec* spec, double* prop,
+                             double* lprior_prop, double* log_mh, double* llh_prop, double learning_rate, double* values,
+                             double* lprior, double* llh, double* lpp, uint8_t* accept_out, uint64_t* accepted,
+                             int32_t* nan_llh, const bcm3hip_proposal* proposal, int64_t chain0, uint64_t seed,
+                             uint64_t iter, int H, int subsampling, float* history, int64_t* counters, int32_t* error,
+                             void* stream);
+/* One exchange round of a single-rank ladder whose pairs cover every chain once (even C), and what
+ * follows it in a pair, in ONE workgroup: bcm3hip_pt_exchange_local (accept flags to acc_exchange),
+ * the round's bcm3hip_ptmh_spec_track and bcm3hip_history_add of every chain (skipped when history
+ * is NULL); C <= 4096. */
+int bcm3hip_ptmh_spec_exchange(int C, int d, int64_t g0, int start, int wrap_local, const double* temps,
+                               double* values, double* llh, double* lprior, double* lpp, uint8_t* acc_exchange,
+                               uint64_t* accepted, uint64_t seed, uint64_t round, const int32_t* partner,
+                               const int32_t* pair_first, const bcm3hip_spec* spec, int H, int subsampling,
+                               float* history, int64_t* counters, void* stream);
 /* dispatch-order bookkeeping (steps_hint = BDF steps of the solve of the state in each slot): after an
  * accept (acc_mutate: the proposals' steps, steps_prop, become the states') or, with acc_mutate NULL,
  * after an exchange round (acc_exchange indexed by pair_first, partner as in spec_select) */
