@@ -325,15 +325,35 @@ BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
         s.tlast = t_;                      \
         __builtin_amdgcn_sched_barrier(0); \
     } while (0)
+// the fast loop's cycles of a whole step, split by kind (plain / recomputing) via selects
+#define BDF_PH_STEP(t0, kp, kg, c)                   \
+    do {                                             \
+        __builtin_amdgcn_sched_barrier(0);           \
+        const long long d_ = clock64() - (t0);       \
+        s.ph[kp] += (c) ? d_ : 0;                    \
+        s.ph[kg] += (c) ? 0 : d_;                    \
+        __builtin_amdgcn_sched_barrier(0);           \
+    } while (0)
+#define BDF_PH_NOW() clock64()
 #elif defined(BCM3_MARKS)
 // ISA study build: a comment per phase boundary in the -S output (tools/step_isa.py)
 #define BDF_PH(k) asm volatile("; BDFMARK " #k)
-#else
+#endif
+#ifndef BDF_PH
 #define BDF_PH(k) \
     do {          \
     } while (0)
 #endif
-constexpr int NPHASES = 10;
+#ifndef BDF_PH_STEP
+#define BDF_PH_STEP(t0, kp, kg, c) \
+    do {                           \
+    } while (0)
+#define BDF_PH_NOW() 0ll
+#endif
+// 0-9: the general step (tools/phase_probe.py NAMES); 10-18: the phases of a fast-loop step
+// (vec::fast_run; 10-15 plain steps only); 19/20: whole plain / recomputing fast-loop steps;
+// 21/22: their counts; 23: the marker's own cost (16 back-to-back markers per trajectory)
+constexpr int NPHASES = 24;
 
 struct BdfCounters {
     int nst_total, nfe, nni, nsetups, nje, netf, ncfn, nreinit;

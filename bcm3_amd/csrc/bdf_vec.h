@@ -420,12 +420,14 @@ BDF_INL void tq_13(S& s, const TqCtx& c)
 }
 
 // one Newton correction (uni::newton_correction)
-template <int NS, class S, class Model>
+// (PHB >= 0: the phases build marks the right-hand side, the solve and the norm as PHB, PHB + 1, PHB + 2)
+template <int NS, int PHB = -1, class S, class Model>
 BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& cscale, bool setup, bool jbad,
                                  int convfail)
 {
     const double y = s.zn[0] + s.acor;
     const double f = mdl.rhs_v(s.tn, y, s.acol);
+    if constexpr (PHB >= 0) BDF_PH(PHB);
     s.cnt.nfe++;
     double delta = rl1 * s.zn[1] + s.acor;
     delta = delta + (-s.gamma) * f;
@@ -449,7 +451,10 @@ BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& csc
     double x = vec::solvevec<NS>(s.icol, -delta);
     x *= cscale;
     s.acor += x;
-    return vec::wrms<NS>(x, s.ewt);
+    if constexpr (PHB >= 0) BDF_PH(PHB + 1);
+    const double del = vec::wrms<NS>(x, s.ewt);
+    if constexpr (PHB >= 0) BDF_PH(PHB + 2);
+    return del;
 }
 
 // Newton iteration (uni::newton_u) after its first correction del (made by attempt_q)
@@ -530,7 +535,7 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
 // FAST: called from fast_run, where the step's first attempt passed, so etamax is the value the
 // previous completion set (ETAMX2 / ETAMX3) or ReInit's ETAMX1 -- never 1
 // cvCompleteStep (complete_head_q) + cvPrepareNextStep (complete_eta_q)
-template <int Q, class S>
+template <int Q, int PH = 7, class S>
 BDF_INL void complete_head_q(S& s)
 {
     constexpr int q = Q;
@@ -549,10 +554,10 @@ BDF_INL void complete_head_q(S& s)
             s.saved_tq5 = s.tq[5];
         }
     }
-    BDF_PH(7);
+    BDF_PH(PH);
 }
 
-template <int Q, int NS, bool FAST, class S>
+template <int Q, int NS, bool FAST, int PH = 8, class S>
 BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
 {
     constexpr int q = Q;
@@ -595,16 +600,16 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
         s.eta = small ? 1.0 : SUNMIN(eta, s.etamax);
         s.hprime = small ? s.h : s.h * s.eta;
     }
-    BDF_PH(8);
+    BDF_PH(PH);
     s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
     s.acor *= s.tq[2];
 }
 
-template <int Q, int NS, bool FAST, class S>
+template <int Q, int NS, bool FAST, int PH0 = 7, class S>
 BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc)
 {
-    vec::complete_head_q<Q>(s);
-    vec::complete_eta_q<Q, NS, FAST>(s, dsm, tc);
+    vec::complete_head_q<Q, PH0>(s);
+    vec::complete_eta_q<Q, NS, FAST, PH0 + 1>(s, dsm, tc);
 }
 
 template <int Q, int NS, bool FAST = false, class S, class Model>
@@ -829,6 +834,8 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
 #ifdef BCM3_MARKS
         asm volatile("; BDFMARK fast_top Q=%0" ::"i"(Q));
 #endif
+        BDF_PH(18);  // the loop's exit test and back edge
+        const long long ph_t0 = BDF_PH_NOW();
         vec::ewt_set(s);
         const double saved_t = s.tn;
         const double eta_eff = (s.hprime != s.h) ? s.eta : 1.0;
@@ -846,15 +853,15 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         const bool plain = reuse & (s.nst < s.nstlp + MSBP) & (s.gamrat == gamrat_h);
         bool setup = false;
         double cscale, del;
-        BDF_PH(2);
         if (BDF_LIKELY(plain)) {
+            BDF_PH(10);
             vec::predict_q<Q>(s);
-            BDF_PH(3);
-            BDF_PH(4);
+            BDF_PH(11);
             cscale = cscale_h;
             s.acor = 0.0;
-            del = vec::newton_correction<NS>(s, mdl, rl1, cscale, false, false, CONV_NONE);
+            del = vec::newton_correction<NS, 12>(s, mdl, rl1, cscale, false, false, CONV_NONE);
         } else {
+            BDF_PH(2);
             // cvStep's attempt at order Q (attempt_q with nflag == FIRST_CALL, nst > 0)
 #ifdef BCM3_MARKS
             asm volatile("; BDFMARK general");
@@ -880,7 +887,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         if (BDF_LIKELY(div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4]) & (dsm <= 1.0))) {
             s.acnrm = del;
             s.nls_jcur = 0;
-            BDF_PH(5);
+            BDF_PH(15);
         } else {
             const bool conv = vec::newton_rest<NS>(s, mdl, rl1, CONV_NONE, setup, cscale, del);
             BDF_PH(5);
@@ -896,10 +903,15 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
                 return NEED_ATTEMPTS;
             }
         }
-        vec::complete_q<Q, NS, true>(s, dsm, tc);
+        vec::complete_q<Q, NS, true, 16>(s, dsm, tc);
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         const bool quiet = (fabs(s.tn - s.tstop) > troundoff) & !((s.tn + s.hprime - s.tstop) * s.h > 0.0) &
                            (s.tn < tlim) & (s.qprime == Q) & (current_step + 1 != max_steps);
+        BDF_PH_STEP(ph_t0, 19, 20, plain);
+#ifdef BCM3_PHASES
+        s.ph[21] += plain ? 1 : 0;
+        s.ph[22] += plain ? 0 : 1;
+#endif
         if (BDF_UNLIKELY(!quiet)) return vec::finish_step<NS>(s, yout, tret);
         current_step++;
     }

@@ -17,6 +17,11 @@ from bcm3_amd import _hip  # noqa: E402
 
 NAMES = ["driver(out/cb/reinit)", "entry+ewt", "adjust+rescale", "predict", "set_bdf", "newton",
          "errtest/fail", "complete", "eta/next", "tstop/return"]
+# the fast loop (vec::fast_run): 10-15 are timed on plain steps only (coefficients held), 16-18 on
+# every fast-loop step; 19/20 whole plain / recomputing steps, 21/22 their counts, 23 the marker
+FAST = ["ewt + plain test", "predict", "newton: rhs", "newton: solve (I-gJ)^-1", "newton: wrms norm",
+        "conv + error test", "complete: zn, tau", "complete: eta (root)", "exit test + back edge"]
+NPH = 24
 
 
 def main():
@@ -27,7 +32,8 @@ def main():
     vals = S.prior_draws(1, n, 7)
     g = ctx.eval(vals, detail=True)
     ms = ctx.last_kernel_ms()
-    ph = g["traj"].reshape(n, -1)[:, :len(NAMES)]
+    allph = g["traj"].reshape(n, -1)[:, :NPH]
+    ph = allph[:, :len(NAMES)]
     nst = g["stats"]["nst"][:, 0].astype(np.float64)
     tot = ph.sum(axis=1)
     imax = int(np.argmax(tot))
@@ -47,8 +53,36 @@ def main():
     for k, name in enumerate(NAMES):
         print(f"  {name:24s} {per[k]:8.0f}  {100 * per[k] / per.sum():5.1f}%")
     print("stats means:", {k: float(g["stats"][k].mean()) for k in g["stats"].dtype.names})
-    qh = g["traj"].reshape(n, -1)[:, len(NAMES):len(NAMES) + 5].sum(axis=0)
+    qh = g["traj"].reshape(n, -1)[:, NPH:NPH + 5].sum(axis=0)
     print("successful steps by order q=1..5 (UNI solver):", (qh / qh.sum()).round(3).tolist())
+    fast_report(allph, nst, ms, tot)
+
+
+def fast_report(allph, nst, ms, tot):
+    """the plain fast-loop step's cycles by phase, the marker's own cost subtracted"""
+    mark = allph[:, 23].sum() / (16 * allph.shape[0])
+    n_plain, n_gen = allph[:, 21].sum(), allph[:, 22].sum()
+    if n_plain == 0:
+        print("no fast-loop steps (not the VEC solver?)")
+        return
+    c_plain = allph[:, 19].sum() / n_plain
+    c_gen = allph[:, 20].sum() / max(n_gen, 1)
+    n_fast = n_plain + n_gen
+    print(f"\nfast loop: {n_fast / nst.sum():.1%} of all steps; plain (coefficients held) {n_plain / n_fast:.1%} of them")
+    print(f"marker cost {mark:.0f} cycles (16 back-to-back per trajectory)")
+    # markers inside one plain step: 10..15 (6), 16, 17 (complete) = 8, plus the step total's own read
+    k_plain = 8
+    print(f"whole step, loop top to exit test: plain {c_plain:.0f} cycles ({c_plain - k_plain * mark:.0f} without its "
+          f"{k_plain} markers), recomputing {c_gen:.0f}")
+    per = [allph[:, 10 + i].sum() / n_plain for i in range(6)] + \
+          [allph[:, 16 + i].sum() / n_fast for i in range(3)]
+    net = [max(v - mark, 0.0) for v in per]
+    print(f"{'phase':28s} {'cycles':>8s} {'- marker':>9s} {'share':>6s}")
+    for name, v, w in zip(FAST, per, net):
+        print(f"  {name:26s} {v:8.0f} {w:9.0f} {100 * w / sum(net):5.1f}%")
+    print(f"  {'sum':26s} {sum(per):8.0f} {sum(net):9.0f}")
+    # the product build's rate for comparison: cycles per step of the slowest trajectory
+    print(f"(phases build: kernel {ms:.3f} ms; markers slow each step by about {k_plain + 1} x {mark:.0f} cycles)")
 
 
 if __name__ == "__main__":
