@@ -337,7 +337,7 @@ BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
 #define BDF_PH_NOW() clock64()
 #elif defined(BCM3_MARKS)
 // ISA study build: a comment per phase boundary in the -S output (tools/step_isa.py)
-#define BDF_PH(k) asm volatile("; BDFMARK " #k)
+#define BDF_PH(k) asm volatile("; BDFMARK %0" ::"i"(k))
 #endif
 #ifndef BDF_PH
 #define BDF_PH(k) \

@@ -251,6 +251,15 @@ def histogram(blocks, path):
     return h, ph
 
 
+# fast_run's markers (bdf_vec.h; the phases build times the same boundaries, tools/phase_probe.py):
+# a plain step passes 10 .. 17 in order; the instructions after marker k belong to the next phase
+PLAIN = ["10", "11", "12", "13", "14", "15", "16", "17"]
+PHASE_NAMES = {"top": "ewt + plain test", "18": "ewt + plain test", "10": "predict", "11": "newton: rhs",
+               "12": "newton: solve", "13": "newton: wrms norm", "14": "conv + error test",
+               "15": "complete: zn, tau", "16": "complete: eta (root)", "17": "exit test + back edge",
+               "general": "rescale", "2": "predict", "3": "set_bdf", "4": "newton"}
+
+
 def fmt(c):
     v = sum(c[k] for k in ("valu_f64", "valu_other", "v_dpp", "v_readlane"))
     s = c["salu"] + c["smem"]
@@ -279,9 +288,10 @@ def main():
         # rescale, cvSet, setup and scale tests), the latter with the cvSet region entered
         general = bool(marked(blocks, order, "general"))
         for label, sb, seq, avoid in (
-                ("plain step (coefficients held)", False, ["2", "3", "4", "5", "7", "8"], ("general",)),
+                ("plain step (coefficients held)", False, PLAIN, ("general",)),
                 ("general attempt recomputing them (set_bdf)", True,
-                 (["general", "3", "4", "5", "7", "8"] if general else ["2", "3", "4", "5", "7", "8"]), ())):
+                 (["general", "2", "3", "4", "15", "16", "17"] if general else ["2", "3", "4", "15", "16", "17"]),
+                 ())):
             p = step_path(blocks, order, top, seq, sb, avoid)
             if not p:
                 print(f"  {label}: no path")
@@ -290,9 +300,9 @@ def main():
             if "--dump" in sys.argv and q == int(sys.argv[sys.argv.index("--dump") + 1]):
                 dump(blocks, p)
             print(f"  {label} ({len(p) - 1} blocks): {fmt(h)}")
-            for k in ("top", "2", "3", "4", "5", "7", "8", "tail"):
+            for k in ("top", "18", "general", "2", "3", "4") + tuple(PLAIN) + ("tail",):
                 if k in ph:
-                    print(f"     phase {k:>4}: {fmt(ph[k])}")
+                    print(f"     phase {k:>7} {PHASE_NAMES.get(k, ''):24s}: {fmt(ph[k])}")
 
 
 if __name__ == "__main__":
