@@ -23,9 +23,16 @@
 #ifdef __HIP__
 #include <hip/hip_runtime.h>
 #define XM_FN __host__ __device__ __forceinline__
-// the public functions are called off the solvers' hot loops (parameter map, observation model):
-// out of line, so that their registers do not add to the pressure of the kernels that call them
+// exp, log, log1p, erf and erfc come in two forms: name_i always inline, and name out of line (a
+// call), so that their registers do not add to the pressure of a kernel that calls them off its
+// hot loop. lib<COLD> picks one at a call site: the one-trajectory-per-wavefront PopPK kernel with
+// vector state calls them out of line; the other kernels inline them (a call from the scalar-state
+// two-compartment transit kernel was miscompiled: every solve failed on its first step)
+#ifdef BCM3_XM_INLINE
+#define XM_COLD XM_FN
+#else
 #define XM_COLD __host__ __device__ __attribute__((noinline)) inline
+#endif
 #else
 #include <cmath>
 #define XM_FN inline
@@ -95,7 +102,7 @@ constexpr double SIXTH_HI = 0.16666666666666666, SIXTH_LO = 9.25185853854297e-18
 // for results below the normal range the low part is meaningless). Reduction x = k ln2 + r,
 // |r| <= ln2/2, r = 2^8 s, expm1(s) by its Taylor series (dd up to s^3), then eight steps of
 // expm1(2s) = expm1(s) (expm1(s) + 2), which keep the relative error of expm1 from doubling.
-XM_COLD dd exp_dd(double x)
+XM_FN dd exp_dd(double x)
 {
     const double k = __builtin_rint(x * INV_LN2);
     const double r1 = x - k * LN2_1;  // exact (Sterbenz; k * LN2_1 exact)
@@ -131,7 +138,7 @@ XM_COLD dd exp_dd(double x)
 }
 
 // glibc exp (correctly rounded result)
-XM_COLD double exp(double x)
+XM_FN double exp_i(double x)
 {
     if (!(x == x)) return x + x;
     if (x > 709.782712893384) return __builtin_inf();
@@ -142,7 +149,7 @@ XM_COLD double exp(double x)
 
 // glibc log (correctly rounded result): one Newton step y0 + log1p(x e^-y0 - 1) from the
 // library estimate y0, with e^-y0 in double-double
-XM_COLD double log(double x)
+XM_FN double log_i(double x)
 {
     if (!(x > 0.0) || x == __builtin_inf()) {
         if (x == 0.0) return -__builtin_inf();
@@ -246,7 +253,7 @@ XM_FN double with_hi_word(double x, int h)
 }
 XM_FN double with_lo_zero(double x) { return as_double(as_bits(x) & ~0xffffffffLL); }
 
-XM_COLD double log1p(double x)
+XM_FN double log1p_i(double x)
 {
     constexpr double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
     constexpr double Lp1 = 6.666666666666735130e-01, Lp2 = 3.999999999940941908e-01,
@@ -403,10 +410,10 @@ XM_FN double erf_tail_r(double ax, bool lo)
         S = S1 + s2 * S2 + s4 * S3 + s6 * S4;
     }
     const double z = with_lo_zero(ax);
-    return xm::exp(-z * z - 0.5625) * xm::exp((z - ax) * (z + ax) + R / S);
+    return exp_i(-z * z - 0.5625) * exp_i((z - ax) * (z + ax) + R / S);
 }
 
-XM_COLD double erf(double x)
+XM_FN double erf_i(double x)
 {
     const int hx = hi_word(x);
     const int ix = hx & 0x7fffffff;
@@ -426,7 +433,7 @@ XM_COLD double erf(double x)
     return (hx >= 0) ? 1.0 - r / ax : r / ax - 1.0;
 }
 
-XM_COLD double erfc(double x)
+XM_FN double erfc_i(double x)
 {
     const int hx = hi_word(x);
     const int ix = hx & 0x7fffffff;
@@ -457,5 +464,40 @@ XM_COLD double erfc(double x)
     }
     return (hx > 0) ? 0.0 : 2.0;
 }
+
+XM_COLD double exp(double x) { return exp_i(x); }
+XM_COLD double log(double x) { return log_i(x); }
+XM_COLD double log1p(double x) { return log1p_i(x); }
+XM_COLD double erf(double x) { return erf_i(x); }
+XM_COLD double erfc(double x) { return erfc_i(x); }
+
+template <bool COLD>
+struct lib {
+    static XM_FN double exp(double x)
+    {
+        if constexpr (COLD) return xm::exp(x);
+        else return exp_i(x);
+    }
+    static XM_FN double log(double x)
+    {
+        if constexpr (COLD) return xm::log(x);
+        else return log_i(x);
+    }
+    static XM_FN double log1p(double x)
+    {
+        if constexpr (COLD) return xm::log1p(x);
+        else return log1p_i(x);
+    }
+    static XM_FN double erf(double x)
+    {
+        if constexpr (COLD) return xm::erf(x);
+        else return erf_i(x);
+    }
+    static XM_FN double erfc(double x)
+    {
+        if constexpr (COLD) return xm::erfc(x);
+        else return erfc_i(x);
+    }
+};
 
 }  // namespace xm

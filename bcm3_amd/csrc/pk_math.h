@@ -8,20 +8,23 @@
 
 namespace bcm3hip {
 
-// libm's exp / log / log1p / erf / erfc through libm_exact.h (the glibc results of the oracle)
-BDF_INL double fastpow10(double x) { return xm::exp(x * 2.3025850929940459); }
+// libm's exp / log / log1p / erf / erfc through libm_exact.h (the glibc results of the oracle);
+// COLD: call them out of line (xm::lib)
+template <bool COLD = false>
+BDF_INL double fastpow10(double x) { return xm::lib<COLD>::exp(x * 2.3025850929940459); }
 
+template <bool COLD = false>
 BDF_INL double transform_var(int tf, double x)
 {
     switch (tf) {
-    case 1: return xm::exp(x);
-    case 2: return fastpow10(x);
+    case 1: return xm::lib<COLD>::exp(x);
+    case 2: return fastpow10<COLD>(x);
     case 3:
         if (x > 0) {
-            double z = xm::exp(-x);
+            double z = xm::lib<COLD>::exp(-x);
             return 1.0 / (1.0 + z);
         } else {
-            double z = xm::exp(x);
+            double z = xm::lib<COLD>::exp(x);
             return z / (1.0 + z);
         }
     default: return x;
@@ -75,10 +78,11 @@ __device__ double quantile_normal(double p, double mu, double sigma)
     return r;
 }
 
+template <bool COLD = false>
 BDF_INL double log_pdf_tnu4(double x, double mu, double sigma)
 {
     double xn = (x - mu) / sigma;
-    return -0.9808292530117262 - 2.5 * xm::log1p(0.25 * xn * xn) - xm::log(sigma);
+    return -0.9808292530117262 - 2.5 * xm::lib<COLD>::log1p(0.25 * xn * xn) - xm::lib<COLD>::log(sigma);
 }
 
 }  // namespace bcm3hip
