@@ -10,8 +10,9 @@
  * space-free). The writing calls NetCDF4.cpp makes for the sampler's output files (nc_create,
  * nc_def_grp / _dim / _var, nc_put_vara_double / _uint / _string, nc_sync, nc_close) build the same
  * model in memory and write it back as such a manifest; a value never written is the type's default
- * fill (NC_FILL_DOUBLE 9.969209968386869e36, NC_FILL_UINT 4294967295). Anything else returns an
- * error code. */
+ * fill (NC_FILL_DOUBLE 9.969209968386869e36, NC_FILL_UINT 4294967295). Up to MAXF datasets are
+ * open at once (the sampler writes output.nc and sampler_adaptation.nc side by side); an ncid is
+ * (dataset << 24) | ((group + 1) << 16). Anything else returns an error code. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -29,14 +30,61 @@ typedef struct {
     char** str;
 } Var;
 
-static int ng, nd, nv;
-static int gparent[MAXG];
-static char gname[MAXG][128];
-static char dname[MAXD][128];
-static size_t dlen[MAXD];
-static Var vars[MAXV];
+#define MAXF 8
+typedef struct {
+    int used, writing;
+    int ng, nd, nv;
+    int gparent[MAXG];
+    char gname[MAXG][128];
+    char dname[MAXD][128];
+    size_t dlen[MAXD];
+    Var vars[MAXV];
+    char wpath[4096];
+} DS;
+static DS files[MAXF];
 
-static int gid(int ncid) { return ncid / 65536 - 1; }
+static int gid(int ncid) { return ((ncid >> 16) & 0xff) - 1; }
+static DS* ds_of(int ncid)
+{
+    const int f = ncid >> 24;
+    return (f >= 0 && f < MAXF && files[f].used) ? &files[f] : NULL;
+}
+static int ncid_of(const DS* d, int g) { return (int)((d - files) << 24) | ((g + 1) << 16); }
+static DS* ds_new(void)
+{
+    for (int f = 0; f < MAXF; f++)
+        if (!files[f].used) {
+            DS* d = &files[f];
+            d->used = 1;
+            d->writing = 0;
+            d->ng = 1;
+            d->nd = d->nv = 0;
+            d->gparent[0] = -1;
+            strcpy(d->gname[0], "/");
+            return d;
+        }
+    return NULL;
+}
+static void ds_free(DS* d)
+{
+    for (int i = 0; i < d->nv; i++) {
+        free(d->vars[i].num);
+        if (d->vars[i].str)
+            for (size_t k = 0; k < d->vars[i].count; k++) free(d->vars[i].str[k]);
+        free(d->vars[i].str);
+    }
+    d->used = 0;
+}
+#define ng (d->ng)
+#define nd (d->nd)
+#define nv (d->nv)
+#define gparent (d->gparent)
+#define gname (d->gname)
+#define dname (d->dname)
+#define dlen (d->dlen)
+#define vars (d->vars)
+#define writing (d->writing)
+#define wpath (d->wpath)
 
 int nc_open(const char* path, int mode, int* ncidp)
 {
@@ -51,10 +99,11 @@ int nc_open(const char* path, int mode, int* ncidp)
     int c;
     while ((c = fgetc(f)) != EOF && c != '\n') {
     }
-    ng = 1;
-    nd = nv = 0;
-    gparent[0] = -1;
-    strcpy(gname[0], "/");
+    DS* d = ds_new();
+    if (!d) {
+        fclose(f);
+        return -34; /* NC_ENFILE */
+    }
     char tag[4];
     while (fscanf(f, "%3s", tag) == 1) {
         if (tag[0] == 'G') {
@@ -88,27 +137,29 @@ int nc_open(const char* path, int mode, int* ncidp)
         }
     }
     fclose(f);
-    *ncidp = 65536;
+    *ncidp = ncid_of(d, 0);
     return 0;
 }
 
-static int write_manifest(void);
-static int writing;
+static int write_manifest(DS* d);
 
 int nc_close(int ncid)
 {
-    (void)ncid;
-    if (!writing) return 0;
-    writing = 0;
-    return write_manifest();
+    DS* d = ds_of(ncid);
+    if (!d) return -33; /* NC_EBADID */
+    const int r = writing ? write_manifest(d) : 0;
+    ds_free(d);
+    return r;
 }
 
 int nc_inq_grps(int ncid, int* numgrps, int* ncids)
 {
+    DS* d = ds_of(ncid);
+    if (!d) return -33;
     int g = gid(ncid), n = 0;
     for (int i = 1; i < ng; i++)
         if (gparent[i] == g) {
-            if (ncids) ncids[n] = (i + 1) * 65536;
+            if (ncids) ncids[n] = ncid_of(d, i);
             n++;
         }
     if (numgrps) *numgrps = n;
@@ -117,12 +168,16 @@ int nc_inq_grps(int ncid, int* numgrps, int* ncids)
 
 int nc_inq_grpname(int ncid, char* name)
 {
+    DS* d = ds_of(ncid);
+    if (!d) return -33;
     strcpy(name, gname[gid(ncid)]);
     return 0;
 }
 
 static Var* var_of(int ncid, int varid)
 {
+    DS* d = ds_of(ncid);
+    if (!d) return NULL;
     int g = gid(ncid), k = 0;
     for (int i = 0; i < nv; i++)
         if (vars[i].group == g) {
@@ -134,6 +189,8 @@ static Var* var_of(int ncid, int varid)
 
 int nc_inq_varids(int ncid, int* nvars, int* varids)
 {
+    DS* d = ds_of(ncid);
+    if (!d) return -33;
     int g = gid(ncid), n = 0;
     for (int i = 0; i < nv; i++)
         if (vars[i].group == g) {
@@ -159,7 +216,8 @@ int nc_inq_var(int ncid, int varid, char* name, int* xtypep, int* ndimsp, int* d
 
 int nc_inq_dim(int ncid, int dimid, char* name, size_t* lenp)
 {
-    (void)ncid;
+    DS* d = ds_of(ncid);
+    if (!d) return -33;
     if (dimid < 0 || dimid >= nd) return -46; /* NC_EBADDIM */
     if (name) strcpy(name, dname[dimid]);
     if (lenp) *lenp = dlen[dimid];
@@ -176,6 +234,7 @@ int nc_get_var_double(int ncid, int varid, double* ip)
 
 int nc_get_var_text(int ncid, int varid, char* ip)
 {
+    DS* d = ds_of(ncid);
     Var* v = var_of(ncid, varid);
     if (!v || v->type != 2) return -56;
     size_t w = dlen[v->dims[v->ndims - 1]];
@@ -225,9 +284,7 @@ const char* nc_strerror(int ncerr)
 }
 
 /* ---- writing ---- */
-static char wpath[4096];
-
-static size_t var_count(const Var* v)
+static size_t var_count(const DS* d, const Var* v)
 {
     size_t n = 1;
     for (int k = 0; k < v->ndims; k++) n *= dlen[v->dims[k]];
@@ -237,36 +294,29 @@ static size_t var_count(const Var* v)
 int nc_create(const char* path, int cmode, int* ncidp)
 {
     if (!(cmode & 0x1000)) return -128; /* only NC_NETCDF4 */
-    for (int i = 0; i < nv; i++) {
-        free(vars[i].num);
-        if (vars[i].str)
-            for (size_t k = 0; k < vars[i].count; k++) free(vars[i].str[k]);
-        free(vars[i].str);
-    }
-    ng = 1;
-    nd = nv = 0;
-    gparent[0] = -1;
-    strcpy(gname[0], "/");
+    DS* d = ds_new();
+    if (!d) return -34;
     snprintf(wpath, sizeof wpath, "%s", path);
     writing = 1;
-    *ncidp = 65536;
+    *ncidp = ncid_of(d, 0);
     return 0;
 }
 
 int nc_def_grp(int parent_ncid, const char* name, int* new_ncid)
 {
-    if (ng >= MAXG) return -1;
+    DS* d = ds_of(parent_ncid);
+    if (!d || ng >= MAXG) return -1;
     gparent[ng] = gid(parent_ncid);
     snprintf(gname[ng], sizeof gname[ng], "%s", name);
-    *new_ncid = (ng + 1) * 65536;
+    *new_ncid = ncid_of(d, ng);
     ng++;
     return 0;
 }
 
 int nc_def_dim(int ncid, const char* name, size_t len, int* idp)
 {
-    (void)ncid;
-    if (nd >= MAXD) return -1;
+    DS* d = ds_of(ncid);
+    if (!d || nd >= MAXD) return -1;
     snprintf(dname[nd], sizeof dname[nd], "%s", name);
     dlen[nd] = len;
     *idp = nd++;
@@ -275,7 +325,8 @@ int nc_def_dim(int ncid, const char* name, size_t len, int* idp)
 
 int nc_def_var(int ncid, const char* name, int xtype, int ndims, const int* dimidsp, int* varidp)
 {
-    if (nv >= MAXV || ndims > 8 || (xtype != 6 && xtype != 9 && xtype != 12)) return -1;
+    DS* d = ds_of(ncid);
+    if (!d || nv >= MAXV || ndims > 8 || (xtype != 6 && xtype != 9 && xtype != 12)) return -1;
     int g = gid(ncid), k = 0;
     for (int i = 0; i < nv; i++)
         if (vars[i].group == g) k++;
@@ -286,7 +337,7 @@ int nc_def_var(int ncid, const char* name, int xtype, int ndims, const int* dimi
     v->ndims = ndims;
     for (int d = 0; d < ndims; d++) v->dims[d] = dimidsp[d];
     snprintf(v->name, sizeof v->name, "%s", name);
-    v->count = var_count(v);
+    v->count = var_count(d, v);
     if (xtype == 12) {
         v->str = calloc(v->count + 1, sizeof(char*));
         for (size_t i = 0; i < v->count; i++) v->str[i] = strdup("");
@@ -299,7 +350,7 @@ int nc_def_var(int ncid, const char* name, int xtype, int ndims, const int* dimi
 }
 
 /* row-major offset of each element of the hyperslab, in order */
-static int slab(const Var* v, const size_t* start, const size_t* count, size_t* n, size_t** offs)
+static int slab(const DS* d, const Var* v, const size_t* start, const size_t* count, size_t* n, size_t** offs)
 {
     size_t total = 1;
     for (int k = 0; k < v->ndims; k++) {
@@ -327,7 +378,7 @@ int nc_put_vara_double(int ncid, int varid, const size_t* startp, const size_t* 
     Var* v = var_of(ncid, varid);
     size_t n, *o;
     if (!v || v->type != 6) return -56;
-    int r = slab(v, startp, countp, &n, &o);
+    int r = slab(ds_of(ncid), v, startp, countp, &n, &o);
     if (r) return r;
     for (size_t e = 0; e < n; e++) v->num[o[e]] = op[e];
     free(o);
@@ -339,7 +390,7 @@ int nc_put_vara_uint(int ncid, int varid, const size_t* startp, const size_t* co
     Var* v = var_of(ncid, varid);
     size_t n, *o;
     if (!v || v->type != 9) return -56;
-    int r = slab(v, startp, countp, &n, &o);
+    int r = slab(ds_of(ncid), v, startp, countp, &n, &o);
     if (r) return r;
     for (size_t e = 0; e < n; e++) v->num[o[e]] = (double)op[e];
     free(o);
@@ -351,7 +402,7 @@ int nc_put_vara_string(int ncid, int varid, const size_t* startp, const size_t* 
     Var* v = var_of(ncid, varid);
     size_t n, *o;
     if (!v || v->type != 12) return -56;
-    int r = slab(v, startp, countp, &n, &o);
+    int r = slab(ds_of(ncid), v, startp, countp, &n, &o);
     if (r) return r;
     for (size_t e = 0; e < n; e++) {
         free(v->str[o[e]]);
@@ -361,7 +412,7 @@ int nc_put_vara_string(int ncid, int varid, const size_t* startp, const size_t* 
     return 0;
 }
 
-static int write_manifest(void)
+static int write_manifest(DS* d)
 {
     FILE* f = fopen(wpath, "wb");
     if (!f) return -31;
@@ -388,6 +439,7 @@ static int write_manifest(void)
 
 int nc_sync(int ncid)
 {
-    (void)ncid;
-    return writing ? write_manifest() : 0;
+    DS* d = ds_of(ncid);
+    if (!d) return -33;
+    return writing ? write_manifest(d) : 0;
 }

@@ -248,12 +248,14 @@ def test_netcdf4_outputs_through_libnetcdf(tmp_path, monkeypatch):
     def run(tag):
         s = _native(*C2, 16, 6, 0, adapt_proposal_samples=40, adapt_proposal_times=2)
         out, ad = str(tmp_path / f"output_{tag}.nc"), str(tmp_path / f"adapt_{tag}.nc")
-        s.set_output(out, 130, flush_every=16)
-        s.set_adaptation_output(ad)
-        s.iterate(130)
-        s.synchronize()
-        s.flush_output()
-        s.close()
+        try:
+            s.set_output(out, 130, flush_every=16)
+            s.set_adaptation_output(ad)
+            s.iterate(130)
+            s.synchronize()
+            s.flush_output()
+        finally:
+            s.close()
         return out, ad
 
     monkeypatch.setenv("BCM3_LIBNETCDF", so)
