@@ -275,13 +275,10 @@ BDF_INL double eta_exact(double bx, int k)
 }
 
 // cvNlsConvTest (cvode_nls.c:262-263): dcon = del * min(1, crate) / tol, converged when dcon <= 1,
-// tol = tq[4] = CORTES / tq[2]. RN(a / b) <= 1 iff a <= b (1 + 2^-53) (the midpoint 1 + 2^-53
-// rounds to even, i.e. to 1), decided without the division: for b < a <= 2b the difference a - b
-// is exact (Sterbenz). a >= 0 or NaN (false), b > 0.
-BDF_INL bool div_le_one(double a, double b)
-{
-    return (a <= b) | ((a <= 2.0 * b) & ((a - b) <= b * 0x1p-53));
-}
+// tol = tq[4] = CORTES / tq[2]. RN(a / b) <= 1 iff a / b <= 1 + 2^-53 (the midpoint rounds to even,
+// i.e. to 1) iff a <= b: for finite b > 0 no double lies in (b, b (1 + 2^-53)] (the successor of b
+// is b (1 + 2^-52 / m), mantissa m < 2). a >= 0 or NaN (false).
+BDF_INL bool div_le_one(double a, double b) { return a <= b; }
 
 // SUNRpowerI for exponent 1..7 (repeated multiplication, sundials_math.c:28-38)
 BDF_INL double powI(double base, int e)

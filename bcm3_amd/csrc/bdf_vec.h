@@ -535,16 +535,20 @@ BDF_INL int attempt_q(S& s, const Model& mdl, double eta_eff, double saved_t, in
 // FAST: called from fast_run, where the step's first attempt passed, so etamax is the value the
 // previous completion set (ETAMX2 / ETAMX3) or ReInit's ETAMX1 -- never 1
 // cvCompleteStep (complete_head_q) + cvPrepareNextStep (complete_eta_q)
-template <int Q, int PH = 7, class S>
+// HELD: fast_run's plain step, where tau[1..Q] all equal h (the coefficients are held), so the
+// shift of tau[1..Q] would store the values they have
+template <int Q, int PH = 7, bool HELD = false, class S>
 BDF_INL void complete_head_q(S& s)
 {
     constexpr int q = Q;
     s.nst++;
     s.cnt.nst_total++;
     s.hu = s.h;
-    cfor_down<Q, 2>([&](auto i) __attribute__((always_inline)) { s.tau[CI(i)] = s.tau[CI(i) - 1]; });
-    if constexpr (q == 1) s.tau[2] = (s.nst > 1) ? s.tau[1] : s.tau[2];
-    s.tau[1] = s.h;
+    if constexpr (!HELD) {
+        cfor_down<Q, 2>([&](auto i) __attribute__((always_inline)) { s.tau[CI(i)] = s.tau[CI(i) - 1]; });
+        if constexpr (q == 1) s.tau[2] = (s.nst > 1) ? s.tau[1] : s.tau[2];
+        s.tau[1] = s.h;
+    }
     cfor<0, Q + 1>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j)] = s.zn[CI(j)] + s.l[CI(j)] * s.acor; });
     s.qwait--;
     if constexpr (q != QMAX) {
@@ -561,13 +565,20 @@ template <int Q, int NS, bool FAST, int PH = 8, class S>
 BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
 {
     constexpr int q = Q;
-    if (BDF_UNLIKELY(!FAST && (s.etamax == 1.0))) {
+    const double bx = BIAS2 * dsm;
+    if (BDF_LIKELY(FAST && (s.qwait != 0) & (bx > uni::eta_cut(q + 1)))) {
+        // the usual outcome: no order-change check due and etaq below THRESH (eta_candidate's 0):
+        // cvSetEta keeps h (eta = 1)
+        s.qprime = q;
+        s.eta = 1.0;
+        s.hprime = s.h;
+    } else if (BDF_UNLIKELY(!FAST && (s.etamax == 1.0))) {
         s.qwait = SUNMAX(s.qwait, 2);
         s.qprime = q;
         s.hprime = s.h;
         s.eta = 1.0;
     } else {
-        const double etaq = uni::eta_candidate<q + 1>(BIAS2 * dsm);
+        const double etaq = uni::eta_candidate<q + 1>(bx);
         double eta = etaq;
         s.qprime = q;
         if (s.qwait == 0) {
@@ -605,10 +616,10 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
     s.acor *= s.tq[2];
 }
 
-template <int Q, int NS, bool FAST, int PH0 = 7, class S>
+template <int Q, int NS, bool FAST, int PH0 = 7, bool HELD = false, class S>
 BDF_INL void complete_q(S& s, double dsm, const TqCtx& tc)
 {
-    vec::complete_head_q<Q, PH0>(s);
+    vec::complete_head_q<Q, PH0, HELD>(s);
     vec::complete_eta_q<Q, NS, FAST, PH0 + 1>(s, dsm, tc);
 }
 
@@ -851,15 +862,43 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         // clears `have`) and gamrat has not changed. One branch instead of the rescale, cvSet,
         // setup and scale tests.
         const bool plain = reuse & (s.nst < s.nstlp + MSBP) & (s.gamrat == gamrat_h);
-        bool setup = false;
-        double cscale, del;
+        // the step's tail, instantiated in each branch: the usual outcome -- Newton converges on its
+        // first correction and the error test passes (a first-iteration convergence has local error
+        // dsm = acnrm tq[2] = del tq[2]) -- is ONE branch; anything else goes on through newton_rest,
+        // which repeats the convergence test. false: the first attempt failed, the attempt loop takes
+        // over. HELD (the plain step): tau[1..Q] all equal h, the completion skips their shift.
+        auto tail = [&](auto held, double del, bool setup, double cscale) __attribute__((always_inline)) {
+            double dsm = del * s.tq[2];
+            if (BDF_LIKELY(div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4]) & (dsm <= 1.0))) {
+                s.acnrm = del;
+                s.nls_jcur = 0;
+                BDF_PH(15);
+            } else {
+                const bool conv = vec::newton_rest<NS>(s, mdl, rl1, CONV_NONE, setup, cscale, del);
+                BDF_PH(5);
+                dsm = s.acnrm * s.tq[2];
+                if (BDF_UNLIKELY(!(conv & (dsm <= 1.0)))) {
+                    vec::restore_q<Q>(s, saved_t);
+                    s.tretlast = saved_t;
+                    pd.saved_t = saved_t;
+                    pd.eta_eff = eta_eff;
+                    pd.r = conv ? uni::ATTEMPT_ERR_FAIL : uni::ATTEMPT_CONV_FAIL;
+                    pd.dsm = dsm;
+                    return false;
+                }
+            }
+            vec::complete_q<Q, NS, true, 16, decltype(held)::value>(s, dsm, tc);
+            return true;
+        };
         if (BDF_LIKELY(plain)) {
             BDF_PH(10);
             vec::predict_q<Q>(s);
             BDF_PH(11);
-            cscale = cscale_h;
             s.acor = 0.0;
-            del = vec::newton_correction<NS, 12>(s, mdl, rl1, cscale, false, false, CONV_NONE);
+            double cscale = cscale_h;
+            const double del = vec::newton_correction<NS, 12>(s, mdl, rl1, cscale, false, false, CONV_NONE);
+            run++;  // have stays set (reuse, no setup)
+            if (!tail(std::true_type{}, del, false, cscale)) return NEED_ATTEMPTS;
         } else {
             BDF_PH(2);
             // cvStep's attempt at order Q (attempt_q with nflag == FIRST_CALL, nst > 0)
@@ -871,39 +910,16 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             BDF_PH(3);
             if (!reuse) rl1 = vec::set_bdf_q<Q, true>(s, tc);
             BDF_PH(4);
-            setup = (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);
-            cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
+            const bool setup = (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);
+            double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
             gamrat_h = s.gamrat;
             cscale_h = cscale;
             s.acor = 0.0;
-            del = vec::newton_correction<NS>(s, mdl, rl1, cscale, setup, false, CONV_NONE);
+            const double del = vec::newton_correction<NS>(s, mdl, rl1, cscale, setup, false, CONV_NONE);
+            have = (reuse | (run >= Q)) & !setup;
+            run++;
+            if (!tail(std::false_type{}, del, setup, cscale)) return NEED_ATTEMPTS;
         }
-        have = (reuse | (run >= Q)) & !setup;
-        run++;
-        // the usual outcome -- Newton converges on its first correction and the error test passes
-        // (a first-iteration convergence has local error dsm = acnrm tq[2] = del tq[2]) -- is ONE
-        // branch; anything else goes on through newton_rest, which repeats the convergence test
-        double dsm = del * s.tq[2];
-        if (BDF_LIKELY(div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4]) & (dsm <= 1.0))) {
-            s.acnrm = del;
-            s.nls_jcur = 0;
-            BDF_PH(15);
-        } else {
-            const bool conv = vec::newton_rest<NS>(s, mdl, rl1, CONV_NONE, setup, cscale, del);
-            BDF_PH(5);
-            dsm = s.acnrm * s.tq[2];
-            if (BDF_UNLIKELY(!(conv & (dsm <= 1.0)))) {
-                // failed first attempt: the attempt loop takes over from here
-                vec::restore_q<Q>(s, saved_t);
-                s.tretlast = saved_t;
-                pd.saved_t = saved_t;
-                pd.eta_eff = eta_eff;
-                pd.r = conv ? uni::ATTEMPT_ERR_FAIL : uni::ATTEMPT_CONV_FAIL;
-                pd.dsm = dsm;
-                return NEED_ATTEMPTS;
-            }
-        }
-        vec::complete_q<Q, NS, true, 16>(s, dsm, tc);
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         const bool quiet = (fabs(s.tn - s.tstop) > troundoff) & !((s.tn + s.hprime - s.tstop) * s.h > 0.0) &
                            (s.tn < tlim) & (s.qprime == Q) & (current_step + 1 != max_steps);
