@@ -15,7 +15,10 @@
 #include <algorithm>
 
 #include "../../include/bcm3hip.h"
+#include "libm_exact.h"
 #include "popk_kernel.h"
+
+bool bcm3_find_glibc_pow(xm::GlibcPow* out);  // libm_tables.cpp
 
 using namespace bcm3hip;
 
@@ -170,6 +173,12 @@ const char* bcm3hip_error_string(int code)
     }
 }
 
+int bcm3hip_libm_pow_tables(void)
+{
+    static xm::GlibcPow t;
+    return bcm3_find_glibc_pow(&t) ? 1 : 0;
+}
+
 int bcm3hip_open_popk(int device, const bcm3hip_popk_model* m, bcm3hip_ctx** out)
 {
     if (!m || !out) return BCM3HIP_ERR_ARG;
@@ -207,6 +216,10 @@ int bcm3hip_open_popk(int device, const bcm3hip_popk_model* m, bcm3hip_ctx** out
     if (r) {
         bcm3hip_close(c);
         return r;
+    }
+    if (popk_prepare_device(nullptr) != hipSuccess) {
+        bcm3hip_close(c);
+        return BCM3HIP_ERR_HIP;
     }
     c->kind = 1;
     c->d = m->d;

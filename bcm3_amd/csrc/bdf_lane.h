@@ -260,19 +260,23 @@ BDF_INL double eta_from(double bx, int k)
 // in their order (no contraction: the reference is compared against its build without FMA
 // contraction, oracle/_ref/libbcm3ref_nofma.so, which the C restatement matches bit for bit),
 // IEEE quotients and square roots (frcp / fdiv / fsqrt above, correctly rounded), and libm's
-// pow through xm::pow_inv_k (libm_exact.h). The cell-population solver keeps eta_from.
+// pow through xm::pow_glibc (libm_exact.h). The cell-population solver keeps eta_from.
+
+// The pow tables (libm_exact.h pow_glibc), uploaded by popk_prepare_device: the host libm's own
+// when it has them, so that the step-size roots are glibc's results bit for bit, else tables
+// computed on the host (libm_tables.cpp bcm3_make_pow_tables: the same algorithm, ~1 ulp)
+static __constant__ xm::GlibcPow g_glibc_pow;
+
+// SUNRpowerR(bx, fl(1/k)) (sundials_math.c:40-52, libm's pow)
+BDF_INL double pow_root(double bx, int k)
+{
+    if (BDF_LIKELY((bx >= 0x1p-1022) & (bx < 0x1p1023))) return xm::pow_glibc(bx, xm::inv_k(k), g_glibc_pow);
+    return (bx > 0.0) ? pow(bx, xm::inv_k(k)) : 0.0;
+}
 
 // eta = ONE / (SUNRpowerR(bx, ONE / k) + ADDON) (cvode.c:2986, 3105, 3163, 3187): the rounded
-// exponent fl(1/k) as the reference passes it, the correctly rounded pow, the IEEE quotient
-BDF_INL double eta_exact(double bx, int k)
-{
-    double p;
-    if (bx > 1e-30 && bx < 1e30)
-        p = xm::pow_inv_k(bx, k);
-    else
-        p = (bx > 0.0) ? pow(bx, xm::inv_k(k)) : 0.0;
-    return frcp(p + ADDON);
-}
+// exponent fl(1/k) as the reference passes it, libm's pow, the IEEE quotient
+BDF_INL double eta_exact(double bx, int k) { return frcp(pow_root(bx, k) + ADDON); }
 
 // cvNlsConvTest (cvode_nls.c:262-263): dcon = del * min(1, crate) / tol, converged when dcon <= 1,
 // tol = tq[4] = CORTES / tq[2]. RN(a / b) <= 1 iff a / b <= 1 + 2^-53 (the midpoint rounds to even,

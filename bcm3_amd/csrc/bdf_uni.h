@@ -125,12 +125,8 @@ BDF_INL double set_bdf_q(S& s)
     return rl1;
 }
 
-// eta_exact of bdf_lane.h with the range check as one scalar branch
-BDF_INL double eta_from_u(double bx, int k)
-{
-    if (!((bx > 1e-30) & (bx < 1e30))) return frcp((bx > 0.0 ? pow(bx, xm::inv_k(k)) : 0.0) + ADDON);
-    return frcp(xm::pow_inv_k(bx, k) + ADDON);
-}
+// eta_exact of bdf_lane.h
+BDF_INL double eta_from_u(double bx, int k) { return eta_exact(bx, k); }
 
 // Step-size ratios below THRESH are discarded (cvSetEta: eta = 1), so an eta candidate only has
 // to be computed exactly when it can reach THRESH. eta = 1 / (bx^(1/k) + ADDON) >= THRESH needs

@@ -241,6 +241,77 @@ XM_FN double pow_inv_k(double x, int k)
 }
 
 // ---------------------------------------------------------------------------------------------
+// glibc's pow itself (sysdeps/ieee754/dbl-64/e_pow.c, glibc >= 2.28: a table-driven log in
+// double-double and a table-driven exp), as the x86-64 libm runs it on FMA/AVX2 hosts (its
+// __pow_fma variant, selected by the ifunc): the operations of that build in its order and with
+// its fused multiply-adds. glibc's pow is not correctly rounded (it differs from pow_inv_k on
+// ~0.08 % of the step-size roots, which alone decided whether 11 % of C3 trajectories came out
+// bit-identical to the reference), so the solvers run this algorithm on the host libm's own tables
+// -- located in the loaded libm at run time (libm_tables.cpp), never shipped -- or, without them,
+// on tables of the same layout computed on the host (about 1 ulp).
+struct GlibcPow {
+    double ln2hi, ln2lo, A[7];      // __pow_log_data: ln2 split, log1p polynomial (A[0] = -1/2)
+    double logtab[128][4];          //   invc, pad, logc, logctail
+    double invln2N, shift, negln2hiN, negln2loN, C[4];  // __exp_data: reduction, C2..C5
+    unsigned long long exptab[256];  //   (tail, sbits) pairs of 2^(i/128)
+};
+
+// pow(x, y) for a positive normal x and 2^-65 <= |y| < 2^63 with |y log x| < 512 (the main path
+// of e_pow.c; the step-size roots: x in (1e-30, 1e30), y = fl(1/k))
+XM_FN double pow_glibc(double x, double y, const GlibcPow& D)
+{
+    // log_inline: x = 2^k z, z/c - 1 = r exact, log x = k ln2 + log c + log1p(r) in double-double
+    const unsigned long long ix = (unsigned long long)as_bits(x);
+    const unsigned long long tmp = ix + 0xC0196AAB00000000ull;  // ix - 0x3fe6955500000000
+    const int i = (int)((tmp >> 45) & 127);
+    const double kd = (double)(int)((long long)tmp >> 52);
+    const double z = as_double((long long)(ix - (tmp & 0xfff0000000000000ull)));
+    const double invc = D.logtab[i][0], logc = D.logtab[i][2], logctail = D.logtab[i][3];
+    const double t1 = __builtin_fma(kd, D.ln2hi, logc);
+    const double r = __builtin_fma(z, invc, -1.0);
+    const double ar = r * D.A[0];
+    const double lo1 = __builtin_fma(kd, D.ln2lo, logctail);
+    const double p12 = __builtin_fma(r, D.A[2], D.A[1]);
+    const double p34 = __builtin_fma(r, D.A[4], D.A[3]);
+    const double t2 = r + t1;
+    const double ar2 = r * ar;
+    const double ar3 = r * ar2;
+    const double lo3 = __builtin_fma(ar, r, -ar2);
+    const double lo2 = (t1 - t2) + r;
+    const double p56 = __builtin_fma(r, D.A[6], D.A[5]);
+    const double hi = t2 + ar2;
+    const double lo4 = (t2 - hi) + ar2;
+    const double q = __builtin_fma(ar2, __builtin_fma(p56, ar2, p34), p12);
+    double lo = ((lo1 + lo2) + lo3) + lo4;
+    lo = __builtin_fma(ar3, q, lo);
+    const double ly = hi + lo;
+    const double ltail = (hi - ly) + lo;
+    // y log x = ehi + elo
+    const double ehi = y * ly;
+    const double elo = __builtin_fma(y, ltail, __builtin_fma(ly, y, -ehi));
+    const int abstop = (int)((as_bits(ehi) >> 52) & 0x7ff);
+    if (abstop < 0x3c9) return 1.0 + ehi;  // |y log x| < 2^-54
+    // exp_inline: ehi = (k + i/128) ln2 + r, 2^(i/128) from the table, exp(r) by its polynomial
+    const double kz = __builtin_fma(ehi, D.invln2N, D.shift);
+    const unsigned long long ki = (unsigned long long)as_bits(kz);
+    const double kk = kz - D.shift;
+    double rr = __builtin_fma(kk, D.negln2hiN, ehi);
+    rr = __builtin_fma(kk, D.negln2loN, rr);
+    const int idx = 2 * (int)(ki & 127);
+    const double tail = as_double((long long)D.exptab[idx]);
+    const unsigned long long sbits = D.exptab[idx + 1] + (ki << 45);
+    rr = elo + rr;
+    const double c23 = __builtin_fma(rr, D.C[1], D.C[0]);
+    const double tr = rr + tail;
+    const double r2 = rr * rr;
+    const double c45 = __builtin_fma(rr, D.C[3], D.C[2]);
+    const double s1 = __builtin_fma(c23, r2, tr);
+    const double t = __builtin_fma(c45, r2 * r2, s1);
+    const double scale = as_double((long long)sbits);
+    return __builtin_fma(t, scale, scale);
+}
+
+// ---------------------------------------------------------------------------------------------
 // glibc's log1p, erf and erfc are the fdlibm algorithms (not correctly rounded), so they are
 // restated operation for operation, with glibc's evaluation order of the polynomials
 // (second-order Horner / Estrin splits) and its constants; exp inside erf / erfc is the CR exp

@@ -26,6 +26,9 @@ struct PopPKDevModel {
     const int32_t* simulate_until;
 };
 
+// the current device's copy of the host libm's pow tables (bdf_lane.h g_glibc_pow), once per
+// device; *glibc: 1 when the solvers use glibc's pow, 0 for the correctly rounded fallback
+hipError_t popk_prepare_device(int* glibc);
 hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
                        double* patient_llh_scratch, int32_t* traj_status_scratch, double* traj_out,
                        bcm3hip_traj_stats* stats_out, int lanes_per_wave, int block_waves, int uni_solver,

@@ -17,6 +17,10 @@
 // whole integrator state lives in VGPRs.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
 #include <cmath>
 #include <cstdint>
 #include <type_traits>
@@ -626,6 +630,39 @@ __global__ void __launch_bounds__(256) popk_reduce_kernel(int64_t n, int P, cons
     }
     logp[e] = acc;
     if (status) status[e] = st;
+}
+
+}  // namespace bcm3hip
+
+bool bcm3_find_glibc_pow(xm::GlibcPow* out);  // libm_tables.cpp
+void bcm3_make_pow_tables(xm::GlibcPow* out);
+
+namespace bcm3hip {
+
+hipError_t popk_prepare_device(int* glibc)
+{
+    static std::mutex mu;
+    static int found = -1;  // tables of the loaded libm: -1 not searched, 0 absent, 1 found
+    static xm::GlibcPow tables;
+    static int state[64] = {};  // per device: 0 not uploaded, 1 glibc's tables, 2 computed ones
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    if (dev >= 0 && dev < 64 && state[dev]) {
+        if (glibc) *glibc = state[dev] == 1;
+        return hipSuccess;
+    }
+    if (found < 0) {
+        const char* env = getenv("BCM3_POW");  // "computed": the host-computed tables (tests)
+        found = (!(env && !strcmp(env, "computed")) && bcm3_find_glibc_pow(&tables)) ? 1 : 0;
+        if (!found) bcm3_make_pow_tables(&tables);
+    }
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_glibc_pow), &tables, sizeof(tables));
+    if (e != hipSuccess) return e;
+    if (dev >= 0 && dev < 64) state[dev] = found ? 1 : 2;
+    if (glibc) *glibc = found;
+    return hipSuccess;
 }
 
 hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,

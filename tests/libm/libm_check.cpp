@@ -11,6 +11,9 @@
 
 #include "../../bcm3_amd/csrc/libm_exact.h"
 
+bool bcm3_find_glibc_pow(xm::GlibcPow* out);  // bcm3_amd/csrc/libm_tables.cpp
+void bcm3_make_pow_tables(xm::GlibcPow* out);
+
 static double cr(__float128 v) { return (double)v; }  // quad -> double rounds to nearest
 
 int main(int argc, char** argv)
@@ -20,6 +23,12 @@ int main(int argc, char** argv)
     std::mt19937_64 rng(atol(argv[3]));
     std::uniform_real_distribution<double> U(0.0, 1.0);
     long ag = 0, ac = 0, gc = 0;
+    static xm::GlibcPow D;
+    if (!strcmp(fn, "powglibc") && !bcm3_find_glibc_pow(&D)) {
+        printf("tables not found\n");
+        return 2;
+    }
+    if (!strcmp(fn, "powcomputed")) bcm3_make_pow_tables(&D);
     for (long i = 0; i < n; i++) {
         double x, mine, lib;
         __float128 q;
@@ -44,6 +53,14 @@ int main(int argc, char** argv)
             mine = e ? xm::erf(x) : xm::erfc(x);
             lib = e ? erf(x) : erfc(x);
             q = e ? erfq((__float128)x) : erfcq((__float128)x);
+        } else if (!strcmp(fn, "powglibc") || !strcmp(fn, "powcomputed")) {
+            // the solvers' step-size roots: x in (1e-30, 1e30), some within 2^-40 of 1
+            const int k = 2 + (int)(i % 6);
+            x = (i % 7 == 0) ? 1.0 + (U(rng) - 0.5) * 0x1p-40 : exp(-69.0 + 138.0 * U(rng));
+            const double y = xm::inv_k(k);
+            mine = xm::pow_glibc(x, y, D);
+            lib = pow(x, y);
+            q = powq((__float128)x, (__float128)y);
         } else {
             const int k = 2 + (int)(i % 6);
             x = exp(-60.0 + 60.0 * U(rng));

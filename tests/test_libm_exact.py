@@ -19,8 +19,8 @@ SRC = os.path.join(ROOT, "tests", "libm", "libm_check.cpp")
 @pytest.fixture(scope="module")
 def checker(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("libm") / "libm_check")
-    subprocess.run(["g++", "-O2", "-std=c++20", "-ffp-contract=off", "-mfma", "-o", exe, SRC, "-lquadmath"],
-                   check=True)
+    subprocess.run(["g++", "-O2", "-std=c++20", "-ffp-contract=off", "-mfma", "-o", exe, SRC,
+                    os.path.join(ROOT, "bcm3_amd", "csrc", "libm_tables.cpp"), "-lquadmath"], check=True)
     return exe
 
 
@@ -47,3 +47,18 @@ def test_log1p_is_glibc(checker):
 def test_erf_is_glibc(checker, fn):
     ag, _, _ = run(checker, fn)
     assert ag > 0.9995, (fn, ag)
+
+
+def test_pow_is_glibc(checker):
+    """xm::pow_glibc with the tables of the loaded libm: glibc's pow bit for bit, including the
+    arguments where glibc is not correctly rounded"""
+    ag, _, gc = run(checker, "powglibc", n=1000000)
+    assert ag == 1.0, ag
+    assert gc < 1.0  # the check sees the non-correctly-rounded cases
+
+
+def test_pow_computed_tables_fallback(checker):
+    """without the libm's tables the same algorithm on host-computed tables: correctly rounded on
+    all but a small fraction of the roots (the fallback)"""
+    _, ac, _ = run(checker, "powcomputed", n=400000)
+    assert ac > 0.99, ac

@@ -11,4 +11,4 @@ cd "${SRC:-$ROOT/bcm3_amd/csrc}"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -mllvm -simplifycfg-sink-common=false \
   -mllvm -structurizecfg-skip-uniform-regions -w -I"$ROOT/build/obj" "$@" -shared -o "$ROOT/varlib/$name.so" \
   popk_kernel.hip expm_pk_kernel.hip analytic_kernel.hip pt_kernels.hip proposal_kernels.hip runtime.hip \
-  cellpop_kernels.hip bcm3hip_api.cpp cellpop_rt.cpp -L/opt/rocm/lib -lrccl -lhiprtc
+  cellpop_kernels.hip bcm3hip_api.cpp cellpop_rt.cpp libm_tables.cpp -L/opt/rocm/lib -lrccl -lhiprtc
