@@ -461,6 +461,10 @@ int bcm3hip_open_expm_pk(int device, const bcm3hip_expm_pk_model* m, bcm3hip_ctx
         bcm3hip_close(c);
         return r;
     }
+    if (expm_prepare_device() != hipSuccess) {
+        bcm3hip_close(c);
+        return BCM3HIP_ERR_HIP;
+    }
     c->kind = 3;
     c->d = m->d;
     ExpmPKDevModel& x = c->xm;

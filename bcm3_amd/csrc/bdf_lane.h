@@ -262,15 +262,14 @@ BDF_INL double eta_from(double bx, int k)
 // IEEE quotients and square roots (frcp / fdiv / fsqrt above, correctly rounded), and libm's
 // pow through xm::pow_glibc (libm_exact.h). The cell-population solver keeps eta_from.
 
-// The pow tables (libm_exact.h pow_glibc), uploaded by popk_prepare_device: the host libm's own
-// when it has them, so that the step-size roots are glibc's results bit for bit, else tables
-// computed on the host (libm_tables.cpp bcm3_make_pow_tables: the same algorithm, ~1 ulp)
-static __constant__ xm::GlibcPow g_glibc_pow;
-
 // SUNRpowerR(bx, fl(1/k)) (sundials_math.c:40-52, libm's pow)
+// with the tables popk_prepare_device uploaded (xm::xm_tables: the host libm's own, so that the
+// roots are glibc's results bit for bit, or computed ones of the same layout, ~1 ulp)
 BDF_INL double pow_root(double bx, int k)
 {
-    if (BDF_LIKELY((bx >= 0x1p-1022) & (bx < 0x1p1023))) return xm::pow_glibc(bx, xm::inv_k(k), g_glibc_pow);
+    if (BDF_LIKELY(xm::xm_tables.ok & (bx >= 0x1p-1022) & (bx < 0x1p1023)))
+        return xm::pow_glibc(bx, xm::inv_k(k), xm::xm_tables);
+    if (bx > 1e-30 && bx < 1e30) return xm::pow_inv_k(bx, k);
     return (bx > 0.0) ? pow(bx, xm::inv_k(k)) : 0.0;
 }
 

@@ -22,9 +22,12 @@
 
 #include <cmath>
 #include <cstdint>
+#include <mutex>
 
 #include "pk_math.h"
 #include "popk_kernel.h"
+
+const xm::GlibcPow* bcm3_pow_tables(int* from_libm);  // libm_tables.cpp
 
 namespace bcm3hip {
 namespace {
@@ -452,6 +455,22 @@ __global__ void __launch_bounds__(64) expm_pk_chain_kernel(ExpmPKDevModel m, int
 }
 
 }  // namespace
+
+// this translation unit's copy of the libm tables (libm_exact.h xm_tables: glibc's exp in the
+// parameter maps), once per device
+hipError_t expm_prepare_device()
+{
+    static std::mutex mu;
+    static bool done[64] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    if (dev >= 0 && dev < 64 && done[dev]) return hipSuccess;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(xm::xm_tables), bcm3_pow_tables(nullptr), sizeof(xm::GlibcPow));
+    if (e == hipSuccess && dev >= 0 && dev < 64) done[dev] = true;
+    return e;
+}
 
 hipError_t launch_expm_pk(const ExpmPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
                           double* exps, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop)

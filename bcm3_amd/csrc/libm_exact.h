@@ -90,6 +90,42 @@ XM_FN long long as_bits(double x) { return __builtin_bit_cast(long long, x); }
 // 2^k for -1022 <= k <= 1023
 XM_FN double pow2i(int k) { return as_double((long long)((unsigned long long)(k + 1023) << 52)); }
 
+// The tables of glibc's pow and exp (e_pow.c, e_exp.c since glibc 2.28; see pow_glibc below)
+struct GlibcPow {
+    double ln2hi, ln2lo, A[7];      // __pow_log_data: ln2 split, log1p polynomial (A[0] = -1/2)
+    double logtab[128][4];          //   invc, pad, logc, logctail
+    double invln2N, shift, negln2hiN, negln2loN, C[4];  // __exp_data: reduction, C2..C5
+    unsigned long long exptab[256];  //   (tail, sbits) pairs of 2^(i/128)
+    int ok;                          // 1: filled (a zero-initialised copy selects the fallbacks)
+};
+
+#ifdef __HIP__
+// the device's copy, per translation unit (popk_prepare_device / expm_prepare_device upload it;
+// never uploaded, ok = 0 selects the correctly rounded functions)
+static __constant__ GlibcPow xm_tables;
+#endif
+
+// glibc's exp for 2^-54 <= |x| < 512 (the main path of e_exp.c as its FMA variant computes it):
+// x = (k + i/128) ln2 + r, 2^(i/128) = scale (1 + tail) from the table, exp(r) by its polynomial
+XM_FN double exp_glibc(double x, const GlibcPow& D)
+{
+    const double kz = __builtin_fma(x, D.invln2N, D.shift);
+    const unsigned long long ki = (unsigned long long)as_bits(kz);
+    const double kd = kz - D.shift;
+    double r = __builtin_fma(kd, D.negln2hiN, x);
+    r = __builtin_fma(kd, D.negln2loN, r);
+    const int idx = 2 * (int)(ki & 127);
+    const unsigned long long sbits = D.exptab[idx + 1] + (ki << 45);
+    const double c23 = __builtin_fma(r, D.C[1], D.C[0]);
+    const double tr = r + as_double((long long)D.exptab[idx]);
+    const double r2 = r * r;
+    const double c45 = __builtin_fma(r, D.C[3], D.C[2]);
+    const double s1 = __builtin_fma(c23, r2, tr);
+    const double t = __builtin_fma(c45, r2 * r2, s1);
+    const double scale = as_double((long long)sbits);
+    return __builtin_fma(scale, t, scale);
+}
+
 // ln 2 = LN2_1 + LN2_2 + LN2_3, LN2_1 and LN2_2 with 42 significant bits (k * LN2_i exact for
 // |k| < 2^11)
 constexpr double LN2_1 = 0.6931471805598903;
@@ -137,14 +173,25 @@ XM_FN dd exp_dd(double x)
     return {y.hi * sc, y.lo * sc};
 }
 
-// glibc exp (correctly rounded result)
-XM_FN double exp_i(double x)
+// exp, correctly rounded
+XM_FN double exp_cr(double x)
 {
     if (!(x == x)) return x + x;
     if (x > 709.782712893384) return __builtin_inf();
     if (x < -745.1332191019412) return 0.0;
     const dd y = exp_dd(x);  // (below ~-708 the result is subnormal and not CR; off the path)
     return y.hi + y.lo;
+}
+
+// glibc's exp: on the device with the uploaded tables (its own results, in the range its main
+// path covers), else the correctly rounded exp (glibc agrees with it on all but ~0.03 %)
+XM_FN double exp_i(double x)
+{
+#if defined(__HIP__) && defined(__HIP_DEVICE_COMPILE__)
+    const double ax = __builtin_fabs(x);
+    if (xm_tables.ok & (ax >= 0x1p-54) & (ax < 512.0)) return exp_glibc(x, xm_tables);
+#endif
+    return exp_cr(x);
 }
 
 // glibc log (correctly rounded result): one Newton step y0 + log1p(x e^-y0 - 1) from the
@@ -249,12 +296,6 @@ XM_FN double pow_inv_k(double x, int k)
 // bit-identical to the reference), so the solvers run this algorithm on the host libm's own tables
 // -- located in the loaded libm at run time (libm_tables.cpp), never shipped -- or, without them,
 // on tables of the same layout computed on the host (about 1 ulp).
-struct GlibcPow {
-    double ln2hi, ln2lo, A[7];      // __pow_log_data: ln2 split, log1p polynomial (A[0] = -1/2)
-    double logtab[128][4];          //   invc, pad, logc, logctail
-    double invln2N, shift, negln2hiN, negln2loN, C[4];  // __exp_data: reduction, C2..C5
-    unsigned long long exptab[256];  //   (tail, sbits) pairs of 2^(i/128)
-};
 
 // pow(x, y) for a positive normal x and 2^-65 <= |y| < 2^63 with |y log x| < 512 (the main path
 // of e_pow.c; the step-size roots: x in (1e-30, 1e30), y = fl(1/k))

@@ -100,6 +100,7 @@ bool bcm3_find_glibc_pow(xm::GlibcPow* out)
     out->negln2loN = f.expd[3];
     std::memcpy(out->C, f.expd + 4, sizeof(double) * 4);
     std::memcpy(out->exptab, f.expd + 14, sizeof(uint64_t) * 256);
+    out->ok = 1;
     return true;
 }
 
@@ -140,4 +141,23 @@ void bcm3_make_pow_tables(xm::GlibcPow* out)
         out->exptab[2 * i] = bits(tail);
         out->exptab[2 * i + 1] = bits(vd) - ((uint64_t)i << 45);
     }
+    out->ok = 1;
+}
+
+// the tables every device copy is filled from: the loaded libm's, else computed ones (BCM3_POW=
+// computed forces those, for tests); *from_libm 1 for the former
+#include <cstdlib>
+#include <mutex>
+const xm::GlibcPow* bcm3_pow_tables(int* from_libm)
+{
+    static std::once_flag once;
+    static xm::GlibcPow t;
+    static int found = 0;
+    std::call_once(once, [] {
+        const char* env = std::getenv("BCM3_POW");
+        found = (!(env && !std::strcmp(env, "computed")) && bcm3_find_glibc_pow(&t)) ? 1 : 0;
+        if (!found) bcm3_make_pow_tables(&t);
+    });
+    if (from_libm) *from_libm = found;
+    return &t;
 }

@@ -75,6 +75,7 @@ struct ExpmPKDevModel {
 };
 
 // exps: [n][n_jobs][n*n] scratch
+hipError_t expm_prepare_device();  // expm_pk_kernel.hip: its copy of the libm tables
 hipError_t launch_expm_pk(const ExpmPKDevModel& m, int64_t n, const double* values, double* logp, int32_t* status,
                           double* exps, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop);
 

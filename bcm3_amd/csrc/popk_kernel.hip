@@ -634,17 +634,14 @@ __global__ void __launch_bounds__(256) popk_reduce_kernel(int64_t n, int P, cons
 
 }  // namespace bcm3hip
 
-bool bcm3_find_glibc_pow(xm::GlibcPow* out);  // libm_tables.cpp
-void bcm3_make_pow_tables(xm::GlibcPow* out);
+const xm::GlibcPow* bcm3_pow_tables(int* from_libm);  // libm_tables.cpp
 
 namespace bcm3hip {
 
 hipError_t popk_prepare_device(int* glibc)
 {
     static std::mutex mu;
-    static int found = -1;  // tables of the loaded libm: -1 not searched, 0 absent, 1 found
-    static xm::GlibcPow tables;
-    static int state[64] = {};  // per device: 0 not uploaded, 1 glibc's tables, 2 computed ones
+    static int state[64] = {};  // per device: 0 not uploaded, 1 libm's tables, 2 computed ones
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -653,12 +650,9 @@ hipError_t popk_prepare_device(int* glibc)
         if (glibc) *glibc = state[dev] == 1;
         return hipSuccess;
     }
-    if (found < 0) {
-        const char* env = getenv("BCM3_POW");  // "computed": the host-computed tables (tests)
-        found = (!(env && !strcmp(env, "computed")) && bcm3_find_glibc_pow(&tables)) ? 1 : 0;
-        if (!found) bcm3_make_pow_tables(&tables);
-    }
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_glibc_pow), &tables, sizeof(tables));
+    int found = 0;
+    const xm::GlibcPow* t = bcm3_pow_tables(&found);
+    e = hipMemcpyToSymbol(HIP_SYMBOL(xm::xm_tables), t, sizeof(*t));
     if (e != hipSuccess) return e;
     if (dev >= 0 && dev < 64) state[dev] = found ? 1 : 2;
     if (glibc) *glibc = found;

@@ -24,7 +24,7 @@ int main(int argc, char** argv)
     std::uniform_real_distribution<double> U(0.0, 1.0);
     long ag = 0, ac = 0, gc = 0;
     static xm::GlibcPow D;
-    if (!strcmp(fn, "powglibc") && !bcm3_find_glibc_pow(&D)) {
+    if ((!strcmp(fn, "powglibc") || !strcmp(fn, "expglibc")) && !bcm3_find_glibc_pow(&D)) {
         printf("tables not found\n");
         return 2;
     }
@@ -53,6 +53,12 @@ int main(int argc, char** argv)
             mine = e ? xm::erf(x) : xm::erfc(x);
             lib = e ? erf(x) : erfc(x);
             q = e ? erfq((__float128)x) : erfcq((__float128)x);
+        } else if (!strcmp(fn, "expglibc")) {
+            // the range of glibc exp's main path, 2^-54 <= |x| < 512
+            x = (i % 2 ? -1.0 : 1.0) * ((i % 5 == 0) ? 0x1p-54 * exp(36.0 * U(rng)) : 500.0 * U(rng) + 0x1p-50);
+            mine = xm::exp_glibc(x, D);
+            lib = exp(x);
+            q = expq((__float128)x);
         } else if (!strcmp(fn, "powglibc") || !strcmp(fn, "powcomputed")) {
             // the solvers' step-size roots: x in (1e-30, 1e30), some within 2^-40 of 1
             const int k = 2 + (int)(i % 6);

@@ -57,6 +57,13 @@ def test_pow_is_glibc(checker):
     assert gc < 1.0  # the check sees the non-correctly-rounded cases
 
 
+def test_exp_is_glibc(checker):
+    """xm::exp_glibc (the device's exp with the uploaded tables) is glibc's exp bit for bit over the
+    range of its main path"""
+    ag, _, gc = run(checker, "expglibc", n=1000000)
+    assert ag == 1.0, ag
+
+
 def test_pow_computed_tables_fallback(checker):
     """without the libm's tables the same algorithm on host-computed tables: correctly rounded on
     all but a small fraction of the roots (the fallback)"""
