@@ -317,24 +317,24 @@ BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
 
 // BCM3_PHASES (profiling build only): per-phase s_memtime cycle accumulators
 #ifdef BCM3_PHASES
-#define BDF_PH(k)                          \
-    do {                                   \
-        __builtin_amdgcn_sched_barrier(0); \
-        const long long t_ = clock64();    \
-        s.ph[k] += t_ - s.tlast;           \
-        s.tlast = t_;                      \
-        __builtin_amdgcn_sched_barrier(0); \
+#define BDF_PH(k)                                  \
+    do {                                           \
+        __builtin_amdgcn_sched_barrier(0);         \
+        const unsigned t_ = (unsigned)clock64();   \
+        s.ph[k] += t_ - s.tlast;                   \
+        s.tlast = t_;                              \
+        __builtin_amdgcn_sched_barrier(0);         \
     } while (0)
 // the fast loop's cycles of a whole step, split by kind (plain / recomputing) via selects
-#define BDF_PH_STEP(t0, kp, kg, c)                   \
-    do {                                             \
-        __builtin_amdgcn_sched_barrier(0);           \
-        const long long d_ = clock64() - (t0);       \
-        s.ph[kp] += (c) ? d_ : 0;                    \
-        s.ph[kg] += (c) ? 0 : d_;                    \
-        __builtin_amdgcn_sched_barrier(0);           \
+#define BDF_PH_STEP(t0, kp, kg, c)                     \
+    do {                                               \
+        __builtin_amdgcn_sched_barrier(0);             \
+        const unsigned d_ = (unsigned)clock64() - (t0); \
+        s.ph[kp] += (c) ? d_ : 0u;                     \
+        s.ph[kg] += (c) ? 0u : d_;                     \
+        __builtin_amdgcn_sched_barrier(0);             \
     } while (0)
-#define BDF_PH_NOW() clock64()
+#define BDF_PH_NOW() ((unsigned)clock64())
 #elif defined(BCM3_MARKS)
 // ISA study build: a comment per phase boundary in the -S output (tools/step_isa.py)
 #define BDF_PH(k) asm volatile("; BDFMARK %0" ::"i"(k))
@@ -348,12 +348,15 @@ BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
 #define BDF_PH_STEP(t0, kp, kg, c) \
     do {                           \
     } while (0)
-#define BDF_PH_NOW() 0ll
+#define BDF_PH_NOW() 0u
 #endif
-// 0-9: the general step (tools/phase_probe.py NAMES); 10-18: the phases of a fast-loop step
-// (vec::fast_run; 10-15 plain steps only); 19/20: whole plain / recomputing fast-loop steps;
-// 21/22: their counts; 23: the marker's own cost (16 back-to-back markers per trajectory)
-constexpr int NPHASES = 24;
+// 32-bit cycle accumulators (wrapping differences of the low word), so that the profiling build
+// adds few scalar registers. 0-9: the general step (tools/phase_probe.py NAMES); 10-17: the phases
+// of a plain fast-loop step (vec::fast_run, coefficients held); 18: the loop's exit test and back
+// edge (every fast-loop step); 19/20: whole plain / recomputing fast-loop steps; 21/22: their
+// counts; 23: the marker's own cost (16 back-to-back markers per trajectory); 24-26: the
+// convergence test and completion of a recomputing fast-loop step
+constexpr int NPHASES = 28;
 
 struct BdfCounters {
     int nst_total, nfe, nni, nsetups, nje, netf, ncfn, nreinit;
@@ -383,8 +386,8 @@ struct BdfState {
     int check_tolsf;  // 0: the too-much-accuracy test cannot fire (rtol >= 1e-10, atol >= 0)
     BdfCounters cnt;
 #ifdef BCM3_PHASES
-    long long ph[NPHASES];
-    long long tlast;
+    unsigned ph[NPHASES];
+    unsigned tlast;
     int qh[QMAX + 1];  // successful steps per order
 #endif
 };

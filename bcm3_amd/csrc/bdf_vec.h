@@ -123,8 +123,8 @@ struct VecState {
     int check_tolsf;
     std::conditional_t<STATS, BdfCounters, NoCounters> cnt;
 #ifdef BCM3_PHASES
-    long long ph[NPHASES];
-    long long tlast;
+    unsigned ph[NPHASES];
+    unsigned tlast;
     int qh[QMAX + 1];
 #endif
 };
@@ -846,7 +846,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         asm volatile("; BDFMARK fast_top Q=%0" ::"i"(Q));
 #endif
         BDF_PH(18);  // the loop's exit test and back edge
-        const long long ph_t0 = BDF_PH_NOW();
+        const unsigned ph_t0 = BDF_PH_NOW();
         vec::ewt_set(s);
         const double saved_t = s.tn;
         const double eta_eff = (s.hprime != s.h) ? s.eta : 1.0;
@@ -872,7 +872,10 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             if (BDF_LIKELY(div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4]) & (dsm <= 1.0))) {
                 s.acnrm = del;
                 s.nls_jcur = 0;
-                BDF_PH(15);
+                if constexpr (decltype(held)::value)
+                    BDF_PH(15);
+                else
+                    BDF_PH(24);
             } else {
                 const bool conv = vec::newton_rest<NS>(s, mdl, rl1, CONV_NONE, setup, cscale, del);
                 BDF_PH(5);
@@ -887,7 +890,7 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
                     return false;
                 }
             }
-            vec::complete_q<Q, NS, true, 16, decltype(held)::value>(s, dsm, tc);
+            vec::complete_q<Q, NS, true, decltype(held)::value ? 16 : 25, decltype(held)::value>(s, dsm, tc);
             return true;
         };
         if (BDF_LIKELY(plain)) {

@@ -391,9 +391,9 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
 #ifdef BCM3_PHASES
     cfor<0, NPHASES>([&](auto k) __attribute__((always_inline)) { s.ph[CI(k)] = 0; });
     cfor<0, QMAX + 1>([&](auto k) __attribute__((always_inline)) { s.qh[CI(k)] = 0; });
-    s.tlast = clock64();
+    s.tlast = (unsigned)clock64();
     for (int k = 0; k < 16; k++) BDF_PH(23);  // the marker's own cost
-    s.tlast = clock64();
+    s.tlast = (unsigned)clock64();
 #endif
 
     // observation term for output index i with state yi (.cpp:412-423)

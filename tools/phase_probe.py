@@ -17,11 +17,13 @@ from bcm3_amd import _hip  # noqa: E402
 
 NAMES = ["driver(out/cb/reinit)", "entry+ewt", "adjust+rescale", "predict", "set_bdf", "newton",
          "errtest/fail", "complete", "eta/next", "tstop/return"]
-# the fast loop (vec::fast_run): 10-15 are timed on plain steps only (coefficients held), 16-18 on
-# every fast-loop step; 19/20 whole plain / recomputing steps, 21/22 their counts, 23 the marker
+# the fast loop (vec::fast_run): 10-17 are timed on plain steps (coefficients held), 18 on every
+# fast-loop step, 24-26 on recomputing fast-loop steps after their Newton correction; 19/20 whole
+# plain / recomputing steps, 21/22 their counts, 23 the marker (bdf_lane.h NPHASES)
 FAST = ["ewt + plain test", "predict", "newton: rhs", "newton: solve (I-gJ)^-1", "newton: wrms norm",
-        "conv + error test", "complete: zn, tau", "complete: eta (root)", "exit test + back edge"]
-NPH = 24
+        "conv + error test", "complete: zn", "complete: eta"]
+GEN = ["conv + error test", "complete: zn, tau", "complete: eta"]
+NPH = 28
 
 
 def main():
@@ -59,31 +61,34 @@ def main():
 
 
 def fast_report(allph, nst, ms, tot):
-    """the plain fast-loop step's cycles by phase, the marker's own cost subtracted"""
+    """cycles per fast-loop step by phase, the marker's own cost subtracted"""
     mark = allph[:, 23].sum() / (16 * allph.shape[0])
     n_plain, n_gen = allph[:, 21].sum(), allph[:, 22].sum()
     if n_plain == 0:
         print("no fast-loop steps (not the VEC solver?)")
         return
+    n_fast = n_plain + n_gen
     c_plain = allph[:, 19].sum() / n_plain
     c_gen = allph[:, 20].sum() / max(n_gen, 1)
-    n_fast = n_plain + n_gen
     print(f"\nfast loop: {n_fast / nst.sum():.1%} of all steps; plain (coefficients held) {n_plain / n_fast:.1%} of them")
     print(f"marker cost {mark:.0f} cycles (16 back-to-back per trajectory)")
-    # markers inside one plain step: 10..15 (6), 16, 17 (complete) = 8, plus the step total's own read
-    k_plain = 8
+    k_plain, k_gen = 8, 7
     print(f"whole step, loop top to exit test: plain {c_plain:.0f} cycles ({c_plain - k_plain * mark:.0f} without its "
-          f"{k_plain} markers), recomputing {c_gen:.0f}")
-    per = [allph[:, 10 + i].sum() / n_plain for i in range(6)] + \
-          [allph[:, 16 + i].sum() / n_fast for i in range(3)]
-    net = [max(v - mark, 0.0) for v in per]
-    print(f"{'phase':28s} {'cycles':>8s} {'- marker':>9s} {'share':>6s}")
-    for name, v, w in zip(FAST, per, net):
-        print(f"  {name:26s} {v:8.0f} {w:9.0f} {100 * w / sum(net):5.1f}%")
-    print(f"  {'sum':26s} {sum(per):8.0f} {sum(net):9.0f}")
-    # the product build's rate for comparison: cycles per step of the slowest trajectory
-    print(f"(phases build: kernel {ms:.3f} ms; markers slow each step by about {k_plain + 1} x {mark:.0f} cycles)")
-
+          f"{k_plain} markers), recomputing {c_gen:.0f} ({c_gen - k_gen * mark:.0f} without its {k_gen})")
+    rows = [(f"plain: {n}", allph[:, 10 + i].sum() / n_plain) for i, n in enumerate(FAST)]
+    rows.append(("exit test + back edge (all)", allph[:, 18].sum() / n_fast))
+    print(f"{'plain step phase':34s} {'cycles':>8s} {'- marker':>9s}")
+    tot_net = 0.0
+    for name, v in rows:
+        net = max(v - mark, 0.0)
+        tot_net += net
+        print(f"  {name:32s} {v:8.0f} {net:9.0f}")
+    print(f"  {'sum':32s} {'':8s} {tot_net:9.0f}")
+    print(f"{'recomputing step: after Newton':34s}")
+    for i, n in enumerate(GEN):
+        v = allph[:, 24 + i].sum() / max(n_gen, 1)
+        print(f"  {n:32s} {v:8.0f} {max(v - mark, 0.0):9.0f}")
+    print(f"(phases build: kernel {ms:.3f} ms)")
 
 if __name__ == "__main__":
     main()
