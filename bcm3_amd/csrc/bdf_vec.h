@@ -419,6 +419,56 @@ BDF_INL void tq_13(S& s, const TqCtx& c)
     s.tq[3] = tq3;
 }
 
+// a / b within 2^-48 relative (v_rcp_f64 and one Newton step): the order-change screen below
+BDF_INL double qdiv(double a, double b)
+{
+    double r = __builtin_amdgcn_rcp(b);
+    r = __builtin_fma(__builtin_fma(-b, r, 1.0), r, r);
+    return a * r;
+}
+
+// Order-change screen (qwait == 0, every other step): an order-change candidate only matters when
+// it reaches THRESH, i.e. when its bx is at most eta_cut (which already carries a 1e-9 relative
+// margin); below that it acts exactly like eta_candidate's 0 in cvChooseEta. The candidates'
+// bx = BIAS (wrms tq) are bounded here from approximate quotients (qdiv, 2^-48) and without the
+// square roots (bx^2 from the sum of squares): when both exceed their cut by 1e-10 relative, the
+// exact evaluation below would return eta_candidate's 0 for both, and it is skipped (tq[1] and
+// tq[3], read only by it, are not needed). The quotients whose operands can cancel keep their
+// exact forms (xi_inv2 and 1 - A6 + A5 are computed as tq_13 computes them).
+template <int Q, int NS, class S>
+BDF_INL bool order_change_skippable(const S& s, const TqCtx& c)
+{
+    constexpr int q = Q;
+    constexpr double margin = 1.0 + 1e-10;
+    bool small = true;
+    if constexpr (q > 1) {
+        const double A3 = c.alpha0 + 1.0 / q;
+        const double A4 = c.alpha0_hat + c.xi_inv;
+        const double tq1 = fabs(qdiv(c.xistar_inv, c.lq) * ((1.0 - A4 + A3) * (1.0 / tq_a3(q))));
+        const double p = s.zn[q] * s.ewt;
+        const double b1 = BIAS1 * tq1;
+        const double bx2 = wave_uniform(lane_sum_v<NS>(p * p) * (1.0 / NS) * (b1 * b1));
+        constexpr double cut = uni::eta_cut(q) * margin;
+        small = bx2 > cut * cut;
+    }
+    if constexpr (q != QMAX) {
+        if (small & (s.saved_tq5 != 0.0)) {
+            const double cquot = qdiv(s.tq[5], s.saved_tq5) * powI(qdiv(s.h, s.tau[2]), q + 1);
+            const double tv = (-cquot) * s.zn[QMAX] + s.acor;
+            const double xi_inv2 = fdiv(s.h, c.hsum2);
+            const double A5 = c.alpha0 - 1.0 / (q + 1);
+            const double A6 = c.alpha0_hat - xi_inv2;
+            const double tq3 = fabs(qdiv(qdiv(1.0 - A6 + A5, c.A2), xi_inv2 * (double)(q + 2) * A5));
+            const double p = tv * s.ewt;
+            const double b3 = BIAS3 * tq3;
+            const double bx2 = wave_uniform(lane_sum_v<NS>(p * p) * (1.0 / NS) * (b3 * b3));
+            constexpr double cut = uni::eta_cut(q + 2) * margin;
+            small = bx2 > cut * cut;
+        }
+    }
+    return small;
+}
+
 // one Newton correction (uni::newton_correction)
 // (PHB >= 0: the phases build marks the right-hand side, the solve and the norm as PHB, PHB + 1, PHB + 2)
 template <int NS, int PHB = -1, class S, class Model>
@@ -581,7 +631,7 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
         const double etaq = uni::eta_candidate<q + 1>(bx);
         double eta = etaq;
         s.qprime = q;
-        if (s.qwait == 0) {
+        if ((s.qwait == 0) && !vec::order_change_skippable<q, NS>(s, tc)) {
             s.qwait = 2;
             vec::tq_13<q>(s, tc);  // qwait was 1 in this step's set_bdf_q
             double etaqm1 = 0.0, etaqp1 = 0.0;
@@ -606,6 +656,9 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
                 s.qprime = q + 1;
                 s.zn[QMAX] = s.acor;
             }
+        } else if (s.qwait == 0) {
+            // both order-change candidates screened below THRESH: cvChooseEta keeps q, eta = etaq
+            s.qwait = 2;
         }
         const bool small = (eta < THRESH);
         s.eta = small ? 1.0 : SUNMIN(eta, s.etamax);

@@ -257,7 +257,8 @@ PLAIN = ["10", "11", "12", "13", "14", "15", "16", "17"]
 PHASE_NAMES = {"top": "ewt + plain test", "18": "ewt + plain test", "10": "predict", "11": "newton: rhs",
                "12": "newton: solve", "13": "newton: wrms norm", "14": "conv + error test",
                "15": "complete: zn, tau", "16": "complete: eta (root)", "17": "exit test + back edge",
-               "general": "rescale", "2": "predict", "3": "set_bdf", "4": "newton"}
+               "general": "rescale", "2": "predict", "3": "set_bdf", "4": "newton",
+               "24": "complete: zn, tau", "25": "complete: eta", "26": "exit test + back edge"}
 
 
 def fmt(c):
@@ -290,7 +291,7 @@ def main():
         for label, sb, seq, avoid in (
                 ("plain step (coefficients held)", False, PLAIN, ("general",)),
                 ("general attempt recomputing them (set_bdf)", True,
-                 (["general", "2", "3", "4", "15", "16", "17"] if general else ["2", "3", "4", "15", "16", "17"]),
+                 (["general", "2", "3", "4", "24", "25", "26"] if general else ["2", "3", "4", "24", "25", "26"]),
                  ())):
             p = step_path(blocks, order, top, seq, sb, avoid)
             if not p:
@@ -300,7 +301,7 @@ def main():
             if "--dump" in sys.argv and q == int(sys.argv[sys.argv.index("--dump") + 1]):
                 dump(blocks, p)
             print(f"  {label} ({len(p) - 1} blocks): {fmt(h)}")
-            for k in ("top", "18", "general", "2", "3", "4") + tuple(PLAIN) + ("tail",):
+            for k in ("top", "18", "general", "2", "3", "4") + tuple(PLAIN) + ("24", "25", "26", "tail"):
                 if k in ph:
                     print(f"     phase {k:>7} {PHASE_NAMES.get(k, ''):24s}: {fmt(ph[k])}")
 
