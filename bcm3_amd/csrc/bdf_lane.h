@@ -335,6 +335,14 @@ BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
         __builtin_amdgcn_sched_barrier(0);             \
     } while (0)
 #define BDF_PH_NOW() ((unsigned)clock64())
+// cycles since t0 into ph[k] (the running phase clock tlast is left alone), and event counts
+#define BDF_PH_ADD(k, t0)                               \
+    do {                                                \
+        __builtin_amdgcn_sched_barrier(0);              \
+        s.ph[k] += (unsigned)clock64() - (t0);          \
+        __builtin_amdgcn_sched_barrier(0);              \
+    } while (0)
+#define BDF_PH_CNT(k, c) (s.ph[k] += (c) ? 1u : 0u)
 #elif defined(BCM3_MARKS)
 // ISA study build: a comment per phase boundary in the -S output (tools/step_isa.py)
 #define BDF_PH(k) asm volatile("; BDFMARK %0" ::"i"(k))
@@ -349,14 +357,22 @@ BDF_INL void sel_row(const double (&zn)[QMAX + 1][NS], int q, double (&r)[NS])
     do {                           \
     } while (0)
 #define BDF_PH_NOW() 0u
+#define BDF_PH_ADD(k, t0) \
+    do {                  \
+    } while (0)
+#define BDF_PH_CNT(k, c) \
+    do {                 \
+    } while (0)
 #endif
 // 32-bit cycle accumulators (wrapping differences of the low word), so that the profiling build
 // adds few scalar registers. 0-9: the general step (tools/phase_probe.py NAMES); 10-17: the phases
 // of a plain fast-loop step (vec::fast_run, coefficients held); 18: the loop's exit test and back
 // edge (every fast-loop step); 19/20: whole plain / recomputing fast-loop steps; 21/22: their
 // counts; 23: the marker's own cost (16 back-to-back markers per trajectory); 24-26: the
-// convergence test and completion of a recomputing fast-loop step
-constexpr int NPHASES = 28;
+// convergence test and completion of a recomputing fast-loop step; 28-31 (vec::complete_eta_q):
+// order-change checks due, checks the screen skipped, cycles in the screen, cycles in the exact
+// evaluation
+constexpr int NPHASES = 32;
 
 struct BdfCounters {
     int nst_total, nfe, nni, nsetups, nje, netf, ncfn, nreinit;

@@ -629,9 +629,18 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
         s.eta = 1.0;
     } else {
         const double etaq = uni::eta_candidate<q + 1>(bx);
+        BDF_PH_CNT(27, !(bx > uni::eta_cut(q + 1)));
         double eta = etaq;
         s.qprime = q;
-        if ((s.qwait == 0) && !vec::order_change_skippable<q, NS>(s, tc)) {
+        const unsigned ph_s0 = BDF_PH_NOW();
+        const bool skip = (s.qwait == 0) && vec::order_change_skippable<q, NS>(s, tc);
+        if (s.qwait == 0) {
+            BDF_PH_ADD(30, ph_s0);
+            BDF_PH_CNT(28, true);
+            BDF_PH_CNT(29, skip);
+        }
+        const unsigned ph_e0 = BDF_PH_NOW();
+        if ((s.qwait == 0) && !skip) {
             s.qwait = 2;
             vec::tq_13<q>(s, tc);  // qwait was 1 in this step's set_bdf_q
             double etaqm1 = 0.0, etaqp1 = 0.0;
@@ -656,6 +665,7 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
                 s.qprime = q + 1;
                 s.zn[QMAX] = s.acor;
             }
+            BDF_PH_ADD(31, ph_e0);
         } else if (s.qwait == 0) {
             // both order-change candidates screened below THRESH: cvChooseEta keeps q, eta = etaq
             s.qwait = 2;

@@ -23,7 +23,7 @@ NAMES = ["driver(out/cb/reinit)", "entry+ewt", "adjust+rescale", "predict", "set
 FAST = ["ewt + plain test", "predict", "newton: rhs", "newton: solve (I-gJ)^-1", "newton: wrms norm",
         "conv + error test", "complete: zn", "complete: eta"]
 GEN = ["conv + error test", "complete: zn, tau", "complete: eta"]
-NPH = 28
+NPH = 32
 
 
 def main():
@@ -88,6 +88,12 @@ def fast_report(allph, nst, ms, tot):
     for i, n in enumerate(GEN):
         v = allph[:, 24 + i].sum() / max(n_gen, 1)
         print(f"  {n:32s} {v:8.0f} {max(v - mark, 0.0):9.0f}")
+    print(f"etaq roots (step size may grow): {allph[:, 27].sum() / nst.sum():.1%} of steps")
+    n_chk, n_skip = allph[:, 28].sum(), allph[:, 29].sum()
+    if n_chk:
+        print(f"order-change checks: {n_chk / nst.sum():.1%} of steps, screened out {n_skip / n_chk:.1%}; screen "
+              f"{allph[:, 30].sum() / n_chk - mark:.0f} cycles per check, exact evaluation "
+              f"{allph[:, 31].sum() / max(n_chk - n_skip, 1) - mark:.0f} cycles per evaluation")
     print(f"(phases build: kernel {ms:.3f} ms)")
 
 if __name__ == "__main__":
