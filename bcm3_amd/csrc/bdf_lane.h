@@ -265,11 +265,29 @@ BDF_INL double eta_from(double bx, int k)
 // SUNRpowerR(bx, fl(1/k)) (sundials_math.c:40-52, libm's pow)
 // with the tables popk_prepare_device uploaded (xm::xm_tables: the host libm's own, so that the
 // roots are glibc's results bit for bit, or computed ones of the same layout, ~1 ulp)
+#ifdef BCM3_TABLES_LDS
+// (variant) a workgroup copy of the tables in LDS, filled at kernel entry (popk_traj_kernel)
+static __shared__ xm::GlibcPow lds_tables;
+#define BDF_ROOT_TABLES lds_tables
+#else
+#define BDF_ROOT_TABLES xm::xm_tables
+#endif
+// The correctly rounded root (pure arithmetic) is glibc's result except within 0.02 ulp of a
+// rounding midpoint; pow_inv_k_checked says when it is certainly far enough, and only the rest
+// (~12 % of the roots) run glibc's table-driven pow.
 BDF_INL double pow_root(double bx, int k)
 {
-    if (BDF_LIKELY(xm::xm_tables.ok & (bx >= 0x1p-1022) & (bx < 0x1p1023)))
-        return xm::pow_glibc(bx, xm::inv_k(k), xm::xm_tables);
-    if (bx > 1e-30 && bx < 1e30) return xm::pow_inv_k(bx, k);
+    if (BDF_LIKELY((bx > 1e-30) & (bx < 1e30))) {
+        bool safe;
+        const double p = xm::pow_inv_k_checked(bx, k, safe);
+#ifndef BCM3_ROOT_CR
+        if (BDF_UNLIKELY(!safe & (BDF_ROOT_TABLES.ok != 0))) return xm::pow_glibc(bx, xm::inv_k(k), BDF_ROOT_TABLES);
+#endif
+        return p;
+    }
+#ifndef BCM3_ROOT_CR
+    if (BDF_ROOT_TABLES.ok & (bx >= 0x1p-1022) & (bx < 0x1p1023)) return xm::pow_glibc(bx, xm::inv_k(k), BDF_ROOT_TABLES);
+#endif
     return (bx > 0.0) ? pow(bx, xm::inv_k(k)) : 0.0;
 }
 

@@ -287,6 +287,46 @@ XM_FN double pow_inv_k(double x, int k)
     return p0 + c;
 }
 
+// pow_inv_k, and whether its result is certainly glibc's too: glibc's pow is within 0.52 ulp of
+// the exact value (e_pow.c), so it can round differently only when the exact root lies within
+// 0.02 ulp of a rounding midpoint. p0 + c carries the root to ~2^-100 relative; `safe` when the
+// rounding residual of p0 + c is below 0.44 ulp (0.06 ulp from a midpoint, three times the bound)
+XM_FN double pow_inv_k_checked(double x, int k, bool& safe)
+{
+    const double rk = inv_k(k);
+    const float lf = seed_log2f((float)x);
+    double z = (double)seed_exp2f(-lf * (float)rk);
+    double zk = z;
+    for (int it = 0; it < 2; it++) {
+        zk = z;
+        for (int i = 2; i <= 7; i++)
+            if (i <= k) zk *= z;
+        const double t = __builtin_fma(-x, zk, 1.0);
+        z = __builtin_fma(z * t, rk, z);
+    }
+    double zk1 = 1.0;
+    for (int i = 1; i <= 6; i++)
+        if (i < k) zk1 *= z;
+    const double p0 = x * zk1;
+    dd P = {p0, 0.0};
+    for (int i = 2; i <= 7; i++) {
+        if (i <= k) {
+            const double h = P.hi * p0;
+            const double e = __builtin_fma(P.hi, p0, -h);
+            P.lo = __builtin_fma(P.lo, p0, e);
+            P.hi = h;
+        }
+    }
+    const double d = (x - P.hi) - P.lo;
+    const double delta = d * (p0 * (zk1 * z)) * rk;
+    const double c = __builtin_fma(p0 * (double)lf, inv_k_err_ln2(k), delta);
+    const double r = p0 + c;
+    const double res = c - (r - p0);  // p0 + c - r, exact (|c| << |p0|)
+    const double ulp = as_double(as_bits(r) & 0x7ff0000000000000LL) * 0x1p-52;
+    safe = __builtin_fabs(res) < 0.44 * ulp;
+    return r;
+}
+
 // ---------------------------------------------------------------------------------------------
 // glibc's pow itself (sysdeps/ieee754/dbl-64/e_pow.c, glibc >= 2.28: a table-driven log in
 // double-double and a table-driven exp), as the x86-64 libm runs it on FMA/AVX2 hosts (its

@@ -266,6 +266,14 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     constexpr bool UNI = (MODE != POPK_LANES);
     constexpr bool VEC = (MODE == POPK_VEC);
     const int lane = threadIdx.x & 63;
+#ifdef BCM3_TABLES_LDS
+    {
+        const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&xm::xm_tables);
+        unsigned long long* dst = reinterpret_cast<unsigned long long*>(&lds_tables);
+        for (int i = threadIdx.x; i < (int)(sizeof(xm::GlibcPow) / 8); i += blockDim.x) dst[i] = src[i];
+        __syncthreads();
+    }
+#endif
     // n_dev: the number of evaluations is a device value (the speculative batches of the sampler
     // size themselves on the device); the grid covers the maximum and the rest return here
     if (n_dev) ntraj = (int64_t)__builtin_amdgcn_readfirstlane(*n_dev) * m.P;

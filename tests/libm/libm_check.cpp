@@ -24,7 +24,7 @@ int main(int argc, char** argv)
     std::uniform_real_distribution<double> U(0.0, 1.0);
     long ag = 0, ac = 0, gc = 0;
     static xm::GlibcPow D;
-    if ((!strcmp(fn, "powglibc") || !strcmp(fn, "expglibc")) && !bcm3_find_glibc_pow(&D)) {
+    if ((!strcmp(fn, "powglibc") || !strcmp(fn, "expglibc") || !strcmp(fn, "powhybrid")) && !bcm3_find_glibc_pow(&D)) {
         printf("tables not found\n");
         return 2;
     }
@@ -59,6 +59,17 @@ int main(int argc, char** argv)
             mine = xm::exp_glibc(x, D);
             lib = exp(x);
             q = expq((__float128)x);
+        } else if (!strcmp(fn, "powhybrid")) {
+            // the device's step-size root (bdf_lane.h pow_root): the checked correctly rounded root,
+            // glibc's algorithm near rounding midpoints
+            const int k = 2 + (int)(i % 6);
+            x = (i % 7 == 0) ? 1.0 + (U(rng) - 0.5) * 0x1p-40 : exp(-69.0 + 138.0 * U(rng));
+            const double y = xm::inv_k(k);
+            bool safe;
+            mine = xm::pow_inv_k_checked(x, k, safe);
+            if (!safe) mine = xm::pow_glibc(x, y, D);
+            lib = pow(x, y);
+            q = powq((__float128)x, (__float128)y);
         } else if (!strcmp(fn, "powglibc") || !strcmp(fn, "powcomputed")) {
             // the solvers' step-size roots: x in (1e-30, 1e30), some within 2^-40 of 1
             const int k = 2 + (int)(i % 6);

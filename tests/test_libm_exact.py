@@ -57,6 +57,13 @@ def test_pow_is_glibc(checker):
     assert gc < 1.0  # the check sees the non-correctly-rounded cases
 
 
+def test_device_root_is_glibc(checker):
+    """the solvers' step-size root (bdf_lane.h pow_root): the correctly rounded root where it is
+    certainly glibc's result, glibc's algorithm near rounding midpoints -- glibc's pow bit for bit"""
+    ag, _, _ = run(checker, "powhybrid", n=2000000)
+    assert ag == 1.0, ag
+
+
 def test_exp_is_glibc(checker):
     """xm::exp_glibc (the device's exp with the uploaded tables) is glibc's exp bit for bit over the
     range of its main path"""
