@@ -272,22 +272,35 @@ static __shared__ xm::GlibcPow lds_tables;
 #else
 #define BDF_ROOT_TABLES xm::xm_tables
 #endif
-// The correctly rounded root (pure arithmetic) is glibc's result except within 0.02 ulp of a
-// rounding midpoint; pow_inv_k_checked says when it is certainly far enough, and only the rest
-// (~12 % of the roots) run glibc's table-driven pow.
+// SUNRpowerR's pow: glibc's table-driven pow (the tables popk_prepare_device uploaded). Measured
+// against the alternatives on one box (profiles/r04n_variants.txt, 256 C3 draws): the correctly
+// rounded Newton root alone is 6 % faster but not glibc's result on ~0.07 % of roots; checking it
+// against the rounding midpoints and falling back to glibc's pow near them (BCM3_ROOT_HYBRID,
+// xm::pow_inv_k_checked) is glibc's result everywhere but 4 % slower than this -- two root code
+// paths inlined at every call site cost more than the table loads.
+#ifdef BCM3_ROOT_CALL
+__device__ __attribute__((noinline)) double pow_glibc_call(double bx, int k)
+{
+    return xm::pow_glibc(bx, xm::inv_k(k), BDF_ROOT_TABLES);
+}
+#endif
 BDF_INL double pow_root(double bx, int k)
 {
+#if defined(BCM3_ROOT_HYBRID) || defined(BCM3_ROOT_CALL) || defined(BCM3_ROOT_CR)
     if (BDF_LIKELY((bx > 1e-30) & (bx < 1e30))) {
         bool safe;
         const double p = xm::pow_inv_k_checked(bx, k, safe);
-#ifndef BCM3_ROOT_CR
+#if defined(BCM3_ROOT_CALL)
+        if (BDF_UNLIKELY(!safe & (BDF_ROOT_TABLES.ok != 0))) return pow_glibc_call(bx, k);
+#elif defined(BCM3_ROOT_HYBRID)
         if (BDF_UNLIKELY(!safe & (BDF_ROOT_TABLES.ok != 0))) return xm::pow_glibc(bx, xm::inv_k(k), BDF_ROOT_TABLES);
 #endif
         return p;
     }
-#ifndef BCM3_ROOT_CR
-    if (BDF_ROOT_TABLES.ok & (bx >= 0x1p-1022) & (bx < 0x1p1023)) return xm::pow_glibc(bx, xm::inv_k(k), BDF_ROOT_TABLES);
 #endif
+    if (BDF_LIKELY(BDF_ROOT_TABLES.ok & (bx >= 0x1p-1022) & (bx < 0x1p1023)))
+        return xm::pow_glibc(bx, xm::inv_k(k), BDF_ROOT_TABLES);
+    if (bx > 1e-30 && bx < 1e30) return xm::pow_inv_k(bx, k);
     return (bx > 0.0) ? pow(bx, xm::inv_k(k)) : 0.0;
 }
 

@@ -58,8 +58,9 @@ def test_pow_is_glibc(checker):
 
 
 def test_device_root_is_glibc(checker):
-    """the solvers' step-size root (bdf_lane.h pow_root): the correctly rounded root where it is
-    certainly glibc's result, glibc's algorithm near rounding midpoints -- glibc's pow bit for bit"""
+    """the checked root of bdf_lane.h's BCM3_ROOT_HYBRID / BCM3_ROOT_CALL variants: the correctly
+    rounded root where it is certainly glibc's result, glibc's algorithm near rounding midpoints --
+    glibc's pow bit for bit"""
     ag, _, _ = run(checker, "powhybrid", n=2000000)
     assert ag == 1.0, ag
 
