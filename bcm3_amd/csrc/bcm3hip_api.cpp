@@ -18,7 +18,7 @@
 #include "libm_exact.h"
 #include "popk_kernel.h"
 
-bool bcm3_find_glibc_pow(xm::GlibcPow* out);  // libm_tables.cpp
+const xm::GlibcPow* bcm3_pow_tables(int* from_libm);  // libm_tables.cpp
 
 using namespace bcm3hip;
 
@@ -175,8 +175,10 @@ const char* bcm3hip_error_string(int code)
 
 int bcm3hip_libm_pow_tables(void)
 {
-    static xm::GlibcPow t;
-    return bcm3_find_glibc_pow(&t) ? 1 : 0;
+    // the tables popk_prepare_device uploads (BCM3_POW=computed included)
+    int from_libm = 0;
+    bcm3_pow_tables(&from_libm);
+    return from_libm;
 }
 
 int bcm3hip_open_popk(int device, const bcm3hip_popk_model* m, bcm3hip_ctx** out)

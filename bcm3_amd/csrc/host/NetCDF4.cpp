@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -24,6 +25,22 @@
 #include "log.h"
 
 namespace bcm3 {
+
+// the writing subset (nc_create ... nc_close), resolved separately: a reader-only test double or an
+// old library still serves the data files
+struct NcWriteApi {
+    int (*create)(const char*, int, int*) = nullptr;
+    int (*def_grp)(int, const char*, int*) = nullptr;
+    int (*def_dim)(int, const char*, size_t, int*) = nullptr;
+    int (*def_var)(int, const char*, int, int, const int*, int*) = nullptr;
+    int (*put_vara_double)(int, int, const size_t*, const size_t*, const double*) = nullptr;
+    int (*put_vara_uint)(int, int, const size_t*, const size_t*, const unsigned int*) = nullptr;
+    int (*put_vara_string)(int, int, const size_t*, const size_t*, const char**) = nullptr;
+    int (*sync)(int) = nullptr;
+    int (*close)(int) = nullptr;
+    const char* (*strerror)(int) = nullptr;
+    bool ok = false;
+};
 
 namespace {
 
@@ -46,6 +63,7 @@ struct NcApi {
     void* handle = nullptr;
     std::string error;
     std::string env;  // $BCM3_LIBNETCDF when the library was loaded
+    NcWriteApi write;
 };
 
 constexpr int kNcNoWrite = 0, kNcMaxName = 256, kNcMaxDims = 1024, kNcClobber = 0, kNcNetCDF4 = 0x1000;
@@ -53,19 +71,21 @@ constexpr int kNcByte = 1, kNcChar = 2, kNcShort = 3, kNcInt = 4, kNcFloat = 5, 
 constexpr double kFillDouble = 9.9692099683868690e+36, kFillFloat = 9.9692099683868690e+36f;
 
 // loads libnetcdf on first success; a failed attempt is retried on the next call (a later
-// $BCM3_LIBNETCDF or install is seen), and a change of $BCM3_LIBNETCDF switches libraries
+// $BCM3_LIBNETCDF or install is seen), and a change of $BCM3_LIBNETCDF switches libraries. A
+// loaded library is never unloaded and its NcApi never changes: readers and writers that hold it
+// (NcNetCDF4Writer pins the write API at Create) keep calling into the library their ids came from.
 const NcApi& api()
 {
-    static NcApi a;
     static std::mutex mu;
+    static std::vector<std::unique_ptr<NcApi>> loaded;  // every library loaded so far, never freed
+    static const NcApi* cur = nullptr;
+    static NcApi failed;  // the last failed attempt (error only)
     std::lock_guard<std::mutex> lock(mu);
     const char* env_now = std::getenv("BCM3_LIBNETCDF");
     const std::string env = env_now ? env_now : "";
-    if (a.handle && a.env == env) return a;
-    if (a.handle) {
-        dlclose(a.handle);
-        a = NcApi();
-    }
+    if (cur && cur->env == env) return *cur;
+    for (const auto& l : loaded)
+        if (l->env == env) return *(cur = l.get());
     std::vector<std::string> names;
     if (!env.empty()) names.push_back(env);
     for (const char* n : {"libnetcdf.so", "libnetcdf.so.22", "libnetcdf.so.19", "libnetcdf.so.18", "libnetcdf.so.15"})
@@ -73,39 +93,58 @@ const NcApi& api()
     void* h = nullptr;
     for (const auto& n : names)
         if ((h = dlopen(n.c_str(), RTLD_NOW | RTLD_LOCAL))) break;
+    failed = NcApi();
     if (!h) {
-        a.error = "libnetcdf was not found";
-        return a;
+        failed.error = "libnetcdf was not found";
+        return failed;
     }
-    NcApi t;
+    std::unique_ptr<NcApi> t(new NcApi());
     bool ok = true;
     auto sym = [&](auto& fn, const char* name) {
         fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
         ok &= fn != nullptr;
     };
-    sym(t.open, "nc_open");
-    sym(t.close, "nc_close");
-    sym(t.inq_grps, "nc_inq_grps");
-    sym(t.inq_grpname, "nc_inq_grpname");
-    sym(t.inq_varids, "nc_inq_varids");
-    sym(t.inq_var, "nc_inq_var");
-    sym(t.inq_dim, "nc_inq_dim");
-    sym(t.get_var_double, "nc_get_var_double");
-    sym(t.get_var_text, "nc_get_var_text");
-    sym(t.get_var_string, "nc_get_var_string");
-    sym(t.free_string, "nc_free_string");
-    sym(t.inq_att, "nc_inq_att");
-    sym(t.get_att_double, "nc_get_att_double");
-    sym(t.strerror, "nc_strerror");
+    sym(t->open, "nc_open");
+    sym(t->close, "nc_close");
+    sym(t->inq_grps, "nc_inq_grps");
+    sym(t->inq_grpname, "nc_inq_grpname");
+    sym(t->inq_varids, "nc_inq_varids");
+    sym(t->inq_var, "nc_inq_var");
+    sym(t->inq_dim, "nc_inq_dim");
+    sym(t->get_var_double, "nc_get_var_double");
+    sym(t->get_var_text, "nc_get_var_text");
+    sym(t->get_var_string, "nc_get_var_string");
+    sym(t->free_string, "nc_free_string");
+    sym(t->inq_att, "nc_inq_att");
+    sym(t->get_att_double, "nc_get_att_double");
+    sym(t->strerror, "nc_strerror");
     if (!ok) {
-        dlclose(h);
-        a.error = "the libnetcdf found lacks the netCDF-4 group API";
-        return a;
+        dlclose(h);  // nothing holds this handle yet
+        failed.error = "the libnetcdf found lacks the netCDF-4 group API";
+        return failed;
     }
-    t.handle = h;
-    t.env = env;
-    a = t;
-    return a;
+    t->handle = h;
+    t->env = env;
+    // the writing subset, resolved once (a reader-only test double or an old library leaves it !ok)
+    NcWriteApi& w = t->write;
+    bool wok = true;
+    auto wsym = [&](auto& fn, const char* name) {
+        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+        wok &= fn != nullptr;
+    };
+    wsym(w.create, "nc_create");
+    wsym(w.def_grp, "nc_def_grp");
+    wsym(w.def_dim, "nc_def_dim");
+    wsym(w.def_var, "nc_def_var");
+    wsym(w.put_vara_double, "nc_put_vara_double");
+    wsym(w.put_vara_uint, "nc_put_vara_uint");
+    wsym(w.put_vara_string, "nc_put_vara_string");
+    wsym(w.sync, "nc_sync");
+    wsym(w.close, "nc_close");
+    w.strerror = t->strerror;
+    w.ok = wok;
+    loaded.push_back(std::move(t));
+    return *(cur = loaded.back().get());
 }
 
 void check(const NcApi& a, int rc, const std::string& what)
@@ -225,58 +264,11 @@ void read_group(const NcApi& a, int grp, const std::string& path, Json& doc)
     }
 }
 
-// the writing subset (nc_create ... nc_close), loaded separately: a reader-only test double or an
-// old library still serves the data files
-struct NcWriteApi {
-    int (*create)(const char*, int, int*) = nullptr;
-    int (*def_grp)(int, const char*, int*) = nullptr;
-    int (*def_dim)(int, const char*, size_t, int*) = nullptr;
-    int (*def_var)(int, const char*, int, int, const int*, int*) = nullptr;
-    int (*put_vara_double)(int, int, const size_t*, const size_t*, const double*) = nullptr;
-    int (*put_vara_uint)(int, int, const size_t*, const size_t*, const unsigned int*) = nullptr;
-    int (*put_vara_string)(int, int, const size_t*, const size_t*, const char**) = nullptr;
-    int (*sync)(int) = nullptr;
-    int (*close)(int) = nullptr;
-    const char* (*strerror)(int) = nullptr;
-    bool ok = false;
-    void* handle = nullptr;  // the NcApi library these symbols come from
-};
+const NcWriteApi& wapi() { return api().write; }
 
-const NcWriteApi& wapi()
-{
-    static NcWriteApi w;
-    static std::mutex mu;
-    const NcApi& a = api();
-    std::lock_guard<std::mutex> lock(mu);
-    if (w.ok && w.handle == a.handle) return w;
-    w = NcWriteApi();
-    if (!a.handle) return w;
-    NcWriteApi t;
-    bool ok = true;
-    auto sym = [&](auto& fn, const char* name) {
-        fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(a.handle, name));
-        ok &= fn != nullptr;
-    };
-    sym(t.create, "nc_create");
-    sym(t.def_grp, "nc_def_grp");
-    sym(t.def_dim, "nc_def_dim");
-    sym(t.def_var, "nc_def_var");
-    sym(t.put_vara_double, "nc_put_vara_double");
-    sym(t.put_vara_uint, "nc_put_vara_uint");
-    sym(t.put_vara_string, "nc_put_vara_string");
-    sym(t.sync, "nc_sync");
-    sym(t.close, "nc_close");
-    t.strerror = a.strerror;
-    t.ok = ok;
-    t.handle = a.handle;
-    if (ok) w = t;
-    return w;
-}
-
-bool wcheck(int rc, const std::string& what)
+bool wcheck(const NcWriteApi& w, int rc, const std::string& what)
 {
     if (rc == 0) return true;
-    const NcWriteApi& w = wapi();
     LOGERROR("netCDF-4 output: %s: %s", what.c_str(), w.strerror ? w.strerror(rc) : std::to_string(rc).c_str());
     return false;
 }
@@ -307,7 +299,8 @@ bool NcNetCDF4Writer::Create(const std::string& filename)
     const NcWriteApi& w = wapi();
     if (!w.ok) return false;
     filename_ = filename;
-    return wcheck(w.create(filename.c_str(), kNcClobber | kNcNetCDF4, &nc_), "nc_create " + filename);
+    w_ = &w;  // this file's library until Close, whatever $BCM3_LIBNETCDF does meanwhile
+    return wcheck(w, w.create(filename.c_str(), kNcClobber | kNcNetCDF4, &nc_), "nc_create " + filename);
 }
 
 int NcNetCDF4Writer::Group(const std::string& path)
@@ -321,7 +314,7 @@ int NcNetCDF4Writer::Group(const std::string& path)
     if (parent < 0) return -1;
     int g = -1;
     const std::string name = (slash == std::string::npos) ? path : path.substr(slash + 1);
-    if (!wcheck(wapi().def_grp(parent, name.c_str(), &g), "nc_def_grp " + path)) return -1;
+    if (!wcheck(*w_, w_->def_grp(parent, name.c_str(), &g), "nc_def_grp " + path)) return -1;
     groups_[path] = g;
     return g;
 }
@@ -329,26 +322,26 @@ int NcNetCDF4Writer::Group(const std::string& path)
 int NcNetCDF4Writer::Dim(int grp, const std::string& name, size_t len)
 {
     int d = -1;
-    return wcheck(wapi().def_dim(grp, name.c_str(), len, &d), "nc_def_dim " + name) ? d : -1;
+    return wcheck(*w_, w_->def_dim(grp, name.c_str(), len, &d), "nc_def_dim " + name) ? d : -1;
 }
 
 int NcNetCDF4Writer::Var(int grp, const std::string& name, int type, const std::vector<int>& dims)
 {
     int v = -1;
-    return wcheck(wapi().def_var(grp, name.c_str(), type, (int)dims.size(), dims.data(), &v), "nc_def_var " + name) ? v
+    return wcheck(*w_, w_->def_var(grp, name.c_str(), type, (int)dims.size(), dims.data(), &v), "nc_def_var " + name) ? v
                                                                                                                        : -1;
 }
 
 bool NcNetCDF4Writer::PutDouble(int grp, int var, const std::vector<size_t>& start, const std::vector<size_t>& count,
                                 const double* data)
 {
-    return wcheck(wapi().put_vara_double(grp, var, start.data(), count.data(), data), "nc_put_vara_double");
+    return wcheck(*w_, w_->put_vara_double(grp, var, start.data(), count.data(), data), "nc_put_vara_double");
 }
 
 bool NcNetCDF4Writer::PutUInt(int grp, int var, const std::vector<size_t>& start, const std::vector<size_t>& count,
                               const uint32_t* data)
 {
-    return wcheck(wapi().put_vara_uint(grp, var, start.data(), count.data(), data), "nc_put_vara_uint");
+    return wcheck(*w_, w_->put_vara_uint(grp, var, start.data(), count.data(), data), "nc_put_vara_uint");
 }
 
 bool NcNetCDF4Writer::PutStrings(int grp, int var, const std::vector<std::string>& s)
@@ -356,14 +349,14 @@ bool NcNetCDF4Writer::PutStrings(int grp, int var, const std::vector<std::string
     std::vector<const char*> p;
     for (auto& x : s) p.push_back(x.c_str());
     const size_t start = 0, count = s.size();
-    return wcheck(wapi().put_vara_string(grp, var, &start, &count, p.data()), "nc_put_vara_string");
+    return wcheck(*w_, w_->put_vara_string(grp, var, &start, &count, p.data()), "nc_put_vara_string");
 }
 
-bool NcNetCDF4Writer::Sync() { return nc_ < 0 || wcheck(wapi().sync(nc_), "nc_sync"); }
+bool NcNetCDF4Writer::Sync() { return nc_ < 0 || wcheck(*w_, w_->sync(nc_), "nc_sync"); }
 
 void NcNetCDF4Writer::Close()
 {
-    if (nc_ >= 0) wcheck(wapi().close(nc_), "nc_close " + filename_);
+    if (nc_ >= 0) wcheck(*w_, w_->close(nc_), "nc_close " + filename_);
     nc_ = -1;
     groups_.clear();
 }

@@ -87,6 +87,7 @@ void UnwrapDataVariables(Json& doc);
 // without a libnetcdf that has the writing API, or with BCM3_OUTPUT_FORMAT=classic.
 enum { Nc4Double = 6, Nc4UInt = 9, Nc4String = 12 };
 bool NcNetCDF4WriteAvailable(std::string* why);
+struct NcWriteApi;  // NetCDF4.cpp
 class NcNetCDF4Writer {
 public:
     bool Create(const std::string& filename);
@@ -107,6 +108,7 @@ private:
     int nc_ = -1;
     std::string filename_;
     std::map<std::string, int> groups_;
+    const NcWriteApi* w_ = nullptr;  // the library nc_ belongs to (NetCDF4.cpp), set by Create
 };
 
 // Write: a fixed-size (non-record) CDF-2 file. Layout() assigns offsets; Create() writes the

@@ -17,6 +17,7 @@
 
 #include <cerrno>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -31,7 +32,19 @@ namespace bcm3 {
 
 namespace {
 
-constexpr int kTimeoutMs = 120000;  // a peer that has not answered by then has failed
+// How long a rank waits for a peer (connect, accept, each receive): without limit by default, as
+// RCCL waits -- ranks can legitimately drift far apart between exchanges (a first-launch hipRTC
+// compile, a long adaptation) -- and a peer that died is seen as EOF / POLLHUP on its connection.
+// BCM3_SOCKET_TIMEOUT_MS=<ms> bounds the wait (a run then fails with "receive failed").
+int TimeoutMs()
+{
+    static const int ms = [] {
+        const char* e = std::getenv("BCM3_SOCKET_TIMEOUT_MS");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return (v > 0 && v < 2147483647L) ? (int)v : -1;  // poll(): -1 = no limit
+    }();
+    return ms;
+}
 
 std::string RankPath(const std::string& dir, int r) { return dir + "/bcm3_rank" + std::to_string(r) + ".sock"; }
 
@@ -53,7 +66,7 @@ bool WriteAll(int fd, const void* buf, size_t n)
         const ssize_t w = send(fd, p, n, MSG_NOSIGNAL);
         if (w < 0) {
             if (errno == EINTR) continue;
-            if (errno == EAGAIN && WaitFd(fd, POLLOUT, kTimeoutMs)) continue;
+            if (errno == EAGAIN && WaitFd(fd, POLLOUT, TimeoutMs())) continue;
             return false;
         }
         p += w;
@@ -66,7 +79,7 @@ bool ReadAll(int fd, void* buf, size_t n)
 {
     char* p = static_cast<char*>(buf);
     while (n > 0) {
-        if (!WaitFd(fd, POLLIN, kTimeoutMs)) return false;
+        if (!WaitFd(fd, POLLIN, TimeoutMs())) return false;
         const ssize_t r = recv(fd, p, n, 0);
         if (r < 0 && errno == EINTR) continue;
         if (r <= 0) return false;
@@ -163,7 +176,7 @@ private:
                 return fd;
             }
             close(fd);
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(kTimeoutMs)) return -1;
+            if (TimeoutMs() >= 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(TimeoutMs())) return -1;
             std::this_thread::sleep_for(std::chrono::milliseconds(10));
         }
     }
@@ -174,7 +187,7 @@ private:
         for (;;) {
             auto it = in_.find(peer);
             if (it != in_.end()) return it->second;
-            if (!WaitFd(listen_fd_, POLLIN, kTimeoutMs)) return -1;
+            if (!WaitFd(listen_fd_, POLLIN, TimeoutMs())) return -1;
             const int fd = accept(listen_fd_, nullptr, nullptr);
             if (fd < 0) {
                 if (errno == EINTR) continue;

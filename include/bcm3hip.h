@@ -325,10 +325,11 @@ enum {
 };
 
 int bcm3hip_device_count(void);
-/* 1 when the host libm this process loaded holds glibc's pow tables (bcm3_amd/csrc/libm_tables.cpp):
- * PopPK contexts then compute CVODE's step-size roots with glibc's own pow (libm_exact.h
- * pow_glibc, bit-identical to the reference's libm calls), else with the correctly rounded root;
- * BCM3_POW=cr forces the latter. Host-only query, no device needed. */
+/* 1 when PopPK contexts run on the pow / exp tables of the host libm this process loaded
+ * (bcm3_amd/csrc/libm_tables.cpp): CVODE's step-size roots and the exps are then glibc's own
+ * results (libm_exact.h pow_glibc / exp_glibc, bit-identical to the reference's libm calls);
+ * 0 when tables of the same layout were computed instead (~1 ulp from glibc) -- no such libm, or
+ * BCM3_POW=computed in the environment. Host-only query, no device needed. */
 int bcm3hip_libm_pow_tables(void);
 /* SIMDs of the calling thread's current device (compute units x 4), 0 on error: the wavefronts a
  * launch of one-wavefront workgroups runs one per SIMD */

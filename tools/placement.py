@@ -49,7 +49,8 @@ def analyse(label, ctx, x, nst):
         ms.append(ctx.last_kernel_ms())
     pl = ctx.placement_log(n)
     ctx.set_option(_hip.OPT_PLACEMENT_LOG, 0)
-    key, slot = decode(pl[:, 0], pl[:, 1])
+    key, slot = decode(pl[:, 0] & 0xffffffff, pl[:, 1])
+    cyc = (pl[:, 0] >> np.uint64(32)).astype(np.float64)  # shader-clock cycles per trajectory
     t0 = pl[:, 2].astype(np.int64)
     t1 = pl[:, 3].astype(np.int64)
     base = t0.min()
@@ -77,6 +78,9 @@ def analyse(label, ctx, x, nst):
     print(f"   us/step alone {np.median(upstep[solo]):.3f} (n={int(solo.sum())}), "
           f"sharing >50% {np.median(upstep[shared > 0.5]) if (shared > 0.5).any() else float('nan'):.3f} "
           f"(n={int((shared > 0.5).sum())})")
+    ghz = cyc / np.maximum(dur, 1e-9) / 1e3
+    print(f"   in-kernel shader clock (s_memtime cycles / wall time): median {np.median(ghz):.3f} GHz, "
+          f"longest 32 {np.median(ghz[top]):.3f} GHz, min {ghz.min():.3f} max {ghz.max():.3f}")
     last = int(np.argmax(t1))
     print(f"   last to finish: batch index {last}, steps {nst[last]}, {dur[last]:.0f} us, shared {shared[last]:.2f}, "
           f"start {t0[last]:.1f} us; longest solve: steps {nst[order[0]]}, {dur[order[0]]:.0f} us")

@@ -1,7 +1,9 @@
-"""Time build variants of libbcm3hip.so on the C3 workload (one subprocess per library).
+"""Time build variants of libbcm3hip.so on the C3 workload (one subprocess per library and round).
 
-    python tools/variant_timing.py lib1.so [lib2.so ...]
-Prints kernel ms at n=256 lanes_per_wave=1 (min of 5) and the llh agreement with the oracle.
+    [ROUNDS=3] python tools/variant_timing.py lib1.so [lib2.so ...]
+Prints kernel ms at n=256 and 2048 (lanes_per_wave=1, min of 5 launches) and the llh agreement with
+the oracle; with ROUNDS > 1 the libraries run interleaved (A B A B ...: the chip's clock drifts
+between processes) and a last line gives each library's median over the rounds.
 """
 import os
 import subprocess
@@ -26,7 +28,12 @@ for n in (256, 2048):
         ctx.eval_device(n, v.data_ptr(), lp.data_ptr(), None, None)
         ms.append(ctx.last_kernel_ms())
     out.append(f"n={n}: {min(ms):.3f} ms")
-vals = S.prior_draws(1, int(os.environ.get("NPAR", "512")), 20251019)
+    print("RESULT", LIB, n, min(ms), flush=True)
+npar = int(os.environ.get("NPAR", "512"))
+if npar == 0:
+    print(LIB, ' '.join(out), flush=True)
+    sys.exit(0)
+vals = S.prior_draws(1, npar, 20251019)
 g = ctx.eval(vals)
 o = O.Oracle('restated').popk_eval(prob, vals, nthreads=8, want_traj=False)
 e = parity.llh_err(g[0] if isinstance(g, tuple) else g['logp'], o['logp'])
@@ -35,10 +42,26 @@ print(LIB, ' '.join(out), f"llh<=1e-8 {np.mean(e <= 1e-8):.4f} max {np.max(e):.2
 
 
 def main():
-    for lib in sys.argv[1:]:
-        env = dict(os.environ, BCM3HIP_LIB=os.path.abspath(lib))
-        code = CHILD.replace("ROOT", repr(ROOT)).replace("LIB", repr(os.path.basename(lib)))
-        subprocess.run([sys.executable, "-c", code], env=env, check=False, timeout=300)
+    rounds = int(os.environ.get("ROUNDS", "1"))
+    res = {}
+    for r in range(rounds):
+        for lib in sys.argv[1:]:
+            env = dict(os.environ, BCM3HIP_LIB=os.path.abspath(lib))
+            if r > 0:
+                env["NPAR"] = "0"
+            code = CHILD.replace("ROOT", repr(ROOT)).replace("LIB", repr(os.path.basename(lib)))
+            p = subprocess.run([sys.executable, "-c", code], env=env, check=False, timeout=300,
+                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+            for line in p.stdout.splitlines():
+                if line.startswith("RESULT "):
+                    _, name, n, ms = line.split()
+                    res.setdefault((name, int(n)), []).append(float(ms))
+                elif "amdgpu.ids" not in line:
+                    print(line, flush=True)
+    if rounds > 1:
+        import numpy as np
+        for (name, n), v in sorted(res.items(), key=lambda kv: (kv[0][1], kv[0][0])):
+            print(f"median over {len(v)} rounds: {name} n={n}: {np.median(v):.3f} ms  ({' '.join(f'{x:.3f}' for x in v)})")
 
 
 if __name__ == "__main__":
