@@ -74,6 +74,23 @@ enum { CV_SUCCESS = 0, CV_TSTOP_RETURN = 1, CV_TOO_MUCH_ACC = -2, CV_ERR_FAILURE
        CV_CONV_FAILURE = -4, CV_ILL_INPUT = -22, CV_BAD_T = -26, CV_TOO_CLOSE = -27 };
 
 #define BDF_INL __device__ __forceinline__
+// BCM3_DBL=k (cost-probe builds only, tools/dbl_probe.sh): component k of the step runs twice, the
+// second time on operands laundered through an empty asm and with its results consumed by one, so
+// the solve's results are unchanged and the kernel time grows by what that component costs
+// (1 step-size root, 2 order-change screen, 3 exact order-change evaluation, 4 cvSet coefficients,
+// 5 Newton correction, 6 linear-solver setup, 7 error weights, 8 fast-loop exit test, 9 predict)
+#ifdef BCM3_DBL
+#define BDF_DBL(k) (BCM3_DBL == (k))
+#else
+#define BDF_DBL(k) false
+#endif
+BDF_INL double bdf_launder(double x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+BDF_INL void bdf_consume(double x) { asm volatile("" ::"v"(x)); }
+
 // branch-layout hints for the UNI solver (hot path falls through; rare work out of line)
 #ifdef BCM3_NO_EXPECT
 #define BDF_LIKELY(x) (x)
@@ -306,7 +323,11 @@ BDF_INL double pow_root(double bx, int k)
 
 // eta = ONE / (SUNRpowerR(bx, ONE / k) + ADDON) (cvode.c:2986, 3105, 3163, 3187): the rounded
 // exponent fl(1/k) as the reference passes it, libm's pow, the IEEE quotient
-BDF_INL double eta_exact(double bx, int k) { return frcp(pow_root(bx, k) + ADDON); }
+BDF_INL double eta_exact(double bx, int k)
+{
+    if constexpr (BDF_DBL(1)) bdf_consume(frcp(pow_root(bdf_launder(bx), k) + ADDON));
+    return frcp(pow_root(bx, k) + ADDON);
+}
 
 // cvNlsConvTest (cvode_nls.c:262-263): dcon = del * min(1, crate) / tol, converged when dcon <= 1,
 // tol = tq[4] = CORTES / tq[2]. RN(a / b) <= 1 iff a / b <= 1 + 2^-53 (the midpoint rounds to even,

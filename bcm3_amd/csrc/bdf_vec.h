@@ -92,6 +92,23 @@ BDF_INL double solvevec(const double (&col)[NS], double x)
         return col[0] * bc<0>(x) + col[1] * bc<1>(x);
 }
 
+// cost-probe builds (BCM3_DBL, bdf_lane.h): launder the operands of a component's second run
+template <class S>
+BDF_INL void dbl_launder_state(S& s)
+{
+    cfor<0, QMAX + 1>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j)] = bdf_launder(s.zn[CI(j)]); });
+    cfor<0, QMAX + 2>([&](auto j) __attribute__((always_inline)) { s.tau[CI(j)] = bdf_launder(s.tau[CI(j)]); });
+    cfor<0, 6>([&](auto j) __attribute__((always_inline)) { s.tq[CI(j)] = bdf_launder(s.tq[CI(j)]); });
+    s.ewt = bdf_launder(s.ewt);
+    s.acor = bdf_launder(s.acor);
+    s.h = bdf_launder(s.h);
+    s.tn = bdf_launder(s.tn);
+    s.gamma = bdf_launder(s.gamma);
+    s.gammap = bdf_launder(s.gammap);
+    s.saved_tq5 = bdf_launder(s.saved_tq5);
+    s.unity = bdf_launder(s.unity);
+}
+
 // per-trajectory solver statistics only when the caller asked for them: without, the counters
 // compile to nothing (they would hold 8 SGPRs and a scalar add per event on the hot path)
 struct NoCount {
@@ -132,6 +149,7 @@ struct VecState {
 template <class S>
 BDF_INL void ewt_set(S& s)
 {
+    if constexpr (BDF_DBL(7)) bdf_consume(frcp(s.rtol * fabs(bdf_launder(s.zn[0])) + s.atol));
     s.ewt = frcp(s.rtol * fabs(s.zn[0]) + s.atol);
 }
 
@@ -488,6 +506,11 @@ BDF_INL double newton_correction(S& s, const Model& mdl, double rl1, double& csc
                           ((convfail == CONV_BAD_J) & (dgamma < CVLS_DGMAX)) | (convfail == CONV_OTHER);
         s.cnt.nje += jnew ? 1 : 0;
         s.nstlj = jnew ? s.nst : s.nstlj;
+        if constexpr (BDF_DBL(6)) {
+            double ic2[NS];
+            mdl.lin_setup_v(bdf_launder(s.gamma), ic2);
+            cfor<0, NS>([&](auto k) __attribute__((always_inline)) { bdf_consume(ic2[CI(k)]); });
+        }
         mdl.lin_setup_v(s.gamma, s.icol);
         s.cnt.nsetups++;
         s.nls_jcur = jnew;
@@ -634,6 +657,21 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
         s.qprime = q;
         const unsigned ph_s0 = BDF_PH_NOW();
         const bool skip = (s.qwait == 0) && vec::order_change_skippable<q, NS>(s, tc);
+        if constexpr (BDF_DBL(2)) {
+            if (s.qwait == 0) {
+                S s2 = s;
+                vec::dbl_launder_state(s2);
+                TqCtx tc2 = tc;
+                tc2.alpha0 = bdf_launder(tc2.alpha0);
+                tc2.alpha0_hat = bdf_launder(tc2.alpha0_hat);
+                tc2.xi_inv = bdf_launder(tc2.xi_inv);
+                tc2.xistar_inv = bdf_launder(tc2.xistar_inv);
+                tc2.hsum2 = bdf_launder(tc2.hsum2);
+                tc2.lq = bdf_launder(tc2.lq);
+                tc2.A2 = bdf_launder(tc2.A2);
+                bdf_consume(vec::order_change_skippable<q, NS>(s2, tc2) ? 1.0 : 0.0);
+            }
+        }
         if (s.qwait == 0) {
             BDF_PH_ADD(30, ph_s0);
             BDF_PH_CNT(28, true);
@@ -641,6 +679,22 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
         }
         const unsigned ph_e0 = BDF_PH_NOW();
         if ((s.qwait == 0) && !skip) {
+            if constexpr (BDF_DBL(3)) {
+                S s2 = s;
+                vec::dbl_launder_state(s2);
+                vec::tq_13<q>(s2, tc);
+                double e1 = 0.0, e3 = 0.0;
+                if constexpr (q > 1) e1 = uni::eta_candidate<q>(BIAS1 * (vec::wrms<NS>(s2.zn[q], s2.ewt) * s2.tq[1]));
+                if constexpr (q != QMAX) {
+                    if (s2.saved_tq5 != 0.0) {
+                        const double cq = fdiv(s2.tq[5], s2.saved_tq5) * powI(fdiv(s2.h, s2.tau[2]), q + 1);
+                        const double tv = (-cq) * s2.zn[QMAX] + s2.acor;
+                        e3 = uni::eta_candidate<q + 2>(BIAS3 * (vec::wrms<NS>(tv, s2.ewt) * s2.tq[3]));
+                    }
+                }
+                bdf_consume(e1);
+                bdf_consume(e3);
+            }
             s.qwait = 2;
             vec::tq_13<q>(s, tc);  // qwait was 1 in this step's set_bdf_q
             double etaqm1 = 0.0, etaqp1 = 0.0;
@@ -962,6 +1016,20 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             BDF_PH(11);
             s.acor = 0.0;
             double cscale = cscale_h;
+            if constexpr (BDF_DBL(9)) {
+                S s2 = s;
+                vec::dbl_launder_state(s2);
+                vec::predict_q<Q>(s2);
+                cfor<0, Q + 1>([&](auto k) __attribute__((always_inline)) { bdf_consume(s2.zn[CI(k)]); });
+                bdf_consume(s2.tn);
+            }
+            if constexpr (BDF_DBL(5)) {
+                S s2 = s;
+                vec::dbl_launder_state(s2);
+                double cs2 = bdf_launder(cscale);
+                bdf_consume(vec::newton_correction<NS>(s2, mdl, bdf_launder(rl1), cs2, false, false, CONV_NONE));
+                bdf_consume(s2.acor);
+            }
             const double del = vec::newton_correction<NS, 12>(s, mdl, rl1, cscale, false, false, CONV_NONE);
             run++;  // have stays set (reuse, no setup)
             if (!tail(std::true_type{}, del, false, cscale)) return NEED_ATTEMPTS;
@@ -974,7 +1042,27 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             if (eta_eff != 1.0) vec::rescale_q<Q>(s, eta_eff);
             vec::predict_q<Q>(s);
             BDF_PH(3);
-            if (!reuse) rl1 = vec::set_bdf_q<Q, true>(s, tc);
+            if (!reuse) {
+                if constexpr (BDF_DBL(4)) {
+                    S s2 = s;
+                    vec::dbl_launder_state(s2);
+                    TqCtx tc2;
+                    bdf_consume(vec::set_bdf_q<Q, true>(s2, tc2));
+                    cfor<0, Q + 1>([&](auto k) __attribute__((always_inline)) { bdf_consume(s2.l[CI(k)]); });
+                    bdf_consume(s2.tq[2]);
+                    bdf_consume(s2.tq[4]);
+                    bdf_consume(s2.tq[5]);
+                    bdf_consume(s2.gamma);
+                    bdf_consume(s2.gamrat);
+                    bdf_consume(tc2.alpha0_hat);
+                    bdf_consume(tc2.xi_inv);
+                    bdf_consume(tc2.xistar_inv);
+                    bdf_consume(tc2.hsum2);
+                    bdf_consume(tc2.lq);
+                    bdf_consume(tc2.A2);
+                }
+                rl1 = vec::set_bdf_q<Q, true>(s, tc);
+            }
             BDF_PH(4);
             const bool setup = (s.nst >= s.nstlp + MSBP) | (fabs(s.gamrat - 1.0) > DGMAX);
             double cscale = (s.gamrat != 1.0) ? fdiv(2.0, 1.0 + s.gamrat) : 1.0;
@@ -989,6 +1077,13 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         const bool quiet = (fabs(s.tn - s.tstop) > troundoff) & !((s.tn + s.hprime - s.tstop) * s.h > 0.0) &
                            (s.tn < tlim) & (s.qprime == Q) & (current_step + 1 != max_steps);
+        if constexpr (BDF_DBL(8)) {
+            const double tn2 = bdf_launder(s.tn);
+            const double tr2 = FUZZ_FACTOR * UROUND * (fabs(tn2) + fabs(s.h));
+            const bool q2 = (fabs(tn2 - s.tstop) > tr2) & !((tn2 + s.hprime - s.tstop) * s.h > 0.0) & (tn2 < tlim) &
+                            (s.qprime == Q) & (current_step + 1 != max_steps);
+            bdf_consume(q2 ? 1.0 : 0.0);
+        }
         BDF_PH_STEP(ph_t0, 19, 20, plain);
 #ifdef BCM3_PHASES
         s.ph[21] += plain ? 1 : 0;

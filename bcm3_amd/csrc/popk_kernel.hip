@@ -249,41 +249,6 @@ BDF_INL bool check_give_treatment(double t, const uint8_t* skipped, int intermit
 // state vectors across lanes: bdf_vec.h). All three give the same bits.
 enum { POPK_LANES = 0, POPK_UNI = 1, POPK_VEC = 2 };
 
-// One-trajectory-per-wavefront launches keep each output's concentration x_i in LDS while the solve
-// runs (T doubles per wavefront, dynamic LDS) and evaluate the observation model after it, as the
-// reference does (SolveReturnSolution, then the loop over the outputs, .cpp:405-424): the solve
-// loop then contains no library call (no call-ABI registers and no scratch in the hot loop).
-extern __shared__ double popk_obs_lds[];
-constexpr int kPopkObsLdsMaxT = 1024;  // launch_popk runs larger T on the lane solver
-
-// sum of LogPdfTnu4(x_i, obs_i, sd + sd2 max(x_i, 0)) over the n outputs in output order from 0.0,
-// skipping unobserved rows; -inf when some x_i is NaN and `nan_ends` (population likelihood). The
-// terms are computed lane-parallel (lane k: output c0 + k), the sum runs in output order, so the
-// result is the streamed sum's bit for bit.
-template <bool COLD>
-__device__ __forceinline__ double popk_observation_sum(const double* xo, const double* obs, int n, double sd,
-                                                       double sd2, bool nan_ends)
-{
-    const int lane = (int)(threadIdx.x & 63);
-    double acc = 0.0;
-    for (int c0 = 0; c0 < n; c0 += 64) {
-        const int nc = (n - c0 < 64) ? n - c0 : 64;
-        const int i = c0 + ((lane < nc) ? lane : nc - 1);
-        const double x = xo[i];
-        const double yo = obs[i];
-        const double xm = (x < 0.0) ? 0.0 : x;
-        const double term = log_pdf_tnu4<COLD>(x, yo, sd + sd2 * xm);
-        const uint64_t addm = __ballot(!isnan(yo));
-        const uint64_t nanm = __ballot(isnan(x));
-        if (nan_ends && (nanm & (nc == 64 ? ~0ull : ((1ull << nc) - 1)))) return -INFINITY;
-        for (int k = 0; k < nc; k++) {
-            const double tk = vec::comp(term, k);
-            if ((addm >> k) & 1) acc += tk;
-        }
-    }
-    return acc;
-}
-
 template <int PKT, int MODE, bool STATS>
 __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t ntraj, int lpw,
                                                         const double* __restrict__ values,
@@ -300,13 +265,6 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     constexpr int NS = TR::NS;
     constexpr bool UNI = (MODE != POPK_LANES);
     constexpr bool VEC = (MODE == POPK_VEC);
-    // library functions out of line (libm_exact.h xm::lib) in the vector-state kernel; the
-    // scalar-state kernel inlines them unless BCM3_UNI_COLD (diagnostic builds)
-#ifdef BCM3_UNI_COLD
-    constexpr bool COLD = UNI;
-#else
-    constexpr bool COLD = VEC;
-#endif
     const int lane = threadIdx.x & 63;
 #ifdef BCM3_TABLES_LDS
     {
@@ -342,27 +300,27 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
 
     // ---- parameter map (.cpp:263-310)
     const int sdix = m.sd_ix;
-    const double sd = transform_var<COLD>(m.transforms[sdix], v[sdix]);
-    const double sd2 = transform_var<COLD>(m.transforms[sdix + 1], v[sdix + 1]);
-    PKLane<PKT, COLD> mdl;
+    const double sd = transform_var<VEC>(m.transforms[sdix], v[sdix]);
+    const double sd2 = transform_var<VEC>(m.transforms[sdix + 1], v[sdix + 1]);
+    PKLane<PKT, VEC> mdl;
     // single-patient likelihood (LikelihoodPharmacokineticTrajectory.cpp:226-259): the rates are the
     // transformed variables; the population likelihood draws ka and CL per patient (.cpp:283-286)
     const bool single = (m.param_map == BCM3HIP_PARAM_MAP_SINGLE);
-    const double vod = isnan(m.fixed_vod) ? transform_var<COLD>(m.transforms[3], v[3]) : m.fixed_vod;
+    const double vod = isnan(m.fixed_vod) ? transform_var<VEC>(m.transforms[3], v[3]) : m.fixed_vod;
     if (single) {
-        mdl.ka = transform_var<COLD>(m.transforms[0], v[0]);
-        mdl.ke = transform_var<COLD>(m.transforms[1], v[1]);
-        mdl.kel = transform_var<COLD>(m.transforms[2], v[2]) / vod;
+        mdl.ka = transform_var<VEC>(m.transforms[0], v[0]);
+        mdl.ke = transform_var<VEC>(m.transforms[1], v[1]);
+        mdl.kel = transform_var<VEC>(m.transforms[2], v[2]) / vod;
     } else {
-        mdl.ka = fastpow10<COLD>(quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
-        mdl.ke = transform_var<COLD>(m.transforms[1], v[1]);
-        mdl.kel = fastpow10<COLD>(quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / vod;
+        mdl.ka = fastpow10<VEC>(quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
+        mdl.ke = transform_var<VEC>(m.transforms[1], v[1]);
+        mdl.kel = fastpow10<VEC>(quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / vod;
     }
     mdl.kf = mdl.kb = 0.0;
     if constexpr (TR::two) {
         if (isnan(m.fixed_kf)) {
-            mdl.kf = transform_var<COLD>(m.transforms[4], v[4]);
-            mdl.kb = transform_var<COLD>(m.transforms[5], v[5]);
+            mdl.kf = transform_var<VEC>(m.transforms[4], v[4]);
+            mdl.kb = transform_var<VEC>(m.transforms[5], v[5]);
         } else {
             mdl.kf = m.fixed_kf;
             mdl.kb = m.fixed_kb;
@@ -371,22 +329,22 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     mdl.ktr = mdl.ntr = mdl.lnf = 0.0;
     if constexpr (TR::transit) {
         const int ni = m.n_transit_ix, ti = m.transit_time_ix;
-        mdl.ntr = transform_var<COLD>(m.transforms[ni], v[ni]);
-        mdl.ktr = (mdl.ntr + 1) / transform_var<COLD>(m.transforms[ti], v[ti]);
+        mdl.ntr = transform_var<VEC>(m.transforms[ni], v[ni]);
+        mdl.ktr = (mdl.ntr + 1) / transform_var<VEC>(m.transforms[ti], v[ti]);
         const double n = mdl.ntr;
-        mdl.lnf = 0.9189385332046727 + (n + 0.5) * xm::lib<COLD>::log(n) - n + xm::lib<COLD>::log(1 + 1 / (12.0 * n));
+        mdl.lnf = 0.9189385332046727 + (n + 0.5) * xm::lib<VEC>::log(n) - n + xm::lib<VEC>::log(1 + 1 / (12.0 * n));
     }
     const double interval = m.dosing_interval[j];
     double tsw = 0.0;
     mdl.ka2 = 0.0;
     if constexpr (TR::biphasic) {
         const int bi = m.biphasic_time_ix, ai = m.absorption2_ix;
-        tsw = transform_var<COLD>(m.transforms[bi], v[bi]);
+        tsw = transform_var<VEC>(m.transforms[bi], v[bi]);
         const double lim = interval - 1e-2;
         // (the population likelihood keeps the switch inside the dosing interval, .cpp:303-305;
         //  the single-patient one does not, LikelihoodPharmacokineticTrajectory.cpp:253)
         tsw = (!single && lim < tsw) ? lim : tsw;
-        mdl.ka2 = transform_var<COLD>(m.transforms[ai], v[ai]);
+        mdl.ka2 = transform_var<VEC>(m.transforms[ai], v[ai]);
     }
     if constexpr (UNI && !VEC) {
         // values returned by out-of-line calls (ndtri_lower) count as divergent to the compiler;
@@ -436,7 +394,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     bool llh_done = false;  // NaN concentration seen: llh = -inf, stop accumulating
     int status = BCM3HIP_STATUS_OK;
 
-    std::conditional_t<VEC, vec::VecState<NS, STATS>, BdfState<NS, typename PKLane<PKT, COLD>::Inv>> s;
+    std::conditional_t<VEC, vec::VecState<NS, STATS>, BdfState<NS, typename PKLane<PKT, VEC>::Inv>> s;
     s.cnt = {};
     s.nst = 0;
 #ifdef BCM3_PHASES
@@ -447,20 +405,10 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     s.tlast = (unsigned)clock64();
 #endif
 
-    // one trajectory per wavefront: this wavefront's output concentrations (popk_obs_lds)
-    double* xo = popk_obs_lds + (threadIdx.x >> 6) * T;
-    int nobs = 0;
-
-    // observation term for output index i with state yi (.cpp:412-423); deferred to after the
-    // solve in the one-trajectory-per-wavefront launches (popk_observation_sum)
+    // observation term for output index i with state yi (.cpp:412-423)
     auto observe = [&](int i, const double (&yi)[NS]) __attribute__((always_inline)) {
         if (tro) {
             cfor<0, NS>([&](auto k) __attribute__((always_inline)) { tro[CI(k) * T + i] = yi[CI(k)]; });
-        }
-        if constexpr (UNI) {
-            xo[i] = conversion * yi[1];
-            nobs = i + 1;
-            return;
         }
         if (llh_done) return;
         const double x = conversion * yi[1];
@@ -638,9 +586,6 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             nsteps = current_step;
         }
     }
-    if constexpr (UNI) {
-        if (status == BCM3HIP_STATUS_OK) llh = popk_observation_sum<COLD>(xo, obs, nobs, sd_u, sd2_u, !single);
-    }
     if (status != BCM3HIP_STATUS_OK) llh = -INFINITY;
 
 #ifdef BCM3_PHASES
@@ -740,20 +685,19 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
     const int64_t nblocks = (nwaves + bw - 1) / bw;
     dim3 grid((unsigned)nblocks), block(64 * bw);
     const bool direct = (m.P == 1);
-    // (beyond kPopkObsLdsMaxT outputs the one-trajectory-per-wavefront launch would need more LDS for
-    //  its deferred observation model than is sensible: the lane solver streams it instead)
-    const bool uni = (lpw == 1) && ntraj < (int64_t)1 << 30 && m.T <= kPopkObsLdsMaxT;
+    const bool uni = (lpw == 1) && ntraj < (int64_t)1 << 30;
     const bool vec_state = uni && (uni_solver == 0);
-    if (uni) {
-        const int obs_bytes = bw * m.T * (int)sizeof(double);
-        if (block_lds < obs_bytes) block_lds = obs_bytes;
-    }
     double* logp_direct = direct ? logp : nullptr;
     // one patient: the trajectory status is the evaluation status, written in place (no copy kernel)
     int32_t* tstat = (direct && status) ? status : traj_status_scratch;
     if (ev_start) hipEventRecord(ev_start, stream);
+#ifdef BCM3_VEC_STATS_ALWAYS
+    constexpr bool vec_nostats = false;  // (variant) the counting kernel for every vector-state launch
+#else
+    constexpr bool vec_nostats = true;
+#endif
 #define LAUNCH(PKT)                                                                                           \
-    if (vec_state && !stats_out)                                                                              \
+    if (vec_state && !stats_out && vec_nostats)                                                               \
         hipLaunchKernelGGL((popk_traj_kernel<PKT, POPK_VEC, false>), grid, block, block_lds, stream, m, ntraj, lpw,     \
                            values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr, n_dev, steps_out, place_out); \
     else if (vec_state)                                                                                       \
@@ -768,8 +712,8 @@ hipError_t launch_popk(const PopPKDevModel& m, int64_t n, const double* values, 
 #ifdef BCM3_DEV_TWO_VEC
     // development build (tools/resource_two_vec.sh): only the C3 kernel, compiled in seconds
     if (m.pk_type != BCM3HIP_PK_TWO || !vec_state || stats_out) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((popk_traj_kernel<BCM3HIP_PK_TWO, POPK_VEC, false>), grid, block, block_lds, stream, m, ntraj, lpw,
-                       values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr, n_dev, steps_out, place_out);
+    hipLaunchKernelGGL((popk_traj_kernel<BCM3HIP_PK_TWO, POPK_VEC, !vec_nostats>), grid, block, block_lds, stream, m, ntraj,
+                       lpw, values, logp_direct, patient_llh_scratch, tstat, traj_out, nullptr, n_dev, steps_out, place_out);
 #else
     switch (m.pk_type) {
     case BCM3HIP_PK_ONE: LAUNCH(BCM3HIP_PK_ONE); break;
