@@ -284,6 +284,10 @@ struct SamplerPTDevice::Impl {
     // sample output: [flush][values C*d | lprior C | llh C] staged on the device
     std::unique_ptr<SampleFileWriter> out;
     DevBuf<double> out_buf;
+    // a sharded ladder writing the reference's netCDF-4 file: every rank stages its samples, rank 0
+    // receives the other ranks' staged rows over the transport at each flush and writes all columns
+    bool out_on = false, out_gather = false;
+    DevBuf<double> out_recv;
     int64_t out_samples = 0, out_first = 0, out_pending = 0, emitted = 0;
     int out_flush = 64;
     bool out_overflow_logged = false;
@@ -294,7 +298,7 @@ struct SamplerPTDevice::Impl {
     {
         // SamplerPT::EmitSample (SamplerPT.cpp:321-330): every chain, weight 1
         const int64_t six = emitted++;
-        if (!out) return true;
+        if (!out_on) return true;
         if (six >= out_samples) {
             if (!out_overflow_logged) LOGWARNING("More samples than the output file holds (%lld); later samples are not stored", (long long)out_samples);
             out_overflow_logged = true;
@@ -313,7 +317,8 @@ struct SamplerPTDevice::Impl {
 
     bool Flush()
     {
-        if (!out || out_pending == 0) return true;
+        if (!out_on || out_pending == 0) return true;
+        if (out_gather) return FlushGather();
         std::vector<double> h((size_t)(out_pending * C * (d + 2)));
         if (bcm3hip_memcpy_async(h.data(), out_buf.p, h.size() * sizeof(double), BCM3HIP_D2H, stream) != 0 ||
             bcm3hip_stream_synchronize(stream) != 0)
@@ -322,6 +327,58 @@ struct SamplerPTDevice::Impl {
         for (int64_t k = 0; k < out_pending; k++) {
             const double* r = &h[(size_t)(k * C * (d + 2))];
             if (!out->Write((size_t)(out_first + k), 0, (size_t)C, r, r + C * d, r + C * (d + 1), w.data())) {
+                LOGERROR("Writing sample %lld to the output file failed", (long long)(out_first + k));
+                return false;
+            }
+        }
+        out_pending = 0;
+        return true;
+    }
+
+    // all ranks flush together (Emit runs in lockstep on every rank): ranks > 0 send their staged
+    // [pending][values C*d | lprior C | llh C] block to rank 0, which assembles each sample's rows of
+    // the whole ladder (rank r holds temperatures r*C .. r*C + C - 1) and writes them at once
+    bool FlushGather()
+    {
+        const size_t cnt = (size_t)(out_pending * C * (d + 2));
+        const int world = cfg.world, rank = cfg.rank;
+        if (rank != 0) {
+            const double* sp = out_buf.p;
+            const int peer = 0;
+            if (!transport || !transport->Exchange(1, &sp, &peer, 0, nullptr, nullptr, cnt, stream)) {
+                LOGERROR("Sending sample rows to rank 0 failed (rank %d)", rank);
+                return false;
+            }
+            out_pending = 0;
+            return bcm3hip_stream_synchronize(stream) == 0;
+        }
+        std::vector<double*> recvs((size_t)(world - 1));
+        std::vector<int> peers((size_t)(world - 1));
+        for (int r = 1; r < world; r++) {
+            recvs[(size_t)(r - 1)] = out_recv.p + (size_t)(r - 1) * cnt;
+            peers[(size_t)(r - 1)] = r;
+        }
+        if (!transport || !transport->Exchange(0, nullptr, nullptr, world - 1, recvs.data(), peers.data(), cnt, stream)) {
+            LOGERROR("Receiving the other ranks' sample rows failed");
+            return false;
+        }
+        std::vector<double> h((size_t)world * cnt);
+        if (bcm3hip_memcpy_async(h.data(), out_buf.p, cnt * sizeof(double), BCM3HIP_D2H, stream) != 0 ||
+            (world > 1 && bcm3hip_memcpy_async(h.data() + cnt, out_recv.p, (size_t)(world - 1) * cnt * sizeof(double),
+                                               BCM3HIP_D2H, stream) != 0) ||
+            bcm3hip_stream_synchronize(stream) != 0)
+            return false;
+        const size_t Cw = (size_t)(C * world), dd = (size_t)d;
+        std::vector<double> vals(Cw * dd), lp(Cw), ll(Cw);
+        const std::vector<double> w(Cw, 1.0);
+        for (int64_t k = 0; k < out_pending; k++) {
+            for (int r = 0; r < world; r++) {
+                const double* b = &h[(size_t)r * cnt + (size_t)(k * C * (d + 2))];
+                std::copy(b, b + C * d, vals.begin() + (size_t)r * C * dd);
+                std::copy(b + C * d, b + C * (d + 1), lp.begin() + (size_t)r * C);
+                std::copy(b + C * (d + 1), b + C * (d + 2), ll.begin() + (size_t)r * C);
+            }
+            if (!out->Write((size_t)(out_first + k), 0, Cw, vals.data(), lp.data(), ll.data(), w.data())) {
                 LOGERROR("Writing sample %lld to the output file failed", (long long)(out_first + k));
                 return false;
             }
@@ -956,7 +1013,7 @@ SamplerPTDevice::SamplerPTDevice() : p_(new Impl) {}
 
 SamplerPTDevice::~SamplerPTDevice()
 {
-    if (p_ && p_->out && !p_->Flush()) LOGERROR("Flushing the sample output failed");
+    if (p_ && p_->out_on && !p_->Flush()) LOGERROR("Flushing the sample output failed");
     if (p_ && p_->stream) bcm3hip_stream_synchronize(p_->stream);
     if (p_ && p_->own_stream) bcm3hip_stream_destroy(p_->stream);
 }
@@ -1126,21 +1183,33 @@ bool SamplerPTDevice::SetOutput(const std::string& filename, int64_t num_samples
 {
     Impl& s = *p_;
     const VariableSet* vs = s.ll ? s.ll->GetVariableSet() : nullptr;
-    if (!vs || num_samples < 1 || s.emitted != 0 || s.out) {
+    if (!vs || num_samples < 1 || s.emitted != 0 || s.out_on) {
         LOGERROR("SetOutput: needs an initialised sampler before its first sample, once");
         return false;
     }
     std::vector<std::string> names(vs->GetVariableNames());
     std::vector<int32_t> tr(names.size());
     for (size_t i = 0; i < names.size(); i++) tr[i] = (int32_t)vs->GetVariableTransform(i);
-    auto w = std::make_unique<SampleFileWriter>();
-    if (!w->Initialize(filename, (size_t)num_samples, names, tr,
-                       TemperatureLadder(s.Ctot, s.cfg.temperature_power, s.cfg.temperature_max), (size_t)s.g0,
-                       (size_t)s.C))
-        return false;
+    // a sharded ladder: the reference's netCDF-4 file (SampleHandlerNetCDF.cpp:24-110) written by rank 0
+    // from every rank's rows when libnetcdf can be loaded; otherwise the shared netCDF classic file,
+    // each rank writing its own temperature columns
+    const bool gather = s.cfg.world > 1 && s.transport && NcNetCDF4WriteAvailable(nullptr);
+    std::unique_ptr<SampleFileWriter> w;
+    if (!gather || s.cfg.rank == 0) {
+        w = std::make_unique<SampleFileWriter>();
+        const std::vector<double> ladder = TemperatureLadder(s.Ctot, s.cfg.temperature_power, s.cfg.temperature_max);
+        if (!(gather ? w->Initialize(filename, (size_t)num_samples, names, tr, ladder, 0, (size_t)s.Ctot)
+                     : w->Initialize(filename, (size_t)num_samples, names, tr, ladder, (size_t)s.g0, (size_t)s.C)))
+            return false;
+    }
     s.out_flush = std::max(1, flush_every);
     if (!s.out_buf.alloc((size_t)(s.out_flush * s.C * (s.d + 2)))) return false;
+    if (gather && s.cfg.rank == 0 &&
+        !s.out_recv.alloc((size_t)((s.cfg.world - 1) * s.out_flush * s.C * (s.d + 2))))
+        return false;
     s.out = std::move(w);
+    s.out_on = true;
+    s.out_gather = gather;
     s.out_samples = num_samples;
     s.out_pending = 0;
     return true;

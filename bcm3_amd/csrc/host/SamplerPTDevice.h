@@ -86,9 +86,12 @@ public:
     // diagnostics: the last speculative launch's entries in dispatch order (source ids as in
     // bcm3hip_spec::batch_src, BDF steps); returns the entry count, -1 without speculation
     int64_t SpeculativeBatch(int32_t* src, int32_t* steps, int32_t* unused);
-    // SampleHandlerNetCDF (SampleHandlerNetCDF.cpp:24-110): every emitted sample of this rank's
-    // temperatures goes to `filename` (netCDF classic, NetCDFClassic.h; all ranks share the file),
-    // staged in HBM and written every `flush_every` samples; call before the first iteration
+    // SampleHandlerNetCDF (SampleHandlerNetCDF.cpp:24-110): every emitted sample goes to `filename`,
+    // staged in HBM and written every `flush_every` samples; call on every rank before the first
+    // iteration. netCDF-4 (the reference's format) when libnetcdf can be loaded -- for a sharded
+    // ladder rank 0 then receives the other ranks' staged rows over the transport at each flush and
+    // writes the whole ladder --, else netCDF classic (NetCDFClassic.h), the ranks of a sharded ladder
+    // sharing the file and each writing its own temperature columns
     bool SetOutput(const std::string& filename, int64_t num_samples, int flush_every);
     bool FlushOutput();
     // ptmhsampler.output_proposal_adaptation (SamplerPTChain.cpp:149-166): after every adaptation

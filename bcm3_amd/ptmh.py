@@ -172,8 +172,10 @@ class PTMHNative:
         self.C = L.bcm3_ptmh_num_chains(h)
 
     def set_output(self, filename: str, num_samples: int, flush_every: int = 64):
-        """SampleHandlerNetCDF for this rank's chains (bcm3_ptmh_set_output): the reference's
-        output.nc schema in a netCDF classic file (SampleFile); call before the first iteration."""
+        """SampleHandlerNetCDF (bcm3_ptmh_set_output): the reference's output.nc schema, netCDF-4 when
+        libnetcdf can be loaded (a sharded ladder: rank 0 writes every rank's rows, received over the
+        transport), netCDF classic otherwise (SampleFile); every rank calls it before the first
+        iteration."""
         _check(_lib().bcm3_ptmh_set_output(self.h, filename.encode(), num_samples, flush_every), "bcm3_ptmh_set_output")
 
     def set_adaptation_output(self, filename: str):

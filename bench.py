@@ -62,6 +62,10 @@ def parse():
                     help="measure cycles per BDF step on a plain 256-proposal launch after the timed region "
                          "(0 = skip, so a kernel trace holds only the sampler's launches)")
     ap.add_argument("--extras", type=int, default=1, help="extra: P=64 and circular workloads (0 = skip)")
+    ap.add_argument("--strong-chains", type=int, default=2048,
+                    help="also time this fixed ladder size over all GPUs in the same run (the strong-scaling "
+                         "companion of the weak headline, C5 = 2,048; 0 = skip)")
+    ap.add_argument("--strong-steps", type=int, default=30, help="timed iterations of the strong-scaling run")
     return ap.parse_args()
 
 
@@ -519,6 +523,37 @@ def expm_workloads(device, gen):
     return out
 
 
+def strong_run(ll, args, rank, world, device, dist):
+    import torch
+    cg = args.strong_chains
+    loop = NativeLoop(ll, cg, rank, world, args, dist)
+    loop.run(args.warmup)
+    loop.sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loop.run(args.strong_steps)
+    loop.sync()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+    evals = cg * args.strong_steps * loop.exploration_steps
+    return {"scaling": "strong", "global_chains": cg, "chains_per_gpu": cg // world, "n_gpus": world,
+            "steps": args.strong_steps, "value": evals / dt, "unit": "log-likelihood evals/sec",
+            "ms_per_step": dt / args.strong_steps * 1e3,
+            "config": "C5" if cg == 2048 else "custom",
+            "note": "the same ladder size at every GPU count: speedup(N) = value(N) / value(1); DESIGN.md §6 "
+                    "gives the physical bound (one GPU already runs 2,048 chains near its chip-filling rate)"}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -636,6 +671,12 @@ def main():
         tt, nl, _ = ll.kernel_time_log()
         ll.set_option(_hip.OPT_TIMING_LOG, 0)
         extra["throughput_batch"] = {"n": n, "kernel_ms": tt / nl, "evals_per_s": n / (tt / nl * 1e-3)}
+
+    if args.strong_chains and not args.total_chains and loop_kind == "native" and args.strong_chains % world == 0:
+        # the fixed-size ladder north_star's strong scaling is about (C5: 2,048
+        # chains over all GPUs), timed in the same run with the same barrier / max-over-ranks rule, so a
+        # SCALE curve carries strong-scaling values next to the weak headline
+        extra["strong_scaling"] = strong_run(ll, args, rank, world, device, dist if world > 1 else None)
 
     if rank == 0 and args.extras:
         extra.update(extra_workloads(device, args.seed))

@@ -28,6 +28,9 @@ def main():
     for _ in range(reps):
         ctx.eval_device(n, v.data_ptr(), lp.data_ptr(), None, None)
         ms.append(ctx.last_kernel_ms())
+    if os.environ.get("PROF_NO_DETAIL"):  # (C3-only development libraries have no counting kernel)
+        print(f"n={n} lpw={lpw} kernel ms min {min(ms):.3f} med {np.median(ms):.3f}")
+        return
     # steps of the slowest lane, for per-step cost
     g = ctx.eval(S.prior_draws(1, n, 7), detail=True)
     print(f"n={n} lpw={lpw} kernel ms min {min(ms):.3f} med {np.median(ms):.3f}; steps max {g['stats']['nst'].max()} "
