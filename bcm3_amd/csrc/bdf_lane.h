@@ -303,6 +303,15 @@ __device__ __attribute__((noinline)) double pow_glibc_call(double bx, int k)
 #endif
 BDF_INL double pow_root(double bx, int k)
 {
+#ifdef BCM3_ROOT_LEAN
+    // the tables are always uploaded before a launch (popk_prepare_device: the loaded libm's, else
+    // computed ones of the same layout, ok = 1 either way), so every finite bx > 0 takes glibc's
+    // algorithm (subnormal bx normalised as e_pow.c does); SUNRpowerR's base <= 0 -> 0 and pow's
+    // inf -> inf, NaN -> NaN by selects: one straight-line copy per call site
+    const bool fin = (bx > 0.0) & (bx < __builtin_inf());
+    const double p = xm::pow_glibc_pos(fin ? bx : 1.0, xm::inv_k(k), BDF_ROOT_TABLES);
+    return fin ? p : ((bx > 0.0) ? bx : ((bx == bx) ? 0.0 : bx + bx));
+#endif
 #if defined(BCM3_ROOT_HYBRID) || defined(BCM3_ROOT_CALL) || defined(BCM3_ROOT_CR)
     if (BDF_LIKELY((bx > 1e-30) & (bx < 1e30))) {
         bool safe;

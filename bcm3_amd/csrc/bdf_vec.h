@@ -487,6 +487,50 @@ BDF_INL bool order_change_skippable(const S& s, const TqCtx& c)
     return small;
 }
 
+// The same screen without the quotients of tq[1] and tq[3] (BCM3_SCREEN_DF): bx^2 > cut^2 is decided
+// in cross-multiplied form, tq[1]^2 = (xistar_inv (1 - A4 + A3) / A3)^2 / lq^2 and tq[3]^2 =
+// (1 - A6 + A5)^2 / (A2 xi_inv2 (q + 2) A5)^2 with both denominators moved to the right-hand side;
+// the two candidates' sums of squares are formed side by side and the decision is one branch. Every
+// operand is a product of a few rounded factors (relative error << the 1e-10 margin); a NaN or an
+// overflow to inf on the right-hand side answers "not skippable", which is always safe (the exact
+// evaluation runs). cquot keeps its two approximate quotients (a product of powers could underflow).
+template <int Q, int NS, class S>
+BDF_INL bool order_change_skippable_df(const S& s, const TqCtx& c)
+{
+    constexpr int q = Q;
+    constexpr double margin = 1.0 + 1e-10;
+    bool small1 = true, small3 = true;
+    double lhs1 = 0.0, rhs1 = 0.0, lhs3 = 0.0, rhs3 = 0.0;
+    if constexpr (q > 1) {
+        const double A3 = c.alpha0 + 1.0 / q;
+        const double A4 = c.alpha0_hat + c.xi_inv;
+        const double n1 = c.xistar_inv * (1.0 - A4 + A3);
+        const double p = s.zn[q] * s.ewt;
+        constexpr double cut = uni::eta_cut(q) * margin;
+        constexpr double k1 = BIAS1 * BIAS1 / (NS * tq_a3(q) * tq_a3(q));
+        lhs1 = lane_sum_v<NS>(p * p) * (k1 * (n1 * n1));
+        rhs1 = (cut * cut) * (c.lq * c.lq);
+    }
+    if constexpr (q != QMAX) {
+        const double cquot = qdiv(s.tq[5], s.saved_tq5) * powI(qdiv(s.h, s.tau[2]), q + 1);
+        const double tv = (-cquot) * s.zn[QMAX] + s.acor;
+        const double xi_inv2 = fdiv(s.h, c.hsum2);
+        const double A5 = c.alpha0 - 1.0 / (q + 1);
+        const double A6 = c.alpha0_hat - xi_inv2;
+        const double n3 = 1.0 - A6 + A5;
+        const double d3 = c.A2 * xi_inv2 * ((double)(q + 2) * A5);
+        const double p = tv * s.ewt;
+        constexpr double cut = uni::eta_cut(q + 2) * margin;
+        constexpr double k3 = BIAS3 * BIAS3 / NS;
+        lhs3 = lane_sum_v<NS>(p * p) * (k3 * (n3 * n3));
+        rhs3 = (cut * cut) * (d3 * d3);
+    }
+    // one uniform decision over both candidates (lanes of row 0 hold the sums)
+    if constexpr (q > 1) small1 = lhs1 > rhs1;
+    if constexpr (q != QMAX) small3 = (s.saved_tq5 == 0.0) | (lhs3 > rhs3);
+    return __builtin_amdgcn_readfirstlane((int)(small1 & small3)) != 0;
+}
+
 // one Newton correction (uni::newton_correction)
 // (PHB >= 0: the phases build marks the right-hand side, the solve and the norm as PHB, PHB + 1, PHB + 2)
 template <int NS, int PHB = -1, class S, class Model>
@@ -634,6 +678,29 @@ BDF_INL void complete_head_q(S& s)
     BDF_PH(PH);
 }
 
+// complete_head_q with the plain-step flag at run time (BCM3_ONE_TAIL: one tail per order)
+template <int Q, class S>
+BDF_INL void complete_head_q_rt(S& s, bool held)
+{
+    constexpr int q = Q;
+    s.nst++;
+    s.cnt.nst_total++;
+    s.hu = s.h;
+    if (!held) {
+        cfor_down<Q, 2>([&](auto i) __attribute__((always_inline)) { s.tau[CI(i)] = s.tau[CI(i) - 1]; });
+        if constexpr (q == 1) s.tau[2] = (s.nst > 1) ? s.tau[1] : s.tau[2];
+        s.tau[1] = s.h;
+    }
+    cfor<0, Q + 1>([&](auto j) __attribute__((always_inline)) { s.zn[CI(j)] = s.zn[CI(j)] + s.l[CI(j)] * s.acor; });
+    s.qwait--;
+    if constexpr (q != QMAX) {
+        if (s.qwait == 1) {
+            s.zn[QMAX] = s.acor;
+            s.saved_tq5 = s.tq[5];
+        }
+    }
+}
+
 template <int Q, int NS, bool FAST, int PH = 8, class S>
 BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
 {
@@ -656,7 +723,11 @@ BDF_INL void complete_eta_q(S& s, double dsm, const TqCtx& tc)
         double eta = etaq;
         s.qprime = q;
         const unsigned ph_s0 = BDF_PH_NOW();
+#ifdef BCM3_SCREEN_DF
+        const bool skip = (s.qwait == 0) && vec::order_change_skippable_df<q, NS>(s, tc);
+#else
         const bool skip = (s.qwait == 0) && vec::order_change_skippable<q, NS>(s, tc);
+#endif
         if constexpr (BDF_DBL(2)) {
             if (s.qwait == 0) {
                 S s2 = s;
@@ -984,15 +1055,21 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
         // dsm = acnrm tq[2] = del tq[2]) -- is ONE branch; anything else goes on through newton_rest,
         // which repeats the convergence test. false: the first attempt failed, the attempt loop takes
         // over. HELD (the plain step): tau[1..Q] all equal h, the completion skips their shift.
+#ifdef BCM3_ONE_TAIL
+        auto tail = [&](bool held, double del, bool setup, double cscale) __attribute__((always_inline)) {
+#else
         auto tail = [&](auto held, double del, bool setup, double cscale) __attribute__((always_inline)) {
+#endif
             double dsm = del * s.tq[2];
             if (BDF_LIKELY(div_le_one(del * SUNMIN(1.0, s.crate), s.tq[4]) & (dsm <= 1.0))) {
                 s.acnrm = del;
                 s.nls_jcur = 0;
+#ifndef BCM3_ONE_TAIL
                 if constexpr (decltype(held)::value)
                     BDF_PH(15);
                 else
                     BDF_PH(24);
+#endif
             } else {
                 const bool conv = vec::newton_rest<NS>(s, mdl, rl1, CONV_NONE, setup, cscale, del);
                 BDF_PH(5);
@@ -1007,9 +1084,20 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
                     return false;
                 }
             }
+#ifdef BCM3_ONE_TAIL
+            vec::complete_head_q_rt<Q>(s, held);
+            vec::complete_eta_q<Q, NS, true, 25>(s, dsm, tc);
+#else
             vec::complete_q<Q, NS, true, decltype(held)::value ? 16 : 25, decltype(held)::value>(s, dsm, tc);
+#endif
             return true;
         };
+#ifdef BCM3_ONE_TAIL
+        // one instance of the tail (convergence / error test, Newton iterations, completion with its
+        // order-change evaluation) for both branches: the plain flag decides the tau shift at run time
+        double del_t, cscale_t;
+        bool setup_t;
+#endif
         if (BDF_LIKELY(plain)) {
             BDF_PH(10);
             vec::predict_q<Q>(s);
@@ -1032,7 +1120,13 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             }
             const double del = vec::newton_correction<NS, 12>(s, mdl, rl1, cscale, false, false, CONV_NONE);
             run++;  // have stays set (reuse, no setup)
+#ifdef BCM3_ONE_TAIL
+            del_t = del;
+            cscale_t = cscale;
+            setup_t = false;
+#else
             if (!tail(std::true_type{}, del, false, cscale)) return NEED_ATTEMPTS;
+#endif
         } else {
             BDF_PH(2);
             // cvStep's attempt at order Q (attempt_q with nflag == FIRST_CALL, nst > 0)
@@ -1070,10 +1164,31 @@ BDF_INL int fast_run(S& s, const Model& mdl, double (&yout)[NS], double& tret, d
             cscale_h = cscale;
             s.acor = 0.0;
             const double del = vec::newton_correction<NS>(s, mdl, rl1, cscale, setup, false, CONV_NONE);
+#ifdef BCM3_KEEP_ON_SETUP
+            // a linear-solver setup leaves l, tq and gamma as they are (they depend on h and tau only)
+            // and sets gammap = gamma, gamrat = 1: cvSet would recompute gamrat = gamma / gammap = 1
+            // exactly (a correctly rounded x / x), so the held coefficients stay valid with gamrat 1
+            // and Newton scale 1 -- the next step is plain instead of recomputing cvSet
+            have = reuse | (run >= Q);
+            if (setup) {
+                gamrat_h = 1.0;
+                cscale_h = 1.0;
+            }
+#else
             have = (reuse | (run >= Q)) & !setup;
+#endif
             run++;
+#ifdef BCM3_ONE_TAIL
+            del_t = del;
+            cscale_t = cscale;
+            setup_t = setup;
+#else
             if (!tail(std::false_type{}, del, setup, cscale)) return NEED_ATTEMPTS;
+#endif
         }
+#ifdef BCM3_ONE_TAIL
+        if (!tail(plain, del_t, setup_t, cscale_t)) return NEED_ATTEMPTS;
+#endif
         const double troundoff = FUZZ_FACTOR * UROUND * (fabs(s.tn) + fabs(s.h));
         const bool quiet = (fabs(s.tn - s.tstop) > troundoff) & !((s.tn + s.hprime - s.tstop) * s.h > 0.0) &
                            (s.tn < tlim) & (s.qprime == Q) & (current_step + 1 != max_steps);

@@ -339,10 +339,22 @@ XM_FN double pow_inv_k_checked(double x, int k, bool& safe)
 
 // pow(x, y) for a positive normal x and 2^-65 <= |y| < 2^63 with |y log x| < 512 (the main path
 // of e_pow.c; the step-size roots: x in (1e-30, 1e30), y = fl(1/k))
-XM_FN double pow_glibc(double x, double y, const GlibcPow& D)
+XM_FN double pow_glibc_ix(unsigned long long ix, double y, const GlibcPow& D);
+XM_FN double pow_glibc(double x, double y, const GlibcPow& D) { return pow_glibc_ix((unsigned long long)as_bits(x), y, D); }
+
+// pow(x, y) for every finite x > 0 (e_pow.c: a subnormal x is normalised first, its exponent field
+// going negative: asuint64(x 2^52) - 52 << 52), without a branch
+XM_FN double pow_glibc_pos(double x, double y, const GlibcPow& D)
+{
+    const unsigned long long ix = (unsigned long long)as_bits(x);
+    const unsigned long long ixs = (unsigned long long)as_bits(x * 0x1p52) - (52ull << 52);
+    return pow_glibc_ix((ix < 0x0010000000000000ull) ? ixs : ix, y, D);
+}
+
+// x given as its bit pattern ix (see pow_glibc_pos for subnormal x)
+XM_FN double pow_glibc_ix(unsigned long long ix, double y, const GlibcPow& D)
 {
     // log_inline: x = 2^k z, z/c - 1 = r exact, log x = k ln2 + log c + log1p(r) in double-double
-    const unsigned long long ix = (unsigned long long)as_bits(x);
     const unsigned long long tmp = ix + 0xC0196AAB00000000ull;  // ix - 0x3fe6955500000000
     const int i = (int)((tmp >> 45) & 127);
     const double kd = (double)(int)((long long)tmp >> 52);
@@ -371,7 +383,9 @@ XM_FN double pow_glibc(double x, double y, const GlibcPow& D)
     const double ehi = y * ly;
     const double elo = __builtin_fma(y, ltail, __builtin_fma(ly, y, -ehi));
     const int abstop = (int)((as_bits(ehi) >> 52) & 0x7ff);
+#ifndef BCM3_ROOT_LEAN
     if (abstop < 0x3c9) return 1.0 + ehi;  // |y log x| < 2^-54
+#endif
     // exp_inline: ehi = (k + i/128) ln2 + r, 2^(i/128) from the table, exp(r) by its polynomial
     const double kz = __builtin_fma(ehi, D.invln2N, D.shift);
     const unsigned long long ki = (unsigned long long)as_bits(kz);
@@ -389,7 +403,12 @@ XM_FN double pow_glibc(double x, double y, const GlibcPow& D)
     const double s1 = __builtin_fma(c23, r2, tr);
     const double t = __builtin_fma(c45, r2 * r2, s1);
     const double scale = as_double((long long)sbits);
+#ifdef BCM3_ROOT_LEAN
+    // (the tiny case as a select: the exp path's operands are finite there too)
+    return (abstop < 0x3c9) ? 1.0 + ehi : __builtin_fma(t, scale, scale);  // |y log x| < 2^-54
+#else
     return __builtin_fma(t, scale, scale);
+#endif
 }
 
 // ---------------------------------------------------------------------------------------------

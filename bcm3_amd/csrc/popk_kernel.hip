@@ -265,6 +265,13 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     constexpr int NS = TR::NS;
     constexpr bool UNI = (MODE != POPK_LANES);
     constexpr bool VEC = (MODE == POPK_VEC);
+    // library functions out of line (libm_exact.h xm::lib) in the vector-state kernel; the
+    // scalar-state kernel inlines them unless BCM3_UNI_COLD (diagnostic builds)
+#ifdef BCM3_UNI_COLD
+    constexpr bool COLD = UNI;
+#else
+    constexpr bool COLD = VEC;
+#endif
     const int lane = threadIdx.x & 63;
 #ifdef BCM3_TABLES_LDS
     {
@@ -300,27 +307,27 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
 
     // ---- parameter map (.cpp:263-310)
     const int sdix = m.sd_ix;
-    const double sd = transform_var<VEC>(m.transforms[sdix], v[sdix]);
-    const double sd2 = transform_var<VEC>(m.transforms[sdix + 1], v[sdix + 1]);
-    PKLane<PKT, VEC> mdl;
+    const double sd = transform_var<COLD>(m.transforms[sdix], v[sdix]);
+    const double sd2 = transform_var<COLD>(m.transforms[sdix + 1], v[sdix + 1]);
+    PKLane<PKT, COLD> mdl;
     // single-patient likelihood (LikelihoodPharmacokineticTrajectory.cpp:226-259): the rates are the
     // transformed variables; the population likelihood draws ka and CL per patient (.cpp:283-286)
     const bool single = (m.param_map == BCM3HIP_PARAM_MAP_SINGLE);
-    const double vod = isnan(m.fixed_vod) ? transform_var<VEC>(m.transforms[3], v[3]) : m.fixed_vod;
+    const double vod = isnan(m.fixed_vod) ? transform_var<COLD>(m.transforms[3], v[3]) : m.fixed_vod;
     if (single) {
-        mdl.ka = transform_var<VEC>(m.transforms[0], v[0]);
-        mdl.ke = transform_var<VEC>(m.transforms[1], v[1]);
-        mdl.kel = transform_var<VEC>(m.transforms[2], v[2]) / vod;
+        mdl.ka = transform_var<COLD>(m.transforms[0], v[0]);
+        mdl.ke = transform_var<COLD>(m.transforms[1], v[1]);
+        mdl.kel = transform_var<COLD>(m.transforms[2], v[2]) / vod;
     } else {
-        mdl.ka = fastpow10<VEC>(quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
-        mdl.ke = transform_var<VEC>(m.transforms[1], v[1]);
-        mdl.kel = fastpow10<VEC>(quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / vod;
+        mdl.ka = fastpow10<COLD>(quantile_normal(v[npk + npop * (j + 1) + 0], v[0], v[npk + 0]));
+        mdl.ke = transform_var<COLD>(m.transforms[1], v[1]);
+        mdl.kel = fastpow10<COLD>(quantile_normal(v[npk + npop * (j + 1) + 1], v[2], v[npk + 1])) / vod;
     }
     mdl.kf = mdl.kb = 0.0;
     if constexpr (TR::two) {
         if (isnan(m.fixed_kf)) {
-            mdl.kf = transform_var<VEC>(m.transforms[4], v[4]);
-            mdl.kb = transform_var<VEC>(m.transforms[5], v[5]);
+            mdl.kf = transform_var<COLD>(m.transforms[4], v[4]);
+            mdl.kb = transform_var<COLD>(m.transforms[5], v[5]);
         } else {
             mdl.kf = m.fixed_kf;
             mdl.kb = m.fixed_kb;
@@ -329,22 +336,22 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     mdl.ktr = mdl.ntr = mdl.lnf = 0.0;
     if constexpr (TR::transit) {
         const int ni = m.n_transit_ix, ti = m.transit_time_ix;
-        mdl.ntr = transform_var<VEC>(m.transforms[ni], v[ni]);
-        mdl.ktr = (mdl.ntr + 1) / transform_var<VEC>(m.transforms[ti], v[ti]);
+        mdl.ntr = transform_var<COLD>(m.transforms[ni], v[ni]);
+        mdl.ktr = (mdl.ntr + 1) / transform_var<COLD>(m.transforms[ti], v[ti]);
         const double n = mdl.ntr;
-        mdl.lnf = 0.9189385332046727 + (n + 0.5) * xm::lib<VEC>::log(n) - n + xm::lib<VEC>::log(1 + 1 / (12.0 * n));
+        mdl.lnf = 0.9189385332046727 + (n + 0.5) * xm::lib<COLD>::log(n) - n + xm::lib<COLD>::log(1 + 1 / (12.0 * n));
     }
     const double interval = m.dosing_interval[j];
     double tsw = 0.0;
     mdl.ka2 = 0.0;
     if constexpr (TR::biphasic) {
         const int bi = m.biphasic_time_ix, ai = m.absorption2_ix;
-        tsw = transform_var<VEC>(m.transforms[bi], v[bi]);
+        tsw = transform_var<COLD>(m.transforms[bi], v[bi]);
         const double lim = interval - 1e-2;
         // (the population likelihood keeps the switch inside the dosing interval, .cpp:303-305;
         //  the single-patient one does not, LikelihoodPharmacokineticTrajectory.cpp:253)
         tsw = (!single && lim < tsw) ? lim : tsw;
-        mdl.ka2 = transform_var<VEC>(m.transforms[ai], v[ai]);
+        mdl.ka2 = transform_var<COLD>(m.transforms[ai], v[ai]);
     }
     if constexpr (UNI && !VEC) {
         // values returned by out-of-line calls (ndtri_lower) count as divergent to the compiler;
@@ -394,7 +401,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     bool llh_done = false;  // NaN concentration seen: llh = -inf, stop accumulating
     int status = BCM3HIP_STATUS_OK;
 
-    std::conditional_t<VEC, vec::VecState<NS, STATS>, BdfState<NS, typename PKLane<PKT, VEC>::Inv>> s;
+    std::conditional_t<VEC, vec::VecState<NS, STATS>, BdfState<NS, typename PKLane<PKT, COLD>::Inv>> s;
     s.cnt = {};
     s.nst = 0;
 #ifdef BCM3_PHASES
@@ -415,7 +422,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         const double yo = obs[i];
         if (!isnan(yo)) {
             const double xm = (x < 0.0) ? 0.0 : x;
-            llh += log_pdf_tnu4<VEC>(x, yo, sd_u + sd2_u * xm);
+            llh += log_pdf_tnu4<COLD>(x, yo, sd_u + sd2_u * xm);
         }
         // population likelihood: a NaN concentration ends the patient at -inf (.cpp:418-421); the
         // single-patient likelihood has no such rule, NaN reaches the caller as in the reference

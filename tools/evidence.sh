@@ -17,11 +17,11 @@ if [ -z "$PROFILES_ONLY" ]; then
   timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err
   cat $O/bench.json
 fi
-BENCH="bench.py --steps 40 --warmup 4 --cpu-seconds 0 --throughput-batch 0 --extras 0 --issue-probe 0"
+BENCH="bench.py --steps 40 --warmup 4 --cpu-seconds 0 --throughput-batch 0 --extras 0 --issue-probe 0 --strong-chains 0"
 # the SQ passes count instructions per BDF step on plain 256-proposal launches (one trajectory per wave)
 SQRUN="tools/prof_popk.py 256 1 3"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt -o kt -- python3 $BENCH > $O/kt.log 2>&1
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_extras -o kt -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --throughput-batch 0 --extras 1 > $O/kt_extras.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_extras -o kt -- python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --throughput-batch 0 --extras 1 --strong-chains 0 > $O/kt_extras.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o pmc -- python3 $BENCH > $O/pmc_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o pmc -- python3 $BENCH > $O/pmc_write.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d $O/pmc_sq -o pmc -- python3 $SQRUN > $O/pmc_sq.log 2>&1
