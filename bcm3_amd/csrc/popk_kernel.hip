@@ -249,6 +249,25 @@ BDF_INL bool check_give_treatment(double t, const uint8_t* skipped, int intermit
 // state vectors across lanes: bdf_vec.h). All three give the same bits.
 enum { POPK_LANES = 0, POPK_UNI = 1, POPK_VEC = 2 };
 
+// the kernel's argument list as a struct: the byte offsets of its members are those of the kernarg
+// segment (the code object's .args metadata: logp_direct at 216 ... place_out at 272)
+struct PopkArgsLayout {
+    PopPKDevModel m;
+    int64_t ntraj;
+    int lpw;
+    const double* values;
+    double* logp_direct;
+    double* patient_llh;
+    int32_t* traj_status;
+    double* traj_out;
+    bcm3hip_traj_stats* stats_out;
+    const int32_t* n_dev;
+    int32_t* steps_out;
+    uint64_t* place_out;
+};
+static_assert(offsetof(PopkArgsLayout, logp_direct) == 216 && offsetof(PopkArgsLayout, place_out) == 272,
+              "popk_traj_kernel's kernarg layout changed: re-check the code object's .args offsets");
+
 template <int PKT, int MODE, bool STATS>
 __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t ntraj, int lpw,
                                                         const double* __restrict__ values,
@@ -598,6 +617,21 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
 #ifdef BCM3_PHASES
     if (tro) cfor<0, NPHASES>([&](auto k) __attribute__((always_inline)) { tro[CI(k)] = (double)s.ph[CI(k)]; });
     if (tro) cfor<1, QMAX + 1>([&](auto k) __attribute__((always_inline)) { tro[NPHASES + CI(k) - 1] = (double)s.qh[CI(k)]; });
+#endif
+#ifdef BCM3_LATE_ARGS
+    {
+        // (variant) the output pointers read from the kernarg segment only now, through a laundered
+        // segment pointer, so that none of them holds scalar registers through the solve
+        const char* ka = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(ka));
+        const PopkArgsLayout* A = reinterpret_cast<const PopkArgsLayout*>(ka);
+        logp_direct = A->logp_direct;
+        patient_llh = A->patient_llh;
+        traj_status = A->traj_status;
+        stats_out = A->stats_out;
+        steps_out = A->steps_out;
+        place_out = A->place_out;
+    }
 #endif
     if (logp_direct) logp_direct[e] = 0.0 + llh;  // P == 1: logp = 0 + patient term
     if (patient_llh) patient_llh[g] = llh;
