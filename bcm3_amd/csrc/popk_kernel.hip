@@ -494,9 +494,23 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
             s.tstopset = 1;
             int current_step = 0;
             bool hot = false;  // previous step was a plain CV_SUCCESS (uni::cvode_one_step_u)
+#ifdef BCM3_PRIO_STEPS
+            int prio_level = 0;
+#endif
             for (;;) {
                 double tret = 0.0;
                 int result;
+#ifdef BCM3_PRIO_STEPS
+                // (variant) a trajectory that has run long gets the higher issue priority on a shared
+                // SIMD (s_setprio; the launch waits for its longest trajectory): checked once per
+                // return to this loop
+                if (BDF_UNLIKELY(current_step >= BCM3_PRIO_STEPS * (prio_level + 1) && prio_level < 3)) {
+                    prio_level++;
+                    if (prio_level == 1) __builtin_amdgcn_s_setprio(1);
+                    else if (prio_level == 2) __builtin_amdgcn_s_setprio(2);
+                    else __builtin_amdgcn_s_setprio(3);
+                }
+#endif
                 if constexpr (VEC) {
                     // after a plain step: run the following plain steps in vec::fast_run (same
                     // results, one exit test per step); an order change the last step decided is
