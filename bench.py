@@ -527,6 +527,14 @@ def strong_run(ll, args, rank, world, device, dist):
     import torch
     cg = args.strong_chains
     loop = NativeLoop(ll, cg, rank, world, args, dist)
+    try:
+        return _strong_timed(loop, cg, args, world, device, dist)
+    finally:
+        loop.s.close()
+
+
+def _strong_timed(loop, cg, args, world, device, dist):
+    import torch
     loop.run(args.warmup)
     loop.sync()
     torch.cuda.synchronize()
@@ -675,8 +683,17 @@ def main():
     if args.strong_chains and not args.total_chains and loop_kind == "native" and args.strong_chains % world == 0:
         # the fixed-size ladder north_star's strong scaling is about (C5: 2,048
         # chains over all GPUs), timed in the same run with the same barrier / max-over-ranks rule, so a
-        # SCALE curve carries strong-scaling values next to the weak headline
-        extra["strong_scaling"] = strong_run(ll, args, rank, world, device, dist if world > 1 else None)
+        # SCALE curve carries strong-scaling values next to the weak headline. The weak run's sampler
+        # (and its RCCL communicator) is released first; a failure here is reported in the line and
+        # never costs the headline
+        acc_weak = loop.acceptance()
+        loop.s.close()
+        try:
+            extra["strong_scaling"] = strong_run(ll, args, rank, world, device, dist if world > 1 else None)
+        except Exception as ex:  # noqa: BLE001 -- reported, the weak headline stands
+            extra["strong_scaling"] = {"error": f"{type(ex).__name__}: {ex}"}
+            print(f"bench.py rank {rank}: strong-scaling run failed: {ex}", file=sys.stderr, flush=True)
+        loop.acceptance = lambda: acc_weak  # (the headline's acceptance, read below)
 
     if rank == 0 and args.extras:
         extra.update(extra_workloads(device, args.seed))
