@@ -31,6 +31,13 @@ struct CpSolveArgs {
     int32_t* flags;               // [slot] bit0 ok, bit1 divided, bit2 died, bit3 entered mitosis
     double* event_times;          // [slot][5]
     int32_t* nsteps;              // [slot]
+    // stored integration points (CP_STORED builds, synchronised data): per slot store_cap records of
+    // CP_REC doubles (ODESolverCVODE's CVodeTimepoint: time, tn, h, hu, q, zn[0..q] of the stored
+    // species); the sync pass of every output entry; the synchronisation offset per slot
+    double* store;
+    int32_t store_cap;
+    const int32_t* output_sync;   // [M] BCM3HIP_CP_SYNC_*
+    const double* sync_offset;    // [slot]
 };
 
 }  // namespace cpk

@@ -70,12 +70,16 @@ __device__ double cp_apply(int32_t kind, double x, double v)
 
 
 __global__ void cp_init_kernel(CpStatic m, int32_t n_items, const CpInitItem* items, const double* values,
-                               double* params, double* y0, double* creation, const double* end_y, const double* achieved)
+                               double* params, double* y0, double* creation, const double* end_y, const double* achieved,
+                               double* sync_off)
 {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= n_items) return;
     const CpInitItem it = items[w];
     const double* v = values + (size_t)it.eval * m.d;
+    // Experiment::EvaluateLogProbability's time_offset: the sampled value, before any cell
+    // variability (Experiment.cpp:267-272)
+    if (sync_off) sync_off[it.slot] = cp_ref(m.sync_offset, v, m.transforms, 0.0);
     double* prm = params + (size_t)it.slot * m.d;
     double* y = y0 + (size_t)it.slot * m.NS;
     for (int i = 0; i < m.d; i++) prm[i] = cp_transform(m.transforms[i], v[i]);
@@ -819,11 +823,11 @@ hipError_t launch_cp_assign(int32_t n_problems, int32_t R, int32_t nsim, const d
 
 hipError_t launch_cp_init(const CpStatic& m, int32_t n_items, const CpInitItem* items, const double* values,
                           double* params, double* y0, double* creation, const double* end_y, const double* achieved,
-                          hipStream_t s)
+                          double* sync_off, hipStream_t s)
 {
     if (n_items <= 0) return hipSuccess;
     hipLaunchKernelGGL(cp_init_kernel, dim3((n_items + 127) / 128), dim3(128), 0, s, m, n_items, items, values, params,
-                       y0, creation, end_y, achieved);
+                       y0, creation, end_y, achieved, sync_off);
     return hipGetLastError();
 }
 

@@ -1072,6 +1072,61 @@ BDF_INL double crossing_time(double t, double prev, double threshold, bool above
     return time;
 }
 
+// ---- stored integration points (synchronised data; Cell.cpp:152, 232-233) -----------------------
+#ifndef CP_STORED
+#define CP_STORED 0
+#endif
+#ifndef CP_NSTORE
+#define CP_NSTORE 0
+#endif
+// one CVodeTimepoint record (ODESolverCVODE.cpp:375-401): cvode_time, tn, h, hu, q, then zn[j] of
+// the stored species m at 5 + j * CP_NSTORE + m (the species the data read, kStoreIx)
+constexpr int CP_REC = 5 + (QMAX + 1) * (CP_NSTORE > 0 ? CP_NSTORE : 1);
+
+// the step's interpolating polynomial at `time` in every lane: sum over j = q..0 of s^j zn[j], s =
+// (time - tn) / h, s^j by repeated products (GetInterpolatedY / get_threshold_crossing_time's
+// loop, ODESolverCVODE.cpp:232-240, 292-301)
+template <class S>
+BDF_INL double interp_lane(const S& s, double time)
+{
+    const double sv = (time - s.tn) / s.h;
+    double pw[QMAX + 1];
+    pw[0] = 1.0;
+    cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { pw[CI(j)] = pw[CI(j) - 1] * sv; });
+    double y = 0.0;
+    cfor_down<QMAX, 0>([&](auto j) __attribute__((always_inline)) {
+        if (CI(j) <= s.q) y = __builtin_fma(pw[CI(j)], s.zn[CI(j)], y);
+    });
+    return y;
+}
+
+// get_threshold_crossing_time with stored integration points (ODESolverCVODE.cpp:264-320): ten
+// bisection steps between the previous step's time and t on the polynomial of the step just
+// taken (its record is the solver's current state), species J
+template <int J, class S>
+BDF_INL double crossing_time_stored(const S& s, double t, double prev, double threshold, bool above)
+{
+    double dt = (t - prev) * 0.5;
+    double time = prev + dt;
+    for (int it = 0; it < 10; it++) {
+        const double x = ev_value<J>(interp_lane(s, time));
+        dt *= 0.5;
+        const bool down = above ? (x > threshold) : (x < threshold);
+        time = down ? time - dt : time + dt;
+    }
+    return time;
+}
+
+// GetInterpolatedY's time check on a record (tn, hu): false = "Time error for interpolation" (NaN)
+BDF_INL bool interp_time_ok(double t, double tn, double hu)
+{
+    double tfuzz = 100.0 * UROUND * (fabs(tn) + fabs(hu));
+    if (hu < 0.0) tfuzz = -tfuzz;
+    const double tp = tn - hu - tfuzz;
+    const double tn1 = tn + tfuzz;
+    return !((t - tp) * (t - tn1) > 0.0);
+}
+
 }  // namespace cpk
 
 // One cell per workgroup (64 lanes): Cell::Simulate -> ODESolver::SolveReturnSolution ->
@@ -1104,6 +1159,17 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
     sh.creation = creation;
 #endif
     const double y0 = (ln < NS) ? a.y0[(size_t)slot * NS + ln] : 0.0;
+#if CP_STORED
+    // the stored-species slot of this lane's component (-1: not read by the data)
+    int my_store = -1;
+    cfor<0, NS>([&](auto k) __attribute__((always_inline)) {
+        if (ln == CI(k)) my_store = kStoreIx[CI(k)];
+    });
+    double* const rec0 = a.store + (size_t)slot * a.store_cap * CP_REC;
+    int nrec = 0;
+    bool overflow = false;
+#endif
+    double ylast = y0, tlast = 0.0;  // stored mode: the last step's output and time
     const int M = MM;
     double* outv = sh.outl;
     for (int k = ln; k < M; k += ROW) outv[k] = __builtin_nan("");
@@ -1123,13 +1189,21 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
     int nst = 0;
     // SolveReturnSolution: output times before the cell's t = 0 + DBL_EPSILON get y0
     int ti = 0;
-    while (ti < M && a.output_times[ti] - creation < 2.220446049250313e-16) {
-        const int sp = a.output_species[ti];
-        if (sp >= 0 && ln == sp) outv[ti] = y0;
-        ti++;
+    bool solve;
+    if constexpr (CP_STORED) {
+        // SolveStoreIntegrationPoints (ODESolver.cpp:136-150): the whole simulation time, no outputs
+        solve = sim_end > 2.220446049250313e-16;
+        if (!solve) ok = false;
+    } else {
+        while (ti < M && a.output_times[ti] - creation < 2.220446049250313e-16) {
+            const int sp = a.output_species[ti];
+            if (sp >= 0 && ln == sp) outv[ti] = y0;
+            ti++;
+        }
+        solve = ti < M;
     }
     double yend = y0;
-    if (ti < M) {
+    if (solve) {
         GenState<NS> s;
         s.rtol = a.rtol;
         s.atol = a.atol;
@@ -1179,11 +1253,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
             s.tstopset = 1;
         }
 #endif
-        double end_time = a.output_times[M - 1] - creation;
+        double end_time = CP_STORED ? sim_end : a.output_times[M - 1] - creation;
         double t = 0.0;
         int tpi = ti;
         // the next output time in a register: no global load on every step's critical path
-        double next_out = a.output_times[tpi] - creation;
+        double next_out = a.output_times[(tpi < M) ? tpi : M - 1] - creation;
         for (;;) {
             double tret, y;
             int r;
@@ -1198,7 +1272,33 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
             }
             t = tret;
             nst++;
-            while (tpi < M && tret >= next_out) {
+#if CP_STORED
+            // ODESolverCVODE::Solve (:375-401): the step's record; the buffer holds store_cap records
+            // (max_steps unless the byte budget caps it: then the launch reports the overflow)
+            if (nrec >= a.store_cap) {
+                overflow = true;
+                ok = false;
+                break;
+            }
+            {
+                double* rec = rec0 + (size_t)nrec * CP_REC;
+                if (ln == 0) {
+                    rec[0] = t;
+                    rec[1] = s.tn;
+                    rec[2] = s.h;
+                    rec[3] = s.hu;
+                    rec[4] = (double)s.q;
+                }
+                if (my_store >= 0)
+                    cfor<0, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
+                        if (CI(j) <= s.q) rec[5 + CI(j) * CP_NSTORE + my_store] = s.zn[CI(j)];
+                    });
+                nrec++;
+            }
+            ylast = y;
+            tlast = t;
+#endif
+            while (!CP_STORED && tpi < M && tret >= next_out) {
                 double dky;
                 if (get_dky(s, next_out, dky) != CV_SUCCESS) {
                     ok = false;
@@ -1213,32 +1313,48 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
             // Cell::integration_step_cb (Cell.cpp:463-538) on CVode's output vector
             bool cont = true;
             if constexpr (CP_EV0 >= 0)
-                if (ev[0] != ev[0] && ev_value<CP_EV0>(y) > 1e-4) ev[0] = crossing_time(t, previous_step_time, 1e-4, true);
+                if (ev[0] != ev[0] && ev_value<CP_EV0>(y) > 1e-4) ev[0] = CP_STORED ? crossing_time_stored<CP_EV0>(s, t, previous_step_time, 1e-4, true) : crossing_time(t, previous_step_time, 1e-4, true);
             if constexpr (CP_EV1 >= 0)
-                if (ev[1] != ev[1] && ev_value<CP_EV1>(y) > 1.95) ev[1] = crossing_time(t, previous_step_time, 1.95, true);
+                if (ev[1] != ev[1] && ev_value<CP_EV1>(y) > 1.95) ev[1] = CP_STORED ? crossing_time_stored<CP_EV1>(s, t, previous_step_time, 1.95, true) : crossing_time(t, previous_step_time, 1.95, true);
             if constexpr (CP_EV2 >= 0)
-                if (ev[2] != ev[2] && ev_value<CP_EV2>(y) > 0.5) ev[2] = crossing_time(t, previous_step_time, 0.5, true);
+                if (ev[2] != ev[2] && ev_value<CP_EV2>(y) > 0.5) ev[2] = CP_STORED ? crossing_time_stored<CP_EV2>(s, t, previous_step_time, 0.5, true) : crossing_time(t, previous_step_time, 0.5, true);
             if constexpr (CP_EV3 >= 0)
-                if (ev[3] != ev[3] && ev_value<CP_EV3>(y) < 0.5) ev[3] = crossing_time(t, previous_step_time, 0.5, false);
+                if (ev[3] != ev[3] && ev_value<CP_EV3>(y) < 0.5) ev[3] = CP_STORED ? crossing_time_stored<CP_EV3>(s, t, previous_step_time, 0.5, false) : crossing_time(t, previous_step_time, 0.5, false);
             if constexpr (CP_EV4 >= 0) {
                 if (ev[4] != ev[4] && ev_value<CP_EV4>(y) > 1e-3) {
-                    ev[4] = crossing_time(t, previous_step_time, 1e-3, true);
+                    ev[4] = CP_STORED ? crossing_time_stored<CP_EV4>(s, t, previous_step_time, 1e-3, true)
+                                      : crossing_time(t, previous_step_time, 1e-3, true);
                     sim_end = fmax(sim_end, ev[4] + a.past_cs);
                     end_time = sim_end;
                 }
             }
             if constexpr (CP_EV5 >= 0) {
                 if (a.divide_cells && ev_value<CP_EV5>(y) > 1.0) {
-                    sim_end = t;
-                    yend = y;
+                    if constexpr (CP_STORED) {
+                        // the division time on the step's interpolant and GetInterpolatedY there: the
+                        // solve's iterator finds the last record (the bisection stays inside
+                        // (previous step, t)), NaN when its time check fails (Cell.cpp:502-505)
+                        const double td = crossing_time_stored<CP_EV5>(s, t, previous_step_time, 1.0, true);
+                        sim_end = td;
+                        yend = interp_time_ok(td, s.tn, s.hu) ? interp_lane(s, td) : __builtin_nan("");
+                    } else {
+                        sim_end = t;
+                        yend = y;
+                    }
                     divided = true;
                     cont = false;
                 }
             }
             if constexpr (CP_EV6 >= 0) {
                 if (ev_value<CP_EV6>(y) > 1.0) {
-                    sim_end = t;
-                    yend = y;
+                    if constexpr (CP_STORED) {
+                        const double td = crossing_time_stored<CP_EV6>(s, t, previous_step_time, 1.0, true);
+                        sim_end = td;
+                        yend = interp_time_ok(td, s.tn, s.hu) ? interp_lane(s, td) : __builtin_nan("");
+                    } else {
+                        sim_end = t;
+                        yend = y;
+                    }
                     died = true;
                     cont = false;
                 }
@@ -1279,17 +1395,73 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
 #endif
         }
         if (ok && !divided && !died) {
-            // simulation_end_y = the solution at the last output time
-            double dky = 0.0;
-            get_dky(s, a.output_times[M - 1] - creation, dky);
-            yend = dky;
+            if constexpr (CP_STORED) {
+                // simulation_end_y = the solver's current y (Cell.cpp:247-249)
+                yend = ylast;
+            } else {
+                // simulation_end_y = the solution at the last output time
+                double dky = 0.0;
+                get_dky(s, a.output_times[M - 1] - creation, dky);
+                yend = dky;
+            }
         }
     }
+#if CP_STORED
+    // Experiment::EvaluateLogProbability's passes (Experiment.cpp:277-292): per synchronisation
+    // point in enum order, the interpolation iterator restarted, the entries of that pass in
+    // time order; Cell::GetInterpolatedSpeciesValue (Cell.cpp:280-327) -> GetInterpolatedY: the
+    // first record whose time is past the request, its polynomial, the cached vector while the
+    // time repeats. The records are this row's own stores (visible after the barrier).
+    wave_sync();
+    if (ok) {
+        const double toff = a.sync_offset[slot];
+        for (int p = 0; p <= 4; p++) {
+            const double evp = (p == 0) ? ev[0] : (p == 1) ? ev[2] : (p == 2) ? ev[3] : ev[4];
+            int iter = 0;
+            double itime = __builtin_nan("");
+            bool inan = false;
+            for (int k = 0; k < M; k++) {
+                const int sp = a.output_species[k];
+                if (a.output_sync[k] != p || sp < 0) continue;
+                const double time = a.output_times[k] + toff;
+                const double ct = (p == 4) ? time - creation : time + ((evp != evp) ? sim_end : evp);
+                double x = __builtin_nan("");
+                if (!(ct < 0.0 || ct > sim_end)) {
+                    if (!(ct == itime)) {
+                        while (iter < nrec && rec0[(size_t)iter * CP_REC] <= ct) iter++;
+                        if (iter == nrec) {
+                            itime = __builtin_nan("");
+                            inan = true;
+                        } else {
+                            itime = ct;
+                            const double* r = rec0 + (size_t)iter * CP_REC;
+                            inan = !interp_time_ok(ct, r[1], r[3]);
+                        }
+                    }
+                    if (!inan) {
+                        const double* r = rec0 + (size_t)iter * CP_REC;
+                        const int q = (int)r[4];
+                        const int m = kStoreIx[sp];
+                        const double sv = (ct - r[1]) / r[2];
+                        double pw[QMAX + 1];
+                        pw[0] = 1.0;
+                        cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) { pw[CI(j)] = pw[CI(j) - 1] * sv; });
+                        x = 0.0;
+                        cfor_down<QMAX, 0>([&](auto j) __attribute__((always_inline)) {
+                            if (CI(j) <= q) x = __builtin_fma(pw[CI(j)], r[5 + CI(j) * CP_NSTORE + m], x);
+                        });
+                    }
+                }
+                if (ln == 0) outv[k] = x;
+            }
+        }
+    }
+#endif
     // GetInterpolatedSpeciesValue: NaN outside [0, simulation_end_time] of the cell
     wave_sync();
     for (int k = ln; k < M; k += ROW) {
         const double ct = a.output_times[k] - creation;
-        a.out_values[(size_t)slot * M + k] = (ct < 0.0 || ct > sim_end) ? __builtin_nan("") : outv[k];
+        a.out_values[(size_t)slot * M + k] = (!CP_STORED && (ct < 0.0 || ct > sim_end)) ? __builtin_nan("") : outv[k];
     }
     if (ln < NS) a.end_y[(size_t)slot * NS + ln] = yend;
 #ifdef CP_PHASES
@@ -1298,12 +1470,21 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
     if (ln < 8 && ln < NS) a.end_y[(size_t)slot * NS + ln] = (double)sh.ph[ln];
 #endif
     if (ln == 0) {
+#if CP_STORED
+        // the stored mode ends at the last step taken (Cell.cpp:247-249)
+        const double achieved_cell_time = (divided || died) ? sim_end : tlast;
+#else
         const double achieved_cell_time = (divided || died) ? sim_end : (a.output_times[M - 1] - creation);
+#endif
         a.sim_end[slot] = sim_end;
         a.achieved[slot] = achieved_cell_time + creation;
         // bit4: SimulateCell adds two daughters (divide_cells && divide && achieved_time < target)
         const bool spawn = ok && divided && (achieved_cell_time + creation < a.end_time);
-        a.flags[slot] = (ok ? 1 : 0) | (divided ? 2 : 0) | (died ? 4 : 0) | ((ev[3] == ev[3]) ? 8 : 0) | (spawn ? 16 : 0);
+        int fl = (ok ? 1 : 0) | (divided ? 2 : 0) | (died ? 4 : 0) | ((ev[3] == ev[3]) ? 8 : 0) | (spawn ? 16 : 0);
+#if CP_STORED
+        if (overflow) fl |= 32;  // more steps than the store holds (cellpop_launch reports it)
+#endif
+        a.flags[slot] = fl;
         for (int k = 0; k < 5; k++) a.event_times[(size_t)slot * 5 + k] = ev[k];
         a.nsteps[slot] = nst;
     }

@@ -28,6 +28,7 @@ struct CpStatic {
     const double* output_times;
     int32_t n_data;
     const bcm3hip_cellpop_data* data;  // device copy; observed / entry point to device arrays
+    bcm3hip_value_ref sync_offset;     // synchronization_time_offset (cp_init_kernel -> sync_off[slot])
 };
 
 // one work item = one new cell: slot, eval, parent slot (-1 = initial cell), sobol index, flags
@@ -37,7 +38,7 @@ struct CpInitItem {
 
 hipError_t launch_cp_init(const CpStatic& m, int32_t n_items, const CpInitItem* items, const double* values,
                           double* params, double* y0, double* creation, const double* end_y, const double* achieved,
-                          hipStream_t s);
+                          double* sync_off, hipStream_t s);
 hipError_t launch_cp_popavg(const CpStatic& m, int32_t n, const double* values, const int32_t* ncells,
                             const int32_t* failed, const double* out_values, const double* creation,
                             const double* sim_end, double* avg, const double* tc_logp, const int32_t* tc_ok,

@@ -109,6 +109,27 @@ std::vector<double> SobolPoints(size_t points, size_t dims)
 
 LikelihoodCellPopulation::LikelihoodCellPopulation(size_t sampling_threads, size_t evaluation_threads) {}
 
+// the synchronize attribute of time courses / time points (DataLikelihoodTimeCourse.cpp:27-41,
+// DataLikelihoodTimePoints.cpp:29-43)
+static bool parse_sync(const std::string& s, int32_t& sync)
+{
+    if (s.empty() || s == "none")
+        sync = BCM3HIP_CP_SYNC_NONE;
+    else if (s == "DNA_replication_start")
+        sync = BCM3HIP_CP_SYNC_DNA_REPLICATION_START;
+    else if (s == "PCNA_gfp_increase")
+        sync = BCM3HIP_CP_SYNC_PCNA_GFP_INCREASE;
+    else if (s == "mitosis" || s == "nuclear_envelope_breakdown")
+        sync = BCM3HIP_CP_SYNC_NUCLEAR_ENVELOPE_BREAKDOWN;
+    else if (s == "anaphase" || s == "anaphase_onset")
+        sync = BCM3HIP_CP_SYNC_ANAPHASE_ONSET;
+    else {
+        LOGERROR("Synchronization is specified as \"%s\" which is not a recognized synchronization point", s.c_str());
+        return false;
+    }
+    return true;
+}
+
 bool LikelihoodCellPopulation::ParseRef(const std::string& s, bcm3hip_value_ref& r) const
 {
     // ValueReference::Load (ValueReference.cpp:16-41): sampled variable, else a number
@@ -292,6 +313,24 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
         variability_cov.push_back(cov);
     }
     if (!ParseRef(ex.get("entry_time"), entry_time)) return false;
+    // synchronization_time_offset (Experiment::Initialize / PostInitialize, Experiment.cpp:172-185,
+    // 619): a sampled variable; a number is written to fixed_entry_time in the reference (so it
+    // replaces a constant entry time) and leaves the offset at 0
+    sync_offset = bcm3hip_value_ref{BCM3HIP_REF_NONE, -1, 0.0};
+    if (ex.has_attr("synchronization_time_offset") && !ex.get("synchronization_time_offset").empty()) {
+        const std::string so = ex.get("synchronization_time_offset");
+        const size_t ix = varset->GetVariableIndex(so, false);
+        double v;
+        if (ix != SIZE_MAX) {
+            sync_offset = bcm3hip_value_ref{BCM3HIP_REF_VARIABLE, (int32_t)ix, 0.0};
+        } else if (parse_double(so, v)) {
+            if (entry_time.kind == BCM3HIP_REF_FIXED) entry_time.value = v;
+        } else {
+            LOGERROR("Synchronization time offset was specified as \"%s\", but could not find variable and also could not cast it to a constant real value",
+                     so.c_str());
+            return false;
+        }
+    }
 
     // data (DataLikelihoodBase::Load, DataLikelihoodTimeCourseBase::Load,
     // DataLikelihoodTimeCoursePopulationAverage::Load); the sidecar holds the netCDF group
@@ -364,11 +403,7 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
         }
         if (d.kind == BCM3HIP_CP_DATA_TIME_COURSE) {
             // DataLikelihoodTimeCourse::Load (DataLikelihoodTimeCourse.cpp:27-41)
-            const std::string sync = dn->has_attr("synchronize") ? dn->get("synchronize") : std::string();
-            if (!(sync.empty() || sync == "none")) {
-                LOGERROR("cell_population: synchronized time courses (\"%s\") are not supported", sync.c_str());
-                return false;
-            }
+            if (!parse_sync(dn->has_attr("synchronize") ? dn->get("synchronize") : std::string(), d.sync)) return false;
             // missing_simulation_time_stdev (DataLikelihoodTimeCourseBase.cpp:93-110): a variable
             // or a number, 300 when absent
             d.missing_stdev = bcm3hip_value_ref{BCM3HIP_REF_FIXED, -1, 300.0};
@@ -520,15 +555,7 @@ bool LikelihoodCellPopulation::LoadTimePoints(const XmlNode& dn, DataLikelihood&
     }
     d.stdev_relative_to_scale = dn.get_bool("stdev_relative_to_scale", false) ? 1 : 0;
     d.only_nondivided = dn.get_bool("use_only_nondivided", false) ? 1 : 0;
-    const std::string sync = dn.has_attr("synchronize") ? dn.get("synchronize") : std::string();
-    if (!(sync.empty() || sync == "none")) {
-        if (sync == "DNA_replication_start" || sync == "PCNA_gfp_increase" || sync == "mitosis" ||
-            sync == "nuclear_envelope_breakdown" || sync == "anaphase" || sync == "anaphase_onset")
-            LOGERROR("cell_population: synchronized time points (\"%s\") are not supported", sync.c_str());
-        else
-            LOGERROR("Synchronization is specified as \"%s\" which is not a recognized synchronization point", sync.c_str());
-        return false;
-    }
+    if (!parse_sync(dn.has_attr("synchronize") ? dn.get("synchronize") : std::string(), d.sync)) return false;
     // data: time x cells (x markers)
     const Json* var = group.find(d.data_name);
     const Json* dims = var ? var->find("dims") : nullptr;
@@ -732,16 +759,25 @@ bool LikelihoodCellPopulation::PostInitialize()
         int ti;
         int species;
         int order;
+        int sync;
     };
     std::vector<TP> tps;
     for (size_t k = 0; k < data.size(); k++) {
-        if (data[k].kind == BCM3HIP_CP_DATA_TIME_POINTS) {
-            for (size_t o = 0; o < data[k].species_order.size(); o++)
-                for (size_t i = 0; i < data[k].times.size(); i++)
-                    tps.push_back(TP{(int)k, data[k].times[i], (int)i, data[k].species_order[o], (int)o});
-            continue;
+        const DataLikelihood& d = data[k];
+        if (d.kind == BCM3HIP_CP_DATA_TIME_POINTS) {
+            for (size_t o = 0; o < d.species_order.size(); o++)
+                for (size_t i = 0; i < d.times.size(); i++)
+                    tps.push_back(TP{(int)k, d.times[i], (int)i, d.species_order[o], (int)o, d.sync});
+        } else {
+            for (size_t i = 0; i < d.times.size(); i++) tps.push_back(TP{(int)k, d.times[i], (int)i, d.species_ix, 0, d.sync});
         }
-        for (size_t i = 0; i < data[k].times.size(); i++) tps.push_back(TP{(int)k, data[k].times[i], (int)i, data[k].species_ix, 0});
+        // a synchronised course also simulates its full duration, for negative time points
+        // (DataLikelihoodTimeCourse.cpp:192-199, DataLikelihoodTimePoints.cpp:190-197): an entry
+        // without species
+        if (d.sync != BCM3HIP_CP_SYNC_NONE && !d.times.empty()) {
+            const double last_tp = d.times.back(), full_duration = last_tp - d.times.front();
+            if (full_duration > last_tp) tps.push_back(TP{(int)k, full_duration, -1, -1, 0, d.sync});
+        }
     }
     std::stable_sort(tps.begin(), tps.end(), [](const TP& a, const TP& b) { return a.t < b.t; });
     if (tps.empty()) {
@@ -750,6 +786,7 @@ bool LikelihoodCellPopulation::PostInitialize()
     }
     output_times.clear();
     output_species.clear();
+    output_sync.clear();
     std::vector<std::vector<int32_t>> order_entry(data.size());  // time points: [order][T]
     for (size_t k = 0; k < data.size(); k++) {
         data[k].entry.assign(data[k].times.size(), -1);
@@ -758,6 +795,8 @@ bool LikelihoodCellPopulation::PostInitialize()
     for (size_t k = 0; k < tps.size(); k++) {
         output_times.push_back(tps[k].t);
         output_species.push_back(tps[k].species);
+        output_sync.push_back(tps[k].sync);
+        if (tps[k].ti < 0) continue;
         DataLikelihood& d = data[tps[k].dl];
         if (d.kind == BCM3HIP_CP_DATA_TIME_POINTS)
             order_entry[tps[k].dl][(size_t)tps[k].order * d.times.size() + tps[k].ti] = (int32_t)k;
@@ -902,6 +941,8 @@ bool LikelihoodCellPopulation::PostInitialize()
     model.constant_species = constant_init.data();
     model.output_times = output_times.data();
     model.output_species = output_species.data();
+    model.output_sync = output_sync.data();
+    model.sync_offset = sync_offset;
     model.rtol = rtol;
     model.atol = atol;
     model.hmin = hmin;

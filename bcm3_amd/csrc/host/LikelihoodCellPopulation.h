@@ -7,18 +7,20 @@
 // Supported (the reference's options this path uses): one or more <experiment>s (their
 // log-likelihoods summed in order, CellPopulationLikelihood.cpp:82-101), each with model_file, data_file
 // (netCDF classic, or a JSON sidecar with the netCDF group's variables), num_cells, max_cells,
-// divide_cells, entry_time, trailing_simulation_time, simulate_past_chromatid_separation_time,
+// divide_cells, entry_time, synchronization_time_offset, trailing_simulation_time,
+// simulate_past_chromatid_separation_time,
 // solver_* settings (solver_type CVODE); <set_parameter>; <cell_variability
 // distribution="diagonal_gaussian">; <treatment_trajectory type="pulses">; <data> of type
 // "time_course_population_average" or "time_course" (the default type; single cells matched to
-// the simulated cells, no observed lineage, no synchronisation) with the normal / additive_normal /
+// the simulated cells, no observed lineage; synchronize= any of the reference's points, on stored
+// integration points) with the normal / additive_normal /
 // proportional_normal / additive_proportional_normal / student_t4 error models, stdev /
 // proportional_stdev / offset / scale / stdev_relative_to_scale / weight / relative_to_time_average /
 // missing_simulation_time_stdev, and the cellpop.use_only_cell_ix option; <data type="time_points">
 // (DataLikelihoodTimePoints: cells matched at every time point, ";"-separated species columns, "+"
 // sums, 2-D or 3-D data, value_relative_to_timepoint_ix, use_only_nondivided; normal / student_t4).
-// Not built: the duration likelihood (the reference's reads past its matrix), synchronised time
-// courses / time points, the DP5 solver, full_gaussian variability, non-sampled parameters.
+// Not built: the duration likelihood (the reference's reads past its matrix), the DP5 solver,
+// observed lineages, non-sampled parameters.
 #pragma once
 #include <memory>
 #include <string>
@@ -55,6 +57,7 @@ private:
         int32_t error_model = 0;
         int32_t relative_to_time_average = 0;
         int32_t kind = BCM3HIP_CP_DATA_POPULATION_AVERAGE, stdev_relative_to_scale = 0;
+        int32_t sync = BCM3HIP_CP_SYNC_NONE;  // synchronize (BCM3HIP_CP_SYNC_*)
         bcm3hip_value_ref missing_stdev{};
         std::vector<int32_t> entry;
         // time points (DataLikelihoodTimePoints): observed [R][T][MK]; column l sums the species
@@ -75,7 +78,7 @@ private:
     int32_t max_steps = 10000, num_cells = 1, max_cells = 20;
     bool divide_cells = true;
     double trailing = 0, past_cs = 0;
-    bcm3hip_value_ref entry_time{};
+    bcm3hip_value_ref entry_time{}, sync_offset{};
     struct VarVariable {
         std::string species, parameter;
         bool entry_time = false, negate = false, only_initial = false;
@@ -92,7 +95,7 @@ private:
     std::vector<DataLikelihood> data;
 
     // flat device model and its arrays
-    std::vector<int32_t> transforms, output_species, reset_index;
+    std::vector<int32_t> transforms, output_species, output_sync, reset_index;
     std::vector<double> y_init, constant_init, output_times, reset_value, sobol;
     std::vector<bcm3hip_value_ref> scales;
     std::vector<bcm3hip_variability_action> actions;

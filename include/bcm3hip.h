@@ -292,7 +292,19 @@ typedef struct {
     const int32_t* full_groups;          /* [n_full][2]: first sobol dimension, D */
     const bcm3hip_value_ref* covariance; /* the full groups' D(D-1)/2 references each, in order, entry
                                             (i-1)i/2 + k of a group for the pair (k, i), k < i */
+    /* synchronised time courses / time points (<data synchronize="...">, Experiment.cpp:265-292,
+     * Cell.cpp:280-390): output_sync[M] is the ESynchronizeCellTrajectory of each entry
+     * (BCM3HIP_CP_SYNC_*); NULL or every entry BCM3HIP_CP_SYNC_NONE: no synchronisation. With any
+     * entry synchronised every cell stores its integration points (Cell.cpp:152, 232-233): event
+     * times are bisections of the step's interpolant, a dividing cell ends at its interpolated
+     * division time and state, and every entry's value is read from the stored steps
+     * (ODESolverCVODE::GetInterpolatedY, ODESolverCVODE.cpp:183-242) at data time + sync_offset +
+     * the cell's event time (none: - creation time). */
+    const int32_t* output_sync;
+    bcm3hip_value_ref sync_offset;  /* synchronization_time_offset (a sampled variable; NONE = 0) */
 } bcm3hip_cellpop_model;
+enum { BCM3HIP_CP_SYNC_DNA_REPLICATION_START = 0, BCM3HIP_CP_SYNC_PCNA_GFP_INCREASE = 1,
+       BCM3HIP_CP_SYNC_NUCLEAR_ENVELOPE_BREAKDOWN = 2, BCM3HIP_CP_SYNC_ANAPHASE_ONSET = 3, BCM3HIP_CP_SYNC_NONE = 4 };
 
 /* Per-cell results of the last evaluation (bcm3hip_cellpop_cells), one record per cell slot. */
 typedef struct {

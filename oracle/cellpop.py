@@ -48,7 +48,15 @@ class CellIn(C.Structure):
                 ("ev_replicating", C.c_int), ("ev_replicated", C.c_int), ("ev_pcna", C.c_int),
                 ("ev_nuclear_envelope", C.c_int), ("ev_chromatid_separation", C.c_int), ("ev_cytokinesis", C.c_int),
                 ("ev_apoptosis", C.c_int), ("n_constant", C.c_int), ("n_treat", C.c_int), ("treat_cs", C.c_void_p),
-                ("treat_off", C.c_void_p), ("treat_times", C.c_void_p)]
+                ("treat_off", C.c_void_p), ("treat_times", C.c_void_p), ("stored", C.c_int),
+                ("output_sync", C.c_void_p), ("sync_offset", C.c_double)]
+
+
+# ESynchronizeCellTrajectory (Experiment.h:21-27) of the synchronize attribute
+# (DataLikelihoodTimeCourse.cpp:27-41, DataLikelihoodTimePoints.cpp:29-43)
+SYNC_NONE = 4
+_SYNC = {"": SYNC_NONE, "none": SYNC_NONE, "DNA_replication_start": 0, "PCNA_gfp_increase": 1, "mitosis": 2,
+         "nuclear_envelope_breakdown": 2, "anaphase": 3, "anaphase_onset": 3}
 
 
 class CellOut(C.Structure):
@@ -228,7 +236,9 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
         data = json.load(f)[e["name"]]
     dls = []
     timepoints = []  # Experiment::simulation_timepoints: (dl index, time, time_ix, species_ix)
+    tp_sync = []     # their synchronisation point
     for dl in ex.iter("data"):
+        sync = _SYNC[dl.get("synchronize", "")] if kind_of(dl) != "time_course_population_average" else SYNC_NONE
         kind = dl.get("type", "time_course")  # DataLikelihoodBase::Create (DataLikelihoodBase.cpp:22)
         assert kind in ("time_course_population_average", "time_course", "time_points"), kind
         var = data[dl.get("data_name")]
@@ -238,6 +248,8 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
             for six in d["species_order"]:
                 for ti, t in enumerate(d["times"]):
                     timepoints.append((len(dls), t, ti, six))
+                    tp_sync.append(sync)
+            _full_duration(timepoints, tp_sync, len(dls), d["times"], sync)
             dls.append(d)
             continue
         tdim = var["dims"][0]
@@ -257,7 +269,6 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
                 if use_only_cell_ix != "-1":
                     obs = obs[[int(t) for t in use_only_cell_ix.split(",")]]
             assert e["max_cells"] == obs.shape[0], "max_cells must equal the observed cells (.cpp:174-183)"
-            assert (dl.get("synchronize", "") or "none") == "none"
         else:
             if obs.ndim == 1:
                 obs = obs[:, None]
@@ -283,13 +294,29 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
                  relative_to_time_average=_bool(dl.get("relative_to_time_average"), False))
         for ti, t in enumerate(times):
             timepoints.append((len(dls), t, ti, six))
+            tp_sync.append(sync)
+        _full_duration(timepoints, tp_sync, len(dls), times, sync)
         dls.append(d)
     # bubble sort by time (stable), Experiment.cpp:593-600
-    timepoints.sort(key=lambda x: x[1])
+    order = sorted(range(len(timepoints)), key=lambda k: timepoints[k][1])
     e["data"] = dls
-    e["timepoints"] = timepoints
+    e["timepoints"] = [timepoints[k] for k in order]
+    e["timepoint_sync"] = [tp_sync[k] for k in order]
+    # any synchronised entry: every cell stores its integration points (Experiment.cpp:119-121)
+    e["stored"] = any(x != SYNC_NONE for x in e["timepoint_sync"])
     e["output_times"] = sorted(t[1] for t in timepoints)
     e["entry_time"] = _ref_value(ex.get("entry_time"), variables)
+    # synchronization_time_offset (Experiment.cpp:172-185): a variable, or a number that the
+    # reference writes to fixed_entry_time (replacing a constant entry time), the offset staying 0
+    e["sync_offset"] = ("fixed", 0.0)
+    so = ex.get("synchronization_time_offset", "")
+    if so:
+        if so in variables:
+            e["sync_offset"] = ("var", variables.index(so))
+        else:
+            v = float(so)
+            if e["entry_time"][0] == "fixed":
+                e["entry_time"] = ("fixed", v)
     # derivative code (SBMLModel::GenerateCode) for the host copy
     e["derivative_body"] = model.generate_derivative(variables, forced)
     e["deriv_lib"] = compile_derivative(e["derivative_body"], variant)
@@ -309,6 +336,21 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
     e["y_init"] = np.array([model.species[s]["initial"] for s in model.ode])
     e["constant_init"] = np.array([model.species[s]["initial"] for s in model.constant])
     return e
+
+
+def kind_of(dl):
+    return dl.get("type", "time_course")
+
+
+def _full_duration(timepoints, tp_sync, dli, times, sync):
+    """a synchronised time course / time points also simulates its full duration, for negative
+    time points (DataLikelihoodTimeCourse.cpp:192-199, DataLikelihoodTimePoints.cpp:190-197): an
+    entry without species"""
+    if sync != SYNC_NONE and times:
+        full_duration = times[-1] - times[0]
+        if full_duration > times[-1]:
+            timepoints.append((dli, full_duration, -1, -1))
+            tp_sync.append(sync)
 
 
 def _load_time_points(dl, data, var, model, variables, max_cells, use_only_cell_ix):
@@ -375,7 +417,7 @@ def notify_time_points(e, dli, values):
     d = e["data"][dli]
     traj = np.full((e["max_cells"], len(d["times"]), d["columns"]), np.nan)
     for k, (tdl, t, ti, six) in enumerate(e["timepoints"]):
-        if tdl != dli:
+        if tdl != dli or ti < 0:
             continue
         for c in range(len(values)):
             x = values[c][k]
@@ -528,6 +570,8 @@ def simulate_experiment(e, prob, values):
     t_cs = np.array([t[0] for t in treats] or [0], dtype=np.int32)
     t_off = np.array([0] + list(np.cumsum([len(t[1]) for t in treats])), dtype=np.int32)
     t_times = np.array([x for t in treats for x in t[1]] or [0.0], dtype=float)
+    out_sync = np.array(e.get("timepoint_sync", [SYNC_NONE] * M), dtype=np.int32)
+    sync_offset = _refval(e.get("sync_offset", ("fixed", 0.0)), tv)
     cells = []  # dicts
     fail = False
 
@@ -587,6 +631,9 @@ def simulate_experiment(e, prob, values):
         cin.treat_cs = t_cs.ctypes.data
         cin.treat_off = t_off.ctypes.data
         cin.treat_times = t_times.ctypes.data
+        cin.stored = 1 if e.get("stored") else 0
+        cin.output_sync = out_sync.ctypes.data
+        cin.sync_offset = sync_offset
         cout = CellOut()
         vals = np.empty(M)
         end_y = np.empty(N)
@@ -612,6 +659,8 @@ def simulate_experiment(e, prob, values):
     trajs = [np.full((e["max_cells"], len(d["times"])) + ((d["columns"],) if d["kind"] == "time_points" else ()), np.nan)
              for d in e["data"]]
     for k, (dli, t, ti, six) in enumerate(e["timepoints"]):
+        if ti < 0:
+            continue
         alive = [c for c in cells if 0.0 <= t - c["creation"] <= c["sim_end"]]
         pop = len(alive)
         d = e["data"][dli]
@@ -620,7 +669,8 @@ def simulate_experiment(e, prob, values):
             if x == x:
                 if d["kind"] == "time_points":
                     continue
-                avgs[dli][ti, 0] += x / pop
+                if d["kind"] == "time_course_population_average":
+                    avgs[dli][ti, 0] += x / pop
                 trajs[dli][c["index"], ti] = x
     for dli, d in enumerate(e["data"]):
         if d["kind"] == "time_points" and cells:

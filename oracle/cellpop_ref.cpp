@@ -14,7 +14,11 @@
  * register no analytic Jacobian, Cell.cpp:57-76), the ONE_STEP driver of ODESolverCVODE::Solve
  * (:322-463) with SolveReturnSolution (ODESolver.cpp:93-134), Cell::Simulate (Cell.cpp:193-273)
  * and Cell::integration_step_cb (:463-538) with get_threshold_crossing_time (ODESolverCVODE.cpp:
- * 264-320) in the non-stored mode a cell population without synchronisation runs in.
+ * 264-320) in the non-stored mode a cell population without synchronisation runs in, and the stored
+ * mode of synchronised data (ODESolver::SolveStoreIntegrationPoints, ODESolver.cpp:136-150; the
+ * CVodeTimepoint records of ODESolverCVODE::Solve, :375-401; GetInterpolatedY's iterator, :176-242;
+ * the division / death interpolation of Cell.cpp:499-529 and the evaluation passes of
+ * Experiment.cpp:265-292 with Cell::GetInterpolatedSpeciesValue, Cell.cpp:280-327).
  * N_Vector: the vendored nvector_serial stands in for nvector_serial_eigen.cpp (same formulas).
  * The cell right-hand side is the generated derivative (oracle/sbml_codegen.py) compiled for the
  * host and passed in as a function pointer.
@@ -31,6 +35,7 @@
 
 #include "EigenPartialPivLUSomewhatSparse.h"
 
+#include <cfloat>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -69,6 +74,10 @@ typedef struct {
     const int* treat_cs;
     const int* treat_off;
     const double* treat_times;
+    // synchronised data: store the integration points (Cell::Initialize's calculate_synchronization_points)
+    int stored;
+    const int* output_sync;  // [M] ESynchronizeCellTrajectory of each output (4 = None)
+    double sync_offset;      // Experiment's time_offset
 } cp_cell_in;
 
 typedef struct {
@@ -134,10 +143,64 @@ SUNLinearSolver make_ls(int N)
     return S;
 }
 
+// one CVodeTimepoint (ODESolverCVODE.h): the step's return time, tn, h, hu, q and zn[0..q]
+struct Record {
+    double time, tn, h, hu;
+    int q;
+    std::vector<double> zn;  // [(q + 1) * N], zn[j * N + i]
+};
+
+// the interpolation iterator of ODESolverCVODE (RestartInterpolationIteration / GetInterpolatedY)
+struct Interp {
+    size_t iter = 0;
+    double itime = std::numeric_limits<double>::quiet_NaN();
+    std::vector<double> y;
+    void restart(int N)
+    {
+        y.assign(N, 0.0);
+        iter = 0;
+        itime = std::numeric_limits<double>::quiet_NaN();
+    }
+    const std::vector<double>& get(const std::vector<Record>& recs, int N, double t)
+    {
+        if (t == itime) return y;
+        while (iter < recs.size()) {
+            if (recs[iter].time > t) break;
+            iter++;
+        }
+        if (iter == recs.size()) {
+            itime = std::numeric_limits<double>::quiet_NaN();
+            y.assign(N, std::numeric_limits<double>::quiet_NaN());
+            return y;
+        }
+        itime = t;
+        const Record& r = recs[iter];
+        double tfuzz = 100.0 * DBL_EPSILON * (fabs(r.tn) + fabs(r.hu));
+        if (r.hu < 0.0) tfuzz = -tfuzz;
+        const double tp = r.tn - r.hu - tfuzz;
+        const double tn1 = r.tn + tfuzz;
+        if ((t - tp) * (t - tn1) > 0.0) {
+            y.assign(N, std::numeric_limits<double>::quiet_NaN());
+            return y;
+        }
+        const double s = (t - r.tn) / r.h;
+        y.assign(N, 0.0);
+        for (int j = r.q; j >= 0; j--) {
+            double cval = 1.0;
+            for (int i = 0; i < j; i++) cval *= s;
+            for (int i = 0; i < N; i++) y[i] += cval * r.zn[(size_t)j * N + i];
+        }
+        return y;
+    }
+};
+
 struct Cell {
     const cp_cell_in* in;
     int N;
     void* mem;
+    std::vector<Record> recs;  // stored mode
+    Interp interp;
+    std::vector<double> end_y;  // stored mode: simulation_end_y at a division / death
     std::vector<double> y_copy, work;
     std::vector<double> cs;  // constant_species_y with the treatment concentrations
     // Cell / ODESolver state
@@ -260,40 +323,83 @@ double threshold_crossing_time(const Cell* c, double threshold, bool above, doub
     return time;
 }
 
-// Cell::integration_step_cb (Cell.cpp:463-538), non-stored branch
+// get_threshold_crossing_time with stored integration points (ODESolverCVODE.cpp:264-320): ten
+// bisection steps on the polynomial of the step just taken (the last record)
+double threshold_crossing_time_stored(const Cell* c, int species, double threshold, bool above, double prev_time)
+{
+    const Record& r = c->recs.back();
+    double dt = (c->t - prev_time) * 0.5;
+    double time = prev_time + dt;
+    for (int iter = 0; iter < 10; iter++) {
+        const double s = (time - r.tn) / r.h;
+        double x = 0.0;
+        for (int j = r.q; j >= 0; j--) {
+            double cval = 1.0;
+            for (int i = 0; i < j; i++) cval *= s;
+            x += cval * r.zn[(size_t)j * c->N + species];
+        }
+        dt *= 0.5;
+        if (above) {
+            if (x > threshold) time -= dt; else time += dt;
+        } else {
+            if (x < threshold) time -= dt; else time += dt;
+        }
+    }
+    return time;
+}
+
+double crossing(Cell* c, int species, double threshold, bool above)
+{
+    return c->in->stored ? threshold_crossing_time_stored(c, species, threshold, above, c->previous_integration_step_time)
+                         : threshold_crossing_time(c, threshold, above, c->previous_integration_step_time);
+}
+
+// Cell::integration_step_cb (Cell.cpp:463-538)
 bool step_cb(Cell* c, double t, const double* y, double& end_time)
 {
     const cp_cell_in* in = c->in;
     bool cont = true;
     if (in->ev_replicating >= 0 && c->ev[0] != c->ev[0]) {
-        if (y[in->ev_replicating] > 1e-4) c->ev[0] = threshold_crossing_time(c, 1e-4, true, c->previous_integration_step_time);
+        if (y[in->ev_replicating] > 1e-4) c->ev[0] = crossing(c, in->ev_replicating, 1e-4, true);
     }
     if (in->ev_replicated >= 0 && c->ev[1] != c->ev[1]) {
-        if (y[in->ev_replicated] > 1.95) c->ev[1] = threshold_crossing_time(c, 1.95, true, c->previous_integration_step_time);
+        if (y[in->ev_replicated] > 1.95) c->ev[1] = crossing(c, in->ev_replicated, 1.95, true);
     }
     if (in->ev_pcna >= 0 && c->ev[2] != c->ev[2]) {
-        if (y[in->ev_pcna] > 0.5) c->ev[2] = threshold_crossing_time(c, 0.5, true, c->previous_integration_step_time);
+        if (y[in->ev_pcna] > 0.5) c->ev[2] = crossing(c, in->ev_pcna, 0.5, true);
     }
     if (in->ev_nuclear_envelope >= 0 && c->ev[3] != c->ev[3]) {
-        if (y[in->ev_nuclear_envelope] < 0.5) c->ev[3] = threshold_crossing_time(c, 0.5, false, c->previous_integration_step_time);
+        if (y[in->ev_nuclear_envelope] < 0.5) c->ev[3] = crossing(c, in->ev_nuclear_envelope, 0.5, false);
     }
     if (in->ev_chromatid_separation >= 0 && c->ev[4] != c->ev[4]) {
         if (y[in->ev_chromatid_separation] > 1e-3) {
-            c->ev[4] = threshold_crossing_time(c, 1e-3, true, c->previous_integration_step_time);
+            c->ev[4] = crossing(c, in->ev_chromatid_separation, 1e-3, true);
             c->simulation_end_time = std::max(c->simulation_end_time, c->ev[4] + in->simulate_past_chromatid_separation_time);
             end_time = c->simulation_end_time;
         }
     }
     if (in->divide_cells && in->ev_cytokinesis >= 0) {
         if (y[in->ev_cytokinesis] > 1.0) {
-            c->simulation_end_time = t;
+            if (in->stored) {
+                const double division_time = crossing(c, in->ev_cytokinesis, 1.0, true);
+                c->simulation_end_time = division_time;
+                c->end_y = c->interp.get(c->recs, c->N, division_time);
+            } else {
+                c->simulation_end_time = t;
+            }
             c->divided = true;
             cont = false;
         }
     }
     if (in->ev_apoptosis >= 0) {
         if (y[in->ev_apoptosis] > 1.0) {
-            c->simulation_end_time = t;
+            if (in->stored) {
+                const double death_time = crossing(c, in->ev_apoptosis, 1.0, true);
+                c->simulation_end_time = death_time;
+                c->end_y = c->interp.get(c->recs, c->N, death_time);
+            } else {
+                c->simulation_end_time = t;
+            }
             c->died = true;
             cont = false;
         }
@@ -336,14 +442,23 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
     // SolveReturnSolution (ODESolver.cpp:93-134)
     int ti = 0;
     bool solve = true;
-    while (ti < M && tp[ti] < std::numeric_limits<double>::epsilon()) {
-        for (int i = 0; i < N; i++) sol[(size_t)ti * N + i] = in->y0[i];
-        ti++;
+    if (in->stored) {
+        // SolveStoreIntegrationPoints (ODESolver.cpp:136-141)
+        if (c.simulation_end_time <= std::numeric_limits<double>::epsilon()) {
+            solve = false;
+            result = false;
+        }
+    } else {
+        while (ti < M && tp[ti] < std::numeric_limits<double>::epsilon()) {
+            for (int i = 0; i < N; i++) sol[(size_t)ti * N + i] = in->y0[i];
+            ti++;
+        }
+        if (ti == M) solve = false;
     }
-    if (ti == M) solve = false;
     long nst = 0;
     if (solve) {
-        double end_time = tp[M - 1];
+        double end_time = in->stored ? c.simulation_end_time : tp[M - 1];
+        c.interp.restart(N);
         N_Vector y = N_VNew_Serial(N), atol = N_VNew_Serial(N), tmp = N_VNew_Serial(N);
         for (int i = 0; i < N; i++) {
             NV_Ith_S(y, i) = in->y0[i];
@@ -393,9 +508,26 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
                 break;
             }
             c.t = tret;
+            if (in->stored) {
+                if (current_step >= in->max_steps) {  // "CVODE integration timepoint storage buffer too small"
+                    result = false;
+                    break;
+                }
+                CVodeMem cvm = (CVodeMem)mem;
+                Record r;
+                r.time = c.t;
+                r.tn = cvm->cv_tn;
+                r.h = cvm->cv_h;
+                r.hu = cvm->cv_hu;
+                r.q = cvm->cv_q;
+                r.zn.assign((size_t)(r.q + 1) * N, 0.0);
+                for (int j = r.q; j >= 0; j--)
+                    for (int i = 0; i < N; i++) r.zn[(size_t)j * N + i] = NV_Ith_S(cvm->cv_zn[j], i);
+                c.recs.push_back(r);
+            }
             current_step++;
             // the reference reads past the output vector once all outputs are done; stop there
-            while (tpi < M && tret >= tp[tpi]) {
+            while (!in->stored && tpi < M && tret >= tp[tpi]) {
                 if (CVodeGetDky(mem, tp[tpi], 0, tmp) != CV_SUCCESS) {
                     result = false;
                     break;
@@ -434,10 +566,15 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
         CVodeGetNumNonlinSolvIters(mem, &out->nni);
         CVodeGetNumErrTestFails(mem, &out->netf);
         CVodeGetNumRhsEvals(mem, &out->nfe);
-        if (!c.divided && !c.died && result)
-            for (int i = 0; i < N; i++) end_y[i] = sol[(size_t)(M - 1) * N + i];
-        if (c.divided || c.died)
-            for (int i = 0; i < N; i++) end_y[i] = NV_Ith_S(y, i);
+        if (in->stored) {
+            // simulation_end_y: the interpolated division / death state, else the solver's y
+            for (int i = 0; i < N; i++) end_y[i] = (c.divided || c.died) ? c.end_y[i] : NV_Ith_S(y, i);
+        } else {
+            if (!c.divided && !c.died && result)
+                for (int i = 0; i < N; i++) end_y[i] = sol[(size_t)(M - 1) * N + i];
+            if (c.divided || c.died)
+                for (int i = 0; i < N; i++) end_y[i] = NV_Ith_S(y, i);
+        }
         CVodeFree(&mem);
         SUNNonlinSolFree(NLS);
         SUNLinSolFree(LS);
@@ -456,10 +593,33 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
     if (c.divided || c.died)
         achieved_cell_time = c.simulation_end_time;
     else
-        achieved_cell_time = tp[M - 1];
+        achieved_cell_time = in->stored ? c.previous_integration_step_time : tp[M - 1];
     out->sim_end = c.simulation_end_time;
     out->achieved_time = achieved_cell_time + in->creation_time;
     for (int k = 0; k < 5; k++) out->event_times[k] = c.ev[k];
+    if (in->stored) {
+        // the evaluation passes (Experiment.cpp:277-292): per synchronisation point in enum order the
+        // iterator restarted, the entries of that pass in time order, GetInterpolatedSpeciesValue
+        // (Cell.cpp:280-327) through the stored records
+        if (!result) return 1;
+        for (int p = 0; p <= 4; p++) {
+            c.interp.restart(N);
+            const double evp = p == 0 ? c.ev[0] : p == 1 ? c.ev[2] : p == 2 ? c.ev[3] : c.ev[4];
+            for (int k = 0; k < M; k++) {
+                const int s = in->output_species[k];
+                if (in->output_sync[k] != p || s < 0 || s >= N) continue;
+                const double time = in->output_times[k] + in->sync_offset;
+                double cell_time;
+                if (p == 4)
+                    cell_time = time - in->creation_time;
+                else
+                    cell_time = std::isnan(evp) ? time + c.simulation_end_time : time + evp;
+                if (cell_time < 0.0 || cell_time > c.simulation_end_time) continue;
+                out_values[k] = c.interp.get(c.recs, N, cell_time)[s];
+            }
+        }
+        return 0;
+    }
     // GetInterpolatedSpeciesValue (Cell.cpp:280-360), species without synchronisation
     for (int k = 0; k < M; k++) {
         const int s = in->output_species[k];

@@ -156,7 +156,10 @@ def test_loader_accepts_time_course(tmp_path):
     for data_xml, kw in ((TC, {}), (TC.replace("pcna_cells", "pcna_cell0"), dict(num_cells=1, max_cells=1)),
                          (TC.replace("pcna_cells", "pcna_cells_markers"), {}),
                          (TC.replace('stdev="stdev"', 'stdev="stdev" type="time_course" synchronize="none" '
-                                     'missing_simulation_time_stdev="stdev" error_model="t4" weight="0.5"'), {})):
+                                     'missing_simulation_time_stdev="stdev" error_model="t4" weight="0.5"'), {}),
+                         (TC.replace("/>", ' synchronize="mitosis"/>'), {}),
+                         (TC.replace("/>", ' synchronize="DNA_replication_start"/>'),
+                          dict(experiment_attrs=' divide_cells="false" synchronization_time_offset="k_D"'))):
         _lik(tc_likelihood(tmp_path, data_xml, **kw)).close()
     _lik(tc_likelihood(tmp_path, TC, num_cells=3, max_cells=3), "backend=none;cellpop.use_only_cell_ix=4,0,9").close()
 
@@ -164,7 +167,6 @@ def test_loader_accepts_time_course(tmp_path):
 @pytest.mark.parametrize("data_xml,kw,options", [
     (TC, dict(max_cells=20), None),                                       # more simulated than observed cells
     (TC, dict(max_cells=8, num_cells=8), None),                           # fewer
-    (TC.replace("/>", ' synchronize="mitosis"/>'), {}, None),             # synchronised time course
     (TC.replace("/>", ' synchronize="bogus"/>'), {}, None),
     (TC.replace("/>", ' use_log_ratio="true"/>'), {}, None),
     (TC.replace("/>", ' saturation_scale="2"/>'), {}, None),

@@ -94,14 +94,14 @@ def test_loader_accepts_time_points(tmp_path):
                          (_tp(data_name="pcna_cells_markers", species_name="PCNA_gfp; CycB+CycD", stdev="stdev;0.5"), {}),
                          (_tp(value_relative_to_timepoint_ix="3", synchronize="none"), {}),
                          (_tp(use_only_nondivided="true"), dict(num_cells=4, max_cells=32, experiment_attrs="")),
-                         (TP + TC, {})):
+                         (TP + TC, {}), (_tp(synchronize="mitosis"), {}),
+                         (_tp(synchronize="anaphase_onset") + TC.replace("/>", ' synchronize="PCNA_gfp_increase"/>'), {})):
         _loader_ok(tmp_path, data_xml, **kw)
     _loader_ok(tmp_path, TP, "backend=none;cellpop.use_only_cell_ix=4,0,9", num_cells=3, max_cells=3)
 
 
 @pytest.mark.parametrize("data_xml,kw,options", [
     (_tp(error_model="proportional_normal", proportional_stdev="0.1"), {}, None),  # NaN in the reference
-    (_tp(synchronize="mitosis"), {}, None),
     (_tp(synchronize="bogus"), {}, None),
     (_tp(species_name="PCNA_gfp/CycB"), {}, None),                        # division of species
     (_tp(species_name="mitogen_missing"), {}, None),
