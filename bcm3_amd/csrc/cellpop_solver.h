@@ -1117,6 +1117,78 @@ BDF_INL double crossing_time_stored(const S& s, double t, double prev, double th
     return time;
 }
 
+// ---- solver_type="DP5" (ODESolverDP5, src/odecommon/ODESolverDP5.cpp) ------------------------------
+#ifndef CP_DP5
+#define CP_DP5 0
+#endif
+static_assert(!(CP_DP5 && CP_STORED), "the DP5 solver has no stored integration points");
+// the largest of the components' values, NaN ignored (std::max(maxdiff, diff) from -inf in component
+// order keeps the first of equal values and skips NaN: the maximum of the non-NaN values, exact in
+// any order), uniform over the row
+BDF_INL double row_max_nonnan(double v)
+{
+    double m = (lane() < CP_NS && v == v) ? v : -__builtin_inf();
+    if constexpr (ROW == 16) {
+        cfor<0, 4>([&](auto r) __attribute__((always_inline)) {
+            const double o = shr_d<(1 << CI(r))>(m, -__builtin_inf());
+            m = (m < o) ? o : m;
+        });
+        return rbc<15>(m);
+    } else {
+        for (int k = 0; k < CP_NS; k++) {
+            const double o = bcast(m, k);
+            m = (m < o) ? o : m;
+        }
+        return m;
+    }
+}
+
+// ODESolverDP5::ApplyRK (ODESolverDP5.cpp:327-412): the stages k1..k6, the 5th-order solution ytmp,
+// FSAL k6, and the error ratio max_i |err_i| / (atol + rtol |ytmp_i + k6_i dt|); lane i = component i
+struct Dp5 {
+    double yn, ytmp, k0, k1, k2, k3, k4, k5, k6;
+};
+template <int NS, int NP, int NC, class SH>
+BDF_INL double dp5_apply_rk(SH& sh, Dp5& s, double t, double dt, double rtol, double atol)
+{
+    s.ytmp = s.yn + dt * 0.2 * s.k0;
+    s.k1 = rhs_v<NS, NP, NC>(sh, s.ytmp, t + 0.2 * dt);
+    s.ytmp = s.yn + dt * (+0.075 * s.k0 + 0.225 * s.k1);
+    s.k2 = rhs_v<NS, NP, NC>(sh, s.ytmp, t + 0.3 * dt);
+    s.ytmp = s.yn + dt * (+0.97777777777777777777777777777778 * s.k0 - 3.7333333333333333333333333333333 * s.k1 +
+                          3.5555555555555555555555555555556 * s.k2);
+    s.k3 = rhs_v<NS, NP, NC>(sh, s.ytmp, t + 0.8 * dt);
+    s.ytmp = s.yn + dt * (+2.9525986892242036274958085657674 * s.k0 - 11.595793324188385916780978509374 * s.k1 +
+                          9.8228928516994360615759792714525 * s.k2 - 0.29080932784636488340192043895748 * s.k3);
+    s.k4 = rhs_v<NS, NP, NC>(sh, s.ytmp, t + 0.88888888888888888888888888888889 * dt);
+    s.ytmp = s.yn + dt * (+2.8462752525252525252525252525253 * s.k0 - 10.757575757575757575757575757576 * s.k1 +
+                          8.9064227177434724604535925290642 * s.k2 + 0.27840909090909090909090909090909 * s.k3 -
+                          0.27353130360205831903945111492281 * s.k4);
+    s.k5 = rhs_v<NS, NP, NC>(sh, s.ytmp, t + dt);
+    s.ytmp = s.yn + dt * (+0.09114583333333333333333333333333 * s.k0 + 0.44923629829290206648697214734951 * s.k2 +
+                          0.65104166666666666666666666666667 * s.k3 - 0.32237617924528301886792452830189 * s.k4 +
+                          0.13095238095238095238095238095238 * s.k5);
+    s.k6 = rhs_v<NS, NP, NC>(sh, s.ytmp, t + dt);
+    double error = dt * (+0.00123263888888888888888888888889 * s.k0 - 0.00425277029050613956274333632824 * s.k2 +
+                         0.03697916666666666666666666666667 * s.k3 - 0.05086379716981132075471698113208 * s.k4 +
+                         0.04190476190476190476190476190476 * s.k5 - 0.025 * s.k6);
+    error = fabs(error);
+    const double D = atol + rtol * fabs(s.ytmp + s.k6 * dt);
+    return row_max_nonnan(error / D);
+}
+
+// Hairer's dense output of the step (ODESolverDP5.cpp:205-221; Hairer I, II.5 p179)
+BDF_INL double dp5_dense(const Dp5& s, double theta, double dt)
+{
+    const double thetaSq = theta * theta;
+    const double b1 = theta * (1.0 + theta * (-2.7854166666666669 + theta * (2.8861111111111111 + theta * (-1.0095486111111112))));
+    const double b3 = 33.33333333333333 * thetaSq * (0.11363881401617251 + theta * (-0.1682659478885894 + theta * 0.068104222821203958));
+    const double b4 = -2.5 * thetaSq * (0.675 + theta * (-1.8 + theta * (0.8645833333333333)));
+    const double b5 = 21.491745283018869 * thetaSq * (-0.012 + theta * (0.058666666666666666 + theta * (-0.06166666666666666)));
+    const double b6 = -3.1428571428571428 * thetaSq * (-0.3 + theta * (0.9666666666666666 + theta * (-0.7083333333333333)));
+    return s.yn + dt * (b1 * s.k0 + b3 * s.k2 + b4 * s.k3 + b5 * s.k4 + b6 * s.k5);
+}
+
 // GetInterpolatedY's time check on a record (tn, hu): false = "Time error for interpolation" (NaN)
 BDF_INL bool interp_time_ok(double t, double tn, double hu)
 {
@@ -1203,6 +1275,105 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
         solve = ti < M;
     }
     double yend = y0;
+#if CP_DP5
+    if (solve) {
+        // ODESolverDP5::Solve (ODESolverDP5.cpp:100-285) under SolveReturnSolution: the Solve resets
+        // every output, those before the cell's t = 0 + DBL_EPSILON included, to NaN (:103-105)
+        for (int k = ln; k < ti; k += ROW) outv[k] = __builtin_nan("");
+        double end_time = a.output_times[M - 1] - creation;
+        double t = 0.0, dt = 1.0;  // min(max_dt, 1.0), max_dt = solver_max_timestep = inf
+        Dp5 r;
+        r.yn = y0;
+        r.k0 = rhs_v<NS, NP, NC>(sh, r.yn, 0.0);
+        r.k1 = r.k2 = r.k3 = r.k4 = r.k5 = r.k6 = r.ytmp = 0.0;
+        int tpi = ti;
+        double next_out = a.output_times[tpi] - creation;
+        double ylast_out = __builtin_nan("");  // solver_output's last column (every component)
+        for (;;) {
+            double cur_dt = dt, next_dt = dt;
+            bool succeeded = false;
+            for (int att = 0; att < 10; att++) {
+                double maxdiff = dp5_apply_rk<NS, NP, NC>(sh, r, t, cur_dt, a.rtol, a.atol);
+                if (maxdiff != maxdiff || maxdiff == -__builtin_inf()) {
+                    ok = false;
+                    break;
+                }
+                // Hairer I, II.4 p167 (:152-184)
+                if (maxdiff > 1.1) {
+                    if (cur_dt == a.hmin) break;
+                    double scale = 0.9 * pow(maxdiff, -0.2);
+                    scale = (0.2 < scale) ? scale : 0.2;
+                    cur_dt *= scale;
+                    if (cur_dt < a.hmin) cur_dt = a.hmin;
+                } else if (maxdiff < 0.5) {
+                    maxdiff = (maxdiff < 1e-5) ? 1e-5 : maxdiff;
+                    double scale = 0.9 * pow(maxdiff, -0.2);
+                    scale = (5.0 < scale) ? 5.0 : scale;
+                    next_dt = cur_dt * scale;
+                    succeeded = true;
+                    break;
+                } else {
+                    next_dt = cur_dt;
+                    succeeded = true;
+                    break;
+                }
+            }
+            if (!ok) break;
+            if (!succeeded) {  // "Time step adaptation did not converge"
+                ok = false;
+                break;
+            }
+            // the outputs the step passed (:203-236): all done -> the step is not finished
+            const double target_t = t + cur_dt;
+            bool done = false;
+            while (target_t >= next_out) {
+                const double theta = (next_out - t) / cur_dt;
+                const double v = (theta >= 1.0) ? r.ytmp : dp5_dense(r, theta, cur_dt);
+                const int sp = a.output_species[tpi];
+                if (sp >= 0 && ln == sp) outv[tpi] = v;
+                if (tpi == M - 1) ylast_out = v;
+                tpi++;
+                if (tpi == M) {
+                    done = true;
+                    break;
+                }
+                next_out = a.output_times[tpi] - creation;
+            }
+            if (done) break;
+            r.k0 = r.k6;
+            r.yn = r.ytmp;
+            t += cur_dt;
+            nst++;
+            // Cell::integration_step_cb (Cell.cpp:463-538), its result ignored by the DP5 solver: DP5
+            // has no threshold crossings (get_threshold_crossing_time returns NaN, :322-327), so the
+            // event times stay NaN, max(simulation end, NaN + past) keeps the simulation end, and a
+            // division or death only moves the simulation end to the current step
+            if constexpr (CP_EV4 >= 0)
+                if (ev_value<CP_EV4>(r.yn) > 1e-3) end_time = sim_end;
+            if constexpr (CP_EV5 >= 0) {
+                if (a.divide_cells && ev_value<CP_EV5>(r.yn) > 1.0) {
+                    sim_end = t;
+                    yend = r.yn;
+                    divided = true;
+                }
+            }
+            if constexpr (CP_EV6 >= 0) {
+                if (ev_value<CP_EV6>(r.yn) > 1.0) {
+                    sim_end = t;
+                    yend = r.yn;
+                    died = true;
+                }
+            }
+            if (t >= end_time) break;
+            if (nst == a.max_steps) {
+                ok = false;
+                break;
+            }
+            dt = next_dt;
+        }
+        if (ok && !divided && !died) yend = ylast_out;
+    }
+#else
     if (solve) {
         GenState<NS> s;
         s.rtol = a.rtol;
@@ -1406,6 +1577,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
             }
         }
     }
+#endif
 #if CP_STORED
     // Experiment::EvaluateLogProbability's passes (Experiment.cpp:277-292): per synchronisation
     // point in enum order, the interpolation iterator restarted, the entries of that pass in

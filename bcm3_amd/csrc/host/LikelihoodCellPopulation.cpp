@@ -181,8 +181,13 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
     const std::string model_file = resolve(ex.get("model_file"), vm);
     const std::string data_file = ex.has_attr("data_file") ? ex.get("data_file") : std::string();
     const std::string solver_type = ex.has_attr("solver_type") ? ex.get("solver_type") : std::string("CVODE");
-    if (solver_type != "CVODE") {
-        LOGERROR("cell_population: solver_type \"%s\" is not supported (CVODE only)", solver_type.c_str());
+    // Cell::AllocateSolver (Cell.cpp:57-66)
+    if (solver_type == "DP5")
+        solver = BCM3HIP_CP_SOLVER_DP5;
+    else if (solver_type == "CVODE")
+        solver = BCM3HIP_CP_SOLVER_CVODE;
+    else {
+        LOGERROR("Unknown solver type \"%s\"; accepted options are \"DP5\" or \"CVODE\"", solver_type.c_str());
         return false;
     }
     const double feps4 = 4 * (double)std::numeric_limits<float>::epsilon();
@@ -943,6 +948,21 @@ bool LikelihoodCellPopulation::PostInitialize()
     model.output_species = output_species.data();
     model.output_sync = output_sync.data();
     model.sync_offset = sync_offset;
+    model.solver = solver;
+    // DP5 (ODESolverDP5.cpp): GetInterpolatedY and get_threshold_crossing_time are not implemented in
+    // the reference (NaN, ASSERT compiled out), so synchronised data would read NaN everywhere; its
+    // discontinuity handling (:123-135, 239-254) is not built here
+    if (solver == BCM3HIP_CP_SOLVER_DP5) {
+        for (int32_t x : output_sync)
+            if (x != BCM3HIP_CP_SYNC_NONE) {
+                LOGERROR("cell_population: synchronised data with solver_type DP5 (the reference's DP5 solver does not implement GetInterpolatedY) is not supported");
+                return false;
+            }
+        if (!treat_species.empty()) {
+            LOGERROR("cell_population: treatment trajectories with solver_type DP5 are not supported");
+            return false;
+        }
+    }
     model.rtol = rtol;
     model.atol = atol;
     model.hmin = hmin;

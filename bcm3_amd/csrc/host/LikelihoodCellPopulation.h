@@ -9,7 +9,7 @@
 // (netCDF classic, or a JSON sidecar with the netCDF group's variables), num_cells, max_cells,
 // divide_cells, entry_time, synchronization_time_offset, trailing_simulation_time,
 // simulate_past_chromatid_separation_time,
-// solver_* settings (solver_type CVODE); <set_parameter>; <cell_variability
+// solver_* settings (solver_type CVODE or DP5); <set_parameter>; <cell_variability
 // distribution="diagonal_gaussian">; <treatment_trajectory type="pulses">; <data> of type
 // "time_course_population_average" or "time_course" (the default type; single cells matched to
 // the simulated cells, no observed lineage; synchronize= any of the reference's points, on stored
@@ -19,8 +19,8 @@
 // missing_simulation_time_stdev, and the cellpop.use_only_cell_ix option; <data type="time_points">
 // (DataLikelihoodTimePoints: cells matched at every time point, ";"-separated species columns, "+"
 // sums, 2-D or 3-D data, value_relative_to_timepoint_ix, use_only_nondivided; normal / student_t4).
-// Not built: the duration likelihood (the reference's reads past its matrix), the DP5 solver,
-// observed lineages, non-sampled parameters.
+// Not built: the duration likelihood (the reference's reads past its matrix), DP5 with treatment
+// trajectories, observed lineages, non-sampled parameters.
 #pragma once
 #include <memory>
 #include <string>
@@ -76,6 +76,7 @@ private:
     std::map<std::string, double> forced;
     double rtol = 0, atol = 0, hmin = 0;
     int32_t max_steps = 10000, num_cells = 1, max_cells = 20;
+    int32_t solver = BCM3HIP_CP_SOLVER_CVODE;  // solver_type
     bool divide_cells = true;
     double trailing = 0, past_cs = 0;
     bcm3hip_value_ref entry_time{}, sync_offset{};

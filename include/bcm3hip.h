@@ -302,7 +302,11 @@ typedef struct {
      * the cell's event time (none: - creation time). */
     const int32_t* output_sync;
     bcm3hip_value_ref sync_offset;  /* synchronization_time_offset (a sampled variable; NONE = 0) */
+    int32_t solver;                 /* solver_type: BCM3HIP_CP_SOLVER_CVODE (0) or _DP5 (ODESolverDP5: explicit
+                                       Dormand-Prince 5(4), Hairer's dense output; not with synchronised
+                                       data or treatment trajectories) */
 } bcm3hip_cellpop_model;
+enum { BCM3HIP_CP_SOLVER_CVODE = 0, BCM3HIP_CP_SOLVER_DP5 = 1 };
 enum { BCM3HIP_CP_SYNC_DNA_REPLICATION_START = 0, BCM3HIP_CP_SYNC_PCNA_GFP_INCREASE = 1,
        BCM3HIP_CP_SYNC_NUCLEAR_ENVELOPE_BREAKDOWN = 2, BCM3HIP_CP_SYNC_ANAPHASE_ONSET = 3, BCM3HIP_CP_SYNC_NONE = 4 };
 

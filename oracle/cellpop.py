@@ -49,7 +49,7 @@ class CellIn(C.Structure):
                 ("ev_nuclear_envelope", C.c_int), ("ev_chromatid_separation", C.c_int), ("ev_cytokinesis", C.c_int),
                 ("ev_apoptosis", C.c_int), ("n_constant", C.c_int), ("n_treat", C.c_int), ("treat_cs", C.c_void_p),
                 ("treat_off", C.c_void_p), ("treat_times", C.c_void_p), ("stored", C.c_int),
-                ("output_sync", C.c_void_p), ("sync_offset", C.c_double)]
+                ("output_sync", C.c_void_p), ("sync_offset", C.c_double), ("solver", C.c_int)]
 
 
 # ESynchronizeCellTrajectory (Experiment.h:21-27) of the synchronize attribute
@@ -194,6 +194,8 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
     e["hmin"] = float(ex.get("solver_min_timestep", 1e-8))
     e["hmax"] = float(ex.get("solver_max_timestep", "inf"))
     e["max_steps"] = int(ex.get("solver_max_steps", 10000))
+    # Cell::AllocateSolver (Cell.cpp:57-66): CVODE or DP5 (ODESolverDP5, restated in cellpop_ref.cpp)
+    e["solver"] = {"CVODE": 0, "DP5": 1}[ex.get("solver_type", "CVODE")]
     e["num_cells"] = int(num_cells if num_cells is not None else ex.get("num_cells", 1))
     e["max_cells"] = int(max_cells if max_cells is not None else ex.get("max_cells", 20))
     e["divide_cells"] = _bool(ex.get("divide_cells"), True)
@@ -634,6 +636,7 @@ def simulate_experiment(e, prob, values):
         cin.stored = 1 if e.get("stored") else 0
         cin.output_sync = out_sync.ctypes.data
         cin.sync_offset = sync_offset
+        cin.solver = e.get("solver", 0)
         cout = CellOut()
         vals = np.empty(M)
         end_y = np.empty(N)

@@ -19,6 +19,9 @@
  * CVodeTimepoint records of ODESolverCVODE::Solve, :375-401; GetInterpolatedY's iterator, :176-242;
  * the division / death interpolation of Cell.cpp:499-529 and the evaluation passes of
  * Experiment.cpp:265-292 with Cell::GetInterpolatedSpeciesValue, Cell.cpp:280-327).
+ * solver_type="DP5": ODESolverDP5 (src/odecommon/ODESolverDP5.cpp, the reference's own explicit
+ * Dormand-Prince 5(4) with Hairer's dense output; its source needs Boost through Utils.h, so it is
+ * restated here statement for statement: ApplyRK :327-412, Solve :100-285).
  * N_Vector: the vendored nvector_serial stands in for nvector_serial_eigen.cpp (same formulas).
  * The cell right-hand side is the generated derivative (oracle/sbml_codegen.py) compiled for the
  * host and passed in as a function pointer.
@@ -78,6 +81,7 @@ typedef struct {
     int stored;
     const int* output_sync;  // [M] ESynchronizeCellTrajectory of each output (4 = None)
     double sync_offset;      // Experiment's time_offset
+    int solver;              // 0 CVODE, 1 DP5 (ODESolverDP5, restated below; no treatments, no stored mode)
 } cp_cell_in;
 
 typedef struct {
@@ -350,6 +354,7 @@ double threshold_crossing_time_stored(const Cell* c, int species, double thresho
 
 double crossing(Cell* c, int species, double threshold, bool above)
 {
+    if (c->in->solver == 1) return std::numeric_limits<double>::quiet_NaN();  // ODESolverDP5.cpp:322-327
     return c->in->stored ? threshold_crossing_time_stored(c, species, threshold, above, c->previous_integration_step_time)
                          : threshold_crossing_time(c, threshold, above, c->previous_integration_step_time);
 }
@@ -386,6 +391,7 @@ bool step_cb(Cell* c, double t, const double* y, double& end_time)
                 c->end_y = c->interp.get(c->recs, c->N, division_time);
             } else {
                 c->simulation_end_time = t;
+                c->end_y.assign(y, y + c->N);  // the "temporary hack" branch's simulation_end_y
             }
             c->divided = true;
             cont = false;
@@ -399,6 +405,7 @@ bool step_cb(Cell* c, double t, const double* y, double& end_time)
                 c->end_y = c->interp.get(c->recs, c->N, death_time);
             } else {
                 c->simulation_end_time = t;
+                c->end_y.assign(y, y + c->N);
             }
             c->died = true;
             cont = false;
@@ -406,6 +413,147 @@ bool step_cb(Cell* c, double t, const double* y, double& end_time)
     }
     c->previous_integration_step_time = t;
     return cont;
+}
+
+// ODESolverDP5::ApplyRK (ODESolverDP5.cpp:327-412)
+struct Dp5State {
+    int N;
+    std::vector<double> yn, ytmp, k[7];
+};
+
+double dp5_apply_rk(Cell* c, Dp5State& d, double t, double cur_dt)
+{
+    const int N = d.N;
+    const cp_cell_in* in = c->in;
+    auto f = [&](double tt, const std::vector<double>& y, std::vector<double>& out) {
+        in->rhs(out.data(), y.data(), constants_at(c, tt), in->parameters, in->non_sampled_parameters);
+    };
+    std::vector<double>&yn = d.yn, &ytmp = d.ytmp;
+    std::vector<double>* k = d.k;
+    for (int i = 0; i < N; i++) ytmp[i] = yn[i] + cur_dt * 0.2 * k[0][i];
+    f(t + 0.2 * cur_dt, ytmp, k[1]);
+    for (int i = 0; i < N; i++) ytmp[i] = yn[i] + cur_dt * (+0.075 * k[0][i] + 0.225 * k[1][i]);
+    f(t + 0.3 * cur_dt, ytmp, k[2]);
+    for (int i = 0; i < N; i++)
+        ytmp[i] = yn[i] + cur_dt * (+0.97777777777777777777777777777778 * k[0][i] - 3.7333333333333333333333333333333 * k[1][i] +
+                                    3.5555555555555555555555555555556 * k[2][i]);
+    f(t + 0.8 * cur_dt, ytmp, k[3]);
+    for (int i = 0; i < N; i++)
+        ytmp[i] = yn[i] + cur_dt * (+2.9525986892242036274958085657674 * k[0][i] - 11.595793324188385916780978509374 * k[1][i] +
+                                    9.8228928516994360615759792714525 * k[2][i] - 0.29080932784636488340192043895748 * k[3][i]);
+    f(t + 0.88888888888888888888888888888889 * cur_dt, ytmp, k[4]);
+    for (int i = 0; i < N; i++)
+        ytmp[i] = yn[i] + cur_dt * (+2.8462752525252525252525252525253 * k[0][i] - 10.757575757575757575757575757576 * k[1][i] +
+                                    8.9064227177434724604535925290642 * k[2][i] + 0.27840909090909090909090909090909 * k[3][i] -
+                                    0.27353130360205831903945111492281 * k[4][i]);
+    f(t + cur_dt, ytmp, k[5]);
+    for (int i = 0; i < N; i++)
+        ytmp[i] = yn[i] + cur_dt * (+0.09114583333333333333333333333333 * k[0][i] + 0.44923629829290206648697214734951 * k[2][i] +
+                                    0.65104166666666666666666666666667 * k[3][i] - 0.32237617924528301886792452830189 * k[4][i] +
+                                    0.13095238095238095238095238095238 * k[5][i]);
+    f(t + cur_dt, ytmp, k[6]);
+    double maxdiff = -std::numeric_limits<double>::infinity();
+    for (int i = 0; i < N; i++) {
+        double error = cur_dt * (+0.00123263888888888888888888888889 * k[0][i] - 0.00425277029050613956274333632824 * k[2][i] +
+                                 0.03697916666666666666666666666667 * k[3][i] - 0.05086379716981132075471698113208 * k[4][i] +
+                                 0.04190476190476190476190476190476 * k[5][i] - 0.025 * k[6][i]);
+        error = fabs(error);
+        const double D = in->atol + in->rtol * fabs(ytmp[i] + k[6][i] * cur_dt);
+        const double diff = error / D;
+        maxdiff = (std::max)(maxdiff, diff);
+    }
+    return maxdiff;
+}
+
+// ODESolverDP5::Solve with do_interpolation (SolveReturnSolution, ODESolver.cpp:93-134) and
+// Cell::integration_step_cb, whose result DP5 ignores; sol[(ti) * N + i] the interpolated outputs
+bool dp5_solve(Cell* c, const std::vector<double>& tp, int ti0, std::vector<double>& sol, long& steps_out)
+{
+    const cp_cell_in* in = c->in;
+    const int N = c->N, M = (int)tp.size();
+    for (auto& v : sol) v = std::numeric_limits<double>::quiet_NaN();  // interpolated_output->setConstant(NaN)
+    double end_time = tp[M - 1];
+    Dp5State d;
+    d.N = N;
+    d.yn.assign(in->y0, in->y0 + N);
+    d.ytmp.assign(N, 0.0);
+    for (auto& k : d.k) k.assign(N, 0.0);
+    double t = 0.0;
+    double dt = std::min(in->hmax, 1.0);
+    in->rhs(d.k[0].data(), d.yn.data(), constants_at(c, t), in->parameters, in->non_sampled_parameters);
+    unsigned int steps = 0;
+    size_t ti = ti0;
+    const double min_dt = in->hmin, max_dt = in->hmax;
+    while (1) {
+        double cur_dt = dt, next_dt = dt;
+        bool succeeded = false;
+        for (int i = 0; i < 10; i++) {
+            double maxdiff = dp5_apply_rk(c, d, t, cur_dt);
+            if (std::isnan(maxdiff) || maxdiff == -std::numeric_limits<double>::infinity()) {
+                steps_out = steps;
+                return false;
+            }
+            if (maxdiff > 1.1) {
+                if (cur_dt == min_dt) {
+                    break;
+                } else {
+                    double scale = 0.9 * pow(maxdiff, -0.2);
+                    scale = std::max(0.2, scale);
+                    cur_dt *= scale;
+                    if (cur_dt < min_dt) cur_dt = min_dt;
+                }
+            } else if (maxdiff < 0.5) {
+                maxdiff = std::max(maxdiff, 1e-5);
+                double scale = 0.9 * pow(maxdiff, -0.2);
+                scale = std::min(5.0, scale);
+                next_dt = cur_dt * scale;
+                if (next_dt > max_dt) next_dt = max_dt;
+                succeeded = true;
+                break;
+            } else {
+                next_dt = cur_dt;
+                succeeded = true;
+                break;
+            }
+        }
+        if (!succeeded) {
+            steps_out = steps;
+            return false;
+        }
+        const double target_t = t + cur_dt;
+        while (target_t >= tp[ti]) {
+            const double theta = (tp[ti] - t) / cur_dt;
+            if (theta >= 1.0) {
+                for (int i = 0; i < N; i++) sol[ti * N + i] = d.ytmp[i];
+            } else {
+                const double thetaSq = theta * theta;
+                const double b1 = theta * (1.0 + theta * (-2.7854166666666669 + theta * (2.8861111111111111 + theta * (-1.0095486111111112))));
+                const double b3 = 33.33333333333333 * thetaSq * (0.11363881401617251 + theta * (-0.1682659478885894 + theta * 0.068104222821203958));
+                const double b4 = -2.5 * thetaSq * (0.675 + theta * (-1.8 + theta * (0.8645833333333333)));
+                const double b5 = 21.491745283018869 * thetaSq * (-0.012 + theta * (0.058666666666666666 + theta * (-0.06166666666666666)));
+                const double b6 = -3.1428571428571428 * thetaSq * (-0.3 + theta * (0.9666666666666666 + theta * (-0.7083333333333333)));
+                for (int i = 0; i < N; i++)
+                    sol[ti * N + i] = d.yn[i] + cur_dt * (b1 * d.k[0][i] + b3 * d.k[2][i] + b4 * d.k[3][i] + b5 * d.k[4][i] + b6 * d.k[5][i]);
+            }
+            ti++;
+            if (ti == (size_t)M) break;
+        }
+        if (ti == (size_t)M) break;
+        d.k[0] = d.k[6];
+        d.yn = d.ytmp;
+        t += cur_dt;
+        steps++;
+        c->t = t;
+        step_cb(c, t, d.yn.data(), end_time);  // result ignored (ODESolverDP5.cpp:259-261)
+        if (t >= end_time) break;
+        if ((int)steps == in->max_steps) {
+            steps_out = steps;
+            return false;
+        }
+        dt = next_dt;
+    }
+    steps_out = steps;
+    return true;
 }
 
 }  // namespace
@@ -456,7 +604,10 @@ int cp_simulate_cell(const cp_cell_in* in, cp_cell_out* out, double* out_values,
         if (ti == M) solve = false;
     }
     long nst = 0;
-    if (solve) {
+    if (solve && in->solver == 1) {
+        result = dp5_solve(&c, tp, ti, sol, nst);
+        for (int i = 0; i < N; i++) end_y[i] = (c.divided || c.died) ? c.end_y[i] : sol[(size_t)(M - 1) * N + i];
+    } else if (solve) {
         double end_time = in->stored ? c.simulation_end_time : tp[M - 1];
         c.interp.restart(N);
         N_Vector y = N_VNew_Serial(N), atol = N_VNew_Serial(N), tmp = N_VNew_Serial(N);
