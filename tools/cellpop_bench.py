@@ -20,6 +20,15 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 dev = torch.device("cuda", 0)
 lik, pri = os.path.join(G, "cellpop_likelihood.xml"), os.path.join(G, "cellpop_prior.xml")
+# CP_SOLVER=DP5: the same C4 experiment with solver_type="DP5" (a temporary copy of the likelihood)
+if os.environ.get("CP_SOLVER", "CVODE") == "DP5":
+    import tempfile
+    text = open(lik).read().replace('<experiment name="exp1" ', '<experiment name="exp1" solver_type="DP5" ')
+    text = text.replace('model_file="cellpop_model.xml"', f'model_file="{os.path.join(G, "cellpop_model.xml")}"')
+    text = text.replace('data_file="cellpop_data.json"', f'data_file="{os.path.join(G, "cellpop_data.json")}"')
+    lik = os.path.join(tempfile.mkdtemp(), "cellpop_dp5.xml")
+    with open(lik, "w") as f:
+        f.write(text)
 ll = Likelihood(lik, pri, device=0)
 gen = torch.Generator(device=dev)
 gen.manual_seed(20251018)
