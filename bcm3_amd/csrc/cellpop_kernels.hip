@@ -526,6 +526,72 @@ __device__ double cp_cell_likelihood(const bcm3hip_cellpop_data& dl, const doubl
     return lp;
 }
 
+// CalculateCellLikelihood with an observed lineage (DataLikelihoodTimeCourse.cpp:431-563): observed
+// cell o against simulated cell s (cell index, -1 = "the simulated cell did not divide"), recursing
+// into o's observed children (ascending) and s's two simulated daughters, with the reference's
+// rules: without a simulated cell every observed point of the subtree takes the missing-value
+// penalty at its own time point; a -inf cell stops there; with daughters, either daughter with no
+// finite child likelihood gives -inf, one observed child takes the better daughter and two or more
+// add nothing (the #if TODO block); without daughters each child's penalty REPLACES the sum (the
+// reference assigns instead of adding). Unrolled to 8 generations (the host refuses deeper ones).
+struct CpLineage {
+    const bcm3hip_cellpop_data* dl;
+    const double* times;       // experiment output times (entries)
+    const double* xcells;      // this evaluation's cells' entry values [cell][M]
+    const int32_t* sim_child;  // this evaluation's cells' first daughters
+    int M;
+    double scale, offset, stdev, pstd, msd;
+};
+
+__device__ inline double cp_missing_at(const CpLineage& c, double t)
+{
+    // EvaluateMissingValue (DataLikelihoodTimeCourseBase.cpp:301-315)
+    return (c.dl->error_model == BCM3HIP_CP_ERR_T4) ? log_pdf_tnu4(t, 0.0, c.msd) : cp_log_pdf_normal(t, 0.0, c.msd);
+}
+
+template <int D>
+__device__ __attribute__((noinline)) double cp_lineage_likelihood(const CpLineage& c, int o, int s)
+{
+    if constexpr (D == 0) {
+        return __builtin_nan("");
+    } else {
+        const bcm3hip_cellpop_data& dl = *c.dl;
+        const double* obs = dl.observed + (size_t)o * dl.T;
+        const int c0 = dl.child_off[o], c1 = dl.child_off[o + 1];
+        double lp = 0.0;
+        if (s < 0) {
+            for (int k = 0; k < dl.T; k++)
+                if (obs[k] == obs[k]) lp += cp_missing_at(c, c.times[dl.entry[k]]);
+            for (int q = c0; q < c1; q++) lp += cp_lineage_likelihood<D - 1>(c, dl.child_ix[q], -1);
+            return lp;
+        }
+        lp = cp_cell_likelihood(dl, c.times, obs, c.xcells + (size_t)s * c.M, c.scale, c.offset, c.stdev, c.pstd, c.msd);
+        if (lp == -__builtin_inf()) return lp;
+        if (c1 > c0) {
+            const int d0 = c.sim_child[s];
+            if (d0 >= 0) {
+                int f1 = 0, f2 = 0;
+                double a0 = 0.0, b0 = 0.0;
+                for (int q = c0; q < c1; q++) {
+                    const double a = cp_lineage_likelihood<D - 1>(c, dl.child_ix[q], d0);
+                    const double b = cp_lineage_likelihood<D - 1>(c, dl.child_ix[q], d0 + 1);
+                    if (a > -__builtin_inf()) f1++;
+                    if (b > -__builtin_inf()) f2++;
+                    if (q == c0) {
+                        a0 = a;
+                        b0 = b;
+                    }
+                }
+                if (f1 == 0 || f2 == 0) return -__builtin_inf();
+                if (c1 - c0 == 1) lp += (a0 > b0) ? a0 : b0;
+            } else {
+                for (int q = c0; q < c1; q++) lp = cp_lineage_likelihood<D - 1>(c, dl.child_ix[q], -1);
+            }
+        }
+        return lp;
+    }
+}
+
 // the cost matrix rows' checks and the matching, on the workspace; lane 0 of the block. Returns
 // Evaluate's result (false: a NaN cell likelihood, .cpp:299-302) and the data likelihood's logp
 __device__ bool cp_tc_assign(int R, int nsim, const HgWs& w, const uint8_t* row_nan, const int32_t* row_finite,
@@ -558,14 +624,16 @@ __device__ bool cp_tc_assign(int R, int nsim, const HgWs& w, const uint8_t* row_
 // grid (evaluation, data likelihood); blocks of non-time-course data likelihoods return at once
 __global__ __launch_bounds__(256) void cp_timecourse_kernel(CpStatic m, int32_t n, const double* values,
                                                              const int32_t* ncells, const int32_t* failed,
-                                                             const double* out_values, unsigned char* ws_global,
-                                                             size_t ws_stride, double* tc_logp, int32_t* tc_ok)
+                                                             const double* out_values, const int32_t* sim_child,
+                                                             unsigned char* ws_global, size_t ws_stride,
+                                                             double* tc_logp, int32_t* tc_ok)
 {
     extern __shared__ __align__(16) unsigned char cp_lds[];
     const int e = blockIdx.x, di = blockIdx.y;
     const bcm3hip_cellpop_data dl = m.data[di];
     if (dl.kind != BCM3HIP_CP_DATA_TIME_COURSE || e >= n || failed[e]) return;
-    const int R = dl.R, nsim = ncells[e];
+    // the matched rows: the observed cells without a parent (all of them without a lineage)
+    const int R = (dl.n_roots > 0) ? dl.n_roots : dl.R, nsim = ncells[e];
     const int nw = R > nsim ? R : nsim;
     unsigned char* base = ws_global ? ws_global + ((size_t)e * m.n_data + di) * ws_stride : cp_lds;
     const HgWs w = hg_carve(base, nw);
@@ -579,14 +647,16 @@ __global__ __launch_bounds__(256) void cp_timecourse_kernel(CpStatic m, int32_t 
     const double pstd = cp_ref(dl.proportional_stdev, v, m.transforms, 0.0);
     const double msd = cp_ref(dl.missing_stdev, v, m.transforms, 300.0);
     const size_t cbase = (size_t)e * m.max_cells;
+    const CpLineage lin{&dl, m.output_times, out_values + cbase * m.M, sim_child + cbase, m.M, scale, offset, stdev, pstd, msd};
     for (int p = threadIdx.x; p < R * nsim; p += blockDim.x) {
         const int i = p / nsim, j = p % nsim;
         // simulated cells with a parent are not matched (.cpp:307-309): the initial cells are the
         // first n0 slots
-        const double L = (j < m.n0) ? cp_cell_likelihood(dl, m.output_times, dl.observed + (size_t)i * dl.T,
-                                                         out_values + (cbase + j) * m.M, scale, offset, stdev, pstd,
-                                                         msd)
-                                    : -__builtin_inf();
+        double L = -__builtin_inf();
+        if (j < m.n0)
+            L = (dl.n_roots > 0) ? cp_lineage_likelihood<8>(lin, dl.roots[i], j)
+                                 : cp_cell_likelihood(dl, m.output_times, dl.observed + (size_t)i * dl.T,
+                                                      out_values + (cbase + j) * m.M, scale, offset, stdev, pstd, msd);
         w.cost[(size_t)i * nw + j] = -L;
     }
     __syncthreads();
@@ -611,13 +681,13 @@ __global__ __launch_bounds__(256) void cp_timecourse_kernel(CpStatic m, int32_t 
 
 hipError_t launch_cp_timecourse(const CpStatic& m, int32_t n, int32_t max_R, const double* values,
                                 const int32_t* ncells, const int32_t* failed, const double* out_values,
-                                unsigned char* ws_global, size_t ws_stride, double* tc_logp, int32_t* tc_ok,
-                                hipStream_t s)
+                                const int32_t* sim_child, unsigned char* ws_global, size_t ws_stride,
+                                double* tc_logp, int32_t* tc_ok, hipStream_t s)
 {
     if (n <= 0) return hipSuccess;
     const size_t lds = ws_global ? 0 : hg_ws_bytes(max_R);
     hipLaunchKernelGGL(cp_timecourse_kernel, dim3(n, m.n_data), dim3(256), lds, s, m, n, values, ncells, failed,
-                       out_values, ws_global, ws_stride, tc_logp, tc_ok);
+                       out_values, sim_child, ws_global, ws_stride, tc_logp, tc_ok);
     return hipGetLastError();
 }
 

@@ -45,10 +45,11 @@ hipError_t launch_cp_popavg(const CpStatic& m, int32_t n, const double* values, 
                             double* logp, int32_t* status, hipStream_t s);
 // the time-course data likelihoods: per (evaluation, data likelihood) logp and Evaluate's result;
 // ws_global = nullptr: the matching workspace of max_R cells in LDS (cp_assign_lds_fits)
+// sim_child[slot]: the cell index of the slot's first daughter, -1 = none (observed lineages)
 hipError_t launch_cp_timecourse(const CpStatic& m, int32_t n, int32_t max_R, const double* values,
                                 const int32_t* ncells, const int32_t* failed, const double* out_values,
-                                unsigned char* ws_global, size_t ws_stride, double* tc_logp, int32_t* tc_ok,
-                                hipStream_t s);
+                                const int32_t* sim_child, unsigned char* ws_global, size_t ws_stride,
+                                double* tc_logp, int32_t* tc_ok, hipStream_t s);
 // the time-points data likelihoods, same outputs and workspace as the time courses
 hipError_t launch_cp_timepoints(const CpStatic& m, int32_t n, int32_t max_R, const double* values,
                                 const int32_t* ncells, const int32_t* failed, const double* out_values,

@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdint>
 #include <fstream>
+#include <functional>
 #include <limits>
 
 #include "NetCDFClassic.h"
@@ -465,10 +466,6 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
                          d.data_name.c_str(), nd);
                 return false;
             }
-            if (group->find("parent")) {
-                LOGERROR("cell_population: observed cell lineages (variable \"parent\") are not supported");
-                return false;
-            }
             const std::string only = option_get(vm, "cellpop.use_only_cell_ix", "-1");
             const size_t ncells_data = nd == 1 ? 1 : values->arr.empty() ? 0 : values->arr[0].arr.size();
             std::vector<size_t> pick;
@@ -507,6 +504,64 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
                                                     : nd == 2 ? row.arr[pick[j]].as_double()
                                                               : row.arr[pick[j]].arr[0].as_double();
                 }
+            // observed lineage (DataLikelihoodTimeCourse.cpp:132-167): "parent" holds the parent's
+            // "cell_id" (INT_MIN: none); children are kept per parent in ascending order
+            if (const Json* par = group->find("parent")) {
+                const Json* pd = par->find("data");
+                const Json* idv = group->find("cell_id");
+                const Json* id = idv ? idv->find("data") : nullptr;
+                if (!pd || !id) {
+                    LOGERROR("cell_population: data group \"%s\" has \"parent\" but no \"cell_id\"", name.c_str());
+                    return false;
+                }
+                std::vector<long long> ids(d.R);
+                for (int j = 0; j < d.R; j++) ids[j] = (long long)id->arr.at(pick[j]).as_double();
+                std::vector<std::vector<int32_t>> children(d.R);
+                d.roots.clear();
+                for (int j = 0; j < d.R; j++) {
+                    const long long p = (long long)pd->arr.at(pick[j]).as_double();
+                    if (p != (long long)std::numeric_limits<int>::min()) {
+                        const auto it = std::find(ids.begin(), ids.end(), p);
+                        if (it == ids.end()) {
+                            LOGERROR("Could not find cell %lld for parent of cell %d", p, j);
+                            return false;
+                        }
+                        children[it - ids.begin()].push_back(j);
+                    } else {
+                        d.roots.push_back(j);
+                    }
+                }
+                d.child_off.assign(1, 0);
+                d.child_ix.clear();
+                for (int j = 0; j < d.R; j++) {
+                    d.child_ix.insert(d.child_ix.end(), children[j].begin(), children[j].end());
+                    d.child_off.push_back((int32_t)d.child_ix.size());
+                }
+                // the device recursion is unrolled to 8 generations of observed cells
+                std::function<int(int)> depth = [&](int c) {
+                    int m = 0;
+                    for (int32_t ch : children[c]) m = std::max(m, depth(ch));
+                    return m + 1;
+                };
+                for (int32_t r : d.roots)
+                    if (depth(r) > 8) {
+                        LOGERROR("cell_population: observed lineages deeper than 8 generations are not supported");
+                        return false;
+                    }
+                if (d.roots.size() != (size_t)d.R) {
+                    // a cell in a parent cycle is nobody's descendant of a root: refuse
+                    size_t reach = 0;
+                    std::function<void(int)> walk = [&](int c) {
+                        reach++;
+                        for (int32_t ch : children[c]) walk(ch);
+                    };
+                    for (int32_t r : d.roots) walk(r);
+                    if (reach != (size_t)d.R) {
+                        LOGERROR("cell_population: the observed lineage of data \"%s\" has a parent cycle", d.data_name.c_str());
+                        return false;
+                    }
+                }
+            }
             if (max_cells < d.R) {
                 LOGERROR("Maximum number of simulated cells (%d) in the experiment is not sufficient for the amount of cells in the data (%d)",
                          max_cells, d.R);
@@ -933,7 +988,9 @@ bool LikelihoodCellPopulation::PostInitialize()
                                                  d.stdev_relative_to_scale, d.missing_stdev, tp ? d.L : 0,
                                                  tp ? d.MK : 0, tp ? d.term_offset.data() : nullptr,
                                                  tp ? d.term_entry.data() : nullptr, tp ? d.col_ref.data() : nullptr,
-                                                 tp ? d.relative_ix : -1, tp ? d.only_nondivided : 0});
+                                                 tp ? d.relative_ix : -1, tp ? d.only_nondivided : 0,
+                                                 (int32_t)d.roots.size(), d.roots.data(), d.child_off.data(),
+                                                 d.child_ix.data()});
     }
     model = bcm3hip_cellpop_model{};
     model.derivative_body = derivative_body.c_str();

@@ -12,7 +12,7 @@
 // solver_* settings (solver_type CVODE or DP5); <set_parameter>; <cell_variability
 // distribution="diagonal_gaussian">; <treatment_trajectory type="pulses">; <data> of type
 // "time_course_population_average" or "time_course" (the default type; single cells matched to
-// the simulated cells, no observed lineage; synchronize= any of the reference's points, on stored
+// the simulated cells, observed lineages through "cell_id" / "parent"; synchronize= any of the reference's points, on stored
 // integration points) with the normal / additive_normal /
 // proportional_normal / additive_proportional_normal / student_t4 error models, stdev /
 // proportional_stdev / offset / scale / stdev_relative_to_scale / weight / relative_to_time_average /
@@ -20,7 +20,7 @@
 // (DataLikelihoodTimePoints: cells matched at every time point, ";"-separated species columns, "+"
 // sums, 2-D or 3-D data, value_relative_to_timepoint_ix, use_only_nondivided; normal / student_t4).
 // Not built: the duration likelihood (the reference's reads past its matrix), DP5 with treatment
-// trajectories, observed lineages, non-sampled parameters.
+// trajectories, non-sampled parameters.
 #pragma once
 #include <memory>
 #include <string>
@@ -66,6 +66,8 @@ private:
         int32_t L = 0, MK = 0, relative_ix = -1, only_nondivided = 0;
         std::vector<int32_t> term_offset, term_species, species_order, term_entry;
         std::vector<bcm3hip_value_ref> col_ref;  // [3L] stdev, offset, scale
+        // observed lineage (time courses): roots in data order, children ascending (CSR)
+        std::vector<int32_t> roots, child_off, child_ix;
     };
     bool LoadExperiment(const XmlNode& ex, const OptionsMap& vm);
     bool LoadTimePoints(const XmlNode& dn, DataLikelihood& d, const Json& group, const OptionsMap& vm) const;

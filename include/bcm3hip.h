@@ -241,6 +241,14 @@ typedef struct {
     const bcm3hip_value_ref* col_ref;     /* [3L] stdev, offset, scale of each column */
     int32_t relative_ix;                  /* value_relative_to_timepoint_ix, -1 = none */
     int32_t only_nondivided;              /* use_only_nondivided: daughters are not simulated cells */
+    /* time courses with observed lineages (the data group's "cell_id" / "parent" variables,
+     * DataLikelihoodTimeCourse.cpp:132-167; CalculateCellLikelihood's recursion, :431-563): the
+     * observed cells without a parent in data order, and each observed cell's children in
+     * ascending order (CSR); n_roots = 0: no lineage, every observed cell is a root */
+    int32_t n_roots;
+    const int32_t* roots;      /* [n_roots] */
+    const int32_t* child_off;  /* [R + 1] */
+    const int32_t* child_ix;   /* [child_off[R]] */
 } bcm3hip_cellpop_data;
 enum { BCM3HIP_CP_DATA_POPULATION_AVERAGE = 0, BCM3HIP_CP_DATA_TIME_COURSE = 1, BCM3HIP_CP_DATA_TIME_POINTS = 2 };
 enum { BCM3HIP_CP_ERR_NORMAL = 0, BCM3HIP_CP_ERR_T4 = 1, BCM3HIP_CP_ERR_PROPORTIONAL = 2,

@@ -260,7 +260,6 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
         if kind == "time_course":
             # DataLikelihoodTimeCourse::Load (DataLikelihoodTimeCourse.cpp:43-130): cells x time
             # points; a third (marker) dimension is read, of which one species uses column 0
-            assert "parent" not in data, "observed lineages"
             if obs.ndim == 1:
                 assert use_only_cell_ix == "-1"
                 obs = obs[None, :]
@@ -271,6 +270,7 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
                 if use_only_cell_ix != "-1":
                     obs = obs[[int(t) for t in use_only_cell_ix.split(",")]]
             assert e["max_cells"] == obs.shape[0], "max_cells must equal the observed cells (.cpp:174-183)"
+            lineage = _load_lineage(data, obs.shape[0], use_only_cell_ix)
         else:
             if obs.ndim == 1:
                 obs = obs[:, None]
@@ -293,7 +293,8 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
                                      if dl.get("proportional_stdev") else None),
                  # DataLikelihoodTimeCourseBase: missing_simulation_time_stdev, fixed 300 by default
                  missing_stdev=_ref_value(msd, variables) if msd else ("fixed", 300.0),
-                 relative_to_time_average=_bool(dl.get("relative_to_time_average"), False))
+                 relative_to_time_average=_bool(dl.get("relative_to_time_average"), False),
+                 lineage=lineage if kind == "time_course" else None)
         for ti, t in enumerate(times):
             timepoints.append((len(dls), t, ti, six))
             tp_sync.append(sync)
@@ -338,6 +339,29 @@ def _load_experiment(ex, base, variables, num_cells, max_cells, variant="", use_
     e["y_init"] = np.array([model.species[s]["initial"] for s in model.ode])
     e["constant_init"] = np.array([model.species[s]["initial"] for s in model.constant])
     return e
+
+
+INT_MIN = -2147483648
+
+
+def _load_lineage(data, ncells, use_only_cell_ix):
+    """observed lineage of a time course (DataLikelihoodTimeCourse.cpp:132-167): "parent" holds the
+    parent's "cell_id" (INT_MIN: none); returns (roots in data order, children per cell ascending)
+    or None without a "parent" variable"""
+    if "parent" not in data:
+        return None
+    ids, par = data["cell_id"]["data"], data["parent"]["data"]
+    pick = list(range(ncells)) if use_only_cell_ix == "-1" else [int(t) for t in use_only_cell_ix.split(",")]
+    idp = [int(ids[p]) for p in pick]
+    children = [[] for _ in pick]
+    roots = []
+    for j, p in enumerate(pick):
+        pv = int(par[p])
+        if pv != INT_MIN:
+            children[idp.index(pv)].append(j)  # ValueError: "Could not find cell ... for parent"
+        else:
+            roots.append(j)
+    return roots, children
 
 
 def kind_of(dl):
@@ -682,9 +706,14 @@ def simulate_experiment(e, prob, values):
     # returns false ends the sum there, and the experiment keeps what it had (it still succeeds)
     logp = 0.0
     roots = [c["parent"] < 0 for c in cells]
+    # NotifyParents (DataLikelihoodTimeCourse.cpp:411-429): each cell's first daughter, -1 = none
+    sim_child = [-1] * len(cells)
+    for c in cells:
+        if c["parent"] >= 0 and sim_child[c["parent"]] < 0:
+            sim_child[c["parent"]] = c["index"]
     for dli, d in enumerate(e["data"]):
         if d["kind"] == "time_course":
-            ok, lp = _timecourse_logp(d, trajs[dli], roots, tv)
+            ok, lp = _timecourse_logp(d, trajs[dli], roots, tv, sim_child)
             if not ok:
                 break
             logp += lp
@@ -715,7 +744,7 @@ def _log_pdf_tnu4(x, mu, sigma):
     return -0.9808292530117262 - 2.5 * math.log1p(0.25 * xn * xn) - math.log(sigma)
 
 
-def _timecourse_logp(d, traj, roots, tv):
+def _timecourse_logp(d, traj, roots, tv, sim_child=None):
     """DataLikelihoodTimeCourse::Evaluate (DataLikelihoodTimeCourse.cpp:230-365) for one species and
     no observed lineage: the likelihood of every observed cell against every simulated initial cell
     (CalculateCellLikelihood, :431-497; missing simulated values: CalculateMissingValueLikelihood,
@@ -779,13 +808,51 @@ def _timecourse_logp(d, traj, roots, tv):
                                 - dd * dd * (np.float64(1.0) / (2.0 * (sigma * sigma))))
         return lp
 
+    lineage = d.get("lineage")
+    if lineage is not None:
+        # CalculateCellLikelihood's recursion over the observed lineage (.cpp:431-563)
+        obs_roots, obs_children = lineage
+
+        def rec(o, s):
+            lp = 0.0
+            if s is None:
+                for k in range(T):
+                    if not math.isnan(obs[o, k]):
+                        lp += _log_pdf_tnu4(times[k], 0.0, msd) if em == "t4" else _log_pdf_normal(times[k], 0.0, msd)
+                for ch in obs_children[o]:
+                    lp += rec(ch, None)
+                return lp
+            lp = cell(o, s)
+            if lp == -math.inf:
+                return lp
+            if obs_children[o]:
+                d0 = sim_child[s] if sim_child is not None else -1
+                if d0 >= 0:
+                    m = [[rec(ch, d0), rec(ch, d0 + 1)] for ch in obs_children[o]]
+                    if sum(1 for a, _ in m if a > -math.inf) == 0 or sum(1 for _, b in m if b > -math.inf) == 0:
+                        return -math.inf
+                    if len(m) == 1:
+                        lp += m[0][0] if m[0][0] > m[0][1] else m[0][1]
+                    # two or more observed children: the reference's #if TODO block adds nothing
+                else:
+                    for ch in obs_children[o]:
+                        lp = rec(ch, None)  # assigned, not added (.cpp:555-557)
+            return lp
+
+        R = len(obs_roots)
+        n = max(R, nsim)
+        row_cell = obs_roots
+    else:
+        def rec(o, s):
+            return cell(o, s)
+        row_cell = list(range(R))
     L = np.full((n, n), 0.0)
     edges = []
     for i in range(R):
         finite = 0
         for j in range(nsim):
             if roots[j]:
-                L[i, j] = cell(i, j)
+                L[i, j] = rec(row_cell[i], j)
                 if math.isnan(L[i, j]):
                     return False, -math.inf
                 if L[i, j] > -math.inf:
