@@ -57,3 +57,29 @@ def test_two_experiments_vs_oracle(tmp_path):
         if np.isfinite(r):
             tol = max(2e-4 * (1 + abs(r)), 3 * abs(r - r2))
             assert abs(g - r) <= tol, (g, r, r2)
+
+
+def test_dp5_and_synchronised_experiments_sum(tmp_path):
+    """one experiment on the DP5 solver, one with synchronised data (the stored-integration-point
+    kernel): each experiment compiles its own cell kernel; the sum is bit-identical to the two
+    likelihoods evaluated separately"""
+    from bcm3_amd.likelihood import Likelihood
+    from test_cellpop_dp5 import dp5_likelihood
+    from test_cellpop_sync import sync_likelihood
+    a = dp5_likelihood(tmp_path, "no_division")
+    b = sync_likelihood(tmp_path, "replication")
+    ta, tb = open(a).read(), open(b).read()
+    exp_b = tb[tb.index("<experiment"):tb.index("</experiment>") + len("</experiment>")]
+    ab = str(tmp_path / "dp5_sync.xml")
+    with open(ab, "w") as f:
+        f.write(ta.replace("</bcm_likelihood>", "  " + exp_b + "\n</bcm_likelihood>"))
+    x = CH.draws(6, 31)
+    out = {}
+    for k, p in (("a", a), ("b", b), ("ab", ab)):
+        ll = Likelihood(p, CH.PRIOR, device=0)
+        out[k] = ll.evaluate_batch(x)
+        ll.close()
+    (la, _), (lb, _), (lab, _) = out["a"], out["b"], out["ab"]
+    assert np.isfinite(la).sum() >= 2 and np.isfinite(lb).sum() >= 2
+    expect = np.where(np.isfinite(la) & np.isfinite(lb), la + lb, -np.inf)
+    assert np.array_equal(lab, expect), (lab, expect)
