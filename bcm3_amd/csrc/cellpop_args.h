@@ -38,6 +38,7 @@ struct CpSolveArgs {
     int32_t store_cap;
     const int32_t* output_sync;   // [M] BCM3HIP_CP_SYNC_*
     const double* sync_offset;    // [slot]
+    double hmax;                  // DP5's max_dt (solver_max_timestep)
 };
 
 }  // namespace cpk

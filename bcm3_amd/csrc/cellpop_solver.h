@@ -1281,7 +1281,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
         // every output, those before the cell's t = 0 + DBL_EPSILON included, to NaN (:103-105)
         for (int k = ln; k < ti; k += ROW) outv[k] = __builtin_nan("");
         double end_time = a.output_times[M - 1] - creation;
-        double t = 0.0, dt = 1.0;  // min(max_dt, 1.0), max_dt = solver_max_timestep = inf
+        double t = 0.0, dt = (1.0 < a.hmax) ? 1.0 : a.hmax;  // std::min(max_dt, 1.0)
         Dp5 r;
         r.yn = y0;
         r.k0 = rhs_v<NS, NP, NC>(sh, r.yn, 0.0);
@@ -1310,6 +1310,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
                     double scale = 0.9 * pow(maxdiff, -0.2);
                     scale = (5.0 < scale) ? 5.0 : scale;
                     next_dt = cur_dt * scale;
+                    if (next_dt > a.hmax) next_dt = a.hmax;
                     succeeded = true;
                     break;
                 } else {

@@ -193,8 +193,14 @@ bool LikelihoodCellPopulation::LoadExperiment(const XmlNode& ex, const OptionsMa
     }
     const double feps4 = 4 * (double)std::numeric_limits<float>::epsilon();
     hmin = ex.get_double("solver_min_timestep", 1e-8);
-    const double hmax = ex.get_double("solver_max_timestep", std::numeric_limits<double>::infinity());
-    if (!std::isinf(hmax)) {
+    hmax = ex.get_double("solver_max_timestep", std::numeric_limits<double>::infinity());
+    // DP5's max_dt (ODESolverDP5::SetSolverParameter, :81-87: must be positive); the CVODE kernel
+    // has no hmax clamp (CVodeSetMaxStep)
+    if (solver == BCM3HIP_CP_SOLVER_DP5 && !(hmax > 0.0)) {
+        LOGERROR("max_dt should be strictly positive, but %g was provided", hmax);
+        return false;
+    }
+    if (solver != BCM3HIP_CP_SOLVER_DP5 && !std::isinf(hmax)) {
         LOGERROR("cell_population: a finite solver_max_timestep is not supported");
         return false;
     }
@@ -1006,6 +1012,7 @@ bool LikelihoodCellPopulation::PostInitialize()
     model.output_sync = output_sync.data();
     model.sync_offset = sync_offset;
     model.solver = solver;
+    model.hmax = hmax;
     // DP5 (ODESolverDP5.cpp): GetInterpolatedY and get_threshold_crossing_time are not implemented in
     // the reference (NaN, ASSERT compiled out), so synchronised data would read NaN everywhere; its
     // discontinuity handling (:123-135, 239-254) is not built here

@@ -79,6 +79,7 @@ private:
     double rtol = 0, atol = 0, hmin = 0;
     int32_t max_steps = 10000, num_cells = 1, max_cells = 20;
     int32_t solver = BCM3HIP_CP_SOLVER_CVODE;  // solver_type
+    double hmax = 0.0;                         // solver_max_timestep (DP5's max_dt)
     bool divide_cells = true;
     double trailing = 0, past_cs = 0;
     bcm3hip_value_ref entry_time{}, sync_offset{};

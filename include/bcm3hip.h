@@ -313,6 +313,7 @@ typedef struct {
     int32_t solver;                 /* solver_type: BCM3HIP_CP_SOLVER_CVODE (0) or _DP5 (ODESolverDP5: explicit
                                        Dormand-Prince 5(4), Hairer's dense output; not with synchronised
                                        data or treatment trajectories) */
+    double hmax;                    /* solver_max_timestep: DP5's max_dt (> 0, inf = none); CVODE: inf only */
 } bcm3hip_cellpop_model;
 enum { BCM3HIP_CP_SOLVER_CVODE = 0, BCM3HIP_CP_SOLVER_DP5 = 1 };
 enum { BCM3HIP_CP_SYNC_DNA_REPLICATION_START = 0, BCM3HIP_CP_SYNC_PCNA_GFP_INCREASE = 1,

@@ -22,6 +22,8 @@ CASES = {
     "division": dict(num_cells=16, max_cells=64, experiment_attrs=' solver_type="DP5"'),
     "no_division": dict(num_cells=16, max_cells=16, experiment_attrs=' solver_type="DP5" divide_cells="false"'),
     "late_entry": dict(num_cells=8, max_cells=32, experiment_attrs=' solver_type="DP5"', entry_time="1.5"),
+    # max_dt (ODESolverDP5::SetSolverParameter: the first step min(max_dt, 1) and the growth clamp)
+    "max_dt": dict(num_cells=16, max_cells=64, experiment_attrs=' solver_type="DP5" solver_max_timestep="0.25"'),
 }
 
 
