@@ -438,6 +438,82 @@ BDF_INL void lin_setup(SH& sh, double gamma)
     if (!(fabs(r) <= 1.7976931348623157e308)) sh.dinv_ok = 0;
 }
 
+// The same factorisation for 16-lane rows (NS <= 16) with the matrix in registers: lane i of the row
+// holds row i, the row swap exchanges two lanes' rows by ds_bpermute, the pivot row reaches the other
+// rows by row broadcasts (the column loop unrolled, so column k is a register and lane k a DPP
+// operand); no LDS round trip or barrier per column. The factors and the permutation go to LDS at the
+// end in the layout lin_solve reads. Same operations per element in the same order as lin_setup
+// (which serves NS > 16): the C4 batch 27.9 -> 25.1 ms with bit-identical logp
+// (profiles/r05ag_cellpop_lu_registers.txt).
+BDF_INL int rowget_i(int v, int k)
+{
+    const int addr = ((int)(threadIdx.x & ~(unsigned)(ROW - 1)) + k) << 2;
+    return __builtin_amdgcn_ds_bpermute(addr, v);
+}
+template <int NS, class SH>
+BDF_INL void lin_setup_reg(SH& sh, double gamma)
+{
+    static_assert(NS <= 16, "register LU: one 16-lane row per cell");
+    const int ln = lane();
+    const bool act = ln < NS;
+    const int li = act ? ln : 0;
+    wave_sync();
+    double a[NS];
+    cfor<0, NS>([&](auto J) __attribute__((always_inline)) { a[CI(J)] = sh.J[CI(J) * NS + li]; });
+    cfor<0, NS>([&](auto J) __attribute__((always_inline)) {
+        double v = (-gamma) * a[CI(J)];
+        if (ln == CI(J)) v += 1.0;
+        a[CI(J)] = v;
+    });
+    int perm = ln;
+    cfor<0, NS>([&](auto K) __attribute__((always_inline)) {
+        constexpr int k = CI(K);
+        const double akk = (ln >= k && act) ? a[k] : 0.0;
+        double v = (ln >= k && act) ? fabs(akk) : -1.0, sv = akk;
+        int ix = ln;
+        cfor<0, 4>([&](auto r) __attribute__((always_inline)) {
+            constexpr int D = 1 << CI(r);
+            const double ov = shr_d<D>(v, -2.0);
+            const double osv = shr_d<D>(sv, 0.0);
+            const int oi = shr_i<D>(ix, ix);
+            const bool take = ov >= v;
+            v = take ? ov : v;
+            sv = take ? osv : sv;
+            ix = take ? oi : ix;
+        });
+        const int p = __builtin_amdgcn_mov_dpp(ix, 0x15F, 0xf, 0xf, false);
+        const double biggest = rbc<15>(v);
+        const double pivot = rbc<15>(sv);
+        if (biggest != 0.0 && p != k) {
+            const int src = (ln == k) ? p : (ln == p) ? k : ln;
+            cfor<0, NS>([&](auto J) __attribute__((always_inline)) { a[CI(J)] = rowget(a[CI(J)], src); });
+            perm = rowget_i(perm, src);
+        }
+        const bool below = act && ln > k;
+        double lik = a[k];
+        if (biggest != 0.0) lik *= 1.0 / pivot;
+        if (below) a[k] = lik;
+        cfor<k + 1, NS>([&](auto J) __attribute__((always_inline)) {
+            const double ukj = rbc<CI(K)>(a[CI(J)]);
+            if (below && ukj != 0.0) a[CI(J)] -= ukj * lik;
+        });
+    });
+    if (act) {
+        cfor<0, NS>([&](auto J) __attribute__((always_inline)) { sh.A[CI(J) * NS + ln] = a[CI(J)]; });
+        sh.perm[ln] = perm;
+    }
+    double diag = 1.0;
+    cfor<0, NS>([&](auto J) __attribute__((always_inline)) { diag = (ln == CI(J)) ? a[CI(J)] : diag; });
+    double r = 1.0;
+    if (act) {
+        r = 1.0 / diag;
+        sh.dinv[ln] = r;
+    }
+    if (ln == 0) sh.dinv_ok = 1;
+    wave_sync();
+    if (!(fabs(r) <= 1.7976931348623157e308)) sh.dinv_ok = 0;
+}
+
 // x / d from r = RN(1 / d): q = RN(x r), then one residual correction RN(q + (x - d q) r) -- the
 // correctly rounded quotient (Markstein) in three dependent operations instead of the IEEE
 // division sequence, which sits on the critical path of the back substitution
@@ -730,7 +806,10 @@ BDF_INL bool newton(SH& sh, S& s, double rl1, int convfail, bool callSetup)
             }
             {
                 CP_PH_BEGIN();
-                lin_setup<NS>(sh, s.gamma);
+                if constexpr (ROW == 16)
+                    lin_setup_reg<NS>(sh, s.gamma);
+                else
+                    lin_setup<NS>(sh, s.gamma);
                 CP_PH_END(sh, 2);
             }
             s.nls_jcur = jnew;
