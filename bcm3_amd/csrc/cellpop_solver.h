@@ -595,12 +595,29 @@ BDF_INL void ewt_set(S& s)
     s.ewt = frcp(__builtin_fma(s.rtol, fabs(s.zn[0]), s.atol));
 }
 
+// q: the order (s.q), or a compile-time order on the path where every cell of the wavefront is at
+// the same order, where the order selects fold away (same operations on the same elements)
+
+// f(QMAX) when every active lane is at the maximum order (72 % of cell steps are, per the reference
+// solver's own step records), else f(s.q): a wave-uniform branch. Paths for every order measured
+// slower than this one (code size; profiles/r05am_cellpop_order_paths.txt)
+template <class F>
+BDF_INL void with_order(int q, F&& f)
+{
+#ifndef CP_NO_ORDER_PATHS
+    if (__all(q == QMAX)) {
+        f(QMAX);
+        return;
+    }
+#endif
+    f(q);
+}
 template <class S>
-BDF_INL void rescale(S& s)
+BDF_INL void rescale(S& s, const int q)
 {
     double c = s.eta;
     cfor<1, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
-        if (CI(j) <= s.q) s.zn[CI(j)] *= c;
+        if (CI(j) <= q) s.zn[CI(j)] *= c;
         c = s.eta * c;
     });
     s.h = s.hscale * s.eta;
@@ -608,23 +625,23 @@ BDF_INL void rescale(S& s)
 }
 
 template <class S>
-BDF_INL void predict(S& s)
+BDF_INL void predict(S& s, const int q)
 {
     s.tn += s.h;
     cfor<1, QMAX + 1>([&](auto k) __attribute__((always_inline)) {
         cfor_down<QMAX, CI(k)>([&](auto j) __attribute__((always_inline)) {
-            if (CI(j) <= s.q) s.zn[CI(j) - 1] += s.zn[CI(j)];
+            if (CI(j) <= q) s.zn[CI(j) - 1] += s.zn[CI(j)];
         });
     });
 }
 
 template <class S>
-BDF_INL void restore(S& s, double saved_t)
+BDF_INL void restore(S& s, double saved_t, const int q)
 {
     s.tn = saved_t;
     cfor<1, QMAX + 1>([&](auto k) __attribute__((always_inline)) {
         cfor_down<QMAX, CI(k)>([&](auto j) __attribute__((always_inline)) {
-            if (CI(j) <= s.q) s.zn[CI(j) - 1] -= s.zn[CI(j)];
+            if (CI(j) <= q) s.zn[CI(j) - 1] -= s.zn[CI(j)];
         });
     });
 }
@@ -719,9 +736,8 @@ BDF_INL int get_dky(const S& s, double t, double& dky)
 }
 
 template <class S>
-BDF_INL double set_bdf(S& s)
+BDF_INL double set_bdf(S& s, const int q)
 {
-    const int q = s.q;
     double alpha0, alpha0_hat, xi_inv, xistar_inv, hsum;
     s.l[0] = s.l[1] = xi_inv = xistar_inv = 1.0;
     cfor<2, QMAX + 1>([&](auto i) __attribute__((always_inline)) {
@@ -990,10 +1006,13 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret, double& yout
     }
     double dsm = 0.0;
     for (;;) {
-        if (do_rescale) rescale(s);
+        double rl1 = 0.0;
+        with_order(s.q, [&](const int q) __attribute__((always_inline)) {
+            if (do_rescale) rescale(s, q);
+            predict(s, q);
+            rl1 = set_bdf(s, q);
+        });
         do_rescale = true;
-        predict(s);
-        const double rl1 = set_bdf(s);
         const int convfail = ((nflag == FIRST_CALL) || (nflag == PREV_ERR_FAIL)) ? CONV_NONE : CONV_OTHER;
         const bool callSetup = (nflag == PREV_CONV_FAIL) || (nflag == PREV_ERR_FAIL) || (s.nst == 0) ||
                                (s.nst >= s.nstlp + MSBP) || (fabs(s.gamrat - 1.0) > DGMAX);
@@ -1008,7 +1027,7 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret, double& yout
             dsm = s.acnrm * s.tq[2];
             if (dsm <= 1.0) break;
         }
-        restore(s, saved_t);
+        restore(s, saved_t, s.q);
         if (!conv) {
             // cvHandleNFlag (cvode.c:2886-2910)
             ncf++;
@@ -1049,14 +1068,17 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret, double& yout
     // cvCompleteStep
     s.nst++;
     s.hu = s.h;
-    cfor_down<QMAX, 2>([&](auto i) __attribute__((always_inline)) {
-        if (CI(i) <= s.q) s.tau[CI(i)] = s.tau[CI(i) - 1];
-    });
-    if ((s.q == 1) && (s.nst > 1)) s.tau[2] = s.tau[1];
-    s.tau[1] = s.h;
-    cfor<0, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
-        if (CI(j) <= s.q) s.zn[CI(j)] = __builtin_fma(s.l[CI(j)], s.acor, s.zn[CI(j)]);
-    });
+    auto complete = [&](const int q) __attribute__((always_inline)) {
+        cfor_down<QMAX, 2>([&](auto i) __attribute__((always_inline)) {
+            if (CI(i) <= q) s.tau[CI(i)] = s.tau[CI(i) - 1];
+        });
+        if ((q == 1) && (s.nst > 1)) s.tau[2] = s.tau[1];
+        s.tau[1] = s.h;
+        cfor<0, QMAX + 1>([&](auto j) __attribute__((always_inline)) {
+            if (CI(j) <= q) s.zn[CI(j)] = __builtin_fma(s.l[CI(j)], s.acor, s.zn[CI(j)]);
+        });
+    };
+    with_order(s.q, complete);
     s.qwait--;
     if ((s.qwait == 1) && (s.q != QMAX)) {
         s.zn[QMAX] = s.acor;

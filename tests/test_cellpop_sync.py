@@ -46,6 +46,10 @@ CASES = {
     # dividing cells in the stored mode: division times and daughters' states on the interpolant
     "division": (_tp("anaphase", "pcna_neg"), dict(num_cells=4, max_cells=32, experiment_attrs=' trailing_simulation_time="8"'),
                  "2,7,11"),
+    # a treatment trajectory in the stored mode: the records of the stop-time returns and restarts
+    "treatment": (POP + _tc("DNA_replication_start"),
+                  dict(experiment_attrs=' divide_cells="false"',
+                       extra='\n    <treatment_trajectory type="pulses" species_name="mitogen" times="13,-1"/>'), None),
     # two synchronisation points and an unsynchronised course in one experiment (three passes)
     "mixed": (POP + _tc("PCNA_gfp_increase") + _tc("mitosis").replace('stdev="stdev"', 'stdev="0.2" error_model="t4"'),
               dict(experiment_attrs=' divide_cells="false"'), None),
