@@ -1084,7 +1084,7 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret, double& yout
         s.zn[QMAX] = s.acor;
         s.saved_tq5 = s.tq[5];
     }
-    // cvPrepareNextStep
+    // cvPrepareNextStep (L = q + 1 throughout: every order change sets both)
     CP_PH_BEGIN();
     if (s.etamax == 1.0) {
         s.qwait = SUNMAX(s.qwait, 2);
@@ -1092,39 +1092,42 @@ BDF_INL int cvode_one_step(SH& sh, S& s, double tout, double& tret, double& yout
         s.hprime = s.h;
         s.eta = 1.0;
     } else {
-        const double etaq = eta_from(BIAS2 * dsm, s.L);
-        double eta = etaq;
-        s.qprime = s.q;
-        if (s.qwait == 0) {
-            s.qwait = 2;
-            double etaqm1 = 0.0, etaqp1 = 0.0;
-            if (s.q > 1) etaqm1 = eta_from(BIAS1 * wrms<NS>(sh, znq_of(s, s.q), s.ewt) * s.tq[1], s.q);
-            if ((s.q != QMAX) && (s.saved_tq5 != 0.0)) {
-                const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), s.L);
-                const double tv = __builtin_fma(-cquot, s.zn[QMAX], s.acor);
-                etaqp1 = eta_from(BIAS3 * wrms<NS>(sh, tv, s.ewt) * s.tq[3], s.L + 1);
+        with_order(s.q, [&](const int q) __attribute__((always_inline)) {
+            const int L = q + 1;
+            const double etaq = eta_from(BIAS2 * dsm, L);
+            double eta = etaq;
+            s.qprime = q;
+            if (s.qwait == 0) {
+                s.qwait = 2;
+                double etaqm1 = 0.0, etaqp1 = 0.0;
+                if (q > 1) etaqm1 = eta_from(BIAS1 * wrms<NS>(sh, znq_of(s, q), s.ewt) * s.tq[1], q);
+                if ((q != QMAX) && (s.saved_tq5 != 0.0)) {
+                    const double cquot = fdiv(s.tq[5], s.saved_tq5) * powI(fdiv(s.h, s.tau[2]), L);
+                    const double tv = __builtin_fma(-cquot, s.zn[QMAX], s.acor);
+                    etaqp1 = eta_from(BIAS3 * wrms<NS>(sh, tv, s.ewt) * s.tq[3], L + 1);
+                }
+                const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
+                if (etam < THRESH) {
+                    eta = 1.0;
+                } else if (etam == etaq) {
+                    eta = etaq;
+                } else if (etam == etaqm1) {
+                    eta = etaqm1;
+                    s.qprime = q - 1;
+                } else {
+                    eta = etaqp1;
+                    s.qprime = q + 1;
+                    s.zn[QMAX] = s.acor;
+                }
             }
-            const double etam = SUNMAX(etaqm1, SUNMAX(etaq, etaqp1));
-            if (etam < THRESH) {
-                eta = 1.0;
-            } else if (etam == etaq) {
-                eta = etaq;
-            } else if (etam == etaqm1) {
-                eta = etaqm1;
-                s.qprime = s.q - 1;
+            if (eta < THRESH) {
+                s.eta = 1.0;
+                s.hprime = s.h;
             } else {
-                eta = etaqp1;
-                s.qprime = s.q + 1;
-                s.zn[QMAX] = s.acor;
+                s.eta = SUNMIN(eta, s.etamax);
+                s.hprime = s.h * s.eta;
             }
-        }
-        if (eta < THRESH) {
-            s.eta = 1.0;
-            s.hprime = s.h;
-        } else {
-            s.eta = SUNMIN(eta, s.etamax);
-            s.hprime = s.h * s.eta;
-        }
+        });
     }
     CP_PH_END(sh, 7);
     s.etamax = (s.nst <= SMALL_NST) ? ETAMX2 : ETAMX3;
