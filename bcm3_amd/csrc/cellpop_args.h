@@ -5,6 +5,12 @@
 
 namespace cpk {
 
+// one stored integration point (ODESolverCVODE's CVodeTimepoint, .cpp:375-401): cvode_time, tn, h,
+// hu, q, then the Nordsieck rows zn[0..qmax] of the nstore species the data read. One definition
+// for the kernel (CP_REC, cellpop_solver.h, with qmax = QMAX) and the host that sizes the store.
+constexpr int cp_record_doubles(int qmax, int nstore) { return 5 + (qmax + 1) * (nstore > 0 ? nstore : 1); }
+constexpr int CP_STORE_QMAX = 5;  // = QMAX of bdf_lane.h (static_assert in cellpop_solver.h)
+
 struct CpSolveArgs {
     const int32_t* work;          // [n_work] cell slots of this launch
     int32_t n_work;
@@ -31,9 +37,11 @@ struct CpSolveArgs {
     int32_t* flags;               // [slot] bit0 ok, bit1 divided, bit2 died, bit3 entered mitosis
     double* event_times;          // [slot][5]
     int32_t* nsteps;              // [slot]
-    // stored integration points (CP_STORED builds, synchronised data): per slot store_cap records of
-    // CP_REC doubles (ODESolverCVODE's CVodeTimepoint: time, tn, h, hu, q, zn[0..q] of the stored
-    // species); the sync pass of every output entry; the synchronisation offset per slot
+    // stored integration points (CP_STORED builds, synchronised data): per work item of the launch
+    // store_cap records of CP_REC doubles (ODESolverCVODE's CVodeTimepoint: time, tn, h, hu, q,
+    // zn[0..q] of the stored species -- needed only during the cell's own solve, whose evaluation
+    // passes read them back before it ends); the sync pass of every output entry; the
+    // synchronisation offset per slot
     double* store;
     int32_t store_cap;
     const int32_t* output_sync;   // [M] BCM3HIP_CP_SYNC_*

@@ -159,11 +159,16 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
     // cell; the sum keeps the cell order and the same quotients (0.95 -> 0.63 ms per C4 batch)
     __shared__ double cr_s[64], se_s[64];
     __shared__ double tile[64][65];
+    // CountCellsAtTime(st.time + time_offset, None) (Experiment.cpp:285, 301): the population is
+    // counted at the data time plus the experiment's synchronization_time_offset, the time its values
+    // were read at (the stored mode's evaluation passes; without synchronised data the loader refuses
+    // a sampled offset, so it is 0 there)
+    const double toff = cp_ref(m.sync_offset, v, m.transforms, 0.0);
     for (int k0 = 0; k0 < m.M; k0 += 64) {
         const int k = k0 + ln;
         const bool kv = k < m.M;
         const int kw = (m.M - k0 < 64) ? m.M - k0 : 64;
-        const double t = kv ? m.output_times[k] : 0.0;
+        const double t = kv ? m.output_times[k] + toff : 0.0;
         int pop = 0;
         for (int c0 = 0; c0 < nc; c0 += 64) {
             const int cn = (nc - c0 < 64) ? nc - c0 : 64;

