@@ -47,6 +47,7 @@ struct CpSolveArgs {
     const int32_t* output_sync;   // [M] BCM3HIP_CP_SYNC_*
     const double* sync_offset;    // [slot]
     double hmax;                  // DP5's max_dt (solver_max_timestep)
+    const void* pow_tables;       // xm::GlibcPow (libm_exact.h): glibc's pow for DP5's step-size factor
 };
 
 }  // namespace cpk

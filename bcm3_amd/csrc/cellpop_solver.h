@@ -1248,6 +1248,17 @@ BDF_INL double row_max_nonnan(double v)
     }
 }
 
+// pow(maxdiff, -0.2) of Hairer's step-size factor (ODESolverDP5.cpp:158, 174): glibc's pow on the
+// loaded libm's tables (xm::pow_glibc_pos: e_pow.c's main path, which every finite x > 0 takes for
+// y = -0.2), so the step sequence is the reference's; 0, inf and NaN through the device's pow (the
+// IEEE special values, the same in both)
+BDF_INL double dp5_pow_m02(double x, const void* tables)
+{
+    const xm::GlibcPow* T = static_cast<const xm::GlibcPow*>(tables);
+    if (T && T->ok && x > 0.0 && x < __builtin_inf()) return xm::pow_glibc_pos(x, -0.2, *T);
+    return pow(x, -0.2);
+}
+
 // ODESolverDP5::ApplyRK (ODESolverDP5.cpp:327-412): the stages k1..k6, the 5th-order solution ytmp,
 // FSAL k6, and the error ratio max_i |err_i| / (atol + rtol |ytmp_i + k6_i dt|); lane i = component i
 struct Dp5 {
@@ -1408,13 +1419,13 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
                 // Hairer I, II.4 p167 (:152-184)
                 if (maxdiff > 1.1) {
                     if (cur_dt == a.hmin) break;
-                    double scale = 0.9 * pow(maxdiff, -0.2);
+                    double scale = 0.9 * dp5_pow_m02(maxdiff, a.pow_tables);
                     scale = (0.2 < scale) ? scale : 0.2;
                     cur_dt *= scale;
                     if (cur_dt < a.hmin) cur_dt = a.hmin;
                 } else if (maxdiff < 0.5) {
                     maxdiff = (maxdiff < 1e-5) ? 1e-5 : maxdiff;
-                    double scale = 0.9 * pow(maxdiff, -0.2);
+                    double scale = 0.9 * dp5_pow_m02(maxdiff, a.pow_tables);
                     scale = (5.0 < scale) ? 5.0 : scale;
                     next_dt = cur_dt * scale;
                     if (next_dt > a.hmax) next_dt = a.hmax;

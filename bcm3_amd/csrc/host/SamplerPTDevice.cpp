@@ -269,6 +269,7 @@ struct SamplerPTDevice::Impl {
     DevBuf<double> sp_cand_x, sp_cand_lp, sp_cand_lmh, sp_cand_llh, sp_cand_sc, sp_batch_x, sp_batch_llh;
     DevBuf<int32_t> sp_cand_sel, sp_cand_upd, sp_cand_steps, sp_steps_hint, sp_steps_prop, sp_batch_status,
         sp_batch_steps, sp_batch_src, sp_batch_n, sp_err;
+    DevBuf<int32_t> sp_pos;    // batch position of each entry (bcm3hip_spec::batch_pos)
     DevBuf<int64_t> sp_total;  // entries of all speculative batches (bcm3hip_spec::batch_total)
     DevBuf<uint8_t> sp_cand_active, acc_mut, acc_mut2, acc_exc;
     DevBuf<int32_t> partner[2], pair_first[2];
@@ -753,9 +754,9 @@ struct SamplerPTDevice::Impl {
             LOGERROR("EvaluateLogProbabilityBatchDeviceCounted failed");
             return false;
         }
-        // accept r, its dispatch-order tracking and the history add in one launch (spec_commit)
-        if (!Launch(bcm3hip_ptmh_spec_scatter((int)C, &S, llh_prop.p, stream), "ptmh_spec_scatter") ||
-            !Launch(bcm3hip_ptmh_spec_commit((int)C, d, 0, temps.p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+        // the batch's results to their chains, accept r, its dispatch-order tracking and the history
+        // add in one launch (spec_commit reads the batch through S.batch_pos: no spec_scatter launch)
+        if (!Launch(bcm3hip_ptmh_spec_commit((int)C, d, 0, temps.p, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
                                              &S, prop.p, lprior_prop.p, log_mh.p, llh_prop.p, cfg.learning_rate,
                                              values.p, lprior.p, llh.p, lpp.p, acc_mut.p, acc_mutate.p, nan_flag.p, &P,
                                              g0, cfg.seed, (uint64_t)iter, H, sub, hist.p, hcount.p, sp_err.p, stream),
@@ -821,7 +822,7 @@ struct SamplerPTDevice::Impl {
                   acc_mut2.alloc(C) &&
                   acc_exc.alloc(C) && sp_send_last.alloc(2 * d) && sp_send_first.alloc(2 * d) &&
                   sp_remote.alloc(4 * d) && cross_acc.alloc(2) && sp_pred.alloc(N) && sp_inv_scale.alloc(d) &&
-                  sp_total.alloc(1);
+                  sp_total.alloc(1) && sp_pos.alloc(N);
         for (int st = 0; st < 2 && ok; st++) ok = partner[st].alloc(C) && pair_first[st].alloc(C);
         if (!ok) {
             LOGERROR("SamplerPTDevice: speculative buffers could not be allocated");
@@ -881,6 +882,7 @@ struct SamplerPTDevice::Impl {
         S.batch_n = sp_batch_n.p;
         S.pred_steps = sp_pred.p;
         S.batch_total = sp_total.p;
+        S.batch_pos = sp_pos.p;
         return true;
     }
 

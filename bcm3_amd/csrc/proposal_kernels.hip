@@ -702,7 +702,7 @@ __device__ bool accept_one(int c, int d, const double* __restrict__ temps, const
         *ema += ((acc ? 1.0 : 0.0) - *ema) * alpha;
     }
     if (acc) {
-        for (int i = 0; i < d; i++) values[(int64_t)c * d + i] = prop[(int64_t)c * d + i];
+        copy_row(values + (int64_t)c * d, prop + (int64_t)c * d, d);
         lprior[c] = nq;
         llh[c] = nl;
         lpp[c] = npp;
@@ -736,12 +736,13 @@ __device__ void history_one(int c, int d, int H, int subsampling, const double* 
 {
     if (temps[c] == 0.0 || (mask && !mask[c])) return;
     int64_t* n = counters + 2 * (int64_t)c;
-    n[1]++;
-    if (n[1] == subsampling) {
-        const int64_t ix = n[0] % H;
-        for (int i = 0; i < d; i++) hist[((int64_t)c * H + ix) * d + i] = (float)values[(int64_t)c * d + i];
-        n[0]++;
+    const int64_t n0 = n[0], n1 = n[1] + 1;  // both counters in one memory round trip
+    if (n1 == subsampling) {
+        copy_row(hist + ((int64_t)c * H + n0 % H) * d, values + (int64_t)c * d, d);
+        n[0] = n0 + 1;
         n[1] = 0;
+    } else {
+        n[1] = n1;
     }
 }
 
@@ -829,29 +830,35 @@ __global__ void __launch_bounds__(64) ptmh_spec_candidates_kernel(
 // The solve length of an entry, predicted from the previous launch's entries (batch_x / batch_steps
 // before this pair's batch overwrites them): the mean steps of its 4 nearest neighbours in parameter
 // space, coordinates scaled by 1 / (prior sd). On C3 prior draws this ranks solve lengths with a
-// Spearman correlation of 0.93 (the state's own last solve: 0.58). One wavefront per entry, 16 per
-// workgroup; the workgroup stages the previous entries through LDS in chunks (one coalesced pass
-// over them per workgroup instead of one per entry: 26.6 -> a few us per pair, round 6), each lane
-// scans every 64th of a chunk and keeps its 4 nearest, a wave merge takes the 4 nearest of the
-// lanes' lists. Entries with nothing to compare against (first pair) keep the steps_hint of their
-// source. The prediction orders the launch only: which neighbours tie does not change any result.
+// Spearman correlation of 0.93 (the state's own last solve: 0.58). A workgroup serves kPredQ entries,
+// kPredWaves wavefronts each; it stages the previous entries through LDS (component-major, so a
+// wavefront's lanes read consecutive words) in chunks -- one pass over them per kPredQ entries
+// instead of one per entry from L2, whose traffic bounded the round-5 form at 26.6 us per pair. Each
+// lane keeps the 4 nearest of the entries it scans, a wave merge the 4 nearest of its lanes, lane 0 of
+// an entry's first wavefront the 4 nearest of its wavefronts. Entries with nothing to compare against
+// (first pair) keep the steps_hint of their source. The prediction orders the launch only: which of
+// equally near neighbours are taken changes no result.
 constexpr int kKnn = 4;
-constexpr int kPredWaves = 16;
-constexpr int kPredLdsBytes = 60 * 1024;  // chunk rows (d doubles + the steps) + the queries
-__global__ void __launch_bounds__(64 * kPredWaves) ptmh_spec_predict_kernel(int C, int d, const double* __restrict__ prop,
-                                                                            const int32_t* __restrict__ partner,
-                                                                            const double* __restrict__ inv_scale,
-                                                                            bcm3hip_spec S)
+constexpr int kPredQ = 4;      // entries per workgroup
+constexpr int kPredWaves = 4;  // wavefronts per entry
+constexpr int kPredLdsBytes = 60 * 1024;
+__global__ void __launch_bounds__(64 * kPredQ * kPredWaves) ptmh_spec_predict_kernel(
+    int C, int d, const double* __restrict__ prop, const int32_t* __restrict__ partner,
+    const double* __restrict__ inv_scale, bcm3hip_spec S)
 {
     extern __shared__ double lds_pred[];
+    __shared__ double wd[kPredQ * kPredWaves * kKnn];
+    __shared__ int ws[kPredQ * kPredWaves * kKnn];
+    constexpr int NT = 64 * kPredQ * kPredWaves;
     const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int e = (int)blockIdx.x * kPredWaves + wv;
-    // queries [kPredWaves][d], scale [d], then the chunk: rows [ch][d] and steps [ch]
+    const int qi = wv / kPredWaves, part = wv - qi * kPredWaves;
+    const int e = (int)blockIdx.x * kPredQ + qi;
+    // queries [kPredQ][d], scale [d], then the chunk: components [d][ch] and steps [ch]
     double* qx = lds_pred;
-    double* isc = qx + kPredWaves * d;
+    double* isc = qx + kPredQ * d;
     double* mx = isc + d;
-    const int ch = (int)((kPredLdsBytes / 8 - (kPredWaves + 1) * d) * 8 / (8 * d + 4));
+    const int ch = (int)((kPredLdsBytes / 8 - (kPredQ + 1) * d) * 8 / (8 * d + 4));
     int* ms = reinterpret_cast<int*>(mx + (size_t)ch * d);
     bool active = e < n_all;
     const double* x = nullptr;
@@ -869,12 +876,12 @@ __global__ void __launch_bounds__(64 * kPredWaves) ptmh_spec_predict_kernel(int 
     }
     const int mem_n = S.batch_n[0];  // uniform: every thread returns here or none does
     if (mem_n <= 0) {
-        if (active && lane == 0) S.pred_steps[e] = S.steps_hint[src];
+        if (active && part == 0 && lane == 0) S.pred_steps[e] = S.steps_hint[src];
         return;
     }
-    if (active)
-        for (int j = lane; j < d; j += 64) qx[wv * d + j] = x[j];
-    for (int j = tid; j < d; j += 64 * kPredWaves) isc[j] = inv_scale[j];
+    if (active && part == 0)
+        for (int j = lane; j < d; j += 64) qx[qi * d + j] = x[j];
+    for (int j = tid; j < d; j += NT) isc[j] = inv_scale[j];
     double bd[kKnn];
     int bs[kKnn];
     for (int q = 0; q < kKnn; q++) {
@@ -884,16 +891,33 @@ __global__ void __launch_bounds__(64 * kPredWaves) ptmh_spec_predict_kernel(int 
     for (int base = 0; base < mem_n; base += ch) {
         const int cn = (mem_n - base < ch) ? mem_n - base : ch;
         __syncthreads();
-        for (int t = tid; t < cn * d; t += 64 * kPredWaves) mx[t] = S.batch_x[(int64_t)base * d + t];
-        for (int t = tid; t < cn; t += 64 * kPredWaves) ms[t] = S.batch_steps[base + t];
+        // the chunk's loads all in flight before the LDS stores (a loop of load-store pairs waited one
+        // memory round trip per element)
+        constexpr int U = 8;
+        for (int t0 = tid; t0 < cn * d; t0 += U * NT) {
+            double v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int t = t0 + u * NT;
+                v[u] = (t < cn * d) ? S.batch_x[(int64_t)base * d + t] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const int t = t0 + u * NT;
+                if (t < cn * d) {
+                    const int m = t / d, j = t - m * d;
+                    mx[(size_t)j * ch + m] = v[u];
+                }
+            }
+        }
+        for (int t = tid; t < cn; t += NT) ms[t] = S.batch_steps[base + t];
         __syncthreads();
         if (!active) continue;
-        const double* q = qx + wv * d;
-        for (int m = lane; m < cn; m += 64) {
-            const double* y = mx + (size_t)m * d;
+        const double* q = qx + qi * d;
+        for (int m = part * 64 + lane; m < cn; m += 64 * kPredWaves) {
             double dist = 0.0;
             for (int j = 0; j < d; j++) {
-                const double t = (q[j] - y[j]) * isc[j];
+                const double t = (q[j] - mx[(size_t)j * ch + m]) * isc[j];
                 dist = __builtin_fma(t, t, dist);
             }
             if (dist < bd[kKnn - 1]) {
@@ -909,30 +933,49 @@ __global__ void __launch_bounds__(64 * kPredWaves) ptmh_spec_predict_kernel(int 
             }
         }
     }
-    if (!active) return;
-    // the kKnn smallest of the wavefront: repeatedly take the minimum head
-    int sum = 0, got = 0;
+    // the kKnn smallest of each wavefront: repeatedly take the minimum head
     for (int r = 0; r < kKnn; r++) {
         double mn = bd[0];
         for (int off = 32; off >= 1; off >>= 1) {
             const double o = __shfl_xor(mn, off);
             mn = (o < mn) ? o : mn;
         }
-        if (mn == INFINITY) break;
-        // the lowest lane holding the minimum pops it
-        const unsigned long long who = __ballot(bd[0] == mn);
-        const int owner = __builtin_ctzll(who);
-        sum += __shfl(bs[0], owner);
-        got++;
-        if (lane == owner) {
-            for (int q = 0; q < kKnn - 1; q++) {
-                bd[q] = bd[q + 1];
-                bs[q] = bs[q + 1];
+        int st = 0;
+        if (mn != INFINITY) {
+            // the lowest lane holding the minimum pops it
+            const unsigned long long who = __ballot(bd[0] == mn);
+            const int owner = __builtin_ctzll(who);
+            st = __shfl(bs[0], owner);
+            if (lane == owner) {
+                for (int q = 0; q < kKnn - 1; q++) {
+                    bd[q] = bd[q + 1];
+                    bs[q] = bs[q + 1];
+                }
+                bd[kKnn - 1] = INFINITY;
             }
-            bd[kKnn - 1] = INFINITY;
+        }
+        if (lane == 0) {
+            wd[wv * kKnn + r] = mn;
+            ws[wv * kKnn + r] = st;
         }
     }
-    if (lane == 0) S.pred_steps[e] = got ? sum / got : S.steps_hint[src];
+    __syncthreads();
+    if (active && part == 0 && lane == 0) {
+        // the kKnn smallest of the entry's wavefronts' lists
+        double* w = wd + qi * kPredWaves * kKnn;
+        const int* wsq = ws + qi * kPredWaves * kKnn;
+        int sum = 0, got = 0;
+        for (int r = 0; r < kKnn; r++) {
+            int best = -1;
+            for (int i = 0; i < kPredWaves * kKnn; i++)
+                if (w[i] != INFINITY && (best < 0 || w[i] < w[best])) best = i;
+            if (best < 0) break;
+            sum += wsq[best];
+            got++;
+            w[best] = INFINITY;
+        }
+        S.pred_steps[e] = got ? sum / got : S.steps_hint[src];
+    }
 }
 
 // one workgroup: the batch of iteration r's proposals and the active candidates, ordered by the
@@ -959,12 +1002,20 @@ __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, con
     __syncthreads();
     constexpr int kPer = kSpecSortMax / 1024;
     int bk[kPer], rk[kPer];
+    // every entry's flag and prediction loaded first (one memory round trip, not two per entry)
+    int act[kPer], pst[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+        const int i = tid + q * 1024;
+        act[q] = (i < C) ? 1 : (i < n_all) ? (int)S.cand_active[i - C] : 0;
+        pst[q] = (i < n_all) ? S.pred_steps[i] : 0;
+    }
     for (int q = 0; q < kPer; q++) {
         const int i = tid + q * 1024;
         bk[q] = -1;
-        const bool on = (i < C) || (i < n_all && S.cand_active[i - C]);
+        const bool on = act[q] != 0;
         if (on) {
-            int h = S.pred_steps[i];
+            int h = pst[q];
             h = h < 0 ? 0 : (h >> 1);
             h = h > kSpecBuckets - 1 ? kSpecBuckets - 1 : h;
             bk[q] = kSpecBuckets - 1 - h;  // longest first
@@ -1010,11 +1061,13 @@ __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, con
         if (S.batch_total) S.batch_total[0] += M;
     }
     __syncthreads();
-    for (int i = tid; i < n_all; i += blockDim.x)
+    for (int i = tid; i < n_all; i += blockDim.x) {
         if (pos_of[i] >= 0) S.batch_src[pos_of[i]] = i;
+        if (S.batch_pos) S.batch_pos[i] = pos_of[i];
+    }
     // the rows in batch order: eight loads in flight per thread before their stores (the copy was a
     // chain of dependent load-store round trips)
-    constexpr int U = 8;
+    constexpr int U = 16;
     for (int t0 = tid; t0 < n_all * d; t0 += U * 1024) {
         double v[U];
         int64_t dst[U];
@@ -1096,7 +1149,7 @@ __device__ void select_one(int c, int d, const double* __restrict__ temps, const
         llh_prop[c] = __builtin_nan("");
         return;
     }
-    for (int i = 0; i < d; i++) prop[(int64_t)c * d + i] = S.cand_x[(int64_t)sl * d + i];
+    copy_row(prop + (int64_t)c * d, S.cand_x + (int64_t)sl * d, d);
     lprior_prop[c] = S.cand_lp[sl];
     log_mh[c] = S.cand_lmh[sl];
     llh_prop[c] = S.cand_llh[sl];
@@ -1142,6 +1195,23 @@ __global__ void ptmh_spec_commit_kernel(int C, int d, int select, const double* 
 {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= C) return;
+    if (!select && S.batch_pos) {
+        // the batch's results of this chain's entries -- its proposal and its candidates -- through
+        // the inverse permutation (ptmh_spec_scatter_kernel's writes for chain c, in this launch)
+        const int p = S.batch_pos[c];
+        if (p >= 0) {
+            llh_prop[c] = S.batch_llh[p];
+            S.steps_prop[c] = S.batch_steps[p];
+        }
+        for (int k = 0; k < BCM3HIP_SPEC_SLOTS; k++) {
+            const int sl = c * BCM3HIP_SPEC_SLOTS + k;
+            const int q = S.batch_pos[C + sl];
+            if (q >= 0) {
+                S.cand_llh[sl] = S.batch_llh[q];
+                S.cand_steps[sl] = S.batch_steps[q];
+            }
+        }
+    }
     if (select)
         select_one(c, d, temps, partner, pair_first, acc_prev, acc_exc, cross_acc, remote, values, S, prop, lprior_prop,
                    log_mh, llh_prop, P, error);
@@ -1299,7 +1369,7 @@ int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* par
         first_round < 0 || !spec_ok(spec) || !spec->pred_steps)
         return BCM3HIP_ERR_ARG;
     const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
-    hipLaunchKernelGGL(ptmh_spec_predict_kernel, dim3((n_all + kPredWaves - 1) / kPredWaves), dim3(64 * kPredWaves),
+    hipLaunchKernelGGL(ptmh_spec_predict_kernel, dim3((n_all + kPredQ - 1) / kPredQ), dim3(64 * kPredQ * kPredWaves),
                        kPredLdsBytes, (hipStream_t)stream, C, d, prop, partner, inv_scale, *spec);
     hipLaunchKernelGGL(ptmh_spec_batch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, prop, partner,
                        first_round, *spec);

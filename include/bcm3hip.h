@@ -555,6 +555,9 @@ typedef struct {
     int32_t* batch_n;     /* [1] entries in use (0 before the first launch) */
     int32_t* pred_steps;  /* [7C] predicted solve length of each entry (batch order key) */
     int64_t* batch_total; /* [1] running sum of the entries of every batch built (NULL: not kept) */
+    int32_t* batch_pos;   /* [7C] batch position of each entry (-1: not in the batch), the inverse of
+                             batch_src; NULL: not kept. When kept, bcm3hip_ptmh_spec_commit with
+                             select = 0 takes the batch's results itself (no spec_scatter launch) */
 } bcm3hip_spec;
 /* candidates of iteration iter_next = r + 1 (after bcm3hip_ptmh_propose_adaptive of iteration r, whose
  * proposals are in prop); partner[c] = exchange partner of chain c in round r + 1 (-1 none) */

@@ -4,10 +4,10 @@ CP_DP5 path, cellpop_solver.h) against the oracle's restatement of the reference
 
 The device evaluates the same Dormand-Prince stages, error ratio (a NaN-skipping row maximum, exact
 in any order) and Hairer dense output as the reference, uncontracted; the step-size factor's pow is
-the device's (~1 ulp from glibc), so the step sequences can part after a near-tie of the acceptance
-thresholds. Bar: logp within the cell-population envelope (cellpop_helpers.logp_bar: 1e-6 (1 + |logp|)
+glibc's (xm::pow_glibc_pos on the loaded libm's tables, round 6; round 5 used the device's pow, ~1 ulp
+from glibc, so step sequences could part after a near-tie of the acceptance thresholds). Bar: logp within the cell-population envelope (cellpop_helpers.logp_bar: 1e-6 (1 + |logp|)
 or 10x the oracle's own FMA / no-FMA difference on the draw) with an identical -inf pattern, the same cell counts and division decisions, simulation ends within 1e-3 h, and the same
-step count on >= 95 % of cells."""
+step count on >= 99 % of cells."""
 import math
 
 import numpy as np
@@ -54,4 +54,6 @@ def test_dp5_matches_oracle(dp5_case):
             assert (np.isnan(vals[c]) == np.isnan(oc["values"])).all(), (name, i, c)
             same_steps += int(rec["nsteps"][c] == oc["nsteps"])
             total += 1
-    assert total > 0 and same_steps >= 0.95 * total, (name, same_steps, total)
+    import parity
+    parity.log_summary({"dp5_steps_equal": same_steps / max(1, total), "cells": total, "case": name}, n=len(x))
+    assert total > 0 and same_steps >= 0.99 * total, (name, same_steps, total)
