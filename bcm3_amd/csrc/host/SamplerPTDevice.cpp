@@ -1195,14 +1195,52 @@ bool SamplerPTDevice::SetOutput(const std::string& filename, int64_t num_samples
     // a sharded ladder: the reference's netCDF-4 file (SampleHandlerNetCDF.cpp:24-110) written by rank 0
     // from every rank's rows when libnetcdf can be loaded; otherwise the shared netCDF classic file,
     // each rank writing its own temperature columns
-    const bool gather = s.cfg.world > 1 && s.transport && NcNetCDF4WriteAvailable(nullptr);
+    // Rank 0 decides (only its libnetcdf matters: it alone writes the gathered file) and tells every
+    // other rank over the transport, together with whether its writer opened, so the ranks never
+    // disagree on the mode nor wait at a flush for rows a failed rank 0 will not take.
+    const std::vector<double> ladder = TemperatureLadder(s.Ctot, s.cfg.temperature_power, s.cfg.temperature_max);
     std::unique_ptr<SampleFileWriter> w;
-    if (!gather || s.cfg.rank == 0) {
+    bool gather = false;
+    auto open_writer = [&](bool all) {
         w = std::make_unique<SampleFileWriter>();
-        const std::vector<double> ladder = TemperatureLadder(s.Ctot, s.cfg.temperature_power, s.cfg.temperature_max);
-        if (!(gather ? w->Initialize(filename, (size_t)num_samples, names, tr, ladder, 0, (size_t)s.Ctot)
-                     : w->Initialize(filename, (size_t)num_samples, names, tr, ladder, (size_t)s.g0, (size_t)s.C)))
+        return all ? w->Initialize(filename, (size_t)num_samples, names, tr, ladder, 0, (size_t)s.Ctot)
+                   : w->Initialize(filename, (size_t)num_samples, names, tr, ladder, (size_t)s.g0, (size_t)s.C);
+    };
+    if (s.cfg.world > 1 && s.transport) {
+        double code = 0.0;  // rank 0's decision: 1 gather, 0 every rank its own columns, -1 rank 0 failed
+        if (s.cfg.rank == 0) {
+            gather = NcNetCDF4WriteAvailable(nullptr);
+            code = open_writer(gather) ? (gather ? 1.0 : 0.0) : -1.0;
+        }
+        DevBuf<double> msg;
+        if (!msg.alloc(1)) return false;
+        std::vector<const double*> sends;
+        std::vector<int> speer;
+        double* recv = msg.p;
+        const int from0 = 0;
+        bool ok;
+        if (s.cfg.rank == 0) {
+            ok = bcm3hip_memcpy_async(msg.p, &code, sizeof(double), BCM3HIP_H2D, s.stream) == 0;
+            for (int r = 1; r < s.cfg.world; r++) {
+                sends.push_back(msg.p);
+                speer.push_back(r);
+            }
+            ok = ok && s.transport->Exchange((int)sends.size(), sends.data(), speer.data(), 0, nullptr, nullptr, 1,
+                                             s.stream) &&
+                 bcm3hip_stream_synchronize(s.stream) == 0;
+        } else {
+            ok = s.transport->Exchange(0, nullptr, nullptr, 1, &recv, &from0, 1, s.stream) &&
+                 bcm3hip_memcpy_async(&code, msg.p, sizeof(double), BCM3HIP_D2H, s.stream) == 0 &&
+                 bcm3hip_stream_synchronize(s.stream) == 0;
+        }
+        if (!ok || code < 0.0) {
+            LOGERROR("SetOutput: %s", ok ? "rank 0 could not open the sample file" : "the transport failed");
             return false;
+        }
+        gather = code > 0.0;
+        if (!gather && s.cfg.rank != 0 && !open_writer(false)) return false;
+    } else if (!open_writer(false)) {
+        return false;
     }
     s.out_flush = std::max(1, flush_every);
     if (!s.out_buf.alloc((size_t)(s.out_flush * s.C * (s.d + 2)))) return false;

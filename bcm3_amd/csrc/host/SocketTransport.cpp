@@ -46,6 +46,14 @@ int TimeoutMs()
     return ms;
 }
 
+// Connecting to a peer's listener and accepting a peer's connection happen when the ranks start: a
+// peer that never starts fails the run after BCM3_SOCKET_TIMEOUT_MS, or 300 s by default (the
+// receives of a running exchange stay unbounded by default, above)
+int ConnectTimeoutMs()
+{
+    return TimeoutMs() >= 0 ? TimeoutMs() : 300000;
+}
+
 std::string RankPath(const std::string& dir, int r) { return dir + "/bcm3_rank" + std::to_string(r) + ".sock"; }
 
 bool WaitFd(int fd, short ev, int ms)
@@ -176,7 +184,7 @@ private:
                 return fd;
             }
             close(fd);
-            if (TimeoutMs() >= 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(TimeoutMs())) return -1;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ConnectTimeoutMs())) return -1;
             std::this_thread::sleep_for(std::chrono::milliseconds(10));
         }
     }
@@ -187,7 +195,7 @@ private:
         for (;;) {
             auto it = in_.find(peer);
             if (it != in_.end()) return it->second;
-            if (!WaitFd(listen_fd_, POLLIN, TimeoutMs())) return -1;
+            if (!WaitFd(listen_fd_, POLLIN, ConnectTimeoutMs())) return -1;
             const int fd = accept(listen_fd_, nullptr, nullptr);
             if (fd < 0) {
                 if (errno == EINTR) continue;

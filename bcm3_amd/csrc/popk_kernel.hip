@@ -284,12 +284,15 @@ __global__ void __launch_bounds__(256) popk_traj_kernel(PopPKDevModel m, int64_t
     constexpr int NS = TR::NS;
     constexpr bool UNI = (MODE != POPK_LANES);
     constexpr bool VEC = (MODE == POPK_VEC);
-    // library functions out of line (libm_exact.h xm::lib) in the vector-state kernel; the
-    // scalar-state kernel inlines them unless BCM3_UNI_COLD (diagnostic builds)
-#ifdef BCM3_UNI_COLD
-    constexpr bool COLD = UNI;
-#else
+    // library functions out of line (libm_exact.h xm::lib) in both one-trajectory-per-wavefront
+    // kernels. Round 6 closed the round-4 question: the scalar-state kernel built this way under the
+    // product's flags is bit-identical to the inlining build on all 6 PK models x 7 dosing rules x 3
+    // solver forms (tools/flag_diff.py, profiles/r06e_flag_diff.txt), so the inline workaround is
+    // dropped; BCM3_UNI_INLINE restores it for diagnostics
+#ifdef BCM3_UNI_INLINE
     constexpr bool COLD = VEC;
+#else
+    constexpr bool COLD = UNI;
 #endif
     const int lane = threadIdx.x & 63;
 #ifdef BCM3_TABLES_LDS

@@ -830,107 +830,61 @@ __global__ void __launch_bounds__(64) ptmh_spec_candidates_kernel(
 // The solve length of an entry, predicted from the previous launch's entries (batch_x / batch_steps
 // before this pair's batch overwrites them): the mean steps of its 4 nearest neighbours in parameter
 // space, coordinates scaled by 1 / (prior sd). On C3 prior draws this ranks solve lengths with a
-// Spearman correlation of 0.93 (the state's own last solve: 0.58). A workgroup serves kPredQ entries,
-// kPredWaves wavefronts each; it stages the previous entries through LDS (component-major, so a
-// wavefront's lanes read consecutive words) in chunks -- one pass over them per kPredQ entries
-// instead of one per entry from L2, whose traffic bounded the round-5 form at 26.6 us per pair. Each
-// lane keeps the 4 nearest of the entries it scans, a wave merge the 4 nearest of its lanes, lane 0 of
-// an entry's first wavefront the 4 nearest of its wavefronts. Entries with nothing to compare against
-// (first pair) keep the steps_hint of their source. The prediction orders the launch only: which of
-// equally near neighbours are taken changes no result.
+// Spearman correlation of 0.93 (the state's own last solve: 0.58). One workgroup of 4 wavefronts
+// per entry, each scanning a quarter of the previous entries; entries with nothing to compare
+// against (first pair) keep the steps_hint of their source.
 constexpr int kKnn = 4;
-constexpr int kPredQ = 4;      // entries per workgroup
-constexpr int kPredWaves = 4;  // wavefronts per entry
-constexpr int kPredLdsBytes = 60 * 1024;
-__global__ void __launch_bounds__(64 * kPredQ * kPredWaves) ptmh_spec_predict_kernel(
-    int C, int d, const double* __restrict__ prop, const int32_t* __restrict__ partner,
-    const double* __restrict__ inv_scale, bcm3hip_spec S)
+constexpr int kKnnWaves = 4;
+__global__ void __launch_bounds__(64 * kKnnWaves) ptmh_spec_predict_kernel(int C, int d, const double* __restrict__ prop,
+                                                                           const int32_t* __restrict__ partner,
+                                                                           const double* __restrict__ inv_scale,
+                                                                           bcm3hip_spec S)
 {
-    extern __shared__ double lds_pred[];
-    __shared__ double wd[kPredQ * kPredWaves * kKnn];
-    __shared__ int ws[kPredQ * kPredWaves * kKnn];
-    constexpr int NT = 64 * kPredQ * kPredWaves;
+    __shared__ double wd[kKnnWaves * kKnn];
+    __shared__ int ws[kKnnWaves * kKnn];
+    const int e = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
     const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
+    if (e >= n_all) return;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int qi = wv / kPredWaves, part = wv - qi * kPredWaves;
-    const int e = (int)blockIdx.x * kPredQ + qi;
-    // queries [kPredQ][d], scale [d], then the chunk: components [d][ch] and steps [ch]
-    double* qx = lds_pred;
-    double* isc = qx + kPredQ * d;
-    double* mx = isc + d;
-    const int ch = (int)((kPredLdsBytes / 8 - (kPredQ + 1) * d) * 8 / (8 * d + 4));
-    int* ms = reinterpret_cast<int*>(mx + (size_t)ch * d);
-    bool active = e < n_all;
-    const double* x = nullptr;
-    int src = 0;
-    if (active) {
-        if (e < C) {
-            x = prop + (int64_t)e * d;
-            src = e;
-        } else {
-            const int sl = e - C, c = sl / BCM3HIP_SPEC_SLOTS, k = sl - c * BCM3HIP_SPEC_SLOTS;
-            active = S.cand_active[sl] != 0;
-            x = S.cand_x + (int64_t)sl * d;
-            src = (k <= 1 || partner[c] < 0) ? c : partner[c];
-        }
+    const double* x;
+    int src;
+    if (e < C) {
+        x = prop + (int64_t)e * d;
+        src = e;
+    } else {
+        const int sl = e - C, c = sl / BCM3HIP_SPEC_SLOTS, k = sl - c * BCM3HIP_SPEC_SLOTS;
+        if (!S.cand_active[sl]) return;
+        x = S.cand_x + (int64_t)sl * d;
+        src = (k <= 1 || partner[c] < 0) ? c : partner[c];
     }
-    const int mem_n = S.batch_n[0];  // uniform: every thread returns here or none does
+    const int mem_n = S.batch_n[0];
     if (mem_n <= 0) {
-        if (active && part == 0 && lane == 0) S.pred_steps[e] = S.steps_hint[src];
+        if (tid == 0) S.pred_steps[e] = S.steps_hint[src];
         return;
     }
-    if (active && part == 0)
-        for (int j = lane; j < d; j += 64) qx[qi * d + j] = x[j];
-    for (int j = tid; j < d; j += NT) isc[j] = inv_scale[j];
     double bd[kKnn];
     int bs[kKnn];
     for (int q = 0; q < kKnn; q++) {
         bd[q] = INFINITY;
         bs[q] = 0;
     }
-    for (int base = 0; base < mem_n; base += ch) {
-        const int cn = (mem_n - base < ch) ? mem_n - base : ch;
-        __syncthreads();
-        // the chunk's loads all in flight before the LDS stores (a loop of load-store pairs waited one
-        // memory round trip per element)
-        constexpr int U = 8;
-        for (int t0 = tid; t0 < cn * d; t0 += U * NT) {
-            double v[U];
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int t = t0 + u * NT;
-                v[u] = (t < cn * d) ? S.batch_x[(int64_t)base * d + t] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const int t = t0 + u * NT;
-                if (t < cn * d) {
-                    const int m = t / d, j = t - m * d;
-                    mx[(size_t)j * ch + m] = v[u];
-                }
-            }
+    for (int m = tid; m < mem_n; m += 64 * kKnnWaves) {
+        const double* y = S.batch_x + (int64_t)m * d;
+        double dist = 0.0;
+        for (int j = 0; j < d; j++) {
+            const double t = (x[j] - y[j]) * inv_scale[j];
+            dist = __builtin_fma(t, t, dist);
         }
-        for (int t = tid; t < cn; t += NT) ms[t] = S.batch_steps[base + t];
-        __syncthreads();
-        if (!active) continue;
-        const double* q = qx + qi * d;
-        for (int m = part * 64 + lane; m < cn; m += 64 * kPredWaves) {
-            double dist = 0.0;
-            for (int j = 0; j < d; j++) {
-                const double t = (q[j] - mx[(size_t)j * ch + m]) * isc[j];
-                dist = __builtin_fma(t, t, dist);
+        if (dist < bd[kKnn - 1]) {
+            int q = kKnn - 1;
+            const int st = S.batch_steps[m];
+            while (q > 0 && bd[q - 1] > dist) {
+                bd[q] = bd[q - 1];
+                bs[q] = bs[q - 1];
+                q--;
             }
-            if (dist < bd[kKnn - 1]) {
-                int r = kKnn - 1;
-                const int st = ms[m];
-                while (r > 0 && bd[r - 1] > dist) {
-                    bd[r] = bd[r - 1];
-                    bs[r] = bs[r - 1];
-                    r--;
-                }
-                bd[r] = dist;
-                bs[r] = st;
-            }
+            bd[q] = dist;
+            bs[q] = st;
         }
     }
     // the kKnn smallest of each wavefront: repeatedly take the minimum head
@@ -960,19 +914,17 @@ __global__ void __launch_bounds__(64 * kPredQ * kPredWaves) ptmh_spec_predict_ke
         }
     }
     __syncthreads();
-    if (active && part == 0 && lane == 0) {
-        // the kKnn smallest of the entry's wavefronts' lists
-        double* w = wd + qi * kPredWaves * kKnn;
-        const int* wsq = ws + qi * kPredWaves * kKnn;
+    if (tid == 0) {
+        // the kKnn smallest of the wavefronts' lists
         int sum = 0, got = 0;
         for (int r = 0; r < kKnn; r++) {
             int best = -1;
-            for (int i = 0; i < kPredWaves * kKnn; i++)
-                if (w[i] != INFINITY && (best < 0 || w[i] < w[best])) best = i;
+            for (int i = 0; i < kKnnWaves * kKnn; i++)
+                if (wd[i] != INFINITY && (best < 0 || wd[i] < wd[best])) best = i;
             if (best < 0) break;
-            sum += wsq[best];
+            sum += ws[best];
             got++;
-            w[best] = INFINITY;
+            wd[best] = INFINITY;
         }
         S.pred_steps[e] = got ? sum / got : S.steps_hint[src];
     }
@@ -1002,20 +954,12 @@ __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, con
     __syncthreads();
     constexpr int kPer = kSpecSortMax / 1024;
     int bk[kPer], rk[kPer];
-    // every entry's flag and prediction loaded first (one memory round trip, not two per entry)
-    int act[kPer], pst[kPer];
-#pragma unroll
-    for (int q = 0; q < kPer; q++) {
-        const int i = tid + q * 1024;
-        act[q] = (i < C) ? 1 : (i < n_all) ? (int)S.cand_active[i - C] : 0;
-        pst[q] = (i < n_all) ? S.pred_steps[i] : 0;
-    }
     for (int q = 0; q < kPer; q++) {
         const int i = tid + q * 1024;
         bk[q] = -1;
-        const bool on = act[q] != 0;
+        const bool on = (i < C) || (i < n_all && S.cand_active[i - C]);
         if (on) {
-            int h = pst[q];
+            int h = S.pred_steps[i];
             h = h < 0 ? 0 : (h >> 1);
             h = h > kSpecBuckets - 1 ? kSpecBuckets - 1 : h;
             bk[q] = kSpecBuckets - 1 - h;  // longest first
@@ -1065,30 +1009,12 @@ __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, con
         if (pos_of[i] >= 0) S.batch_src[pos_of[i]] = i;
         if (S.batch_pos) S.batch_pos[i] = pos_of[i];
     }
-    // the rows in batch order: eight loads in flight per thread before their stores (the copy was a
-    // chain of dependent load-store round trips)
-    constexpr int U = 16;
-    for (int t0 = tid; t0 < n_all * d; t0 += U * 1024) {
-        double v[U];
-        int64_t dst[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const int t = t0 + u * 1024;
-            dst[u] = -1;
-            v[u] = 0.0;
-            if (t < n_all * d) {
-                const int id = t / d, j = t - id * d;
-                const int p = pos_of[id];
-                if (p >= 0) {
-                    const double* src = (id < C) ? prop + (int64_t)id * d : S.cand_x + (int64_t)(id - C) * d;
-                    v[u] = src[j];
-                    dst[u] = (int64_t)p * d + j;
-                }
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++)
-            if (dst[u] >= 0) S.batch_x[dst[u]] = v[u];
+    for (int t = tid; t < n_all * d; t += blockDim.x) {
+        const int id = t / d, j = t - id * d;
+        const int p = pos_of[id];
+        if (p < 0) continue;
+        const double* src = (id < C) ? prop + (int64_t)id * d : S.cand_x + (int64_t)(id - C) * d;
+        S.batch_x[(int64_t)p * d + j] = src[j];
     }
 }
 
@@ -1368,9 +1294,9 @@ int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* par
     if (C <= 0 || d <= 0 || C * (1 + BCM3HIP_SPEC_SLOTS) > kSpecSortMax || !prop || !partner || !inv_scale ||
         first_round < 0 || !spec_ok(spec) || !spec->pred_steps)
         return BCM3HIP_ERR_ARG;
-    const int n_all = C * (1 + BCM3HIP_SPEC_SLOTS);
-    hipLaunchKernelGGL(ptmh_spec_predict_kernel, dim3((n_all + kPredQ - 1) / kPredQ), dim3(64 * kPredQ * kPredWaves),
-                       kPredLdsBytes, (hipStream_t)stream, C, d, prop, partner, inv_scale, *spec);
+    hipLaunchKernelGGL(ptmh_spec_predict_kernel, dim3(C * (1 + BCM3HIP_SPEC_SLOTS)), dim3(64 * kKnnWaves), 0,
+                       (hipStream_t)stream,
+                       C, d, prop, partner, inv_scale, *spec);
     hipLaunchKernelGGL(ptmh_spec_batch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, prop, partner,
                        first_round, *spec);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;

@@ -479,6 +479,69 @@ def cellpop_cpu_baseline(draws, budget_s: float):
                       "(reference CVODE 5.3.0 + PartialPivLUExtended per cell, experiment logic restated)"}
 
 
+def circular_in_sampler(device, seed, steps=400, warmup=40):
+    """Config C2 in the sampler: the C++ PT-MH loop (bcm3_ptmh_iterate) over the
+    circular-ridge likelihood, 256 chains on this GPU -- the config where the sampler loop itself, not
+    the likelihood, is the cost. Rate = chains x iterations / wall time, timed like the headline
+    (synchronize on both sides)."""
+    import torch
+    from bcm3_amd.likelihood import Likelihood
+    from bcm3_amd.ptmh import PTMHNative
+    lik, pri = os.path.join(GOLDEN, "circular_likelihood.xml"), os.path.join(GOLDEN, "circular_prior.xml")
+    ll = Likelihood(lik, pri, device=device.index or 0)
+    s = PTMHNative(ll, pri, 256, seed=seed)
+    try:
+        s.iterate(warmup)
+        s.synchronize()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s.iterate(steps)
+        s.synchronize()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        c = s.counters()
+    finally:
+        s.close()
+        ll.close()
+    return {"chains": 256, "iterations": steps, "evals_per_s": 256 * steps / dt, "ms_per_iteration": dt / steps * 1e3,
+            "likelihood_launches_per_iteration": c["likelihood_launches"] / max(1, c["iterations"]),
+            "sampler_loop": "C++ host loop (libbcm3.so bcm3_ptmh_iterate), every kernel of the iteration on the GPU",
+            "data": "synthetic; chains start at prior draws"}
+
+
+def circular_cpu_baseline(budget_s: float, seed: int):
+    """The C2 likelihood on the host cores: TestLikelihoodCircular::EvaluateLogProbability restated in C
+    (oracle/liboracle.so orc_circular_eval, TestLikelihoodCircular.cpp:42-53) over uniform draws, one
+    batch per thread. The likelihood alone: the reference's loop adds its proposals, accepts and
+    exchanges on top of this, so this is an upper bound of its rate (the reference sampler needs Boost,
+    absent here)."""
+    import concurrent.futures as cf
+    import ctypes
+    sys.path[:0] = [os.path.join(ROOT, "oracle")]
+    import numpy as np
+    import oracle as O
+    orc = O.Oracle("restated")
+    cores = host_cores()
+    per = 1 << 16
+    rng = np.random.default_rng(seed)
+    xs = [rng.uniform(-6.0, 6.0, size=(per, 2)) for _ in range(cores)]
+    outs = [np.empty(per) for _ in range(cores)]
+    fn = orc.lib.orc_circular_eval
+
+    def one(k):
+        fn(per, 2, 2.0, 3.5, 0.1, xs[k].ctypes.data, outs[k].ctypes.data)
+
+    n, t0 = 0, time.perf_counter()
+    with cf.ThreadPoolExecutor(cores) as pool:
+        while time.perf_counter() - t0 < budget_s:
+            list(pool.map(one, range(cores)))
+            n += per * cores
+    el = time.perf_counter() - t0
+    return {"value": n / el, "unit": "log-likelihood evals/sec", "cores": cores, "kind": "port",
+            "sample": f"{n} uniform draws in [-6, 6]^2 of the circular ridge (dimension 2, offset 3.5, radius 2, "
+                      f"width 0.1), {cores} threads, {el:.1f} s; the likelihood alone (no proposals / accepts)"}
+
+
 def extra_workloads(device, seed):
     """Secondary lines (not the headline): the P=64 population variant of C3 (256 chains x 64
     patient trajectories per launch) and config C2 (circular ridge, 256 chains)."""
@@ -498,6 +561,7 @@ def extra_workloads(device, seed):
             rec["trajectories_per_s"] = 64 * n / (ms * 1e-3)
         out[tag] = rec
         ll.close()
+    out["circular_256chains"]["in_sampler"] = circular_in_sampler(device, seed)
     out.update(expm_workloads(device, gen))
     out["cellpop_c4_64chains"] = cellpop_workload(device, gen)
     return out
@@ -713,6 +777,8 @@ def main():
                     extra[tag]["cpu_baseline"] = rec
             if "popk_p64_256chains" in extra:
                 extra["popk_p64_256chains"]["cpu_baseline"] = p64_cpu_baseline(6.0, args.seed)
+            if "circular_256chains" in extra:
+                extra["circular_256chains"]["cpu_baseline"] = circular_cpu_baseline(2.0, args.seed)
             if "cellpop_c4_64chains" in extra:
                 extra["cellpop_c4_64chains"]["cpu_baseline"] = cellpop_cpu_baseline(extra["cellpop_c4_64chains"]["draws"], 8.0)
     for rec in extra.values():

@@ -16,3 +16,11 @@ for i in 1 2; do
 timeout -k 10 300 python bench.py --steps 60 --warmup 6 --cpu-seconds 0 --extras 0 --throughput-batch 0 --issue-probe 0 --strong-chains 0 > $O/bench_short$i.json 2> $O/bench_short.err
 python3 -c "import json; d=json.load(open('$O/bench_short$i.json')); print('bench', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_avg'], d['kernel_share_of_step'])"
 done
+timeout -k 10 200 python -c "
+import json, torch, bench
+print('circular in sampler', json.dumps(bench.circular_in_sampler(torch.device('cuda', 0), 1)))" > $O/c2_in_sampler.txt 2>&1 || true
+tail -1 $O/c2_in_sampler.txt
+if [ -f gpuvar/uni_cold.so ]; then
+  timeout -k 10 600 python tools/flag_diff.py gpuvar/product.so gpuvar/uni_cold.so > $O/flag_diff.txt 2>&1
+  tail -4 $O/flag_diff.txt
+fi
