@@ -270,6 +270,7 @@ struct SamplerPTDevice::Impl {
     DevBuf<int32_t> sp_cand_sel, sp_cand_upd, sp_cand_steps, sp_steps_hint, sp_steps_prop, sp_batch_status,
         sp_batch_steps, sp_batch_src, sp_batch_n, sp_err;
     DevBuf<int32_t> sp_pos;    // batch position of each entry (bcm3hip_spec::batch_pos)
+    DevBuf<float> sp_xs;       // the batch's scaled single-precision coordinates (bcm3hip_spec::batch_xs)
     DevBuf<int64_t> sp_total;  // entries of all speculative batches (bcm3hip_spec::batch_total)
     DevBuf<uint8_t> sp_cand_active, acc_mut, acc_mut2, acc_exc;
     DevBuf<int32_t> partner[2], pair_first[2];
@@ -714,6 +715,16 @@ struct SamplerPTDevice::Impl {
                       "ptmh_spec_track");
     }
 
+    // can the rest of a pair after its likelihood launch run as one spec_tail launch: a single rank
+    // whose exchange pairs cover every chain in round r + 1 (PairExchange's one-launch case), and no
+    // sample output copied between the two iterations (Emit after iteration r)
+    bool TailFusable() const
+    {
+        const int st = (int)(round % 2);
+        return cfg.world == 1 && mask_all[st] && Ctot >= 2 && C <= 4096 && S.batch_pos &&
+               !(out_on && (cnt.samples_done + 1) % cfg.use_every_nth == 0) && getenv("BCM3_NO_SPEC_TAIL") == nullptr;
+    }
+
     bool IterationPair(bool last)
     {
         if (!PairExchange()) return false;
@@ -753,6 +764,32 @@ struct SamplerPTDevice::Impl {
                                                           S.batch_llh, S.batch_status, S.batch_steps, stream)) {
             LOGERROR("EvaluateLogProbabilityBatchDeviceCounted failed");
             return false;
+        }
+        if (TailFusable()) {
+            // accept r, the exchange round of r + 1 and accept r + 1 in one launch (spec_tail: the three
+            // launches below in one workgroup); the host's bookkeeping in the same order
+            const int st = (int)(round % 2);
+            const bool wrap_local = (Ctot - 1 - st) % 2 == 0;
+            int64_t attempted = wrap_local ? 1 : 0;
+            for (int64_t i = 0; i + 1 < C; i++)
+                if (((g0 + i - st) % 2 + 2) % 2 == 0) attempted++;
+            if (!Launch(bcm3hip_ptmh_spec_tail((int)C, d, g0, st, wrap_local ? 1 : 0, temps.p, partner[st].p,
+                                               pair_first[st].p, acc_mut.p, acc_mut2.p, acc_exc.p, cross_acc.p,
+                                               sp_remote.p, acc_mutate.p, acc_exchange.p, &S, prop.p, lprior_prop.p,
+                                               log_mh.p, llh_prop.p, cfg.learning_rate, values.p, lprior.p, llh.p, lpp.p,
+                                               nan_flag.p, &P, cfg.seed, (uint64_t)iter, (uint64_t)round, H, sub, hist.p,
+                                               hcount.p, sp_err.p, stream),
+                        "ptmh_spec_tail"))
+                return false;
+            cnt.attempted_mutate += C;
+            iter++;
+            if (!PostIteration(false)) return false;  // (no device work: TailFusable)
+            cnt.attempted_exchange += attempted;
+            round++;
+            cnt.attempted_mutate += C;
+            iter++;
+            spec_pairs++;
+            return PostIteration(last);
         }
         // the batch's results to their chains, accept r, its dispatch-order tracking and the history
         // add in one launch (spec_commit reads the batch through S.batch_pos: no spec_scatter launch)
@@ -822,7 +859,7 @@ struct SamplerPTDevice::Impl {
                   acc_mut2.alloc(C) &&
                   acc_exc.alloc(C) && sp_send_last.alloc(2 * d) && sp_send_first.alloc(2 * d) &&
                   sp_remote.alloc(4 * d) && cross_acc.alloc(2) && sp_pred.alloc(N) && sp_inv_scale.alloc(d) &&
-                  sp_total.alloc(1) && sp_pos.alloc(N);
+                  sp_total.alloc(1) && sp_pos.alloc(N) && sp_xs.alloc(N * d);
         for (int st = 0; st < 2 && ok; st++) ok = partner[st].alloc(C) && pair_first[st].alloc(C);
         if (!ok) {
             LOGERROR("SamplerPTDevice: speculative buffers could not be allocated");
@@ -883,6 +920,7 @@ struct SamplerPTDevice::Impl {
         S.pred_steps = sp_pred.p;
         S.batch_total = sp_total.p;
         S.batch_pos = sp_pos.p;
+        S.batch_xs = sp_xs.p;
         return true;
     }
 

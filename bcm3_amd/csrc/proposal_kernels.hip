@@ -664,7 +664,7 @@ __global__ void __launch_bounds__(64) ptmh_propose_adaptive_kernel(
 }
 
 // Sampler::TestSample / MutateMove's accept of chain c (one thread per chain); returns the flag
-__device__ bool accept_one(int c, int d, const double* __restrict__ temps, const double* __restrict__ prop,
+__device__ __forceinline__ bool accept_one(int c, int d, const double* __restrict__ temps, const double* __restrict__ prop,
                            const double* __restrict__ lprior_prop, const double* __restrict__ llh_prop,
                            const double* __restrict__ log_mh, double learning_rate, double* __restrict__ values,
                            double* __restrict__ lprior, double* __restrict__ llh, double* __restrict__ lpp,
@@ -730,7 +730,7 @@ __global__ void ptmh_accept_adaptive_kernel(int C, int d, const double* __restri
 
 // SampleHistory::AddSample for the chains with T != 0 (and mask[c] != 0 when a mask is given):
 // every `subsampling`-th call stores the values as float in slot n % H of the chain's ring
-__device__ void history_one(int c, int d, int H, int subsampling, const double* __restrict__ temps,
+__device__ __forceinline__ void history_one(int c, int d, int H, int subsampling, const double* __restrict__ temps,
                             const double* __restrict__ values, const uint8_t* __restrict__ mask,
                             float* __restrict__ hist, int64_t* __restrict__ counters)
 {
@@ -868,6 +868,33 @@ __global__ void __launch_bounds__(64 * kKnnWaves) ptmh_spec_predict_kernel(int C
         bd[q] = INFINITY;
         bs[q] = 0;
     }
+    if (S.batch_xs) {
+        // (round 6) the previous entries as single-precision coordinates pre-scaled by 1 / prior sd,
+        // written by the batch kernel: half the L2 traffic of the double rows, which bounded this
+        // kernel; the distances only order the launch
+        __shared__ float qs[64];
+        if (tid < d) qs[tid] = (float)(x[tid] * inv_scale[tid]);
+        __syncthreads();
+        for (int m = tid; m < mem_n; m += 64 * kKnnWaves) {
+            const float* y = S.batch_xs + (int64_t)m * d;
+            float dist = 0.0f;
+            for (int j = 0; j < d; j++) {
+                const float t = qs[j] - y[j];
+                dist = __builtin_fmaf(t, t, dist);
+            }
+            if (dist < bd[kKnn - 1]) {
+                int q = kKnn - 1;
+                const int st = S.batch_steps[m];
+                while (q > 0 && bd[q - 1] > dist) {
+                    bd[q] = bd[q - 1];
+                    bs[q] = bs[q - 1];
+                    q--;
+                }
+                bd[q] = dist;
+                bs[q] = st;
+            }
+        }
+    } else
     for (int m = tid; m < mem_n; m += 64 * kKnnWaves) {
         const double* y = S.batch_x + (int64_t)m * d;
         double dist = 0.0;
@@ -943,7 +970,7 @@ constexpr int kSpecSortMax = 4096;
 constexpr int kSpecBuckets = 2048;
 __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, const double* __restrict__ prop,
                                                                const int32_t* __restrict__ partner, int first_round,
-                                                               bcm3hip_spec S)
+                                                               const double* __restrict__ inv_scale, bcm3hip_spec S)
 {
     __shared__ int cnt[kSpecBuckets];
     __shared__ int wsum[16];
@@ -1014,7 +1041,9 @@ __global__ void __launch_bounds__(1024) ptmh_spec_batch_kernel(int C, int d, con
         const int p = pos_of[id];
         if (p < 0) continue;
         const double* src = (id < C) ? prop + (int64_t)id * d : S.cand_x + (int64_t)(id - C) * d;
-        S.batch_x[(int64_t)p * d + j] = src[j];
+        const double v = src[j];
+        S.batch_x[(int64_t)p * d + j] = v;
+        if (S.batch_xs) S.batch_xs[(int64_t)p * d + j] = (float)(v * inv_scale[j]);
     }
 }
 
@@ -1033,7 +1062,7 @@ __global__ void ptmh_spec_scatter_kernel(int C, bcm3hip_spec S, double* __restri
 }
 
 // one thread per chain: the candidate that the accept of r and the exchange of r + 1 made real
-__device__ void select_one(int c, int d, const double* __restrict__ temps, const int32_t* __restrict__ partner,
+__device__ __forceinline__ void select_one(int c, int d, const double* __restrict__ temps, const int32_t* __restrict__ partner,
                            const int32_t* __restrict__ pair_first, const uint8_t* __restrict__ acc_mut,
                            const uint8_t* __restrict__ acc_exc, const uint8_t* __restrict__ cross_acc,
                            const double* __restrict__ remote, const double* __restrict__ values, const bcm3hip_spec& S,
@@ -1106,21 +1135,19 @@ __global__ void ptmh_spec_select_kernel(int C, int d, const double* __restrict__
 // per chain the operations of ptmh_spec_select / ptmh_accept_adaptive / ptmh_spec_track_accept /
 // history_add in that order. Every write is to the thread's own chain; the one cross-chain read, the
 // partner's accept flag of iteration r in select, comes from acc_prev, never from acc_out.
-__global__ void ptmh_spec_commit_kernel(int C, int d, int select, const double* __restrict__ temps,
-                                        const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first,
-                                        const uint8_t* __restrict__ acc_prev, const uint8_t* __restrict__ acc_exc,
-                                        const uint8_t* __restrict__ cross_acc, const double* __restrict__ remote,
-                                        bcm3hip_spec S, double* __restrict__ prop, double* __restrict__ lprior_prop,
-                                        double* __restrict__ log_mh, double* __restrict__ llh_prop,
-                                        double learning_rate, double* __restrict__ values, double* __restrict__ lprior,
-                                        double* __restrict__ llh, double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
-                                        unsigned long long* __restrict__ accepted, int32_t* __restrict__ nan_llh,
-                                        bcm3hip_proposal P, int64_t chain0, uint64_t seed, uint64_t iter, int H,
-                                        int subsampling, float* __restrict__ hist, int64_t* __restrict__ counters,
-                                        int32_t* __restrict__ error)
+__device__ __forceinline__ void commit_one(int c, int C, int d, int select, const double* __restrict__ temps,
+                           const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first,
+                           const uint8_t* __restrict__ acc_prev, const uint8_t* __restrict__ acc_exc,
+                           const uint8_t* __restrict__ cross_acc, const double* __restrict__ remote,
+                           const bcm3hip_spec& S, double* __restrict__ prop, double* __restrict__ lprior_prop,
+                           double* __restrict__ log_mh, double* __restrict__ llh_prop, double learning_rate,
+                           double* __restrict__ values, double* __restrict__ lprior, double* __restrict__ llh,
+                           double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
+                           unsigned long long* __restrict__ accepted, int32_t* __restrict__ nan_llh,
+                           const bcm3hip_proposal& P, int64_t chain0, uint64_t seed, uint64_t iter, int H,
+                           int subsampling, float* __restrict__ hist, int64_t* __restrict__ counters,
+                           int32_t* __restrict__ error)
 {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= C) return;
     if (!select && S.batch_pos) {
         // the batch's results of this chain's entries -- its proposal and its candidates -- through
         // the inverse permutation (ptmh_spec_scatter_kernel's writes for chain c, in this launch)
@@ -1145,6 +1172,26 @@ __global__ void ptmh_spec_commit_kernel(int C, int d, int select, const double* 
                                 lpp, acc_out, accepted, nan_llh, P, chain0, seed, iter);
     if (acc) S.steps_hint[c] = S.steps_prop[c];
     if (hist) history_one(c, d, H, subsampling, temps, values, nullptr, hist, counters);
+}
+
+__global__ void ptmh_spec_commit_kernel(int C, int d, int select, const double* __restrict__ temps,
+                                        const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first,
+                                        const uint8_t* __restrict__ acc_prev, const uint8_t* __restrict__ acc_exc,
+                                        const uint8_t* __restrict__ cross_acc, const double* __restrict__ remote,
+                                        bcm3hip_spec S, double* __restrict__ prop, double* __restrict__ lprior_prop,
+                                        double* __restrict__ log_mh, double* __restrict__ llh_prop,
+                                        double learning_rate, double* __restrict__ values, double* __restrict__ lprior,
+                                        double* __restrict__ llh, double* __restrict__ lpp, uint8_t* __restrict__ acc_out,
+                                        unsigned long long* __restrict__ accepted, int32_t* __restrict__ nan_llh,
+                                        bcm3hip_proposal P, int64_t chain0, uint64_t seed, uint64_t iter, int H,
+                                        int subsampling, float* __restrict__ hist, int64_t* __restrict__ counters,
+                                        int32_t* __restrict__ error)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= C) return;
+    commit_one(c, C, d, select, temps, partner, pair_first, acc_prev, acc_exc, cross_acc, remote, S, prop, lprior_prop,
+               log_mh, llh_prop, learning_rate, values, lprior, llh, lpp, acc_out, accepted, nan_llh, P, chain0, seed,
+               iter, H, subsampling, hist, counters, error);
 }
 
 // dispatch-order bookkeeping of the pairs: steps_hint[c] = BDF steps of the solve of the state now in
@@ -1178,11 +1225,12 @@ __global__ void __launch_bounds__(1024) ptmh_spec_track_exchange_kernel(int C, c
 // pair after them, the dispatch-order tracking of the round (ptmh_spec_track_exchange_kernel) and
 // SampleHistory::AddSample of every chain (ExchangeMove adds both chains of each pair,
 // SamplerPTChain.cpp:374-379; history_add_kernel) -- the same per-chain operations in the same order.
-__global__ void __launch_bounds__(1024) ptmh_spec_exchange_kernel(
-    int C, int d, int64_t g0, int start, int wrap_local, const double* temps, double* values, double* llh,
-    double* lprior, double* lpp, uint8_t* acc_mask, unsigned long long* accepted, uint64_t seed, uint64_t round,
-    const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first, bcm3hip_spec S, int H,
-    int subsampling, float* __restrict__ hist, int64_t* __restrict__ counters)
+__device__ __forceinline__ void exchange_round(int C, int d, int64_t g0, int start, int wrap_local, const double* temps, double* values,
+                               double* llh, double* lprior, double* lpp, uint8_t* acc_mask,
+                               unsigned long long* accepted, uint64_t seed, uint64_t round,
+                               const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first,
+                               const bcm3hip_spec& S, int H, int subsampling, float* __restrict__ hist,
+                               int64_t* __restrict__ counters)
 {
     const int par = (int)(((g0 - start) % 2 + 2) % 2);
     for (int p = threadIdx.x;; p += blockDim.x) {
@@ -1206,6 +1254,47 @@ __global__ void __launch_bounds__(1024) ptmh_spec_exchange_kernel(
         S.steps_hint[c] = v[n];
         if (hist) history_one(c, d, H, subsampling, temps, values, nullptr, hist, counters);
     }
+}
+
+__global__ void __launch_bounds__(1024) ptmh_spec_exchange_kernel(
+    int C, int d, int64_t g0, int start, int wrap_local, const double* temps, double* values, double* llh,
+    double* lprior, double* lpp, uint8_t* acc_mask, unsigned long long* accepted, uint64_t seed, uint64_t round,
+    const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first, bcm3hip_spec S, int H,
+    int subsampling, float* __restrict__ hist, int64_t* __restrict__ counters)
+{
+    exchange_round(C, d, g0, start, wrap_local, temps, values, llh, lprior, lpp, acc_mask, accepted, seed, round, partner,
+                   pair_first, S, H, subsampling, hist, counters);
+}
+
+// The end of a speculative pair of a single-rank ladder in ONE workgroup (round 6): the commit of
+// iteration r (ptmh_spec_commit_kernel, select = 0), the exchange round of r + 1
+// (ptmh_spec_exchange_kernel) and the commit of r + 1 (select = 1) -- the three launches' per-chain
+// operations in their order, a workgroup barrier where a kernel boundary was (each phase reads what the
+// previous ones wrote: partners' accept flags, the exchanged states). Saves two launches and their
+// memory round trips per pair.
+__global__ void __launch_bounds__(1024) ptmh_spec_tail_kernel(
+    int C, int d, int64_t g0, int start, int wrap_local, const double* __restrict__ temps,
+    const int32_t* __restrict__ partner, const int32_t* __restrict__ pair_first, uint8_t* __restrict__ acc_mut,
+    uint8_t* __restrict__ acc_mut2, uint8_t* __restrict__ acc_exc, const uint8_t* __restrict__ cross_acc,
+    const double* __restrict__ remote, unsigned long long* __restrict__ acc_mutate,
+    unsigned long long* __restrict__ acc_exchange, bcm3hip_spec S, double* __restrict__ prop,
+    double* __restrict__ lprior_prop, double* __restrict__ log_mh, double* __restrict__ llh_prop, double learning_rate,
+    double* __restrict__ values, double* __restrict__ lprior, double* __restrict__ llh, double* __restrict__ lpp,
+    int32_t* __restrict__ nan_llh, bcm3hip_proposal P, uint64_t seed, uint64_t iter, uint64_t round, int H,
+    int subsampling, float* __restrict__ hist, int64_t* __restrict__ counters, int32_t* __restrict__ error)
+{
+    for (int c = threadIdx.x; c < C; c += blockDim.x)
+        commit_one(c, C, d, 0, temps, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, S, prop, lprior_prop, log_mh,
+                   llh_prop, learning_rate, values, lprior, llh, lpp, acc_mut, acc_mutate, nan_llh, P, g0, seed, iter, H,
+                   subsampling, hist, counters, error);
+    __syncthreads();
+    exchange_round(C, d, g0, start, wrap_local, temps, values, llh, lprior, lpp, acc_exc, acc_exchange, seed, round,
+                   partner, pair_first, S, H, subsampling, hist, counters);
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += blockDim.x)
+        commit_one(c, C, d, 1, temps, partner, pair_first, acc_mut, acc_exc, cross_acc, remote, S, prop, lprior_prop,
+                   log_mh, llh_prop, learning_rate, values, lprior, llh, lpp, acc_mut2, acc_mutate, nan_llh, P, g0, seed,
+                   iter + 1, H, subsampling, hist, counters, error);
 }
 
 bool proposal_ok(const bcm3hip_proposal* P, int C, int d)
@@ -1298,7 +1387,7 @@ int bcm3hip_ptmh_spec_batch(int C, int d, const double* prop, const int32_t* par
                        (hipStream_t)stream,
                        C, d, prop, partner, inv_scale, *spec);
     hipLaunchKernelGGL(ptmh_spec_batch_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, prop, partner,
-                       first_round, *spec);
+                       first_round, inv_scale, *spec);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 
@@ -1360,6 +1449,27 @@ int bcm3hip_ptmh_spec_exchange(int C, int d, int64_t g0, int start, int wrap_loc
     hipLaunchKernelGGL(ptmh_spec_exchange_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, g0, start,
                        wrap_local, temps, values, llh, lprior, lpp, acc_exchange, (unsigned long long*)accepted, seed,
                        round, partner, pair_first, *spec, H, subsampling, history, counters);
+    return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
+}
+
+int bcm3hip_ptmh_spec_tail(int C, int d, int64_t g0, int start, int wrap_local, const double* temps,
+                           const int32_t* partner, const int32_t* pair_first, uint8_t* acc_mut, uint8_t* acc_mut2,
+                           uint8_t* acc_exc, const uint8_t* cross_acc, const double* remote, uint64_t* accepted_mutate,
+                           uint64_t* accepted_exchange, const bcm3hip_spec* spec, double* prop, double* lprior_prop,
+                           double* log_mh, double* llh_prop, double learning_rate, double* values, double* lprior,
+                           double* llh, double* lpp, int32_t* nan_llh, const bcm3hip_proposal* proposal, uint64_t seed,
+                           uint64_t iter, uint64_t round, int H, int subsampling, float* history, int64_t* counters,
+                           int32_t* error, void* stream)
+{
+    if (C < 2 || C > 4096 || d <= 0 || !spec_ok(spec) || !spec->batch_pos || !proposal_ok(proposal, C, d) || !temps ||
+        !partner || !pair_first || !acc_mut || !acc_mut2 || acc_mut == acc_mut2 || !acc_exc || !prop || !lprior_prop ||
+        !log_mh || !llh_prop || !values || !lprior || !llh || !lpp || (history && (H <= 0 || subsampling <= 0 || !counters)))
+        return BCM3HIP_ERR_ARG;
+    hipLaunchKernelGGL(ptmh_spec_tail_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, d, g0, start, wrap_local,
+                       temps, partner, pair_first, acc_mut, acc_mut2, acc_exc, cross_acc, remote,
+                       (unsigned long long*)accepted_mutate, (unsigned long long*)accepted_exchange, *spec, prop,
+                       lprior_prop, log_mh, llh_prop, learning_rate, values, lprior, llh, lpp, nan_llh, *proposal, seed,
+                       iter, round, H, subsampling, history, counters, error);
     return hipGetLastError() == hipSuccess ? 0 : BCM3HIP_ERR_HIP;
 }
 

@@ -558,6 +558,8 @@ typedef struct {
     int32_t* batch_pos;   /* [7C] batch position of each entry (-1: not in the batch), the inverse of
                              batch_src; NULL: not kept. When kept, bcm3hip_ptmh_spec_commit with
                              select = 0 takes the batch's results itself (no spec_scatter launch) */
+    float* batch_xs;      /* [7C][d] the launch's vectors in single precision, scaled by 1 / prior sd
+                             (the dispatch-order predictor's distances); NULL: not kept */
 } bcm3hip_spec;
 /* candidates of iteration iter_next = r + 1 (after bcm3hip_ptmh_propose_adaptive of iteration r, whose
  * proposals are in prop); partner[c] = exchange partner of chain c in round r + 1 (-1 none) */
@@ -614,6 +616,20 @@ int bcm3hip_ptmh_spec_exchange(int C, int d, int64_t g0, int start, int wrap_loc
 /* dispatch-order bookkeeping (steps_hint = BDF steps of the solve of the state in each slot): after an
  * accept (acc_mutate: the proposals' steps, steps_prop, become the states') or, with acc_mutate NULL,
  * after an exchange round (acc_exchange indexed by pair_first, partner as in spec_select) */
+/* The end of a speculative pair on a single-rank ladder whose exchange pairs cover every chain (the
+ * condition of bcm3hip_ptmh_spec_exchange) in ONE launch: bcm3hip_ptmh_spec_commit(select = 0,
+ * iteration `iter`, flags to acc_mut), bcm3hip_ptmh_spec_exchange(start, wrap_local, round; flags to
+ * acc_exc) and bcm3hip_ptmh_spec_commit(select = 1, iteration iter + 1, acc_prev = acc_mut, flags to
+ * acc_mut2) -- bit-identical to the three launches (SamplerPT.cpp:203-212 twice). spec->batch_pos is
+ * required (the first commit reads the batch through it); C <= 4096. */
+int bcm3hip_ptmh_spec_tail(int C, int d, int64_t g0, int start, int wrap_local, const double* temps,
+                           const int32_t* partner, const int32_t* pair_first, uint8_t* acc_mut, uint8_t* acc_mut2,
+                           uint8_t* acc_exc, const uint8_t* cross_acc, const double* remote, uint64_t* accepted_mutate,
+                           uint64_t* accepted_exchange, const bcm3hip_spec* spec, double* prop, double* lprior_prop,
+                           double* log_mh, double* llh_prop, double learning_rate, double* values, double* lprior,
+                           double* llh, double* lpp, int32_t* nan_llh, const bcm3hip_proposal* proposal, uint64_t seed,
+                           uint64_t iter, uint64_t round, int H, int subsampling, float* history, int64_t* counters,
+                           int32_t* error, void* stream);
 int bcm3hip_ptmh_spec_track(int C, const uint8_t* acc_mutate, const int32_t* partner, const int32_t* pair_first,
                             const uint8_t* acc_exchange, const bcm3hip_spec* spec, void* stream);
 /* The propose kernel's mixture arithmetic (GMM::CalculateResponsibilities, src/stats/GMM.cpp:172-186,
