@@ -476,7 +476,12 @@ def cellpop_cpu_baseline(draws, budget_s: float):
     el = time.perf_counter() - t0
     return {"value": done / el, "unit": "log-likelihood evals/sec", "cores": cores, "kind": "reference",
             "sample": f"{done} of the GPU line's prior draws, one evaluation per thread on {cores} threads, {el:.1f} s "
-                      "(reference CVODE 5.3.0 + PartialPivLUExtended per cell, experiment logic restated)"}
+                      "(reference CVODE 5.3.0 + PartialPivLUExtended per cell, experiment logic restated)",
+            "threading": "one evaluation per host thread, cells in the reference's FIFO order; the reference itself "
+                         "runs one evaluation per sampling thread AND evaluation_threads auxiliary threads per "
+                         "experiment (Experiment.cpp:691-782), which splits an evaluation's cells across cores -- "
+                         "lower latency per evaluation, the same cores for the same total work, so at most this "
+                         "throughput when every core is busy"}
 
 
 def circular_in_sampler(device, seed, steps=400, warmup=40):

@@ -24,3 +24,7 @@ if [ -f gpuvar/uni_cold.so ]; then
   timeout -k 10 600 python tools/flag_diff.py gpuvar/product.so gpuvar/uni_cold.so > $O/flag_diff.txt 2>&1
   tail -4 $O/flag_diff.txt
 fi
+if [ -n "$C4P3" ]; then
+  timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FMA_F64 --output-format csv -d $O/c4p3 -o pmc -- python3 tools/cellpop_bench.py 64 2 > $O/c4p3.log 2>&1 || echo "c4 p3 pass failed"
+  tail -3 $O/c4p3.log
+fi
