@@ -290,8 +290,9 @@ class Context:
         return float(ms.value)
 
     def placement_log(self, n_max: int):
-        """(n, 4) uint64 rows of the last PopPK launch with OPT_PLACEMENT_LOG on: HW_ID, XCC_ID,
-        wall clock (100 MHz) at start and at end of each trajectory."""
+        """(n, 4) uint64 rows of the last PopPK launch with OPT_PLACEMENT_LOG on: HW_ID in the low 32 bits
+        of word 0 with the trajectory's shader-clock cycles in its high 32 bits, XCC_ID, wall clock
+        (100 MHz) at start and at end of each trajectory (include/bcm3hip.h)."""
         import numpy as np
         out = np.zeros((n_max, 4), dtype=np.uint64)
         m = lib().bcm3hip_placement_log(self.h, n_max, out.ctypes.data)

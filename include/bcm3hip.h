@@ -412,9 +412,10 @@ int bcm3hip_eval_batch_device_counted(bcm3hip_ctx* ctx, size_t n_max, const int3
                                       double* logp_dev, int32_t* status_dev, int32_t* steps_dev, void* stream);
 int bcm3hip_last_kernel_ms(bcm3hip_ctx* ctx, float* ms);
 /* With BCM3HIP_OPT_PLACEMENT_LOG on: the placement of the trajectories of the most recent PopPK
- * launch, 4 words per trajectory in launch order: the wavefront's HW_ID register (wave, SIMD, CU,
- * shader array, shader engine fields), its XCC_ID register, and the constant-rate wall clock
- * (100 MHz) when the trajectory started and when it finished. Copies min(n_max, trajectories) rows
+ * launch, 4 words per trajectory in launch order: word 0 packs the wavefront's HW_ID register (wave,
+ * SIMD, CU, shader array, shader engine fields) in its low 32 bits and the shader-clock cycles the
+ * trajectory took (s_memtime difference) in its high 32 bits; word 1 its XCC_ID register; words 2 and
+ * 3 the constant-rate wall clock (100 MHz) when the trajectory started and when it finished. Copies min(n_max, trajectories) rows
  * (synchronises with the launch) and returns that count, or a negative error. */
 int64_t bcm3hip_placement_log(bcm3hip_ctx* ctx, int64_t n_max, uint64_t* host_out);
 /* The observed-to-simulated cell assignment of the time-course data likelihood alone
