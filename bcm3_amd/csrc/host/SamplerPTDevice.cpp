@@ -266,6 +266,7 @@ struct SamplerPTDevice::Impl {
     // speculative iteration pairs (bcm3hip_ptmh_spec_*): candidate / batch buffers, per round parity
     // the exchange partner and the first chain of each chain's pair, accept flags of both moves
     bool spec_on = false;
+    bool spec_tail_on = true;  // BCM3_NO_SPEC_TAIL (read once, SetupSpeculation): the three separate launches
     DevBuf<double> sp_cand_x, sp_cand_lp, sp_cand_lmh, sp_cand_llh, sp_cand_sc, sp_batch_x, sp_batch_llh;
     DevBuf<int32_t> sp_cand_sel, sp_cand_upd, sp_cand_steps, sp_steps_hint, sp_steps_prop, sp_batch_status,
         sp_batch_steps, sp_batch_src, sp_batch_n, sp_err;
@@ -722,7 +723,7 @@ struct SamplerPTDevice::Impl {
     {
         const int st = (int)(round % 2);
         return cfg.world == 1 && mask_all[st] && Ctot >= 2 && C <= 4096 && S.batch_pos &&
-               !(out_on && (cnt.samples_done + 1) % cfg.use_every_nth == 0) && getenv("BCM3_NO_SPEC_TAIL") == nullptr;
+               !(out_on && (cnt.samples_done + 1) % cfg.use_every_nth == 0) && spec_tail_on;
     }
 
     bool IterationPair(bool last)
@@ -844,6 +845,7 @@ struct SamplerPTDevice::Impl {
 
     bool SetupSpeculation()
     {
+        spec_tail_on = getenv("BCM3_NO_SPEC_TAIL") == nullptr;
         spec_on = cfg.speculate != 0 && adaptive && (cfg.world == 1 || transport) && cfg.swapping_scheme == 0 &&
                   cfg.exploration_steps == 1 && Ctot >= 2 && d <= 64 && C * (1 + BCM3HIP_SPEC_SLOTS) <= 4096 &&
                   ll->SupportsCountedBatch();

@@ -337,6 +337,23 @@ def test_speculative_pairs_bit_identical_large_batches(C):
     assert c1["likelihood_launches"] < c0["likelihood_launches"] and c1["evaluated_entries"] > c0["evaluated_entries"]
 
 
+def test_spec_tail_matches_separate_launches(monkeypatch):
+    """the end of a speculative pair in one launch (bcm3hip_ptmh_spec_tail: commit r, exchange r + 1,
+    commit r + 1 in one workgroup) against the three launches it replaces (BCM3_NO_SPEC_TAIL): the
+    same chains and counters bit for bit, 256 chains (the bench's ladder)"""
+    res = []
+    for off in (False, True):
+        if off:
+            monkeypatch.setenv("BCM3_NO_SPEC_TAIL", "1")
+        s = _native(*C3, 256, 29, 0, speculate=1)
+        s.iterate(24)
+        s.synchronize()
+        res.append((s.state(), s.counters()))
+        s.close()
+    _compare(res[0][0], res[1][0])
+    assert _semantic(res[0][1]) == _semantic(res[1][1])
+
+
 def test_speculation_is_used_for_popk():
     """the C3 sampler runs its iterations as speculative pairs: one likelihood launch per two
     iterations (the timing log counts launches)"""
