@@ -50,4 +50,25 @@ struct CpSolveArgs {
     const void* pow_tables;       // xm::GlibcPow (libm_exact.h): glibc's pow for DP5's step-size factor
 };
 
+// The cell work queue of CP_QUEUE builds (cellpop_solver.h cp_queue_kernel, cellpop_rt.cpp): the
+// reference simulates a mother's daughters from a queue as soon as it divides (Experiment.cpp:691-782);
+// here every wavefront of one persistent launch takes the next cells from the queue and enqueues the
+// daughters of the cells it ends. Items are indexed by queue position (qi); the FIFO numbering of the
+// reference is restored afterwards (cp_number_kernel), so every sum runs in the reference's cell order.
+struct CpQueueItem {
+    int32_t slot, eval, parent, sobol_ix, is_initial;  // = bcm3hip::CpInitItem (slot = qi)
+};
+struct CpQueueArgs {
+    CpQueueItem* items;      // [cap]
+    int32_t* ready;          // [cap] 1 once the item is written (initial cells: preset)
+    int32_t* counters;       // [4] head (next item to take), tail (items reserved), outstanding (items
+                             //     not finished), error (a bounded wait ran out)
+    int32_t* child_qi;       // [cap][2] queue indices of the daughters (-1)
+    int32_t* ncells_eval;    // [n] cells of each evaluation (initial cells + daughters enqueued)
+    int32_t* failed_eval;    // [n] a cell failed or a limit was hit: the evaluation is -inf
+    double* creation;        // [cap] the cells' creation times (written by the queue's initialisation)
+    const double* values;    // [n][d]
+    int32_t cap, n0, max_cells, sobol_points, sobol_dims;
+};
+
 }  // namespace cpk

@@ -22,50 +22,11 @@
 #include <cstdint>
 
 #include "../../include/bcm3hip.h"
+#include "cellpop_init.h"
 #include "cellpop_static.h"
 #include "pk_math.h"
 
 namespace bcm3hip {
-
-
-
-__device__ double cp_transform(int32_t tf, double x)
-{
-    // VariableSet::TransformVariable (src/sampler/VariableSet.cpp:97-124)
-    switch (tf) {
-    case BCM3HIP_TF_LOG: return exp(x);
-    case BCM3HIP_TF_LOG10: return exp(x * 2.3025850929940459);  // bcm3::fastpow10
-    case BCM3HIP_TF_LOGIT:
-        if (x > 0) {
-            const double z = exp(-x);
-            return 1.0 / (1.0 + z);
-        } else {
-            const double z = exp(x);
-            return z / (1.0 + z);
-        }
-    default: return x;
-    }
-}
-
-__device__ double cp_ref(const bcm3hip_value_ref& r, const double* values, const int32_t* transforms, double none)
-{
-    if (r.kind == BCM3HIP_REF_VARIABLE) return cp_transform(transforms[r.index], values[r.index]);
-    if (r.kind == BCM3HIP_REF_FIXED) return r.value;
-    return none;
-}
-
-__device__ double cp_apply(int32_t kind, double x, double v)
-{
-    switch (kind) {
-    case BCM3HIP_APPLY_ADDITIVE: return x + v;
-    case BCM3HIP_APPLY_ADDITIVE_LOG: return x + exp(v);
-    case BCM3HIP_APPLY_ADDITIVE_LOG2: return x + pow(2.0, v);
-    case BCM3HIP_APPLY_MULTIPLICATIVE: return x * v;
-    case BCM3HIP_APPLY_MULTIPLICATIVE_LOG: return x * exp(v);
-    case BCM3HIP_APPLY_MULTIPLICATIVE_LOG2: return x * pow(2.0, v);
-    default: return v;  // replace
-    }
-}
 
 
 
@@ -75,67 +36,7 @@ __global__ void cp_init_kernel(CpStatic m, int32_t n_items, const CpInitItem* it
 {
     const int w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= n_items) return;
-    const CpInitItem it = items[w];
-    const double* v = values + (size_t)it.eval * m.d;
-    // Experiment::EvaluateLogProbability's time_offset: the sampled value, before any cell
-    // variability (Experiment.cpp:267-272)
-    if (sync_off) sync_off[it.slot] = cp_ref(m.sync_offset, v, m.transforms, 0.0);
-    double* prm = params + (size_t)it.slot * m.d;
-    double* y = y0 + (size_t)it.slot * m.NS;
-    for (int i = 0; i < m.d; i++) prm[i] = cp_transform(m.transforms[i], v[i]);
-    if (it.parent < 0) {
-        for (int i = 0; i < m.NS; i++) y[i] = m.y_init[i];
-        creation[it.slot] = cp_ref(m.entry_time, v, m.transforms, 0.0);
-    } else {
-        const double* pe = end_y + (size_t)it.parent * m.NS;
-        for (int i = 0; i < m.NS; i++) y[i] = pe[i];
-        for (int r = 0; r < m.n_reset; r++) y[m.reset_index[r]] = m.reset_value[r];
-        creation[it.slot] = achieved[it.parent];
-    }
-    if (m.sobol_dims == 0) return;
-    // pseudorandom vector, diagonal gaussian (VariabilityDescription.cpp:60-67)
-    constexpr int DMAX = 32;
-    double pr[DMAX];
-    const double* sob = m.sobol + (size_t)it.sobol_ix * m.sobol_dims;
-    for (int k = 0; k < m.sobol_dims && k < DMAX; k++)
-        pr[k] = quantile_normal(sob[k], 0.0, 1.0) * exp(cp_ref(m.scales[k], v, m.transforms, 0.0));
-    // full gaussian groups (VariabilityDescription.cpp:69-128): z = QuantileNormal(sobol) and
-    // L(i, j) = exp(scale_i) * prod_{k < i, k <= j} (k == j ? cos : sin)(cov(k, i) * pi), j <= i; the
-    // vector is L z (Eigen's MatrixXd * VectorXd, summed over j in order)
-    const bcm3hip_value_ref* cov = m.covariance;
-    for (int g = 0; g < m.n_full; g++) {
-        const int g0 = m.full_groups[2 * g], D = m.full_groups[2 * g + 1];
-        double z[DMAX];
-        for (int i = 0; i < D; i++) z[i] = quantile_normal(sob[g0 + i], 0.0, 1.0);
-        for (int i = 0; i < D; i++) {
-            const double exp_scale = exp(cp_ref(m.scales[g0 + i], v, m.transforms, 0.0));
-            double acc = 0.0;
-            for (int j = 0; j < D; j++) {
-                double lij = 0.0;
-                if (j <= i) {
-                    lij = exp_scale;
-                    for (int k = 0; k < i; k++) {
-                        if (k <= j) {
-                            const double cv = cp_ref(cov[(i - 1) * i / 2 + k], v, m.transforms, 0.0) * M_PI;
-                            lij *= (k == j) ? cos(cv) : sin(cv);
-                        }
-                    }
-                }
-                acc = (j == 0) ? lij * z[0] : acc + lij * z[j];
-            }
-            pr[g0 + i] = acc;
-        }
-        cov += D * (D - 1) / 2;
-    }
-    for (int a = 0; a < m.n_actions; a++) {
-        const bcm3hip_variability_action act = m.actions[a];
-        if (act.only_initial_cells && !it.is_initial) continue;
-        const double r = act.negate ? -pr[act.dim] : pr[act.dim];
-        if (act.target_kind == 0)
-            prm[act.target_index] = cp_apply(act.apply, prm[act.target_index], r);
-        else
-            y[act.target_index] = cp_apply(act.apply, y[act.target_index], r);
-    }
+    cp_init_cell(m, items[w], values, params, y0, creation, end_y, achieved, sync_off);
 }
 
 // one wavefront per evaluation; lanes over output entries
@@ -954,6 +855,97 @@ hipError_t launch_cp_gather(const int32_t* work, int32_t n, const int32_t* flags
 {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(cp_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, s, work, n, flags, out);
+    return hipGetLastError();
+}
+
+// one workgroup per evaluation: the FIFO numbering level by level -- a generation's cells in cell order,
+// each dividing cell's daughters (child_qi, in enqueue order: first, second) appended by a prefix sum
+__global__ __launch_bounds__(256) void cp_number_kernel(int32_t max_cells, int32_t n0, const int32_t* first_pos,
+                                                        const int32_t* child_qi, const int32_t* failed_eval,
+                                                        int32_t* perm, int32_t* ncells, int32_t* failed,
+                                                        int32_t* sim_child)
+{
+    __shared__ int32_t scan[256];
+    const int e = blockIdx.x, t = threadIdx.x;
+    int32_t* pe = perm + (size_t)e * max_cells;
+    int32_t* sc = sim_child + (size_t)e * max_cells;
+    for (int i = t; i < n0; i += 256) pe[i] = e * n0 + first_pos[i];
+    __syncthreads();
+    int lo = 0, hi = n0;
+    while (lo < hi) {
+        int next = hi;  // the next generation's first slot
+        for (int c0 = lo; c0 < hi; c0 += 256) {
+            const int j = c0 + t;
+            int a = -1, b = -1;
+            if (j < hi) {
+                const int q = pe[j];
+                a = child_qi[2 * q];
+                b = child_qi[2 * q + 1];
+            }
+            const int k = (a >= 0) + (b >= 0);
+            scan[t] = k;
+            __syncthreads();
+            for (int o = 1; o < 256; o <<= 1) {
+                const int v = (t >= o) ? scan[t - o] : 0;
+                __syncthreads();
+                scan[t] += v;
+                __syncthreads();
+            }
+            const int at = next + scan[t] - k;
+            if (j < hi) {
+                sc[j] = (a >= 0 && at < max_cells) ? at : -1;
+                if (a >= 0 && at < max_cells) pe[at] = a;
+                if (b >= 0 && at + 1 < max_cells) pe[at + 1] = b;
+            }
+            next += scan[255];
+            __syncthreads();
+        }
+        lo = hi;
+        hi = next < max_cells ? next : max_cells;
+    }
+    for (int j = hi + t; j < max_cells; j += 256) sc[j] = -1;
+    if (t == 0) {
+        ncells[e] = hi;
+        failed[e] = failed_eval[e];
+    }
+}
+
+hipError_t launch_cp_number(int32_t n, int32_t max_cells, int32_t n0, const int32_t* first_pos, const int32_t* child_qi,
+                            const int32_t* failed_eval, int32_t* perm, int32_t* ncells, int32_t* failed,
+                            int32_t* sim_child, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cp_number_kernel, dim3(n), dim3(256), 0, s, max_cells, n0, first_pos, child_qi, failed_eval, perm,
+                       ncells, failed, sim_child);
+    return hipGetLastError();
+}
+
+// one wavefront per slot, lanes over the cell's entries (coalesced rows)
+__global__ __launch_bounds__(256) void cp_permute_kernel(int32_t max_cells, int32_t M, int32_t NS, const int32_t* perm,
+                                                         const int32_t* ncells, CpCellArrays src, CpCellArrays dst)
+{
+    const int e = blockIdx.y;
+    const int j = blockIdx.x * 4 + (int)threadIdx.x / 64, ln = (int)threadIdx.x & 63;
+    if (j >= ncells[e]) return;
+    const size_t d = (size_t)e * max_cells + j, q = (size_t)perm[d];
+    for (int k = ln; k < M; k += 64) dst.out_values[d * M + k] = src.out_values[q * M + k];
+    for (int k = ln; k < NS; k += 64) dst.end_y[d * NS + k] = src.end_y[q * NS + k];
+    if (ln < 5) dst.event_times[d * 5 + ln] = src.event_times[q * 5 + ln];
+    if (ln == 0) {
+        dst.creation[d] = src.creation[q];
+        dst.sim_end[d] = src.sim_end[q];
+        dst.achieved[d] = src.achieved[q];
+        dst.flags[d] = src.flags[q];
+        dst.nsteps[d] = src.nsteps[q];
+    }
+}
+
+hipError_t launch_cp_permute(int32_t n, int32_t max_cells, int32_t M, int32_t NS, const int32_t* perm,
+                             const int32_t* ncells, CpCellArrays src, CpCellArrays dst, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cp_permute_kernel, dim3((max_cells + 3) / 4, n), dim3(256), 0, s, max_cells, M, NS, perm, ncells,
+                       src, dst);
     return hipGetLastError();
 }
 

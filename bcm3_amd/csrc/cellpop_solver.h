@@ -25,12 +25,18 @@
 #pragma once
 #include "bdf_lane.h"
 #include "cellpop_args.h"
+#if defined(CP_QUEUE) && CP_QUEUE
+#include "cellpop_init.h"
+#endif
 
 namespace cpk {
 using namespace bcm3hip;
 
 #ifndef CP_NTREAT
 #define CP_NTREAT 0
+#endif
+#ifndef CP_QUEUE
+#define CP_QUEUE 0
 #endif
 constexpr int WAVE = 64;
 // A cell's state lives in one ROW of lanes (component i in lane i of the row). With NS <= 16 four
@@ -1327,26 +1333,44 @@ BDF_INL bool interp_time_ok(double t, double tn, double hu)
 #define CP_WAVES_PER_EU ((CP_NS <= 16) ? 2 : 3)
 #endif
 // CP_CELLS_PER_WAVE cells per workgroup (one wavefront): cell blockIdx.x * CPW + row
-extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CP_WAVES_PER_EU))) void cp_solve_kernel(cpk::CpSolveArgs a)
+namespace cpk {
+using CellShared = Shared<CP_NS, CP_NP, CP_NC, CP_M>;
+
+// the work queue's per-row cell inputs in LDS (cp_queue_kernel's init writes them, and sh.prm)
+struct CellIn {
+    double y0[CP_NS];
+    double creation;
+};
+// a cell's end state: read by its daughters' initialisation, which the work queue runs on any wavefront
+// of the launch -- stored device-coherent there (no cache write-back of the whole L2 to publish it)
+__device__ __forceinline__ void st_end(double* p, double v)
 {
-    using namespace cpk;
+#if CP_QUEUE
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
+
+// One cell on this lane's row: Cell::Simulate (Cell.cpp:193-273) from params / y0 / creation[slot] (or,
+// in the work queue, sh.prm and `in`) to the cell's outputs at [slot]; wi = the row's index in the launch
+// (the stored mode's records)
+__device__ __forceinline__ void cp_solve_cell(const CpSolveArgs& a, CellShared& sh, const int slot, const int wi,
+                                              const CellIn* in = nullptr)
+{
     constexpr int NS = CP_NS, NP = CP_NP, NC = CP_NC;
     constexpr int MM = CP_M;
-    __shared__ Shared<NS, NP, NC, MM> shs[CPW];
-    const int wi = (int)blockIdx.x * CPW + row();
-    if (wi >= a.n_work) return;  // the whole row: rows are cells
-    Shared<NS, NP, NC, MM>& sh = shs[row()];
-    const int slot = a.work[wi];
     const int ln = lane();
-    for (int k = ln; k < NP; k += ROW) sh.prm[k] = a.params[(size_t)slot * NP + k];
+    if (!in)
+        for (int k = ln; k < NP; k += ROW) sh.prm[k] = a.params[(size_t)slot * NP + k];
     for (int k = ln; k < NC; k += ROW) sh.cs[k] = a.constant_species[k];
-    const double creation = a.creation[slot];
+    const double creation = in ? in->creation : a.creation[slot];
 #if CP_NTREAT > 0
     sh.treat_times = a.treat_times;
     for (int k = ln; k <= CP_NTREAT; k += ROW) sh.treat_off[k] = a.treat_offset[k];
     sh.creation = creation;
 #endif
-    const double y0 = (ln < NS) ? a.y0[(size_t)slot * NS + ln] : 0.0;
+    const double y0 = (ln < NS) ? (in ? in->y0[ln] : a.y0[(size_t)slot * NS + ln]) : 0.0;
 #if CP_STORED
     // the stored-species slot of this lane's component (-1: not read by the data)
     int my_store = -1;
@@ -1754,7 +1778,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
         const double ct = a.output_times[k] - creation;
         a.out_values[(size_t)slot * M + k] = (!CP_STORED && (ct < 0.0 || ct > sim_end)) ? __builtin_nan("") : outv[k];
     }
-    if (ln < NS) a.end_y[(size_t)slot * NS + ln] = yend;
+    if (ln < NS) st_end(a.end_y + (size_t)slot * NS + ln, yend);
 #ifdef CP_PHASES
     if (ln == 0) sh.ph[5] = clock64() - ph_kernel0;
     wave_sync();
@@ -1768,7 +1792,7 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
         const double achieved_cell_time = (divided || died) ? sim_end : (a.output_times[M - 1] - creation);
 #endif
         a.sim_end[slot] = sim_end;
-        a.achieved[slot] = achieved_cell_time + creation;
+        st_end(a.achieved + slot, achieved_cell_time + creation);
         // bit4: SimulateCell adds two daughters (divide_cells && divide && achieved_time < target)
         const bool spawn = ok && divided && (achieved_cell_time + creation < a.end_time);
         int fl = (ok ? 1 : 0) | (divided ? 2 : 0) | (died ? 4 : 0) | ((ev[3] == ev[3]) ? 8 : 0) | (spawn ? 16 : 0);
@@ -1780,3 +1804,197 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
         a.nsteps[slot] = nst;
     }
 }
+}  // namespace cpk
+
+#if !CP_QUEUE
+// the cells of one generation launch, four per wavefront (one per 16-lane row)
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CP_WAVES_PER_EU))) void cp_solve_kernel(cpk::CpSolveArgs a)
+{
+    __shared__ cpk::CellShared shs[cpk::CPW];
+    const int wi = (int)blockIdx.x * cpk::CPW + cpk::row();
+    if (wi >= a.n_work) return;  // the whole row: rows are cells
+    cpk::cp_solve_cell(a, shs[cpk::row()], a.work[wi], wi);
+}
+#endif
+
+
+#if CP_QUEUE
+namespace cpk {
+// the queue's counters, flags, items and the end states crossing wavefronts: device-scope relaxed atomics
+// (coherent loads and stores across the XCDs' L2s); the order a publication needs is the completion of
+// the earlier stores (q_drain) before the flag, and the flag's value before the later loads
+template <class T> __device__ __forceinline__ T q_load(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <class T> __device__ __forceinline__ void q_store(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ int q_add(int32_t* p, int v) { return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ bool q_cas(int32_t* p, int expected, int desired)
+{
+    return __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+}
+// every memory operation the wavefront issued has completed (and the compiler moves none across)
+__device__ __forceinline__ void q_drain()
+{
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+// a bounded wait: 2^22 polls of >= 512 cycles (seconds) before the launch gives up with the error
+// counter set (a lost item would otherwise keep the persistent grid alive)
+constexpr long kQueueSpins = 1l << 22;
+enum { Q_HEAD = 0, Q_TAIL = 1, Q_OUTSTANDING = 2, Q_ERROR = 3 };
+}  // namespace cpk
+
+// One persistent launch for all cells of a batch. Queue positions are handed out as tickets (one
+// fetch-and-add per wavefront and round, no compare-and-swap retries): each row of a wavefront holds a
+// ticket, and a round solves the rows whose ticket's item is ready -- initialised (cp_init_cell: the
+// parent's end state, the variabilities), solved, and the daughters of the cells that divide enqueued
+// under the failure rules of the generation launches (cellpop_rt.cpp): a failed cell, a daughter
+// beyond max_cells or past the Sobol points fails the evaluation, whose cells then enqueue nothing. A
+// row whose ticket is not filled yet waits while its sisters' cells run; a ticket past the queue's
+// capacity, or one unfilled once no cell is outstanding, ends the row; the wavefront ends with its four
+// rows. (No deadlock: a ticket is unfilled only when every reserved item has been handed out, and a row
+// holding a filled ticket always runs in its wavefront's next round.) Outputs are indexed by queue
+// position; cp_number_kernel and cp_permute_kernel (cellpop_kernels.hip) restore the reference's cell
+// numbering.
+extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CP_WAVES_PER_EU))) void cp_queue_kernel(
+    cpk::CpSolveArgs a, cpk::CpQueueArgs q, bcm3hip::CpStatic m)
+{
+    using namespace cpk;
+    enum { NEED = -1, DONE = -2 };
+    __shared__ CellShared shs[CPW];
+    __shared__ CellIn qin[CPW];
+    __shared__ double qpe[CPW][CP_NS];  // the mother's end state and end time
+    __shared__ double qach[CPW];
+    __shared__ int ticket[CPW];  // the row's queue position, NEED or DONE
+    __shared__ int run[CPW];     // the row's item is ready: it runs this round
+    __shared__ int ndau[CPW], deval[CPW], dsob[CPW][2];  // the daughters a row's cell enqueues
+    const int r = row(), ln = lane();
+    if (threadIdx.x < CPW) ticket[threadIdx.x] = NEED;
+    __syncthreads();
+    long idle = 0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            // tickets for the rows that need one, in row order
+            int need = 0;
+            for (int k = 0; k < CPW; k++) need += ticket[k] == NEED;
+            if (need > 0) {
+                int t = q_add(q.counters + Q_HEAD, need);
+                for (int k = 0; k < CPW; k++)
+                    if (ticket[k] == NEED) ticket[k] = (t < q.cap) ? t++ : DONE;
+            }
+            bool any = false, live = false;
+            for (int k = 0; k < CPW; k++) {
+                run[k] = ticket[k] >= 0 && q_load(q.ready + ticket[k]) == 1;
+                any |= run[k] != 0;
+                live |= ticket[k] >= 0;
+            }
+            if (!any && live) {
+                // nothing ready: tickets still unfilled once no cell is outstanding never fill
+                if (q_load(q.counters + Q_OUTSTANDING) == 0) {
+                    for (int k = 0; k < CPW; k++)
+                        if (ticket[k] >= 0 && q_load(q.ready + ticket[k]) != 1) ticket[k] = DONE;
+                    for (int k = 0; k < CPW; k++) run[k] = ticket[k] >= 0;  // (filled meanwhile)
+                } else if (++idle >= kQueueSpins) {
+                    q_add(q.counters + Q_ERROR, 1);
+                    for (int k = 0; k < CPW; k++) ticket[k] = DONE;
+                } else {
+                    __builtin_amdgcn_s_sleep(8);
+                }
+            }
+            if (any) idle = 0;
+        }
+        __syncthreads();
+        bool all_done = true;
+        for (int k = 0; k < CPW; k++) all_done &= ticket[k] == DONE;
+        if (all_done) return;
+        const bool mine = run[r] != 0;
+        const int qi = ticket[r];
+        __syncthreads();
+        CpQueueItem it{};
+        it.eval = -1;
+        if (mine && ln == 0) {
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the item after its flag
+            CpQueueItem* src = q.items + qi;
+            it.eval = q_load(&src->eval);
+            it.parent = q_load(&src->parent);
+            it.sobol_ix = q_load(&src->sobol_ix);
+            it.is_initial = q_load(&src->is_initial);
+            if (it.parent >= 0) {
+                for (int i = 0; i < CP_NS; i++) qpe[r][i] = q_load(a.end_y + (size_t)it.parent * CP_NS + i);
+                qach[r] = q_load(a.achieved + it.parent);
+            }
+            // the cell's inputs into this row's LDS (parameters: the solve's own sh.prm)
+            const bcm3hip::CpInitItem ii{0, it.eval, it.parent >= 0 ? 0 : -1, it.sobol_ix, it.is_initial};
+            bcm3hip::cp_init_cell(m, ii, q.values, shs[r].prm, qin[r].y0, &qin[r].creation, qpe[r], qach + r, nullptr);
+            q.creation[qi] = qin[r].creation;  // (the numbering's copy, after the launch)
+        }
+        __syncthreads();
+        if (mine) cp_solve_cell(a, shs[r], qi, 0, qin + r);
+        // the cells' end states (the daughters' inputs, every lane's stores) before their items are published
+        q_drain();
+        if (mine && ln == 0) {
+            const int e = it.eval;
+            const int f = a.flags[qi];
+            int nd = 0;
+            if (q_load(q.failed_eval + e) == 0) {
+                if (!(f & 1)) {
+                    q_store(q.failed_eval + e, 1);
+                } else if (f & 16) {
+                    for (int child = 0; child < 2; child++) {
+                        const int sidx = q.n0 + it.sobol_ix * 2 + child;
+                        if (q.sobol_dims > 0 && sidx >= q.sobol_points) {
+                            q_store(q.failed_eval + e, 1);
+                            break;
+                        }
+                        if (q_add(q.ncells_eval + e, 1) >= q.max_cells) {
+                            q_store(q.failed_eval + e, 1);
+                            break;
+                        }
+                        dsob[r][nd++] = sidx;
+                    }
+                }
+            }
+            ndau[r] = nd;
+            deval[r] = e;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            // the wavefront's daughters enqueued together, in row order (sisters side by side, the
+            // daughters of neighbouring cells next to each other, as the generation launches order them)
+            int total = 0, ran = 0;
+            for (int k = 0; k < CPW; k++)
+                if (run[k]) {
+                    total += ndau[k];
+                    ran++;
+                }
+            if (total > 0) {
+                // outstanding first: the launch cannot drain while these cells (still outstanding) add
+                q_add(q.counters + Q_OUTSTANDING, total);
+                int t = q_add(q.counters + Q_TAIL, total);
+                const int t0 = t;
+                for (int k = 0; k < CPW; k++) {
+                    if (!run[k]) continue;
+                    for (int j = 0; j < ndau[k]; j++, t++) {
+                        CpQueueItem* dst = q.items + t;
+                        q_store(&dst->slot, t);
+                        q_store(&dst->eval, deval[k]);
+                        q_store(&dst->parent, ticket[k]);
+                        q_store(&dst->sobol_ix, dsob[k][j]);
+                        q_store(&dst->is_initial, 0);
+                        q.child_qi[2 * ticket[k] + j] = t;
+                    }
+                }
+                q_drain();  // the items before their flags
+                for (int k = t0; k < t; k++) q_store(q.ready + k, 1);
+            }
+            if (ran > 0) {
+                q_drain();
+                q_add(q.counters + Q_OUTSTANDING, -ran);
+            }
+            for (int k = 0; k < CPW; k++)
+                if (run[k]) ticket[k] = NEED;
+        }
+        __syncthreads();
+    }
+}
+#endif

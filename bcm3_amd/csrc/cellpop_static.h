@@ -5,7 +5,12 @@
 
 #include <cstdint>
 
+// (the run-time compiled cell kernel's work queue includes this header too: hipRTC finds it by name)
+#if defined(__HIPCC_RTC__)
+#include "bcm3hip.h"
+#else
 #include "../../include/bcm3hip.h"
+#endif
 
 namespace bcm3hip {
 
@@ -36,6 +41,14 @@ struct CpInitItem {
     int32_t slot, eval, parent, sobol_ix, is_initial;
 };
 
+// the per-cell outputs a batch leaves (cellpop_cells, the data likelihoods)
+struct CpCellArrays {
+    double *out_values, *end_y, *creation, *sim_end, *achieved, *event_times;
+    int32_t *flags, *nsteps;
+};
+
+// the host launchers (cellpop_kernels.hip), not for the run-time compiled program
+#if !defined(__HIPCC_RTC__)
 hipError_t launch_cp_init(const CpStatic& m, int32_t n_items, const CpInitItem* items, const double* values,
                           double* params, double* y0, double* creation, const double* end_y, const double* achieved,
                           double* sync_off, hipStream_t s);
@@ -62,11 +75,24 @@ size_t cp_assign_ws_bytes(int n);  // the matching workspace of n x n cells
 // the dynamic workspace plus the larger kernel's static LDS (cp_timepoints_kernel, ~8.4 KB) stay within
 // 64 KB, the workgroup limit of parts smaller than gfx950's 160 KB
 inline bool cp_assign_lds_fits(int n) { return cp_assign_ws_bytes(n) <= 52 * 1024; }
+// the work queue of the cell kernel (cellpop_solver.h cp_queue_kernel) indexes cells by queue position;
+// cp_number_kernel numbers them as the generation launches do (the reference's FIFO: the initial
+// cells, then per generation the two daughters of each dividing cell in cell order): perm[e][slot] =
+// queue position, ncells / failed per evaluation, sim_child[e][slot] = the slot's first daughter's
+// cell index (-1); first_pos[i] = the queue position of initial cell i within its evaluation's n0
+hipError_t launch_cp_number(int32_t n, int32_t max_cells, int32_t n0, const int32_t* first_pos, const int32_t* child_qi,
+                            const int32_t* failed_eval, int32_t* perm, int32_t* ncells, int32_t* failed,
+                            int32_t* sim_child, hipStream_t s);
+// dst[slot] = src[perm[slot]] for the slots of every evaluation's cells
+hipError_t launch_cp_permute(int32_t n, int32_t max_cells, int32_t M, int32_t NS, const int32_t* perm,
+                             const int32_t* ncells, CpCellArrays src, CpCellArrays dst, hipStream_t s);
 // out[w] = flags[work[w]]
 hipError_t launch_cp_gather(const int32_t* work, int32_t n, const int32_t* flags, int32_t* out, hipStream_t s);
 // the next experiment's (x, xstatus) into the running sum (logp, status) of
 // CellPopulationLikelihood::EvaluateLogProbability (CellPopulationLikelihood.cpp:90-98)
 hipError_t launch_cp_accumulate(int32_t n, double* logp, int32_t* status, const double* x, const int32_t* xstatus,
                                 hipStream_t s);
+
+#endif
 
 }  // namespace bcm3hip

@@ -65,9 +65,9 @@ __device__ double quantile_normal(double p, double mu, double sigma)
 {
     double z;
     if (!(p > 0.0))
-        z = (p == 0.0) ? -INFINITY : NAN;
+        z = (p == 0.0) ? -__builtin_inf() : __builtin_nan("");
     else if (!(p < 1.0))
-        z = (p == 1.0) ? INFINITY : NAN;
+        z = (p == 1.0) ? __builtin_inf() : __builtin_nan("");
     else if (p <= 0.5)
         z = ndtri_lower(p);
     else

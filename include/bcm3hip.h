@@ -28,8 +28,10 @@
 #ifndef BCM3HIP_H
 #define BCM3HIP_H
 
+#if !defined(__HIPCC_RTC__)  /* (the run-time compiled cell kernel: hipRTC defines these types itself) */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {

@@ -1,7 +1,8 @@
 """Static instruction categories of the C4 cell kernel (cp_solve_kernel) by loop depth.
 
     BCM3_CP_DUMP=/tmp/cp_model.hip <create the C4 likelihood>    (cellpop_rt.cpp writes its program text)
-    python tools/cp_isa_stats.py /tmp/cp_model.hip
+    python tools/cp_isa_stats.py /tmp/cp_model.hip [kernel]    (kernel: cp_solve_kernel, or cp_queue_kernel
+                                                                of a BCM3_CP_QUEUE=1 dump)
 
 Compiles the dumped hipRTC program with the runtime's options (hipcc --cuda-device-only -S) and splits
 cp_solve_kernel's instructions by the loop depth LLVM annotates (1: the cell driver's step loop, 2: the
@@ -48,7 +49,8 @@ def main():
                     "-ffp-contract=off", "-DBCM3_CORRECTLY_ROUNDED", "-I" + os.path.join(ROOT, "bcm3_amd", "csrc"), "-w",
                     "-o", asm, src], check=True)
     lines = open(asm).read().split("\n")
-    start = next(i for i, l in enumerate(lines) if l.startswith("cp_solve_kernel:"))
+    kernel = sys.argv[2] if len(sys.argv) > 2 else "cp_solve_kernel"
+    start = next(i for i, l in enumerate(lines) if l.startswith(kernel + ":"))
     end = next(i for i, l in enumerate(lines) if i > start and l.strip().startswith(".Lfunc_end"))
     depth = 0
     stats = collections.defaultdict(collections.Counter)
@@ -68,7 +70,7 @@ def main():
     for d in sorted(stats):
         tot = sum(stats[d].values())
         allc.update(stats[d])
-        print(f"{names.get(d, d):24s}" + "".join(f"{stats[d][c]:>10d} {100 * stats[d][c] / tot:4.1f}%" for c in cats)
+        print(f"{names.get(d, 'depth ' + str(d)):24s}" + "".join(f"{stats[d][c]:>10d} {100 * stats[d][c] / tot:4.1f}%" for c in cats)
               + f"{tot:>8d}")
     tot = sum(allc.values())
     print(f"{'whole kernel':24s}" + "".join(f"{allc[c]:>10d} {100 * allc[c] / tot:4.1f}%" for c in cats) + f"{tot:>8d}")
