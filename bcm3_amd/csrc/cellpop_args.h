@@ -61,7 +61,7 @@ struct CpQueueItem {
 struct CpQueueArgs {
     CpQueueItem* items;      // [cap]
     int32_t* ready;          // [cap] 1 once the item is written (initial cells: preset)
-    int32_t* counters;       // [4] head (next item to take), tail (items reserved), outstanding (items
+    int32_t* counters;       // [6] head (next item to take), tail (items reserved), outstanding (items
                              //     not finished), error (a bounded wait ran out)
     int32_t* child_qi;       // [cap][2] queue indices of the daughters (-1)
     int32_t* ncells_eval;    // [n] cells of each evaluation (initial cells + daughters enqueued)

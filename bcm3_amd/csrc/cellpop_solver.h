@@ -1841,7 +1841,16 @@ __device__ __forceinline__ void q_drain()
 // a bounded wait: 2^22 polls of >= 512 cycles (seconds) before the launch gives up with the error
 // counter set (a lost item would otherwise keep the persistent grid alive)
 constexpr long kQueueSpins = 1l << 22;
-enum { Q_HEAD = 0, Q_TAIL = 1, Q_OUTSTANDING = 2, Q_ERROR = 3 };
+enum { Q_HEAD = 0, Q_TAIL = 1, Q_OUTSTANDING = 2, Q_ERROR = 3, Q_ROUNDS = 4, Q_ROWS = 5 };
+// the kernel arguments re-read where the queue's bookkeeping uses them: without this the compiler keeps
+// their fields in SGPRs across the whole persistent loop, and the cell solve's own scalars then spill
+// into VGPR lanes inside its Newton loop
+template <class T> __device__ __forceinline__ const T& opaque(const T& x)
+{
+    const T* p = &x;
+    asm volatile("" : "+s"(p));
+    return *p;
+}
 }  // namespace cpk
 
 // One persistent launch for all cells of a batch. Queue positions are handed out as tickets (one
@@ -1857,7 +1866,7 @@ enum { Q_HEAD = 0, Q_TAIL = 1, Q_OUTSTANDING = 2, Q_ERROR = 3 };
 // position; cp_number_kernel and cp_permute_kernel (cellpop_kernels.hip) restore the reference's cell
 // numbering.
 extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(CP_WAVES_PER_EU))) void cp_queue_kernel(
-    cpk::CpSolveArgs a, cpk::CpQueueArgs q, bcm3hip::CpStatic m)
+    cpk::CpSolveArgs a_, cpk::CpQueueArgs q_, bcm3hip::CpStatic m_)
 {
     using namespace cpk;
     enum { NEED = -1, DONE = -2 };
@@ -1868,12 +1877,16 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
     __shared__ int ticket[CPW];  // the row's queue position, NEED or DONE
     __shared__ int run[CPW];     // the row's item is ready: it runs this round
     __shared__ int ndau[CPW], deval[CPW], dsob[CPW][2];  // the daughters a row's cell enqueues
+    __shared__ int isob[CPW];    // the row's cell's Sobol index (nothing of the item stays live in registers
+                                 // across the solve)
+    __shared__ long idle;        // rounds without a ready ticket
     const int r = row(), ln = lane();
     if (threadIdx.x < CPW) ticket[threadIdx.x] = NEED;
+    if (threadIdx.x == 0) idle = 0;
     __syncthreads();
-    long idle = 0;
     for (;;) {
         if (threadIdx.x == 0) {
+            const CpQueueArgs& q = opaque(q_);
             // tickets for the rows that need one, in row order
             int need = 0;
             for (int k = 0; k < CPW; k++) need += ticket[k] == NEED;
@@ -1901,7 +1914,14 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
                     __builtin_amdgcn_s_sleep(8);
                 }
             }
-            if (any) idle = 0;
+            if (any) {
+                idle = 0;
+                // statistics: rounds that solve, cells solved (BCM3_CP_QUEUE_VERBOSE prints them)
+                int rows = 0;
+                for (int k = 0; k < CPW; k++) rows += run[k] != 0;
+                q_add(q.counters + Q_ROUNDS, 1);
+                q_add(q.counters + Q_ROWS, rows);
+            }
         }
         __syncthreads();
         bool all_done = true;
@@ -1910,9 +1930,11 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
         const bool mine = run[r] != 0;
         const int qi = ticket[r];
         __syncthreads();
-        CpQueueItem it{};
-        it.eval = -1;
         if (mine && ln == 0) {
+            CpQueueItem it{};
+            const CpQueueArgs& q = opaque(q_);
+            const CpSolveArgs& a = opaque(a_);
+            const bcm3hip::CpStatic& m = opaque(m_);
             __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the item after its flag
             CpQueueItem* src = q.items + qi;
             it.eval = q_load(&src->eval);
@@ -1927,21 +1949,25 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
             const bcm3hip::CpInitItem ii{0, it.eval, it.parent >= 0 ? 0 : -1, it.sobol_ix, it.is_initial};
             bcm3hip::cp_init_cell(m, ii, q.values, shs[r].prm, qin[r].y0, &qin[r].creation, qpe[r], qach + r, nullptr);
             q.creation[qi] = qin[r].creation;  // (the numbering's copy, after the launch)
+            deval[r] = it.eval;
+            isob[r] = it.sobol_ix;
         }
         __syncthreads();
-        if (mine) cp_solve_cell(a, shs[r], qi, 0, qin + r);
+        if (mine) cp_solve_cell(a_, shs[r], qi, 0, qin + r);
         // the cells' end states (the daughters' inputs, every lane's stores) before their items are published
         q_drain();
-        if (mine && ln == 0) {
-            const int e = it.eval;
-            const int f = a.flags[qi];
+        if (run[r] && ln == 0) {  // (re-read from LDS: nothing of the round stays live across the solve)
+            const CpQueueArgs& q = opaque(q_);
+            const CpSolveArgs& a = opaque(a_);
+            const int e = deval[r];
+            const int f = a.flags[ticket[r]];
             int nd = 0;
             if (q_load(q.failed_eval + e) == 0) {
                 if (!(f & 1)) {
                     q_store(q.failed_eval + e, 1);
                 } else if (f & 16) {
                     for (int child = 0; child < 2; child++) {
-                        const int sidx = q.n0 + it.sobol_ix * 2 + child;
+                        const int sidx = q.n0 + isob[r] * 2 + child;
                         if (q.sobol_dims > 0 && sidx >= q.sobol_points) {
                             q_store(q.failed_eval + e, 1);
                             break;
@@ -1955,10 +1981,10 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
                 }
             }
             ndau[r] = nd;
-            deval[r] = e;
         }
         __syncthreads();
         if (threadIdx.x == 0) {
+            const CpQueueArgs& q = opaque(q_);
             // the wavefront's daughters enqueued together, in row order (sisters side by side, the
             // daughters of neighbouring cells next to each other, as the generation launches order them)
             int total = 0, ran = 0;
