@@ -388,7 +388,9 @@ int bcm3hip_open_cellpop_experiments(int device, const bcm3hip_cellpop_model* mo
 /* compile (or find in the cache) the model's cell kernel without a device (build time) */
 int bcm3hip_cellpop_precompile(const bcm3hip_cellpop_model* model);
 /* cells of item `item` of the last cellpop evaluation: *count cells, records / values[count*M]
- * (the data likelihood's values per output entry) / end_y[count*NS] may be NULL */
+ * (the data likelihood's values per output entry) / end_y[count*NS] may be NULL. In the reference's
+ * cell numbering; for an evaluation that failed (logp -inf) under the device work queue the list ends
+ * where that evaluation stopped enqueueing. */
 int bcm3hip_cellpop_cells(bcm3hip_ctx* ctx, size_t item, int32_t* count, bcm3hip_cell_record* records,
                           double* values, double* end_y);
 int bcm3hip_close(bcm3hip_ctx* ctx);
