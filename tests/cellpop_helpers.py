@@ -117,3 +117,41 @@ def check_logp(lp, status, ref, ref_nofma=None, name=""):
     parity.log_summary(rec, n=len(ref))
     assert worst <= 1.0, rec
     return dev, spread
+
+
+def write_wide_model(directory, extra=6):
+    """the C4 model with `extra` reporter species appended (a chain driven by CycB, each decaying,
+    nothing feeding back): NS = 15 + extra ODE species, past the 16-lane row of the four-cell build, so
+    the cell kernel takes its one-cell-per-wavefront form (cellpop_solver.h ROW = 64)"""
+    text = open(os.path.join(GOLDEN, "cellpop_model.xml")).read()
+    sp = "".join(f'      <species id="X{i}" name="X{i}" compartment="cell" initialAmount="0.{i}"/>\n'
+                 for i in range(1, extra + 1))
+    text = text.replace("    </listOfSpecies>", sp + "    </listOfSpecies>", 1)
+    mm = 'xmlns="http://www.w3.org/1998/Math/MathML"'
+    rx = []
+    for i in range(1, extra + 1):
+        src = "CycB" if i == 1 else f"X{i - 1}"
+        rx.append(f'      <reaction id="rx{i}_make" reversible="false">\n'
+                  f'        <listOfProducts><speciesReference species="X{i}" stoichiometry="1"/></listOfProducts>\n'
+                  f'        <listOfModifiers><modifierSpeciesReference species="{src}"/></listOfModifiers>\n'
+                  f'        <kineticLaw><math {mm}><apply><times/><cn> 0.{i + 2} </cn><ci> {src} </ci></apply></math></kineticLaw>\n'
+                  f'      </reaction>\n'
+                  f'      <reaction id="rx{i}_decay" reversible="false">\n'
+                  f'        <listOfReactants><speciesReference species="X{i}"/></listOfReactants>\n'
+                  f'        <kineticLaw><math {mm}><apply><times/><cn> 0.5 </cn><ci> X{i} </ci></apply></math></kineticLaw>\n'
+                  f'      </reaction>\n')
+    text = text.replace("    </listOfReactions>", "".join(rx) + "    </listOfReactions>", 1)
+    path = os.path.join(str(directory), "cellpop_model_wide.xml")
+    with open(path, "w") as f:
+        f.write(text)
+    return path
+
+
+def write_wide_likelihood(directory, num_cells, max_cells, extra=6, **attrs):
+    """a likelihood on write_wide_model's model (the C4 data and variabilities)"""
+    path = os.path.join(str(directory), "cellpop_wide_likelihood.xml")
+    with open(path, "w") as f:
+        f.write(F.likelihood_text(num_cells=num_cells, max_cells=max_cells,
+                                  data_file=os.path.join(GOLDEN, "cellpop_data.json"),
+                                  model_file=write_wide_model(directory, extra), **attrs))
+    return path

@@ -22,6 +22,14 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 dev = torch.device("cuda", 0)
 lik, pri = os.path.join(G, "cellpop_likelihood.xml"), os.path.join(G, "cellpop_prior.xml")
+M, NS = 21, 15
+# WIDE=1: the C4 workload on the model with six reporter species (NS = 21, one cell per wavefront)
+if os.environ.get("WIDE") == "1":
+    import tempfile
+    sys.path[:0] = [os.path.join(ROOT, "tests"), G, os.path.join(ROOT, "oracle")]
+    import cellpop_helpers as CH  # noqa: E402
+    lik = CH.write_wide_likelihood(tempfile.mkdtemp(), 500, 2048)
+    NS = 21
 
 
 def make(queue):
@@ -47,8 +55,8 @@ print(f"logp bit-identical {int(same.sum())}/{n} (finite {int(fin.sum())}, queue
       flush=True)
 cells_ok = 0
 for i in np.nonzero(fin)[0]:
-    ra, va, ya = paths["generations"].cellpop_cells(int(i), 21, 15)
-    rb, vb, yb = paths["queue"].cellpop_cells(int(i), 21, 15)
+    ra, va, ya = paths["generations"].cellpop_cells(int(i), M, NS)
+    rb, vb, yb = paths["queue"].cellpop_cells(int(i), M, NS)
     ok = len(ra) == len(rb) and ra.tobytes() == rb.tobytes() and va.tobytes() == vb.tobytes() and ya.tobytes() == yb.tobytes()
     cells_ok += ok
     if not ok:
