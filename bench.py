@@ -411,8 +411,9 @@ def expm_cpu_baseline(budget_s: float, seed: int):
 def cellpop_workload(device, gen, n=64):
     """Config C4 (BASELINE.json configs[3]): the cell-population likelihood (synthetic cell-cycle SBML
     model, 15 ODE species, 500 initial heterogeneous cells dividing over 20 h, ~1,500 cell
-    trajectories per evaluation), 64 chains' proposals per launch -- the whole generation loop
-    (init, solve, division bookkeeping, data likelihood) timed with HIP events."""
+    trajectories per evaluation), 64 chains' proposals per launch -- the whole batch (the device-side cell
+    work queue: init, solve, division bookkeeping and the reference's numbering in one persistent
+    launch, then the data likelihood) timed with HIP events."""
     from bcm3_amd.likelihood import Likelihood
     from bcm3_amd.sampler import DevicePrior, load_prior
     lik, pri = os.path.join(GOLDEN, "cellpop_likelihood.xml"), os.path.join(GOLDEN, "cellpop_prior.xml")
@@ -424,7 +425,7 @@ def cellpop_workload(device, gen, n=64):
         rec, _, _ = ll.cellpop_cells(i, 21, 15)
         cells += len(rec)
         steps += int(rec["nsteps"].sum())
-    # evaluations that fail (-inf: too many cells, a solver failure) stop adding generations
+    # evaluations that fail (-inf: too many cells, a solver failure) stop enqueueing cells
     # (cellpop_rt.cpp), so the all-draws rate mixes full and truncated evaluations:
     # the same launch size over finite draws only gives the full-evaluation rate
     import numpy as np
@@ -451,8 +452,8 @@ def cellpop_workload(device, gen, n=64):
             "cells_per_eval": cells / n, "roofline": roof,
             "cell_trajectories_per_s": cells / (ms * 1e-3), "bdf_steps_per_cell": steps / max(1, cells),
             "cell_bdf_steps_per_s": steps / (ms * 1e-3), "cells_per_wavefront": 4,
-            "note": "throughput-bound (every SIMD busy); four cells per wavefront, one 16-lane row each "
-                    "(DESIGN.md §4 'cell population')",
+            "note": "throughput-bound (every SIMD busy); four cells per wavefront, one 16-lane row each, "
+                    "from a device-side work queue in one persistent launch (DESIGN.md §4 'cell population')",
             "draws": x.detach().cpu().numpy()}
 
 
