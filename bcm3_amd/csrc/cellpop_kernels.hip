@@ -58,8 +58,10 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
     // lane k: entry k. The cells are staged through LDS 64 at a time with coalesced loads (every lane
     // loads), so the per-entry loops in cell order read LDS instead of waiting on one global load per
     // cell; the sum keeps the cell order and the same quotients (0.95 -> 0.63 ms per C4 batch)
-    __shared__ double cr_s[64], se_s[64];
+    __shared__ double cr_s[64], se_s[64], pop_s[64];
     __shared__ double tile[64][65];
+    // a NaN payload no arithmetic produces: "this cell's value is NaN, skip it"
+    constexpr long long kPopSkip = 0x7ff8dead5eed0001ll;
     // CountCellsAtTime(st.time + time_offset, None) (Experiment.cpp:285, 301): the population is
     // counted at the data time plus the experiment's synchronization_time_offset, the time its values
     // were read at (the stored mode's evaluation passes; without synchronised data the loader refuses
@@ -70,33 +72,80 @@ __global__ __launch_bounds__(64) void cp_popavg_kernel(CpStatic m, int32_t n, co
         const bool kv = k < m.M;
         const int kw = (m.M - k0 < 64) ? m.M - k0 : 64;
         const double t = kv ? m.output_times[k] + toff : 0.0;
+        // each chunk's global loads are issued before the previous chunk's LDS work (software
+        // pipelining: a chunk's latency hides behind the other's compares and sums)
         int pop = 0;
+        double ncr = 0.0, nse = 0.0;
+        if (ln < nc) {
+            ncr = creation[base + ln];
+            nse = sim_end[base + ln];
+        }
         for (int c0 = 0; c0 < nc; c0 += 64) {
             const int cn = (nc - c0 < 64) ? nc - c0 : 64;
             __syncthreads();
             if (ln < cn) {
-                cr_s[ln] = creation[base + c0 + ln];
-                se_s[ln] = sim_end[base + c0 + ln];
+                cr_s[ln] = ncr;
+                se_s[ln] = nse;
+            }
+            if (c0 + 64 + ln < nc) {
+                ncr = creation[base + c0 + 64 + ln];
+                nse = sim_end[base + c0 + 64 + ln];
             }
             __syncthreads();
+            // (unrolled: the LDS reads of eight cells issue together, then the dependent updates)
+#pragma unroll 8
             for (int j = 0; j < cn; j++) {
                 const double ct = t - cr_s[j];
-                pop += (ct >= 0.0 && ct <= se_s[j]) ? 1 : 0;
+                const double se = se_s[j];
+                pop += (int)(ct >= 0.0) & (int)(ct <= se);  // (no short circuit: both reads issue together)
             }
         }
+        // the quotients x / pop are formed in parallel (lane = cell of the chunk) and only the sum runs in
+        // cell order (a division's dependent chain per cell was the serial loop's cost); a cell whose value
+        // is NaN is skipped as in the reference (the test is on the value, so a 0 / 0 still adds its NaN)
+        pop_s[ln] = (double)pop;
         double s = 0.0;
+        constexpr int PF = 32;  // values per lane of a chunk held for the next one (kw <= PF)
+        double nx[PF];
+        auto fetch = [&](int c0) {
+            const int n_el = ((nc - c0 < 64) ? nc - c0 : 64) * kw;
+#pragma unroll
+            for (int r = 0; r < PF; r++) {
+                const int idx = ln + 64 * r;
+                if (idx < n_el) {
+                    const int j = idx / kw, kk = idx - j * kw;
+                    nx[r] = out_values[(base + c0 + j) * m.M + k0 + kk];
+                }
+            }
+        };
+        if (kw <= PF && nc > 0) fetch(0);
         for (int c0 = 0; c0 < nc; c0 += 64) {
             const int cn = (nc - c0 < 64) ? nc - c0 : 64;
             __syncthreads();
-            for (int idx = ln; idx < cn * kw; idx += 64) {
-                const int j = idx / kw, kk = idx - j * kw;
-                tile[j][kk] = out_values[(base + c0 + j) * m.M + k0 + kk];
+            if (kw <= PF) {
+#pragma unroll
+                for (int r = 0; r < PF; r++) {
+                    const int idx = ln + 64 * r;
+                    if (idx < cn * kw) {
+                        const int j = idx / kw, kk = idx - j * kw;
+                        const double x = nx[r];
+                        tile[j][kk] = (x == x) ? x / pop_s[kk] : __longlong_as_double(kPopSkip);
+                    }
+                }
+                if (c0 + 64 < nc) fetch(c0 + 64);
+            } else {
+                for (int idx = ln; idx < cn * kw; idx += 64) {
+                    const int j = idx / kw, kk = idx - j * kw;
+                    const double x = out_values[(base + c0 + j) * m.M + k0 + kk];
+                    tile[j][kk] = (x == x) ? x / pop_s[kk] : __longlong_as_double(kPopSkip);
+                }
             }
             __syncthreads();
             if (kv)
+#pragma unroll 8
                 for (int j = 0; j < cn; j++) {
-                    const double x = tile[j][ln];
-                    if (x == x) s += x / (double)pop;
+                    const double q = tile[j][ln];
+                    if (__double_as_longlong(q) != kPopSkip) s += q;
                 }
         }
         if (kv) avg[(size_t)e * m.M + k] = s;
