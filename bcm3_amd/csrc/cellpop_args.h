@@ -69,6 +69,7 @@ struct CpQueueArgs {
     double* creation;        // [cap] the cells' creation times (written by the queue's initialisation)
     const double* values;    // [n][d]
     int32_t cap, n0, max_cells, sobol_points, sobol_dims;
+    int64_t idle_limit;      // wall-clock ticks a wavefront may find nothing ready before the launch fails
 };
 
 }  // namespace cpk

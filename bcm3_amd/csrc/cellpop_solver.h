@@ -1838,9 +1838,10 @@ __device__ __forceinline__ void q_drain()
     __builtin_amdgcn_s_waitcnt(0);
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
-// a bounded wait: 2^22 polls of >= 512 cycles (seconds) before the launch gives up with the error
-// counter set (a lost item would otherwise keep the persistent grid alive)
-constexpr long kQueueSpins = 1l << 22;
+// a bounded wait: a wavefront that finds nothing ready for q.idle_limit ticks of the constant-rate wall
+// clock (60 s: far beyond any cell's solve, which other wavefronts may still be running) gives up with
+// the error counter set (a lost item would otherwise keep the persistent grid alive); its polls back
+// off from ~0.2 to ~3 us between reads of the shared counters
 enum { Q_HEAD = 0, Q_TAIL = 1, Q_OUTSTANDING = 2, Q_ERROR = 3, Q_ROUNDS = 4, Q_ROWS = 5 };
 // the kernel arguments re-read where the queue's bookkeeping uses them: without this the compiler keeps
 // their fields in SGPRs across the whole persistent loop, and the cell solve's own scalars then spill
@@ -1879,7 +1880,8 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
     __shared__ int ndau[CPW], deval[CPW], dsob[CPW][2];  // the daughters a row's cell enqueues
     __shared__ int isob[CPW];    // the row's cell's Sobol index (nothing of the item stays live in registers
                                  // across the solve)
-    __shared__ long idle;        // rounds without a ready ticket
+    __shared__ long idle;        // polls without a ready ticket
+    __shared__ unsigned long long idle_t0;  // wall clock at the first of them
     const int r = row(), ln = lane();
     if (threadIdx.x < CPW) ticket[threadIdx.x] = NEED;
     if (threadIdx.x == 0) idle = 0;
@@ -1907,11 +1909,17 @@ extern "C" __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(C
                     for (int k = 0; k < CPW; k++)
                         if (ticket[k] >= 0 && q_load(q.ready + ticket[k]) != 1) ticket[k] = DONE;
                     for (int k = 0; k < CPW; k++) run[k] = ticket[k] >= 0;  // (filled meanwhile)
-                } else if (++idle >= kQueueSpins) {
-                    q_add(q.counters + Q_ERROR, 1);
-                    for (int k = 0; k < CPW; k++) ticket[k] = DONE;
                 } else {
-                    __builtin_amdgcn_s_sleep(8);
+                    const unsigned long long now = wall_clock64();
+                    if (idle++ == 0) idle_t0 = now;
+                    if (now - idle_t0 > (unsigned long long)q.idle_limit) {
+                        q_add(q.counters + Q_ERROR, 1);
+                        for (int k = 0; k < CPW; k++) ticket[k] = DONE;
+                    } else if (idle < 64) {
+                        __builtin_amdgcn_s_sleep(8);
+                    } else {
+                        __builtin_amdgcn_s_sleep(127);
+                    }
                 }
             }
             if (any) {

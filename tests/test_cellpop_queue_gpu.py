@@ -105,3 +105,22 @@ def test_queue_bench_size(monkeypatch):
     assert _same(gen, que, x[::-1].copy()) > 0
     gen.close()
     que.close()
+
+
+def test_queue_stall_is_reported(tmp_path, monkeypatch):
+    """the queue's bounded wait: with a 0 ms bound every wavefront that finds nothing ready gives up at
+    once, the launch drains and the host reports the stall as an error instead of a result (the 60 s
+    default is far beyond any cell's solve)"""
+    from bcm3_amd.likelihood import Likelihood
+    path = CH.write_likelihood(tmp_path, 40, 256)
+    monkeypatch.setenv("BCM3_CP_QUEUE", "1")
+    monkeypatch.setenv("BCM3_CP_QUEUE_IDLE_MS", "0")
+    ll = Likelihood(path, CH.PRIOR, device=0)
+    with pytest.raises(Exception):
+        ll.evaluate_batch(CH.draws(4, 11))
+    ll.close()
+    monkeypatch.delenv("BCM3_CP_QUEUE_IDLE_MS")
+    gen, que = _pair(path, CH.PRIOR, monkeypatch)
+    _same(gen, que, CH.draws(4, 11))  # (a fresh likelihood with the default bound is unaffected)
+    gen.close()
+    que.close()
