@@ -71,10 +71,35 @@ def main():
             for k in kids.get((c[0], c[1]), []):
                 cnt += 1
                 heapq.heappush(pending, (te, 10 ** 9 + cnt, k))
+    # daughters first: a free slot takes the daughters already enqueued before the remaining initial
+    # cells (the deepest chains start early; initial cells fill the end), initial cells in their order
+    lo = [c for c in cells if c[3] == 0]
+    lo.reverse()
+    hi = []
+    slots = [0.0] * SLOTS
+    end_p, cnt = 0.0, 0
+    while lo or hi:
+        st = heapq.heappop(slots)
+        batch = []
+        while hi and len(batch) < 4 and hi[0][0] <= st:
+            ta, _, c = heapq.heappop(hi)
+            batch.append((ta, c))
+        while lo and len(batch) < 4:
+            batch.append((0.0, lo.pop()))
+        while hi and len(batch) < 4:
+            ta, _, c = heapq.heappop(hi)
+            batch.append((ta, c))
+        te = max(st, max(b[0] for b in batch)) + max(b[1][4] for b in batch)
+        end_p = max(end_p, te)
+        heapq.heappush(slots, te)
+        for _, c in batch:
+            for k in kids.get((c[0], c[1]), []):
+                cnt += 1
+                heapq.heappush(hi, (te, cnt, k))
     work = sum(waves_of(sorted(cells, key=lambda c: (c[3], c[0], c[1])))) / SLOTS
     print(f"{len(cells)} cells of {len(set(c[0] for c in cells))} finite evaluations, {ngen} generations, {SLOTS} wave slots")
     print(f"generation launches: {t:.0f} step-times; wave-level queue: {end:.0f} ({t / end:.3f}x); work / slots bound: "
-          f"{work:.0f} ({t / work:.3f}x)")
+          f"{work:.0f} ({t / work:.3f}x); daughters-first queue: {end_p:.0f} ({t / end_p:.3f}x)")
 
 
 if __name__ == "__main__":
